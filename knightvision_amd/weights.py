@@ -1,0 +1,183 @@
+"""ChessNet parameters: the reference state_dict layout, build-defined synthetic
+weights, and the folded NHWC packing the HIP kernels read.
+
+Reference architecture: ``ai/model.py:27-77`` (ChessNet) and ``ai/model.py:8-25``
+(ResidualBlock). Every conv has ``bias=True`` followed by an eval-mode
+BatchNorm2d (eps 1e-5), which folds to a per-channel ``scale``/``shift``:
+
+    y = (conv(x) + b - mean) * gamma / sqrt(var + eps) + beta
+      = conv(x) * scale + shift
+
+The packed layout (one contiguous fp32 blob, offsets in ``PACK_LAYOUT``) is what
+``kv_net_load`` in ``include/kv.h`` consumes.
+"""
+from __future__ import annotations
+
+import collections
+import numpy as np
+
+BN_EPS = 1e-5
+N_RES = 5
+
+# (name, shape) in the reference state_dict order (ai/model.py:31-49).
+def _bn(prefix, c):
+    return [(prefix + ".weight", (c,)), (prefix + ".bias", (c,)),
+            (prefix + ".running_mean", (c,)), (prefix + ".running_var", (c,)),
+            (prefix + ".num_batches_tracked", ())]
+
+
+def _conv(prefix, cout, cin, k):
+    return [(prefix + ".weight", (cout, cin, k, k)), (prefix + ".bias", (cout,))]
+
+
+def state_dict_spec():
+    spec = []
+    spec += _conv("conv1", 256, 12, 3) + _bn("bn1", 256)
+    spec += _conv("conv2", 512, 256, 3) + _bn("bn2", 512)
+    for i in range(N_RES):
+        p = f"res_blocks.{i}"
+        spec += _conv(p + ".conv1", 512, 512, 3) + _bn(p + ".bn1", 512)
+        spec += _conv(p + ".conv2", 512, 512, 3) + _bn(p + ".bn2", 512)
+    spec += _conv("policy_conv", 2, 512, 1) + _bn("policy_bn", 2)
+    spec += [("policy_fc.weight", (4096, 128)), ("policy_fc.bias", (4096,))]
+    spec += _conv("value_conv", 1, 512, 1) + _bn("value_bn", 1)
+    spec += [("value_fc1.weight", (512, 64)), ("value_fc1.bias", (512,))]
+    spec += [("value_fc2.weight", (1, 512)), ("value_fc2.bias", (1,))]
+    return spec
+
+
+def synthetic_state_dict(seed: int = 42, variant: str = "init") -> "collections.OrderedDict[str, np.ndarray]":
+    """Deterministic ChessNet weights (numpy PCG64 stream, key order above).
+
+    variant:
+      "init"   -- PyTorch default-init scale: weights and biases U(-1/sqrt(fan_in), +),
+                  BN at its init state (gamma 1, beta 0, mean 0, var 1).
+      "bn"     -- same convs/FCs, BN affine + running stats randomised.
+      "peaked" -- "bn" with policy_fc x30 so move choice depends on the network.
+    """
+    if variant not in ("init", "bn", "peaked"):
+        raise ValueError(f"unknown weight variant {variant!r}")
+    rng = np.random.default_rng(seed)
+    out = collections.OrderedDict()
+    for name, shape in state_dict_spec():
+        if name.endswith("num_batches_tracked"):
+            out[name] = np.array(0, dtype=np.int64)
+            continue
+        leaf = name.rsplit(".", 1)[1]
+        owner = name.rsplit(".", 1)[0]
+        is_bn = "bn" in owner.rsplit(".", 1)[-1]
+        if is_bn:
+            c = shape[0]
+            if variant == "init":
+                val = {"weight": np.ones(c), "bias": np.zeros(c),
+                       "running_mean": np.zeros(c), "running_var": np.ones(c)}[leaf]
+                # consume the stream identically in every variant
+                rng.random(c)
+            else:
+                u = rng.random(c)
+                val = {"weight": 0.5 + u, "bias": (u - 0.5) * 0.4,
+                       "running_mean": (u - 0.5) * 0.4, "running_var": 0.5 + 1.5 * u}[leaf]
+            out[name] = val.astype(np.float32)
+            continue
+        # conv / linear weight or bias: fan_in from the owning weight
+        wshape = dict(state_dict_spec())[owner + ".weight"]
+        fan_in = int(np.prod(wshape[1:]))
+        bound = 1.0 / np.sqrt(fan_in)
+        u = rng.random(int(np.prod(shape)) if shape else 1)
+        val = ((u * 2.0 - 1.0) * bound).reshape(shape)
+        if variant == "peaked" and owner == "policy_fc":
+            val = val * 30.0
+        out[name] = val.astype(np.float32)
+    return out
+
+
+def _fold(sd, conv, bn):
+    w = sd[conv + ".weight"].astype(np.float64)
+    b = sd[conv + ".bias"].astype(np.float64)
+    g = sd[bn + ".weight"].astype(np.float64)
+    beta = sd[bn + ".bias"].astype(np.float64)
+    mu = sd[bn + ".running_mean"].astype(np.float64)
+    var = sd[bn + ".running_var"].astype(np.float64)
+    scale = g / np.sqrt(var + BN_EPS)
+    shift = beta + (b - mu) * scale
+    return w, scale.astype(np.float32), shift.astype(np.float32)
+
+
+# conv tower packing: weights [Cout][tap=ky*3+kx][Cin_pad] (the GEMM B operand
+# stored column-major in K so a K-chunk of one output channel is contiguous).
+CIN_PAD_STEM = 16
+
+
+def _pack_conv3(w, cin_pad):
+    cout, cin = w.shape[0], w.shape[1]
+    o = np.zeros((cout, 9, cin_pad), dtype=np.float32)
+    o[:, :, :cin] = w.transpose(0, 2, 3, 1).reshape(cout, 9, cin)
+    return o.reshape(-1)
+
+
+def pack_weights(sd) -> tuple[np.ndarray, "collections.OrderedDict[str, tuple[int, int]]"]:
+    """Fold BN and pack into one fp32 blob. Returns (blob, layout{name: (offset, count)})."""
+    parts = collections.OrderedDict()
+
+    def add(name, arr):
+        parts[name] = np.ascontiguousarray(arr, dtype=np.float32).reshape(-1)
+
+    convs = [("conv1", "bn1", CIN_PAD_STEM), ("conv2", "bn2", 256)]
+    for i in range(N_RES):
+        p = f"res_blocks.{i}"
+        convs += [(p + ".conv1", p + ".bn1", 512), (p + ".conv2", p + ".bn2", 512)]
+    for li, (conv, bn, cin_pad) in enumerate(convs):
+        w, scale, shift = _fold(sd, conv, bn)
+        add(f"L{li}.w", _pack_conv3(w.astype(np.float32), cin_pad))
+        add(f"L{li}.scale", scale)
+        add(f"L{li}.shift", shift)
+    # heads: 1x1 convs as [out][512] rows + folded BN
+    pw, ps, pb = _fold(sd, "policy_conv", "policy_bn")
+    vw, vs, vb = _fold(sd, "value_conv", "value_bn")
+    add("head.w", np.concatenate([pw.reshape(2, 512), vw.reshape(1, 512)], 0).astype(np.float32))
+    add("head.scale", np.concatenate([ps, vs]))
+    add("head.shift", np.concatenate([pb, vb]))
+    # policy FC: the reference flattens NCHW (index c*64 + sq, ai/model.py:65);
+    # the head kernel emits features in that same order, so the FC keeps [4096][128].
+    add("pfc.w", sd["policy_fc.weight"])
+    add("pfc.b", sd["policy_fc.bias"])
+    add("vfc1.w", sd["value_fc1.weight"])   # [512][64]
+    add("vfc1.b", sd["value_fc1.bias"])
+    add("vfc2.w", sd["value_fc2.weight"].reshape(512))
+    add("vfc2.b", sd["value_fc2.bias"].reshape(1))
+    layout = collections.OrderedDict()
+    off = 0
+    for k, v in parts.items():
+        # keep every tensor 64-byte aligned inside the blob
+        layout[k] = (off, v.size)
+        off += (v.size + 15) // 16 * 16
+    blob = np.zeros(off, dtype=np.float32)
+    for k, v in parts.items():
+        o, n = layout[k]
+        blob[o:o + n] = v
+    return blob, layout
+
+
+PACK_ORDER = ([f"L{i}.{s}" for i in range(12) for s in ("w", "scale", "shift")]
+              + ["head.w", "head.scale", "head.shift", "pfc.w", "pfc.b",
+                 "vfc1.w", "vfc1.b", "vfc2.w", "vfc2.b"])
+
+
+def state_dict_to_numpy(sd) -> "collections.OrderedDict[str, np.ndarray]":
+    """Accept a torch state_dict (or checkpoint dict with 'model_state_dict',
+    self_play.py:72-76) and return numpy arrays under the reference keys."""
+    if isinstance(sd, dict) and "model_state_dict" in sd:
+        sd = sd["model_state_dict"]
+    out = collections.OrderedDict()
+    names = [n for n, _ in state_dict_spec()]
+    missing = [n for n in names if n not in sd and not n.endswith("num_batches_tracked")]
+    if missing:
+        raise KeyError(f"state_dict is missing keys: {missing[:4]}{'...' if len(missing) > 4 else ''}")
+    for n in names:
+        if n not in sd:
+            continue
+        v = sd[n]
+        if hasattr(v, "detach"):
+            v = v.detach().cpu().numpy()
+        out[n] = np.asarray(v)
+    return out

@@ -1,0 +1,174 @@
+"""ctypes wrapper over oracle/_build/libkvoracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this
+module; the knightvision_amd product never does. See kv_oracle.c for the
+reference lines each entry point restates.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libkvoracle.so")
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, "kv_oracle.c")):
+        subprocess.check_call(["make", "-s", "-C", HERE], stdout=subprocess.DEVNULL)
+    return LIB_PATH
+
+
+EVAL_FN = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float))
+SOFTMAX_FN = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float))
+
+
+class GameCfg(C.Structure):
+    _fields_ = [("max_moves", C.c_int), ("batch", C.c_int), ("eps", C.c_double), ("alpha", C.c_double)]
+
+
+class GameResult(C.Structure):
+    _fields_ = [("plies", C.c_int), ("outcome", C.c_int), ("reward", C.c_float), ("reason", C.c_int),
+                ("n_evals", C.c_int)]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(LIB_PATH)
+        P8 = C.POINTER(C.c_int8)
+        L.kvo_valid_moves.argtypes = [P8, C.POINTER(C.c_uint8), C.c_int]
+        L.kvo_in_check.argtypes = [P8]
+        L.kvo_is_draw.argtypes = [P8]
+        L.kvo_make_valid_move.argtypes = [P8, C.c_int]
+        L.kvo_initial_state.argtypes = [P8]
+        L.kvo_encode_board.argtypes = [P8, C.POINTER(C.c_float)]
+        L.kvo_mt_seed_genrand.argtypes = [C.c_void_p, C.c_uint32]
+        L.kvo_mt_seed_python.argtypes = [C.c_void_p, C.c_uint64]
+        L.kvo_mt_next.argtypes = [C.c_void_p]
+        L.kvo_mt_next.restype = C.c_uint32
+        L.kvo_res53.argtypes = [C.c_void_p]
+        L.kvo_res53.restype = C.c_double
+        L.kvo_dirichlet.argtypes = [C.c_void_p, C.c_double, C.c_int, C.POINTER(C.c_double)]
+        L.kvo_dirichlet.restype = C.c_int64
+        L.kvo_choices.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int]
+        L.kvo_randbelow.argtypes = [C.c_void_p, C.c_int]
+        L.kvo_softmax_f32.argtypes = [C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_float)]
+        L.kvo_play_game.argtypes = [C.POINTER(GameCfg), C.c_void_p, C.c_void_p, EVAL_FN, C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.POINTER(C.c_int8), C.POINTER(C.c_uint16), C.c_int,
+                                    C.POINTER(C.c_int), C.c_int, C.POINTER(GameResult)]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def valid_moves(state: np.ndarray):
+    """-> (moves uint8[n,3], state after the call)."""
+    st = np.array(state, dtype=np.int8, copy=True)
+    out = np.zeros((1024, 3), dtype=np.uint8)
+    n = lib().kvo_valid_moves(_p(st, C.c_int8), _p(out, C.c_uint8), 1024)
+    return out[:n].copy(), st
+
+
+def in_check(state) -> bool:
+    st = np.ascontiguousarray(state, dtype=np.int8)
+    return bool(lib().kvo_in_check(_p(st, C.c_int8)))
+
+
+def is_draw(state) -> bool:
+    st = np.ascontiguousarray(state, dtype=np.int8)
+    return bool(lib().kvo_is_draw(_p(st, C.c_int8)))
+
+
+def make_valid_move(state, index):
+    st = np.array(state, dtype=np.int8, copy=True)
+    if lib().kvo_make_valid_move(_p(st, C.c_int8), int(index)) != 0:
+        raise IndexError(index)
+    return st
+
+
+def initial_state():
+    st = np.zeros(80, dtype=np.int8)
+    lib().kvo_initial_state(_p(st, C.c_int8))
+    return st
+
+
+def encode_board(state):
+    st = np.ascontiguousarray(state, dtype=np.int8)
+    out = np.zeros((12, 8, 8), dtype=np.float32)
+    lib().kvo_encode_board(_p(st, C.c_int8), _p(out, C.c_float))
+    return out
+
+
+class MT:
+    """One MT19937 stream: numpy-legacy seeded (kind='numpy') or CPython (kind='python')."""
+
+    def __init__(self, seed: int, kind: str):
+        self.buf = C.create_string_buffer(2600)
+        if kind == "numpy":
+            lib().kvo_mt_seed_genrand(self.buf, seed & 0xFFFFFFFF)
+        elif kind == "python":
+            lib().kvo_mt_seed_python(self.buf, abs(seed))
+        else:
+            raise ValueError(kind)
+
+    def next_u32(self):
+        return lib().kvo_mt_next(self.buf)
+
+    def random(self):
+        return lib().kvo_res53(self.buf)
+
+    def dirichlet(self, alpha, k):
+        out = np.zeros(k, dtype=np.float64)
+        att = lib().kvo_dirichlet(self.buf, alpha, k, _p(out, C.c_double))
+        return out, int(att)
+
+    def choices_index(self, weights):
+        w = np.ascontiguousarray(weights, dtype=np.float64)
+        return lib().kvo_choices(self.buf, _p(w, C.c_double), len(w))
+
+    def randbelow(self, n):
+        return lib().kvo_randbelow(self.buf, n)
+
+
+class Last:
+    def __init__(self):
+        self.buf = C.create_string_buffer(4096 * 4 + 16)
+
+
+def play_game(eval_fn, np_mt: MT, py_mt: MT, last: Last, max_moves=None, batch=16, eps=0.25, alpha=0.3,
+              softmax_fn=None, cap=4096):
+    """Restated _run_single_game. eval_fn(planes[n,12,8,8]) -> (logits[n,4096], values[n]).
+    Returns dict(moves, states, result, eval_sizes)."""
+
+    def _cb(ctx, planes, n, logits, values):
+        x = np.ctypeslib.as_array(planes, shape=(n, 12, 8, 8)).copy()
+        lg, vl = eval_fn(x)
+        np.ctypeslib.as_array(logits, shape=(n, 4096))[:] = lg
+        np.ctypeslib.as_array(values, shape=(n,))[:] = np.asarray(vl).reshape(n)
+
+    cb = EVAL_FN(_cb)
+    smx = None
+    if softmax_fn is not None:
+        def _sm(ctx, lg, pr):
+            np.ctypeslib.as_array(pr, shape=(4096,))[:] = softmax_fn(np.ctypeslib.as_array(lg, shape=(4096,)).copy())
+        smx = SOFTMAX_FN(_sm)
+    cfg = GameCfg(max_moves if max_moves else 0, batch, eps, alpha)
+    states = np.zeros((cap, 80), dtype=np.int8)
+    moves = np.zeros(cap, dtype=np.uint16)
+    sizes = np.zeros(cap, dtype=np.int32)
+    res = GameResult()
+    n = lib().kvo_play_game(C.byref(cfg), np_mt.buf, py_mt.buf, cb, C.cast(smx, C.c_void_p) if smx else None, None,
+                            last.buf, _p(states, C.c_int8), _p(moves, C.c_uint16), cap, _p(sizes, C.c_int), cap,
+                            C.byref(res))
+    return dict(moves=moves[:n].copy(), states=states[:n].copy(), plies=res.plies, outcome=res.outcome,
+                reward=float(res.reward), reason=res.reason, eval_sizes=sizes[:res.n_evals].copy())

@@ -1,0 +1,400 @@
+"""Generate the committed golden fixtures by importing the REFERENCE itself.
+
+Run in the build container only (the reference does not exist on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [/root/reference]
+
+Import recipe: two sys.modules stubs -- ``chess`` (imported by
+ai/ai.py:1,15 but unused on the list-input path) and ``pygame`` (imported via
+core/__init__.py:2 -> core/chessMain.py:5) -- then load scripts/self_play.py.
+
+Fixtures written next to this script (data only; no reference source):
+  movegen.npz   G1  ordered legal-move lists + inCheck for positions from seeded
+                    random trajectories and hand-built quirk positions
+                    (core/chessEngine.py:277-321, 388-394, makeMove :127-197)
+  nn.npz        G3  ChessNet policy/value for fixed boards under the synthetic
+                    weight variants (ai/model.py:51-77)
+  games.npz     G4  full self-play games: move-index sequences, outcome/reward,
+                    eval batch sizes, per-ply choice margins
+                    (scripts/self_play.py:111-255)
+  unittests.json G5 the reference unittest scenarios, restated as data
+"""
+from __future__ import annotations
+
+import bisect
+import importlib.util
+import itertools
+import json
+import os
+import random as _pyrandom
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+sys.path.insert(0, REPO)
+from knightvision_amd.weights import synthetic_state_dict  # noqa: E402
+
+PIECES = ["--", "wK", "wQ", "wR", "wB", "wN", "wp", "bK", "bQ", "bR", "bB", "bN", "bp"]
+CODE = {p: i for i, p in enumerate(PIECES)}
+
+
+def import_reference(ref):
+    chess = types.ModuleType("chess")
+    chess.SQUARES = range(64)
+    chess.WHITE, chess.BLACK, chess.PAWN = True, False, 1
+    chess.Board = type("Board", (), {})
+    sys.modules["chess"] = chess
+    sys.modules["pygame"] = types.ModuleType("pygame")
+    sys.path.insert(0, ref)
+    os.environ.setdefault("LOG_LEVEL", "ERROR")
+    spec = importlib.util.spec_from_file_location("ref_self_play", os.path.join(ref, "scripts", "self_play.py"))
+    sp = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sp)
+    import logging
+    logging.disable(logging.CRITICAL)
+    from core import chessEngine
+    from ai import model as ref_model
+    from ai import ai as ref_ai
+    return sp, chessEngine, ref_model, ref_ai
+
+
+# ---------------------------------------------------------------- state codec
+def state_vec(gs):
+    v = np.zeros(80, dtype=np.int8)
+    for r in range(8):
+        for c in range(8):
+            v[r * 8 + c] = CODE[gs.board[r][c]]
+    v[64] = 1 if gs.whiteToMove else 0
+    v[65], v[66] = gs.whiteKingLocation
+    v[67], v[68] = gs.blackKingLocation
+    v[69] = gs.wKingMoved
+    v[70] = gs.bKingMoved
+    v[71] = gs.wRookKingsideMoved
+    v[72] = gs.wRookQueensideMoved
+    v[73] = gs.bRookKingsideMoved
+    v[74] = gs.bRookQueensideMoved
+    if gs.enPassantPossible == ():
+        v[75] = v[76] = -1
+    else:
+        v[75], v[76] = gs.enPassantPossible
+    return v
+
+
+def set_state(gs, v):
+    gs.board = [[PIECES[int(v[r * 8 + c])] for c in range(8)] for r in range(8)]
+    gs.whiteToMove = bool(v[64])
+    gs.whiteKingLocation = (int(v[65]), int(v[66]))
+    gs.blackKingLocation = (int(v[67]), int(v[68]))
+    gs.wKingMoved, gs.bKingMoved = bool(v[69]), bool(v[70])
+    gs.wRookKingsideMoved, gs.wRookQueensideMoved = bool(v[71]), bool(v[72])
+    gs.bRookKingsideMoved, gs.bRookQueensideMoved = bool(v[73]), bool(v[74])
+    gs.enPassantPossible = () if v[75] < 0 else (int(v[75]), int(v[76]))
+
+
+def move_triplet(m):
+    flags = (1 if m.isEnPassantMove else 0) | (2 if m.isCastleMove else 0) | (4 if m.isPawnPromotion else 0)
+    return (m.startRow * 8 + m.startCol, m.endRow * 8 + m.endCol, flags)
+
+
+# ---------------------------------------------------------------- G1 movegen
+def quirk_positions(ce):
+    """Hand-built positions exercising the quirk catalog."""
+    out = []
+
+    def mk(pieces, white=True, ep=(), wk=None, bk=None, flags=None):
+        gs = ce.GameState()
+        gs.board = [["--"] * 8 for _ in range(8)]
+        for sq, p in pieces.items():
+            gs.board[8 - int(sq[1])][ord(sq[0]) - 97] = p
+        gs.whiteToMove = white
+        gs.enPassantPossible = ep
+        for r in range(8):
+            for c in range(8):
+                if gs.board[r][c] == "wK":
+                    gs.whiteKingLocation = (r, c)
+                if gs.board[r][c] == "bK":
+                    gs.blackKingLocation = (r, c)
+        if wk:
+            gs.whiteKingLocation = wk
+        if bk:
+            gs.blackKingLocation = bk
+        for k, val in (flags or {}).items():
+            setattr(gs, k, val)
+        out.append(gs)
+
+    # Q1 knight check from the missing (-2,+1) offset: K e1, bN f3
+    mk({"e1": "wK", "a2": "wp", "f3": "bN", "e8": "bK"})
+    # Q2/Q3 Re3 + pd3 checking rook: pawn push squares excluded from king moves
+    mk({"e1": "wK", "e3": "bR", "d3": "bp", "a8": "bK"})
+    # Q5 ep capture exposing king along the rank: Ka5 Pb5 pc5 Rh5, ep c6
+    mk({"a5": "wK", "b5": "wp", "c5": "bp", "h5": "bR", "e8": "bK"}, ep=(2, 2))
+    # Q6 ep capture of a checking pawn disallowed: wK e4? black pawn d5 checks Ke4 after d7d5
+    mk({"e4": "wK", "d5": "bp", "e5": "wp", "h8": "bK"}, ep=(2, 3))
+    # Q4 pinned pawn forward move only when pinDirection == (moveAmount, 0)
+    mk({"e1": "wK", "e2": "wp", "e8": "bR", "a8": "bK"})
+    mk({"e8": "wK", "e7": "wp", "e1": "bR", "a1": "bK"})
+    # castling through attacked squares / with attacked king / stale rook flags
+    mk({"e1": "wK", "h1": "wR", "a1": "wR", "e8": "bK", "f8": "bR"})
+    mk({"e1": "wK", "h1": "wR", "a1": "wR", "e8": "bK", "e7": "bR"})
+    mk({"e1": "wK", "h1": "wR", "a1": "wR", "e8": "bK", "h8": "bR", "a8": "bR"}, white=False)
+    mk({"e1": "wK", "h1": "wR", "a1": "wR", "e8": "bK", "b2": "bp"})
+    mk({"e1": "wK", "h1": "wR", "a1": "wR", "e8": "bK", "h8": "bR", "a8": "bR", "d2": "bp"}, white=False)
+    # opponent castle destination counts as attacked (Q2)
+    mk({"e8": "bK", "h8": "bR", "g2": "wK"}, white=True, flags={"wKingMoved": True})
+    # double check -> king moves only
+    mk({"e1": "wK", "e8": "bR", "b4": "bB", "a8": "bK", "d1": "wQ"})
+    # stale king location: white king captured, location still e1, black rook on e1
+    mk({"e1": "bR", "e8": "bK", "a2": "wp", "h1": "wR", "c3": "bB"}, wk=(7, 4))
+    mk({"e1": "bQ", "e8": "bK", "a2": "wp", "d2": "wN", "e4": "bR", "b4": "bB"}, wk=(7, 4))
+    # promotions incl. capture-promotions, black and white
+    mk({"e1": "wK", "b7": "wp", "a8": "bR", "c8": "bN", "h8": "bK"})
+    mk({"e8": "bK", "g2": "bp", "h1": "wR", "f1": "wB", "a1": "wK"}, white=False)
+    # kings adjacent / king capture available
+    mk({"e4": "wK", "e5": "bK", "a1": "wR"})
+    mk({"e4": "wK", "e6": "bK", "e5": "bp", "d5": "bN"})
+    # pinned pieces along diagonals and files
+    mk({"e1": "wK", "d2": "wB", "c3": "wN", "b4": "bB", "f2": "wR", "h4": "bQ", "e8": "bK"})
+    mk({"a1": "wK", "b2": "wQ", "h8": "bB", "a8": "bR", "a4": "wR", "e8": "bK"})
+    # pawn double push blocked / ep set up for both colours
+    mk({"e1": "wK", "d4": "bp", "e2": "wp", "e3": "bN", "e8": "bK"})
+    mk({"e1": "wK", "d5": "wp", "e5": "bp", "e8": "bK"}, ep=(2, 4))
+    mk({"e8": "bK", "d4": "bp", "e4": "wp", "e1": "wK"}, white=False, ep=(5, 4))
+    return out
+
+
+def gen_movegen(ce, n_traj=36, max_plies=260):
+    states, post, offsets, moves, in_check, src = [], [], [0], [], [], []
+
+    def record(gs, tag):
+        st = state_vec(gs)
+        ml = gs.getValidMoves()
+        # getValidMoves may mutate the board in the stale-king double-check case;
+        # record the state it was called on, as the games do.
+        states.append(st)
+        post.append(state_vec(gs))
+        trip = [move_triplet(m) for m in ml]
+        moves.extend(trip)
+        offsets.append(len(moves))
+        in_check.append(1 if gs.inCheck() else 0)
+        src.append(tag)
+        return ml
+
+    for gs in quirk_positions(ce):
+        record(gs, 0)
+    for t in range(n_traj):
+        rng = _pyrandom.Random(1000 + t)
+        capture_bias = (t % 3 == 1)
+        gs = ce.GameState()
+        for ply in range(max_plies):
+            ml = record(gs, 1 + (t % 3))
+            if not ml:
+                break
+            if capture_bias:
+                caps = [m for m in ml if m.pieceCaptured != "--"]
+                m = rng.choice(caps) if caps and rng.random() < 0.7 else rng.choice(ml)
+            else:
+                m = rng.choice(ml)
+            gs.makeMove(m)
+            if gs.isDraw():
+                record(gs, 4)
+                break
+    # stale-king trajectories: a king vanishes (captured) and play continues
+    # from the stale location, as happens after a Q1 knight-check capture.
+    for t in range(12):
+        rng = _pyrandom.Random(5000 + t)
+        gs = ce.GameState()
+        for ply in range(rng.randint(10, 50)):
+            ml = gs.getValidMoves()
+            if not ml:
+                break
+            gs.makeMove(rng.choice(ml))
+        r, c = gs.whiteKingLocation if gs.whiteToMove else gs.blackKingLocation
+        enemy = "b" if gs.whiteToMove else "w"
+        gs.board[r][c] = [enemy + "Q", enemy + "R", "--"][t % 3]
+        for ply in range(200):
+            ml = record(gs, 5)
+            if not ml:
+                break
+            caps = [m for m in ml if m.pieceCaptured != "--"]
+            m = rng.choice(caps) if caps and rng.random() < 0.5 else rng.choice(ml)
+            gs.makeMove(m)
+            if gs.isDraw():
+                record(gs, 4)
+                break
+    return dict(states=np.stack(states), post_states=np.stack(post), offsets=np.array(offsets, dtype=np.int32),
+                moves=np.array(moves, dtype=np.uint8).reshape(-1, 3),
+                in_check=np.array(in_check, dtype=np.uint8), source=np.array(src, dtype=np.uint8))
+
+
+# ---------------------------------------------------------------- G3 NN
+def planes_from_state(ref_ai, v):
+    board = [[PIECES[int(v[r * 8 + c])] for c in range(8)] for r in range(8)]
+    return ref_ai.encode_board(board)
+
+
+def gen_nn(ref_model, ref_ai, mg, torch):
+    idx = np.linspace(0, len(mg["states"]) - 1, 12).astype(int)
+    planes = np.stack([planes_from_state(ref_ai, mg["states"][i]) for i in idx])
+    out = {"planes": planes}
+    for variant in ("init", "bn", "peaked"):
+        sd = synthetic_state_dict(42, variant)
+        net = ref_model.ChessNet()
+        net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+        net.eval()
+        with torch.no_grad():
+            p, val = net(torch.from_numpy(planes))
+        out[f"policy_{variant}"] = p.numpy()
+        out[f"value_{variant}"] = val.numpy()
+    return out
+
+
+# ---------------------------------------------------------------- G4 games
+class Probe:
+    """Wraps random.choices exactly as CPython 3.10 random.py:506-541 does, to
+    record each ply's decision margin; consumes one random() like the original."""
+
+    def __init__(self):
+        self.margins = []
+
+    def choices(self, population, weights=None, *, cum_weights=None, k=1):
+        assert weights is not None and cum_weights is None and k == 1
+        cum = list(itertools.accumulate(weights))
+        total = cum[-1] + 0.0
+        x = _pyrandom.random() * total
+        i = bisect.bisect_right(cum, x, 0, len(cum) - 1)
+        d = min(abs(x - c) for c in cum[:-1]) / total if len(cum) > 1 else 1.0
+        self.margins.append(d)
+        return [population[i]]
+
+
+def run_games(sp, ref_model, torch, variant, seeds, max_moves, batch, sequential):
+    sd = synthetic_state_dict(42, variant)
+    net = ref_model.ChessNet()
+    net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    net.eval()
+    sizes = []
+    orig_fwd = net.forward
+
+    def fwd(x):
+        sizes.append(int(x.shape[0]))
+        return orig_fwd(x)
+    net.forward = fwd
+    sp._shared_model = net
+    sp.device = torch.device("cpu")
+    sp.BATCH_SIZE = batch
+    probe = Probe()
+    sp.random.choices = probe.choices  # same module object as `random`
+    games = []
+    if sequential:
+        _reseed(sp, torch, seeds[0])
+    for g, seed in enumerate(seeds):
+        if not sequential:
+            _reseed(sp, torch, seed)
+        sizes.clear()
+        probe.margins = []
+        _, recs = sp._run_single_game(g, 0.0, max_moves)
+        games.append(dict(seed=seed, moves=[r[1] for r in recs], reward=recs[0][2] if recs else None,
+                          n=len(recs), sizes=list(sizes), margins=list(probe.margins)))
+    return games
+
+
+def _reseed(sp, torch, seed):
+    sp.random.seed(seed)
+    sp.np.random.seed(seed)
+    torch.manual_seed(seed)
+    if hasattr(sp._run_single_game, "_last_outputs"):
+        del sp._run_single_game._last_outputs
+
+
+def pack_games(groups):
+    out = {}
+    for name, games in groups.items():
+        moves = np.concatenate([np.array(g["moves"], dtype=np.uint16) for g in games])
+        margins = np.concatenate([np.array(g["margins"], dtype=np.float64) for g in games])
+        sizes = np.concatenate([np.array(g["sizes"], dtype=np.int16) for g in games])
+        out[f"{name}.moves"] = moves
+        out[f"{name}.margins"] = margins
+        out[f"{name}.n"] = np.array([g["n"] for g in games], dtype=np.int32)
+        out[f"{name}.seed"] = np.array([g["seed"] for g in games], dtype=np.int64)
+        out[f"{name}.reward"] = np.array([g["reward"] for g in games], dtype=np.float64)
+        out[f"{name}.sizes"] = sizes
+        out[f"{name}.n_sizes"] = np.array([len(g["sizes"]) for g in games], dtype=np.int32)
+    return out
+
+
+# ---------------------------------------------------------------- G5 unittests
+def gen_unittests(ce):
+    cases = []
+    gs = ce.GameState()
+    gs.board = [["--"] * 8 for _ in range(8)]
+    gs.board[0] = ["bR", "--", "--", "--", "bK", "--", "--", "bR"]
+    gs.board[7] = ["wR", "--", "--", "--", "wK", "--", "--", "wR"]
+    for white in (True, False):
+        gs.whiteToMove = white
+        cases.append(dict(name=f"castling_{'w' if white else 'b'}", state=state_vec(gs).tolist(),
+                          moves=[list(move_triplet(m)) for m in gs.getValidMoves()]))
+    # en passant (reference tests/test_en_passant.py scenario): d7d5 then e5xd6 ep
+    gs = ce.GameState()
+    gs.board = [["--"] * 8 for _ in range(8)]
+    gs.board[7][4], gs.board[0][4] = "wK", "bK"
+    gs.board[3][4], gs.board[1][3] = "wp", "bp"
+    gs.whiteToMove = False
+    seq = []
+    m1 = ce.Move((1, 3), (3, 3), gs.board)
+    gs.makeMove(m1)
+    seq.append(dict(after="d7d5", state=state_vec(gs).tolist(),
+                    moves=[list(move_triplet(m)) for m in gs.getValidMoves()]))
+    ep = [m for m in gs.getValidMoves() if m.isEnPassantMove][0]
+    gs.makeMove(ep)
+    seq.append(dict(after="e5d6ep", state=state_vec(gs).tolist(),
+                    moves=[list(move_triplet(m)) for m in gs.getValidMoves()]))
+    cases.append(dict(name="en_passant", seq=seq))
+    # promotion: white pawn a7 -> a8 auto-queen
+    gs = ce.GameState()
+    gs.board = [["--"] * 8 for _ in range(8)]
+    gs.board[7][4], gs.board[0][7] = "wK", "bK"
+    gs.board[1][0] = "wp"
+    gs.whiteKingLocation, gs.blackKingLocation = (7, 4), (0, 7)
+    pm = [m for m in gs.getValidMoves() if m.isPawnPromotion][0]
+    before = state_vec(gs).tolist()
+    gs.makeMove(pm)
+    cases.append(dict(name="promotion", state=before, move=list(move_triplet(pm)),
+                      after=state_vec(gs).tolist()))
+    return cases
+
+
+def main():
+    ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    sp, ce, ref_model, ref_ai = import_reference(ref)
+    import torch
+    torch.set_num_threads(8)
+
+    mg = gen_movegen(ce)
+    np.savez_compressed(os.path.join(HERE, "movegen.npz"), **mg)
+    print("movegen positions", len(mg["states"]), "moves", len(mg["moves"]))
+
+    nn = gen_nn(ref_model, ref_ai, mg, torch)
+    np.savez_compressed(os.path.join(HERE, "nn.npz"), **nn)
+    print("nn boards", nn["planes"].shape)
+
+    groups = {
+        "pg_init_mm80": run_games(sp, ref_model, torch, "init", list(range(42, 42 + 32)), 80, 16, False),
+        "pg_peaked_mm80": run_games(sp, ref_model, torch, "peaked", list(range(42, 42 + 16)), 80, 16, False),
+        "pg_init_b1_mm60": run_games(sp, ref_model, torch, "init", list(range(42, 42 + 8)), 60, 1, False),
+        "pg_init_full": run_games(sp, ref_model, torch, "init", list(range(42, 42 + 6)), None, 16, False),
+        "seq_init_full": run_games(sp, ref_model, torch, "init", [42] * 4, None, 16, True),
+    }
+    for k, v in groups.items():
+        print(k, [g["n"] for g in v], [g["reward"] for g in v])
+    np.savez_compressed(os.path.join(HERE, "games.npz"), **pack_games(groups))
+
+    with open(os.path.join(HERE, "unittests.json"), "w") as f:
+        json.dump(gen_unittests(ce), f)
+    print("done")
+
+
+if __name__ == "__main__":
+    main()
