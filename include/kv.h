@@ -1,0 +1,156 @@
+/*
+ * kv.h -- C ABI of libkv.so, the MI355X-native self-play engine that drops in
+ * under the reference's self-play data-generation path.
+ *
+ * The reference has no native boundary: its callers bind Python names
+ * (SURVEY.md 8b). Each entry point below replaces one of those names; the
+ * Python mirror in knightvision_amd/ (same names, argument meaning and error
+ * behaviour) binds them with ctypes, see INTEGRATION.md.
+ *
+ * Conventions: every call returns int status (0 ok, negative KV_E*); the text
+ * of the last error is kv_last_error(). Pointers named *_dev are HIP device
+ * pointers, everything else is host memory owned by the caller. `stream` is a
+ * hipStream_t passed as void* (NULL = the default stream). An engine or net
+ * is not re-entrant: one host thread per object / GPU.
+ */
+#ifndef KV_H
+#define KV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KV_OK 0
+#define KV_EINVAL -1
+#define KV_ENOMEM -2
+#define KV_EHIP -3
+#define KV_EOVERFLOW -4
+
+const char* kv_last_error(void);
+int kv_version(void);
+
+/* ------------------------------------------------------------------ NN ---
+ * ChessNet forward (replaces ai/model.py:51-77 ChessNet.forward).
+ * Packed weights: BN folded into per-channel scale/shift; layout produced by
+ * knightvision_amd/weights.py:pack_weights and re-derived by kv_net_packed_size
+ * (each tensor padded to a multiple of 16 floats):
+ *   12 convs, each: w[Cout][9][CinPad], scale[Cout], shift[Cout]
+ *     (conv1 12->256 CinPad 16, conv2 256->512, 10 residual convs 512->512)
+ *   head.w[3][512] head.scale[3] head.shift[3]   (policy_conv x2, value_conv)
+ *   pfc.w[4096][128] pfc.b[4096] vfc1.w[512][64] vfc1.b[512] vfc2.w[512] vfc2.b[1]
+ */
+typedef struct kv_net kv_net;
+
+size_t kv_net_packed_size(void);
+int kv_net_create(int device, kv_net** out);
+int kv_net_load(kv_net* net, const float* packed, size_t n_floats);
+/* planes_dev: [B][12][8][8] fp32 (encode_board layout, ai/ai.py:17-30);
+ * policy_dev: [B][4096] logits; value_dev: [B] tanh value. */
+int kv_net_forward(kv_net* net, const float* planes_dev, int B, float* policy_dev, float* value_dev, void* stream);
+/* boards_dev: [B][64] int8 piece codes (0 empty, 1..6 wK wQ wR wB wN wp,
+ * 7..12 bK bQ bR bB bN bp; square r*8+c, row 0 = rank 8). */
+int kv_net_forward_boards(kv_net* net, const int8_t* boards_dev, int B, float* policy_dev, float* value_dev,
+                          void* stream);
+/* per-launch timing of the last forward (HIP events on `stream`): ms of the
+ * residual conv launches summed, and count of those launches. */
+int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv);
+int kv_net_set_timing(kv_net* net, int enable);
+void kv_net_destroy(kv_net* net);
+
+/* ------------------------------------------------------------- engine ---
+ * Self-play engine (replaces scripts/self_play.py self_play :258-291 /
+ * _run_single_game :111-255 / _init_worker :52-85 state).
+ */
+#define KV_SEED_PER_GAME 0   /* game g seeded SEED+g in both streams, no carried eval */
+#define KV_SEED_SEQUENTIAL 1 /* one numpy + one CPython stream seeded SEED, games in order */
+
+#define KV_EVAL_FAITHFUL 0 /* every board evaluated once, as the reference does */
+#define KV_EVAL_LAZY 1     /* only the rows the schedule consumes are evaluated */
+
+typedef struct {
+    int device;
+    int slots;            /* concurrent games on this GPU */
+    int64_t n_games;      /* games to play (global ids game_id_base + k*game_id_stride) */
+    int64_t game_id_base; /* first global game id on this rank */
+    int64_t game_id_stride;
+    uint64_t seed;        /* SEED (self_play.py:24) */
+    int seed_mode;        /* KV_SEED_* */
+    int max_moves;        /* <= 0: None */
+    int batch;            /* SELFPLAY_BATCH_SIZE (self_play.py:34) */
+    double eps;           /* DIR_NOISE_EPS */
+    double alpha;         /* DIR_NOISE_ALPHA, must be in (0,1) */
+    int sims;             /* 0: reference move selection; >0: PUCT MCTS sims/move */
+    float c_puct;
+    int eval_mode;        /* KV_EVAL_* */
+    int64_t record_cap;   /* record buffer capacity */
+    int recycle;          /* 1: a finished slot starts the next game id */
+} kv_config;
+
+typedef struct {
+    int64_t game_id;
+    int32_t ply;
+    uint16_t move;       /* encode_move index (ai/ai.py:51-57) */
+    uint16_t pad;
+    int8_t board[64];    /* position before the move (encode_board input) */
+} kv_record;             /* 80 bytes */
+
+typedef struct {
+    int64_t game_id;
+    int32_t plies;
+    int32_t outcome;     /* +1 white win, 0 draw, -1 black win (self_play.py:211-238) */
+    float reward;        /* 1.0 / 0.2 / -1.0 (self_play.py:245-250) */
+    int32_t reason;      /* 0 max_moves 1 resign 2 mate 3 stalemate 4 draw 5 material */
+    int32_t n_evals;     /* network rows consumed by this game's schedule */
+    int32_t pad;
+} kv_game;               /* 32 bytes */
+
+typedef struct {
+    int64_t steps;        /* ply-steps executed */
+    int64_t plies;        /* moves committed */
+    int64_t games_done;
+    int64_t nn_rows;      /* boards evaluated by the network */
+    int64_t sims;         /* MCTS backups completed */
+    int64_t records;
+    double nn_ms;         /* device time inside network forwards (HIP events) */
+    double step_ms;       /* wall time inside kv_run */
+} kv_stats;
+
+typedef struct kv_engine kv_engine;
+
+int kv_create(const kv_config* cfg, kv_engine** out);
+int kv_load_weights(kv_engine* e, const float* packed, size_t n_floats);
+/* Run up to max_steps ply-steps (< 0: until every game is finished). */
+int kv_run(kv_engine* e, int64_t max_steps);
+int kv_records(kv_engine* e, kv_record* out, size_t cap, size_t* n);
+int kv_games(kv_engine* e, kv_game* out, size_t cap, size_t* n);
+int kv_stats_get(kv_engine* e, kv_stats* out);
+int kv_sync(kv_engine* e);
+void kv_destroy(kv_engine* e);
+
+/* ------------------------------------------------- device test entry points ---
+ * Run one device kernel over host-provided inputs (copies in and out). They
+ * exist so parity tests can call the product kernels through the C ABI. */
+
+/* getValidMoves (core/chessEngine.py:277-321) for n states (80-byte vectors,
+ * see oracle/kv_oracle.c); moves_out [n][cap] as uint16 from|to<<6|flags<<12
+ * (flags bit0 ep, bit1 castle, bit2 promotion); n_moves [n]; states_after
+ * [n][80] (the reference may mutate the board); in_check [n]. */
+int kv_dev_valid_moves(int device, const int8_t* states, int n, uint16_t* moves_out, int cap, int* n_moves,
+                       int8_t* states_after, uint8_t* in_check);
+/* makeMove (chessEngine.py:127-197) of move index[i] of each state's list. */
+int kv_dev_make_move(int device, int8_t* states, const int* index, int n);
+/* numpy RandomState(seed[i]).dirichlet([alpha]*k) `draws` times per stream:
+ * out [n][draws][k] fp64, attempts [n][draws] gamma attempts consumed,
+ * tail [n] = the stream's next random_sample() after the draws. */
+int kv_dev_dirichlet(int device, const uint64_t* seeds, int n, double alpha, int k, int draws, double* out,
+                     int64_t* attempts, double* tail);
+/* CPython random.Random(seed[i]): count random() values -> out [n][count]. */
+int kv_dev_py_random(int device, const uint64_t* seeds, int n, int count, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KV_H */

@@ -1,0 +1,99 @@
+"""ctypes binding of libkv.so (include/kv.h). The product has no CPU fallback:
+if the HIP library is missing or fails to load, every entry point raises."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libkv.so")
+
+_lib = None
+
+
+class KVError(RuntimeError):
+    pass
+
+
+class Config(C.Structure):
+    _fields_ = [("device", C.c_int), ("slots", C.c_int), ("n_games", C.c_int64), ("game_id_base", C.c_int64),
+                ("game_id_stride", C.c_int64), ("seed", C.c_uint64), ("seed_mode", C.c_int),
+                ("max_moves", C.c_int), ("batch", C.c_int), ("eps", C.c_double), ("alpha", C.c_double),
+                ("sims", C.c_int), ("c_puct", C.c_float), ("eval_mode", C.c_int), ("record_cap", C.c_int64),
+                ("recycle", C.c_int)]
+
+
+class Record(C.Structure):
+    _fields_ = [("game_id", C.c_int64), ("ply", C.c_int32), ("move", C.c_uint16), ("pad", C.c_uint16),
+                ("board", C.c_int8 * 64)]
+
+
+class Game(C.Structure):
+    _fields_ = [("game_id", C.c_int64), ("plies", C.c_int32), ("outcome", C.c_int32), ("reward", C.c_float),
+                ("reason", C.c_int32), ("n_evals", C.c_int32), ("pad", C.c_int32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("steps", C.c_int64), ("plies", C.c_int64), ("games_done", C.c_int64), ("nn_rows", C.c_int64),
+                ("sims", C.c_int64), ("records", C.c_int64), ("nn_ms", C.c_double), ("step_ms", C.c_double)]
+
+
+assert C.sizeof(Record) == 80 and C.sizeof(Game) == 32
+
+
+def _declare(L):
+    vp, i, i64, sz = C.c_void_p, C.c_int, C.c_int64, C.c_size_t
+    P = C.POINTER
+    sig = {
+        "kv_last_error": ([], C.c_char_p),
+        "kv_version": ([], i),
+        "kv_net_packed_size": ([], sz),
+        "kv_net_create": ([i, P(vp)], i),
+        "kv_net_load": ([vp, P(C.c_float), sz], i),
+        "kv_net_forward": ([vp, vp, i, vp, vp, vp], i),
+        "kv_net_forward_boards": ([vp, vp, i, vp, vp, vp], i),
+        "kv_net_set_timing": ([vp, i], i),
+        "kv_net_last_timing": ([vp, P(C.c_float), P(i)], i),
+        "kv_net_destroy": ([vp], None),
+        "kv_create": ([P(Config), P(vp)], i),
+        "kv_load_weights": ([vp, P(C.c_float), sz], i),
+        "kv_run": ([vp, i64], i),
+        "kv_records": ([vp, P(Record), sz, P(sz)], i),
+        "kv_games": ([vp, P(Game), sz, P(sz)], i),
+        "kv_stats_get": ([vp, P(Stats)], i),
+        "kv_sync": ([vp], i),
+        "kv_destroy": ([vp], None),
+        "kv_dev_valid_moves": ([i, P(C.c_int8), i, P(C.c_uint16), i, P(i), P(C.c_int8), P(C.c_uint8)], i),
+        "kv_dev_make_move": ([i, P(C.c_int8), P(i), i], i),
+        "kv_dev_dirichlet": ([i, P(C.c_uint64), i, C.c_double, i, i, P(C.c_double), P(i64), P(C.c_double)], i),
+        "kv_dev_py_random": ([i, P(C.c_uint64), i, i, P(C.c_double)], i),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    return L
+
+
+EXPORTED = ["kv_last_error", "kv_version", "kv_net_packed_size", "kv_net_create", "kv_net_load", "kv_net_forward",
+            "kv_net_forward_boards", "kv_net_set_timing", "kv_net_last_timing", "kv_net_destroy", "kv_create",
+            "kv_load_weights", "kv_run", "kv_records", "kv_games", "kv_stats_get", "kv_sync", "kv_destroy",
+            "kv_dev_valid_moves", "kv_dev_make_move", "kv_dev_dirichlet", "kv_dev_py_random"]
+
+
+def lib():
+    """Load libkv.so (build it first if this is a source tree with hipcc)."""
+    global _lib
+    if _lib is None:
+        import torch  # noqa: F401  -- load torch's HIP runtime first so both share one
+        if not os.path.exists(LIB_PATH):
+            raise KVError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "(the HIP library is required; there is no CPU fallback)")
+        _lib = _declare(C.CDLL(LIB_PATH))
+    return _lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib().kv_last_error().decode(errors="replace")
+        raise KVError(f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,540 @@
+// ChessNet forward on MI355X (gfx950): replaces ai/model.py:51-77.
+//
+// Layout: activations NHWC fp32 [board][64 squares][C]. Every 3x3 conv is an
+// implicit GEMM  out[M = boards*64, N = Cout] = im2col(in)[M, K = 9*Cin] x W[K, N]
+// on the f32-input MFMA (v_mfma_f32_32x32x2_f32, exact fp32 fma chain).
+// A workgroup owns 2 boards x 256 output channels (8 waves = 2 boards x 4
+// column groups, 64x64 per wave = 2x2 MFMA tiles). For each Cin chunk the two
+// boards are staged once into LDS as a zero-padded 10x10 halo (the 9 taps are
+// 9 shifted reads of the same halo, so activations cross HBM once per chunk,
+// not 9 times); the weight tile [256][CK] of each (chunk, tap) k-tile streams
+// through a double-buffered LDS slot. Pixel / row strides of the halo are
+// chosen so every ds_read_b128 lane group is bank-conflict free. BN (eval) is
+// folded into a per-channel scale/shift applied in the epilogue together with
+// the residual add (ResidualBlock.forward, ai/model.py:19-25) and ReLU.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "kv_common.h"
+
+namespace kv {
+
+static thread_local char g_err[512];
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+// ------------------------------------------------------------- packing --
+struct ConvDesc {
+    int cin, cin_pad, cout;
+};
+static const ConvDesc kConv[12] = {{12, 16, 256}, {256, 256, 512}, {512, 512, 512}, {512, 512, 512},
+                                   {512, 512, 512}, {512, 512, 512}, {512, 512, 512}, {512, 512, 512},
+                                   {512, 512, 512}, {512, 512, 512}, {512, 512, 512}, {512, 512, 512}};
+
+static size_t pad16(size_t n) { return (n + 15) / 16 * 16; }
+
+struct PackOffsets {
+    size_t w[12], scale[12], shift[12];
+    size_t head_w, head_scale, head_shift, pfc_w, pfc_b, vfc1_w, vfc1_b, vfc2_w, vfc2_b;
+    size_t total;
+};
+
+static PackOffsets pack_offsets() {
+    PackOffsets p;
+    size_t o = 0;
+    for (int l = 0; l < 12; ++l) {
+        p.w[l] = o; o += pad16((size_t)kConv[l].cout * 9 * kConv[l].cin_pad);
+        p.scale[l] = o; o += pad16(kConv[l].cout);
+        p.shift[l] = o; o += pad16(kConv[l].cout);
+    }
+    p.head_w = o; o += pad16(3 * 512);
+    p.head_scale = o; o += pad16(3);
+    p.head_shift = o; o += pad16(3);
+    p.pfc_w = o; o += pad16(4096 * 128);
+    p.pfc_b = o; o += pad16(4096);
+    p.vfc1_w = o; o += pad16(512 * 64);
+    p.vfc1_b = o; o += pad16(512);
+    p.vfc2_w = o; o += pad16(512);
+    p.vfc2_b = o; o += pad16(1);
+    p.total = o;
+    return p;
+}
+
+// ---------------------------------------------------------- conv kernel --
+template <int CK>
+struct HaloGeom;
+template <>
+struct HaloGeom<32> {  // conflict-free ds_read_b128 for every tap (searched offline)
+    static constexpr int PS = 36, RS = 416;
+};
+template <>
+struct HaloGeom<16> {
+    static constexpr int PS = 20, RS = 224;
+};
+
+template <int CIN, int CK>
+struct ConvLds {
+    static constexpr int PS = HaloGeom<CK>::PS;
+    static constexpr int RS = HaloGeom<CK>::RS;
+    static constexpr int BOARD = 10 * RS;
+    static constexpr int ABUF = 2 * BOARD;
+    static constexpr int BBUF = 256 * PS;
+    static constexpr int FLOATS = 2 * ABUF + 2 * BBUF;
+    static constexpr size_t BYTES = (size_t)FLOATS * 4;
+};
+
+template <int CIN, int CK, bool RESID>
+__global__ __launch_bounds__(512) void conv3x3_kernel(const float* __restrict__ in, const float* __restrict__ wt,
+                                                      const float* __restrict__ scale,
+                                                      const float* __restrict__ shift,
+                                                      const float* resid, float* out, int cout) {
+    using G = ConvLds<CIN, CK>;
+    constexpr int PS = G::PS, RS = G::RS, BOARD = G::BOARD, ABUF = G::ABUF, BBUF = G::BBUF;
+    constexpr int NCH = CIN / CK;
+    constexpr int NK = 9 * NCH;
+    constexpr int KQ = CK / 4;                   // float4 per CK row
+    constexpr int A_F4 = (128 * KQ) / 512;       // per thread per chunk
+    constexpr int B_F4 = (256 * KQ) / 512;       // per thread per k-tile
+    static_assert(A_F4 >= 1 && B_F4 >= 1, "tile too small");
+
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* const A0 = smem;
+    float* const A1 = smem + ABUF;
+    float* const B0 = smem + 2 * ABUF;
+    float* const B1 = B0 + BBUF;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 2;  // board inside the tile
+    const int wn = wave & 3;   // 64-column group
+    const int n_base = blockIdx.x * 256;
+    const int b0 = blockIdx.y * 2;
+
+    for (int i = tid * 4; i < 2 * ABUF; i += 512 * 4) *(f32x4*)(smem + i) = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    f32x4 ra[A_F4];
+    f32x4 rb[B_F4];
+    auto loadA = [&](int ch) {
+#pragma unroll
+        for (int q = 0; q < A_F4; ++q) {
+            const int idx = tid + q * 512;
+            const int pix = idx / KQ, kq = idx % KQ;
+            ra[q] = *(const f32x4*)(in + ((size_t)(b0 + (pix >> 6)) * 64 + (pix & 63)) * CIN + ch * CK + kq * 4);
+        }
+    };
+    auto storeA = [&](float* Ab) {
+#pragma unroll
+        for (int q = 0; q < A_F4; ++q) {
+            const int idx = tid + q * 512;
+            const int pix = idx / KQ, kq = idx % KQ;
+            const int p = pix & 63;
+            *(f32x4*)(Ab + (pix >> 6) * BOARD + ((p >> 3) + 1) * RS + ((p & 7) + 1) * PS + kq * 4) = ra[q];
+        }
+    };
+    auto loadB = [&](int kt) {
+        const int tap = kt % 9, ch = kt / 9;
+#pragma unroll
+        for (int q = 0; q < B_F4; ++q) {
+            const int idx = tid + q * 512;
+            const int n = idx / KQ, kq = idx % KQ;
+            rb[q] = *(const f32x4*)(wt + ((size_t)(n_base + n) * 9 + tap) * CIN + ch * CK + kq * 4);
+        }
+    };
+    auto storeB = [&](float* Bb) {
+#pragma unroll
+        for (int q = 0; q < B_F4; ++q) {
+            const int idx = tid + q * 512;
+            const int n = idx / KQ, kq = idx % KQ;
+            *(f32x4*)(Bb + n * PS + kq * 4) = rb[q];
+        }
+    };
+
+    const int h = lane >> 5, li = lane & 31;
+    int aoff[2], boff[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+        const int p = mt * 32 + li;
+        aoff[mt] = wm * BOARD + ((p >> 3) + 1) * RS + ((p & 7) + 1) * PS + 4 * h;
+    }
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) boff[nt] = (wn * 64 + nt * 32 + li) * PS + 4 * h;
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    __syncthreads();  // halo zeroed before the first interior store
+    loadA(0);
+    loadB(0);
+    storeA(A0);
+    storeB(B0);
+    __syncthreads();
+
+    for (int kt = 0; kt < NK; ++kt) {
+        const int tap = kt % 9, ch = kt / 9;
+        const bool nextB = kt + 1 < NK;
+        const bool nextA = (tap == 8) && (ch + 1 < NCH);
+        if (nextB) loadB(kt + 1);
+        if (nextA) loadA(ch + 1);
+        const float* Ab = (ch & 1) ? A1 : A0;
+        const float* Bb = (kt & 1) ? B1 : B0;
+        const int toff = (tap / 3 - 1) * RS + (tap % 3 - 1) * PS;
+#pragma unroll
+        for (int s = 0; s < CK / 8; ++s) {
+            const f32x4 a0 = *(const f32x4*)(Ab + aoff[0] + toff + 8 * s);
+            const f32x4 a1 = *(const f32x4*)(Ab + aoff[1] + toff + 8 * s);
+            const f32x4 v0 = *(const f32x4*)(Bb + boff[0] + 8 * s);
+            const f32x4 v1 = *(const f32x4*)(Bb + boff[1] + 8 * s);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[j], v0[j], acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[j], v1[j], acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[j], v0[j], acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[j], v1[j], acc[1][1], 0, 0, 0);
+            }
+        }
+        if (nextB) storeB((kt & 1) ? B0 : B1);
+        if (nextA) storeA((ch & 1) ? A0 : A1);
+        __syncthreads();
+    }
+
+    // epilogue: D[row][col], row = (r&3) + 8*(r>>2) + 4*h, col = li
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        const int n = n_base + wn * 64 + nt * 32 + li;
+        const float sc = scale[n], sh = shift[n];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int pix = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const size_t idx = ((size_t)(b0 + wm) * 64 + pix) * cout + n;
+                float v = acc[mt][nt][r] * sc + sh;
+                if (RESID) v += resid[idx];
+                out[idx] = v > 0.f ? v : 0.f;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------- heads --
+// policy_conv/value_conv (1x1, 512->2 / 512->1) + BN + ReLU, NCHW flatten
+// (c*64+sq, ai/model.py:65), value_fc1 + ReLU, value_fc2 + tanh (:70-73).
+__global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ X, const float* __restrict__ hw,
+                                                    const float* __restrict__ hs, const float* __restrict__ hb,
+                                                    const float* __restrict__ v1w, const float* __restrict__ v1b,
+                                                    const float* __restrict__ v2w, const float* __restrict__ v2b,
+                                                    float* __restrict__ pfeat, float* __restrict__ value) {
+    __shared__ float s_pf[128];
+    __shared__ float s_v[64];
+    __shared__ float s_h[512];
+    __shared__ float s_red[4];
+    const int b = blockIdx.x, t = threadIdx.x;
+    const int p = t >> 2, q = t & 3;
+    const float* xp = X + ((size_t)b * 64 + p) * 512;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+#pragma unroll 8
+    for (int j = 0; j < 32; ++j) {
+        const int c = q * 4 + 16 * j;
+        const f32x4 x = *(const f32x4*)(xp + c);
+        const f32x4 w0 = *(const f32x4*)(hw + c);
+        const f32x4 w1 = *(const f32x4*)(hw + 512 + c);
+        const f32x4 w2 = *(const f32x4*)(hw + 1024 + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            a0 += x[e] * w0[e];
+            a1 += x[e] * w1[e];
+            a2 += x[e] * w2[e];
+        }
+    }
+#pragma unroll
+    for (int m = 1; m < 4; m <<= 1) {
+        a0 += __shfl_xor(a0, m);
+        a1 += __shfl_xor(a1, m);
+        a2 += __shfl_xor(a2, m);
+    }
+    if (q == 0) {
+        const float p0 = a0 * hs[0] + hb[0], p1 = a1 * hs[1] + hb[1], v = a2 * hs[2] + hb[2];
+        s_pf[p] = p0 > 0.f ? p0 : 0.f;
+        s_pf[64 + p] = p1 > 0.f ? p1 : 0.f;
+        s_v[p] = v > 0.f ? v : 0.f;
+    }
+    __syncthreads();
+    if (t < 128) pfeat[(size_t)b * 128 + t] = s_pf[t];
+    for (int o = t; o < 512; o += 256) {
+        float hsum = v1b[o];
+        const float* wr = v1w + (size_t)o * 64;
+#pragma unroll 16
+        for (int k = 0; k < 64; ++k) hsum += wr[k] * s_v[k];
+        s_h[o] = hsum > 0.f ? hsum : 0.f;
+    }
+    __syncthreads();
+    float part = v2w[t] * s_h[t] + v2w[t + 256] * s_h[t + 256];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m);
+    if ((t & 63) == 0) s_red[t >> 6] = part;
+    __syncthreads();
+    if (t == 0) value[b] = tanhf(s_red[0] + s_red[1] + s_red[2] + s_red[3] + v2b[0]);
+}
+
+// --------------------------------------------------------- policy fc --
+// logits[B][4096] = pfeat[B][128] x W^T + b, W [4096][128]: 32 boards x 128
+// outputs per workgroup, one 32x32 MFMA tile per wave, K = 128.
+__global__ __launch_bounds__(256) void policy_fc_kernel(const float* __restrict__ pfeat,
+                                                        const float* __restrict__ w, const float* __restrict__ bias,
+                                                        float* __restrict__ logits, int nb) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5, li = lane & 31;
+    const int n0 = blockIdx.x * 128 + wave * 32;
+    const int b0 = blockIdx.y * 32;
+    const int arow = min(b0 + li, nb - 1);
+    const float* ap = pfeat + (size_t)arow * 128 + 4 * h;
+    const float* bp = w + (size_t)(n0 + li) * 128 + 4 * h;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll 4
+    for (int s = 0; s < 16; ++s) {
+        const f32x4 a = *(const f32x4*)(ap + 8 * s);
+        const f32x4 v = *(const f32x4*)(bp + 8 * s);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], v[j], acc, 0, 0, 0);
+    }
+    const int n = n0 + li;
+    const float bn = bias[n];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = b0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < nb) logits[(size_t)row * 4096 + n] = acc[r] + bn;
+    }
+}
+
+// ------------------------------------------------------------ encoders --
+// encode_board (ai/ai.py:17-30) straight into the stem's NHWC16 input.
+__global__ void encode_boards_kernel(const int8_t* __restrict__ boards, int nb, int nb_pad, float* __restrict__ x16) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // board*64 + square
+    if (i >= nb_pad * 64) return;
+    const int code = (i < nb * 64) ? boards[i] : 0;
+    f32x4* o = (f32x4*)(x16 + (size_t)i * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (code - 1 == q * 4 + e) ? 1.f : 0.f;
+        o[q] = v;
+    }
+}
+
+// [B][12][8][8] NCHW planes -> NHWC16 (any values, not only one-hot)
+__global__ void planes_to_nhwc16_kernel(const float* __restrict__ planes, int nb, int nb_pad,
+                                        float* __restrict__ x16) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // board*64 + square
+    if (i >= nb_pad * 64) return;
+    const int b = i >> 6, sq = i & 63;
+    f32x4* o = (f32x4*)(x16 + (size_t)i * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int c = q * 4 + e;
+            v[e] = (b < nb && c < 12) ? planes[((size_t)b * 12 + c) * 64 + sq] : 0.f;
+        }
+        o[q] = v;
+    }
+}
+
+}  // namespace kv
+
+// ---------------------------------------------------------------- host --
+struct kv_net {
+    int device = 0;
+    float* w = nullptr;  // packed weights on device
+    kv::PackOffsets off;
+    bool loaded = false;
+    int cap = 0;         // boards the workspace holds (even)
+    float* x16 = nullptr;
+    float* X = nullptr;
+    float* T = nullptr;
+    float* pfeat = nullptr;
+    bool timing = false;
+    hipEvent_t ev[24];
+    int n_ev = 0;
+    float conv_ms = 0.f;
+    int n_conv = 0;
+};
+
+template <int CIN, int CK, bool RESID>
+static int launch_conv(const float* in, const float* w, const float* sc, const float* sh, const float* resid,
+                       float* out, int cout, int nb_pad, hipStream_t st) {
+    using G = kv::ConvLds<CIN, CK>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        KV_HIP(hipFuncSetAttribute((const void*)kv::conv3x3_kernel<CIN, CK, RESID>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::BYTES));
+        attr_set = true;
+    }
+    dim3 grid(cout / 256, nb_pad / 2);
+    hipLaunchKernelGGL((kv::conv3x3_kernel<CIN, CK, RESID>), grid, dim3(512), G::BYTES, st, in, w, sc, sh, resid,
+                       out, cout);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+static int net_reserve(kv_net* net, int nb_pad) {
+    if (nb_pad <= net->cap) return KV_OK;
+    int cap = nb_pad < 64 ? 64 : nb_pad;
+    hipFree(net->x16); hipFree(net->X); hipFree(net->T); hipFree(net->pfeat);
+    net->x16 = net->X = net->T = net->pfeat = nullptr;
+    net->cap = 0;
+    KV_HIP(hipMalloc(&net->x16, (size_t)cap * 64 * 16 * 4));
+    KV_HIP(hipMalloc(&net->X, (size_t)cap * 64 * 512 * 4));
+    KV_HIP(hipMalloc(&net->T, (size_t)cap * 64 * 512 * 4));
+    KV_HIP(hipMalloc(&net->pfeat, (size_t)cap * 128 * 4));
+    net->cap = cap;
+    return KV_OK;
+}
+
+// the tower + heads from net->x16 (already encoded, nb_pad rows)
+static int net_tower(kv_net* net, int nb, int nb_pad, float* policy, float* value, hipStream_t st) {
+    const float* W = net->w;
+    const kv::PackOffsets& o = net->off;
+    int rc;
+    const bool tm = net->timing;
+    if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
+    if ((rc = launch_conv<16, 16, false>(net->x16, W + o.w[0], W + o.scale[0], W + o.shift[0], nullptr, net->T, 256,
+                                         nb_pad, st)))
+        return rc;
+    if ((rc = launch_conv<256, 32, false>(net->T, W + o.w[1], W + o.scale[1], W + o.shift[1], nullptr, net->X, 512,
+                                          nb_pad, st)))
+        return rc;
+    if (tm) KV_HIP(hipEventRecord(net->ev[1], st));
+    for (int r = 0; r < 5; ++r) {
+        const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
+        if ((rc = launch_conv<512, 32, false>(net->X, W + o.w[l1], W + o.scale[l1], W + o.shift[l1], nullptr, net->T,
+                                              512, nb_pad, st)))
+            return rc;
+        if ((rc = launch_conv<512, 32, true>(net->T, W + o.w[l2], W + o.scale[l2], W + o.shift[l2], net->X, net->X,
+                                             512, nb_pad, st)))
+            return rc;
+    }
+    if (tm) KV_HIP(hipEventRecord(net->ev[2], st));
+    hipLaunchKernelGGL(kv::heads_kernel, dim3(nb), dim3(256), 0, st, net->X, W + o.head_w, W + o.head_scale,
+                       W + o.head_shift, W + o.vfc1_w, W + o.vfc1_b, W + o.vfc2_w, W + o.vfc2_b, net->pfeat, value);
+    KV_HIP(hipGetLastError());
+    hipLaunchKernelGGL(kv::policy_fc_kernel, dim3(4096 / 128, (nb + 31) / 32), dim3(256), 0, st, net->pfeat,
+                       W + o.pfc_w, W + o.pfc_b, policy, nb);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+extern "C" {
+
+const char* kv_last_error(void) { return kv::g_err; }
+int kv_version(void) { return 1; }
+
+size_t kv_net_packed_size(void) { return kv::pack_offsets().total; }
+
+int kv_net_create(int device, kv_net** out) {
+    KV_REQUIRE(out, KV_EINVAL, "kv_net_create: out is NULL");
+    KV_HIP(hipSetDevice(device));
+    kv_net* net = new kv_net();
+    net->device = device;
+    net->off = kv::pack_offsets();
+    hipError_t e = hipMalloc(&net->w, net->off.total * sizeof(float));
+    if (e != hipSuccess) {
+        delete net;
+        kv::set_error("kv_net_create: hipMalloc weights: %s", hipGetErrorString(e));
+        return KV_EHIP;
+    }
+    for (int i = 0; i < 3; ++i) KV_HIP(hipEventCreate(&net->ev[i]));
+    *out = net;
+    return KV_OK;
+}
+
+int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
+    KV_REQUIRE(net && packed, KV_EINVAL, "kv_net_load: NULL argument");
+    KV_REQUIRE(n_floats == net->off.total, KV_EINVAL, "kv_net_load: expected %zu floats, got %zu", net->off.total,
+               n_floats);
+    KV_HIP(hipSetDevice(net->device));
+    KV_HIP(hipMemcpy(net->w, packed, n_floats * sizeof(float), hipMemcpyHostToDevice));
+    net->loaded = true;
+    return KV_OK;
+}
+
+int kv_net_forward(kv_net* net, const float* planes_dev, int B, float* policy_dev, float* value_dev, void* stream) {
+    KV_REQUIRE(net && net->loaded, KV_EINVAL, "kv_net_forward: net not loaded");
+    KV_REQUIRE(B > 0 && planes_dev && policy_dev && value_dev, KV_EINVAL, "kv_net_forward: bad arguments (B=%d)", B);
+    hipStream_t st = (hipStream_t)stream;
+    const int nb_pad = (B + 1) & ~1;
+    int rc = net_reserve(net, nb_pad);
+    if (rc) return rc;
+    hipLaunchKernelGGL(kv::planes_to_nhwc16_kernel, dim3((nb_pad * 64 + 255) / 256), dim3(256), 0, st, planes_dev, B,
+                       nb_pad, net->x16);
+    KV_HIP(hipGetLastError());
+    return net_tower(net, B, nb_pad, policy_dev, value_dev, st);
+}
+
+int kv_net_forward_boards(kv_net* net, const int8_t* boards_dev, int B, float* policy_dev, float* value_dev,
+                          void* stream) {
+    KV_REQUIRE(net && net->loaded, KV_EINVAL, "kv_net_forward_boards: net not loaded");
+    KV_REQUIRE(B > 0 && boards_dev && policy_dev && value_dev, KV_EINVAL, "kv_net_forward_boards: bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    const int nb_pad = (B + 1) & ~1;
+    int rc = net_reserve(net, nb_pad);
+    if (rc) return rc;
+    hipLaunchKernelGGL(kv::encode_boards_kernel, dim3((nb_pad * 64 + 255) / 256), dim3(256), 0, st, boards_dev, B,
+                       nb_pad, net->x16);
+    KV_HIP(hipGetLastError());
+    return net_tower(net, B, nb_pad, policy_dev, value_dev, st);
+}
+
+int kv_net_set_timing(kv_net* net, int enable) {
+    KV_REQUIRE(net, KV_EINVAL, "kv_net_set_timing: NULL");
+    net->timing = enable != 0;
+    return KV_OK;
+}
+
+int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv) {
+    KV_REQUIRE(net && net->timing, KV_EINVAL, "kv_net_last_timing: timing not enabled");
+    KV_HIP(hipEventSynchronize(net->ev[2]));
+    float ms = 0.f;
+    KV_HIP(hipEventElapsedTime(&ms, net->ev[1], net->ev[2]));
+    if (conv_ms) *conv_ms = ms;
+    if (n_conv) *n_conv = 10;
+    return KV_OK;
+}
+
+void kv_net_destroy(kv_net* net) {
+    if (!net) return;
+    hipSetDevice(net->device);
+    hipFree(net->w);
+    hipFree(net->x16);
+    hipFree(net->X);
+    hipFree(net->T);
+    hipFree(net->pfeat);
+    for (int i = 0; i < 3; ++i) hipEventDestroy(net->ev[i]);
+    delete net;
+}
+
+}  // extern "C"
+
+// internal accessors for the engine (same library)
+namespace kv {
+int net_forward_boards_internal(kv_net* net, const int8_t* boards_dev, int B, float* policy, float* value,
+                                hipStream_t st) {
+    return kv_net_forward_boards(net, boards_dev, B, policy, value, (void*)st);
+}
+}  // namespace kv

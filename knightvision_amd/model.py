@@ -1,0 +1,140 @@
+"""ChessNet: drop-in for ai/model.py ChessNet (same parameter names, shapes and
+state_dict keys, ai/model.py:31-49), whose forward runs on the hand-written
+HIP kernels of libkv.so (knightvision_amd/csrc/kv_nn.hip).
+
+forward(x[N,12,8,8]) -> (policy logits [N,4096], value [N,1]), eval-mode
+BatchNorm semantics (the self-play path always calls model.eval(),
+self_play.py:77, :108). The module keeps torch Parameters so checkpoints load
+and save exactly like the reference's; the kernels read a BN-folded packed copy
+that is rebuilt whenever a parameter changes.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .weights import pack_weights, state_dict_to_numpy
+
+
+class ResidualBlock(nn.Module):
+    """Parameter container for one residual block (ai/model.py:8-25)."""
+
+    def __init__(self, channels: int):
+        super().__init__()
+        self.conv1 = nn.Conv2d(channels, channels, kernel_size=3, padding=1)
+        self.bn1 = nn.BatchNorm2d(channels)
+        self.conv2 = nn.Conv2d(channels, channels, kernel_size=3, padding=1)
+        self.bn2 = nn.BatchNorm2d(channels)
+
+
+class KVNet:
+    """Owner of one kv_net (device weights + workspace) on one GPU."""
+
+    def __init__(self, device_index: int, packed: np.ndarray):
+        L = _lib.lib()
+        if packed.size != L.kv_net_packed_size():
+            raise _lib.KVError(f"packed weights have {packed.size} floats, library expects {L.kv_net_packed_size()}")
+        self.device_index = device_index
+        h = C.c_void_p()
+        _lib.check(L.kv_net_create(device_index, C.byref(h)), "kv_net_create")
+        self.h = h
+        p = np.ascontiguousarray(packed, dtype=np.float32)
+        _lib.check(L.kv_net_load(self.h, p.ctypes.data_as(C.POINTER(C.c_float)), p.size), "kv_net_load")
+
+    def forward_planes(self, x: torch.Tensor):
+        """x: CUDA fp32 [B,12,8,8] -> (policy [B,4096], value [B,1])."""
+        B = x.shape[0]
+        x = x.contiguous()
+        pol = torch.empty((B, 4096), dtype=torch.float32, device=x.device)
+        val = torch.empty((B, 1), dtype=torch.float32, device=x.device)
+        st = torch.cuda.current_stream(x.device).cuda_stream
+        _lib.check(_lib.lib().kv_net_forward(self.h, x.data_ptr(), B, pol.data_ptr(), val.data_ptr(), st),
+                   "kv_net_forward")
+        return pol, val
+
+    def forward_boards(self, boards: torch.Tensor):
+        """boards: CUDA int8 [B,64] piece codes -> (policy [B,4096], value [B,1])."""
+        B = boards.shape[0]
+        boards = boards.contiguous()
+        pol = torch.empty((B, 4096), dtype=torch.float32, device=boards.device)
+        val = torch.empty((B, 1), dtype=torch.float32, device=boards.device)
+        st = torch.cuda.current_stream(boards.device).cuda_stream
+        _lib.check(_lib.lib().kv_net_forward_boards(self.h, boards.data_ptr(), B, pol.data_ptr(), val.data_ptr(), st),
+                   "kv_net_forward_boards")
+        return pol, val
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.lib().kv_net_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ChessNet(nn.Module):
+    """ai/model.py:27-77 ChessNet with the HIP forward."""
+
+    def __init__(self, verbose: bool = False):
+        super().__init__()
+        self.verbose = verbose
+        self.conv1 = nn.Conv2d(12, 256, kernel_size=3, padding=1)
+        self.bn1 = nn.BatchNorm2d(256)
+        self.conv2 = nn.Conv2d(256, 512, kernel_size=3, padding=1)
+        self.bn2 = nn.BatchNorm2d(512)
+        self.res_blocks = nn.ModuleList([ResidualBlock(512) for _ in range(5)])
+        self.policy_conv = nn.Conv2d(512, 2, kernel_size=1)
+        self.policy_bn = nn.BatchNorm2d(2)
+        self.policy_fc = nn.Linear(2 * 8 * 8, 4096)
+        self.value_conv = nn.Conv2d(512, 1, kernel_size=1)
+        self.value_bn = nn.BatchNorm2d(1)
+        self.value_fc1 = nn.Linear(1 * 8 * 8, 512)
+        self.value_fc2 = nn.Linear(512, 1)
+        self._kv = None
+        self._kv_key = None
+
+    # -- packed device weights ------------------------------------------------
+    def _version_key(self, device_index):
+        return (device_index,) + tuple(t._version for t in self.state_dict().values())
+
+    def packed_weights(self) -> np.ndarray:
+        return pack_weights(state_dict_to_numpy(self.state_dict()))[0]
+
+    def kv_net(self, device_index: int) -> KVNet:
+        key = self._version_key(device_index)
+        if self._kv is None or self._kv_key != key:
+            if self._kv is not None:
+                self._kv.close()
+            self._kv = KVNet(device_index, self.packed_weights())
+            self._kv_key = key
+        return self._kv
+
+    def forward(self, x):
+        if self.training:
+            raise RuntimeError("knightvision_amd.ChessNet runs the eval-mode HIP forward; call .eval() "
+                               "(the reference self-play path does, self_play.py:77)")
+        if not isinstance(x, torch.Tensor):
+            x = torch.as_tensor(np.asarray(x))
+        dev = x.device if x.is_cuda else torch.device("cuda", torch.cuda.current_device())
+        x = x.to(device=dev, dtype=torch.float32)
+        if self.verbose:
+            print("📥 Forward input shape:", x.shape)
+        with torch.no_grad():
+            pol, val = self.kv_net(dev.index if dev.index is not None else 0).forward_planes(x)
+        if self.verbose:
+            print("📤 Policy output shape:", pol.shape)
+            print("📤 Value output shape:", val.shape)
+        return pol, val
+
+    def __getstate__(self):
+        d = self.__dict__.copy()
+        d["_kv"] = None
+        d["_kv_key"] = None
+        return d

@@ -1,0 +1,66 @@
+"""HIP ChessNet forward vs the reference's own outputs (golden nn.npz) and vs
+the torch fp32 restatement at several batch sizes. Tolerance: |logit| abs
+error <= 1e-4 (north_star), value abs error <= 1e-5."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from knightvision_amd.weights import synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+TOL_P, TOL_V = 1e-4, 1e-5
+
+
+def _net(variant):
+    from knightvision_amd.model import ChessNet
+    m = ChessNet()
+    sd = synthetic_state_dict(42, variant)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    return m.eval()
+
+
+@pytest.mark.parametrize("variant", ["init", "bn", "peaked"])
+def test_forward_matches_reference_golden(golden_dir, variant):
+    g = np.load(os.path.join(golden_dir, "nn.npz"))
+    m = _net(variant)
+    p, v = m(torch.from_numpy(g["planes"]).cuda())
+    torch.cuda.synchronize()
+    dp = np.abs(p.cpu().numpy() - g[f"policy_{variant}"]).max()
+    dv = np.abs(v.cpu().numpy() - g[f"value_{variant}"]).max()
+    print(variant, "max |dpolicy|", dp, "max |dvalue|", dv)
+    assert dp <= TOL_P and dv <= TOL_V
+
+
+@pytest.mark.parametrize("B", [1, 2, 3, 31, 64, 257])
+def test_forward_batch_sizes_vs_torch(B):
+    from oracle import torch_ref
+    rng = np.random.default_rng(B)
+    codes = rng.integers(0, 13, size=(B, 64)) * (rng.random((B, 64)) < 0.4)
+    from knightvision_amd.ai import codes_to_planes
+    planes = codes_to_planes(codes)
+    sd = synthetic_state_dict(42, "bn")
+    m = _net("bn")
+    p, v = m(torch.from_numpy(planes).cuda())
+    rp, rv = torch_ref.forward(sd, planes)
+    dp = np.abs(p.cpu().numpy() - rp.numpy()).max()
+    dv = np.abs(v.cpu().numpy() - rv.numpy()).max()
+    assert dp <= TOL_P and dv <= TOL_V, (dp, dv)
+    # boards path (int8 codes, on-device encode) is the same computation
+    pb, vb = m.kv_net(0).forward_boards(torch.from_numpy(codes.astype(np.int8)).cuda())
+    assert np.abs(pb.cpu().numpy() - p.cpu().numpy()).max() == 0.0
+    assert np.abs(vb.cpu().numpy() - v.cpu().numpy()).max() == 0.0
+
+
+def test_batch_invariance():
+    """A board's outputs do not depend on the batch it is evaluated in."""
+    from knightvision_amd.ai import codes_to_planes
+    rng = np.random.default_rng(7)
+    codes = rng.integers(0, 13, size=(40, 64)) * (rng.random((40, 64)) < 0.4)
+    planes = torch.from_numpy(codes_to_planes(codes)).cuda()
+    m = _net("peaked")
+    p_all, v_all = m(planes)
+    for i in (0, 17, 39):
+        p1, v1 = m(planes[i:i + 1])
+        assert torch.equal(p1[0], p_all[i]) and torch.equal(v1[0], v_all[i])
