@@ -69,6 +69,8 @@ def _declare(L):
         "kv_dev_py_random": ([i, P(C.c_uint64), i, i, P(C.c_double)], i),
     }
     for name, (args, res) in sig.items():
+        if not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res

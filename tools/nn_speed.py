@@ -2,7 +2,9 @@
 import sys
 import time
 
+import os
 import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 from knightvision_amd.model import ChessNet
