@@ -114,7 +114,8 @@ typedef struct {
     int64_t nn_rows;      /* boards evaluated by the network */
     int64_t sims;         /* MCTS backups completed */
     int64_t records;
-    double nn_ms;         /* device time inside network forwards (HIP events) */
+    double res_conv_ms;   /* device time of the residual-tower conv launches (HIP events) */
+    int64_t res_conv_launches;
     double step_ms;       /* wall time inside kv_run */
 } kv_stats;
 
@@ -122,10 +123,16 @@ typedef struct kv_engine kv_engine;
 
 int kv_create(const kv_config* cfg, kv_engine** out);
 int kv_load_weights(kv_engine* e, const float* packed, size_t n_floats);
-/* Run up to max_steps ply-steps (< 0: until every game is finished). */
-int kv_run(kv_engine* e, int64_t max_steps);
+/* Run ply-steps until every game is finished, or max_steps steps (>= 0), or
+ * stop_after_games games have finished in total (>= 0), whichever is first. */
+int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games);
+/* max_moves for games from now on (_run_single_game's max_moves argument) */
+int kv_set_max_moves(kv_engine* e, int max_moves);
 int kv_records(kv_engine* e, kv_record* out, size_t cap, size_t* n);
+/* finished games (the last 2^20 at most), ordered by game id */
 int kv_games(kv_engine* e, kv_game* out, size_t cap, size_t* n);
+/* drop the records collected so far (between kv_run calls) */
+int kv_reset_records(kv_engine* e);
 int kv_stats_get(kv_engine* e, kv_stats* out);
 int kv_sync(kv_engine* e);
 void kv_destroy(kv_engine* e);

@@ -35,7 +35,8 @@ class Game(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("steps", C.c_int64), ("plies", C.c_int64), ("games_done", C.c_int64), ("nn_rows", C.c_int64),
-                ("sims", C.c_int64), ("records", C.c_int64), ("nn_ms", C.c_double), ("step_ms", C.c_double)]
+                ("sims", C.c_int64), ("records", C.c_int64), ("res_conv_ms", C.c_double),
+                ("res_conv_launches", C.c_int64), ("step_ms", C.c_double)]
 
 
 assert C.sizeof(Record) == 80 and C.sizeof(Game) == 32
@@ -57,11 +58,13 @@ def _declare(L):
         "kv_net_destroy": ([vp], None),
         "kv_create": ([P(Config), P(vp)], i),
         "kv_load_weights": ([vp, P(C.c_float), sz], i),
-        "kv_run": ([vp, i64], i),
+        "kv_run": ([vp, i64, i64], i),
+        "kv_set_max_moves": ([vp, i], i),
         "kv_records": ([vp, P(Record), sz, P(sz)], i),
         "kv_games": ([vp, P(Game), sz, P(sz)], i),
         "kv_stats_get": ([vp, P(Stats)], i),
         "kv_sync": ([vp], i),
+        "kv_reset_records": ([vp], i),
         "kv_destroy": ([vp], None),
         "kv_dev_valid_moves": ([i, P(C.c_int8), i, P(C.c_uint16), i, P(i), P(C.c_int8), P(C.c_uint8)], i),
         "kv_dev_make_move": ([i, P(C.c_int8), P(i), i], i),
@@ -79,7 +82,7 @@ def _declare(L):
 
 EXPORTED = ["kv_last_error", "kv_version", "kv_net_packed_size", "kv_net_create", "kv_net_load", "kv_net_forward",
             "kv_net_forward_boards", "kv_net_set_timing", "kv_net_last_timing", "kv_net_destroy", "kv_create",
-            "kv_load_weights", "kv_run", "kv_records", "kv_games", "kv_stats_get", "kv_sync", "kv_destroy",
+            "kv_load_weights", "kv_run", "kv_set_max_moves", "kv_records", "kv_games", "kv_stats_get", "kv_sync", "kv_reset_records", "kv_destroy",
             "kv_dev_valid_moves", "kv_dev_make_move", "kv_dev_dirichlet", "kv_dev_py_random"]
 
 

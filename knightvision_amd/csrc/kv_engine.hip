@@ -1,0 +1,682 @@
+// Self-play engine on MI355X: replaces scripts/self_play.py _run_single_game
+// :111-255 / self_play :258-291 for `slots` concurrent games per GPU.
+//
+// One ply-step of every live game slot is four launches on one stream:
+//   k_movegen  one lane per slot: reference-exact legal list (kv_movegen.h),
+//              game-over detection, SELFPLAY_BATCH_SIZE schedule bookkeeping
+//   NN         ChessNet over the slots' boards (kv_nn.hip) -- every board is
+//              evaluated once, as the reference does (faithful), or only the
+//              rows the schedule consumes (lazy)
+//   k_sample   one wave per slot: softmax of the consumed row, numpy-legacy
+//              Dirichlet noise on the slot's own MT19937 (wave-parallel),
+//              0.75/0.25 mix in the reference's fp32/fp64 order, CPython
+//              random.choices on the slot's second stream, makeMove, record,
+//              termination (draw / resign / max_moves)
+//   k_finish   one lane per slot: outcome + reward exactly as :210-250, game
+//              record, then the slot starts the next game id (recycling)
+// The host only launches and, every few steps, reads one counter.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <vector>
+
+#include "kv_common.h"
+#include "kv_movegen.h"
+#include "kv_rng.h"
+
+#pragma clang fp contract(off)
+
+namespace kv {
+
+int net_forward_boards_internal(kv_net* net, const int8_t* boards_dev, int B, float* policy, float* value,
+                                hipStream_t st);
+int net_set_res_events(kv_net* net, hipEvent_t a, hipEvent_t b);
+
+enum : int { ST_IDLE = 0, ST_ACTIVE = 1, ST_FINISHED = 2 };
+enum : int { END_NONE = 0, END_NOMOVES = 1, END_DRAW = 2, END_RESIGN = 3, END_MAXED = 4 };
+
+struct Slot {
+    long long game_id;
+    int status;
+    int ply;
+    int wtm, wkr, wkc, bkr, bkc, flags, ep;
+    int nmoves;
+    int buf;
+    int has_last;
+    float last_value;
+    int consumed;
+    int need_flush;
+    int n_evals;
+    int end_kind;
+    int outcome;
+    int reason;
+    int pad[11];
+};
+static_assert(sizeof(Slot) == 128, "slot is one cache line");
+
+struct Ctr {
+    unsigned long long rec_count;
+    unsigned long long games_count;
+    unsigned long long next_game;
+    unsigned long long plies;
+    unsigned long long nn_rows;
+    unsigned long long sims;
+    int active;
+    int error;
+};
+
+struct DevCfg {
+    int slots;
+    long long n_games;
+    long long id_base, id_stride;
+    unsigned long long seed;
+    int seed_mode;
+    int max_moves;
+    int batch;
+    double eps, alpha;
+    long long record_cap;
+    int recycle;
+    int rows;  // NN rows per step (slots, or 2*slots with flush rows)
+    long long games_cap;  // game-record ring capacity
+};
+
+__device__ inline Pos slot_pos(const Slot& s, const int8_t* board) {
+    Pos p;
+    pos_from_board(p, board, s.wtm, s.wkr, s.wkc, s.bkr, s.bkc, s.flags, s.ep);
+    return p;
+}
+
+__device__ inline void slot_store_pos(Slot& s, int8_t* board, const Pos& p) {
+    pos_to_board(p, board);
+    s.wtm = p.wtm;
+    s.wkr = p.kr[0]; s.wkc = p.kc[0]; s.bkr = p.kr[1]; s.bkc = p.kc[1];
+    s.flags = p.flags;
+    s.ep = p.ep;
+}
+
+__constant__ const int8_t kStart[64] = {9, 11, 10, 8, 7, 10, 11, 9, 12, 12, 12, 12, 12, 12, 12, 12,
+                                        0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                        0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                        6, 6, 6, 6, 6, 6, 6, 6, 3, 5, 4, 2, 1, 4, 5, 3};
+
+// GameState() :34-84 + per-game seeding (_init_worker :81-85 with SEED+g)
+__device__ void start_game(const DevCfg& cfg, Slot& s, int8_t* board, uint32_t* np_mt, uint32_t* py_mt,
+                           long long k) {
+    const long long gid = cfg.id_base + k * cfg.id_stride;
+    for (int i = 0; i < 64; ++i) board[i] = kStart[i];
+    s.game_id = gid;
+    s.status = ST_ACTIVE;
+    s.ply = 0;
+    s.wtm = 1; s.wkr = 7; s.wkc = 4; s.bkr = 0; s.bkc = 4; s.flags = 0; s.ep = -1;
+    s.nmoves = 0;
+    s.buf = 0;
+    s.consumed = 0;
+    s.n_evals = 0;
+    s.end_kind = END_NONE;
+    s.outcome = 0;
+    s.reason = -1;
+    if (cfg.seed_mode == KV_SEED_PER_GAME) {
+        const unsigned long long sd = cfg.seed + (unsigned long long)gid;
+        mt_seed_genrand(np_mt, (uint32_t)sd);
+        mt_seed_python(py_mt, sd);
+        s.has_last = 0;
+        s.need_flush = 0;
+    }
+}
+
+__global__ void k_init(DevCfg cfg, Slot* slots, int8_t* boards, uint32_t* np_mt, uint32_t* py_mt, Ctr* ctr) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cfg.slots) return;
+    Slot s;
+    memset(&s, 0, sizeof(s));
+    s.status = ST_IDLE;
+    s.has_last = 0;
+    s.need_flush = 0;
+    if (cfg.seed_mode == KV_SEED_SEQUENTIAL) {  // one pair of streams seeded SEED (self_play.py:270)
+        mt_seed_genrand(np_mt + (size_t)i * MT_WORDS, (uint32_t)cfg.seed);
+        mt_seed_python(py_mt + (size_t)i * MT_WORDS, cfg.seed);
+    }
+    if ((long long)i < cfg.n_games) {
+        start_game(cfg, s, boards + (size_t)i * 64, np_mt + (size_t)i * MT_WORDS, py_mt + (size_t)i * MT_WORDS, i);
+        atomicAdd(&ctr->active, 1);
+    }
+    slots[i] = s;
+}
+
+// ------------------------------------------------------------ movegen ----
+__global__ __launch_bounds__(64) void k_movegen(DevCfg cfg, Slot* slots, int8_t* boards, uint16_t* moves,
+                                                Ctr* ctr) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cfg.slots) return;
+    Slot s = slots[i];
+    if (s.status != ST_ACTIVE) return;
+    int8_t* board = boards + (size_t)i * 64;
+    Pos p = slot_pos(s, board);
+    MoveOut o{moves + (size_t)i * MAXM, 0, MAXM, 0};
+    const int n = valid_moves(p, o);
+    if (o.overflow) atomicOr(&ctr->error, 1);
+    slot_store_pos(s, board, p);  // the reference may mutate the board (stale king, double check)
+    s.nmoves = n < MAXM ? n : MAXM;
+    if (n == 0) {
+        s.end_kind = END_NOMOVES;
+        s.status = ST_FINISHED;
+        s.consumed = 0;
+    } else {
+        // buffer.append(board); eval when len >= BATCH_SIZE or nothing evaluated yet (:129-145)
+        s.buf += 1;
+        const bool has = s.has_last || s.need_flush;
+        s.consumed = (s.buf >= cfg.batch) || !has;
+        atomicAdd(&ctr->nn_rows, 1ull);
+    }
+    slots[i] = s;
+}
+
+// ------------------------------------------------------------- sample ----
+__device__ inline float wave_max(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
+    return v;
+}
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+    return v;
+}
+
+// torch.softmax over 4096 fp32 logits (self_play.py:150): max, exp(x-max),
+// sum, x * (1/sum)
+__device__ void wave_softmax_4096(const float* lg, float* out, int lane) {
+    float v[64];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        v[j] = lg[j * 64 + lane];
+        m = fmaxf(m, v[j]);
+    }
+    m = wave_max(m);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        v[j] = expf(v[j] - m);
+        s += v[j];
+    }
+    s = wave_sum(s);
+    const float inv = 1.0f / s;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) out[j * 64 + lane] = v[j] * inv;
+}
+
+__global__ __launch_bounds__(64) void k_sample(DevCfg cfg, Slot* slots, int8_t* boards, const uint16_t* moves,
+                                               const float* logits, const float* values, float* last_probs,
+                                               double* gam, uint32_t* np_mt, uint32_t* py_mt, kv_record* rec,
+                                               int8_t* last_board, Ctr* ctr) {
+    __shared__ uint32_t mt_a[MT_N], mt_b[MT_N];
+    __shared__ double vals[MAXM];
+    __shared__ double cum[MAXM];
+    __shared__ int s_pick;
+    const int i = blockIdx.x, lane = threadIdx.x;
+    Slot s = slots[i];
+    if (s.status != ST_ACTIVE) return;
+    float* lp = last_probs + (size_t)i * 4096;
+    if (s.need_flush) {  // previous game's final flush row (sequential mode)
+        wave_softmax_4096(logits + (size_t)(cfg.slots + i) * 4096, lp, lane);
+        s.last_value = values[cfg.slots + i];
+        s.has_last = 1;
+        s.need_flush = 0;
+    }
+    if (s.consumed) {
+        wave_softmax_4096(logits + (size_t)i * 4096, lp, lane);
+        s.last_value = values[i];
+        s.has_last = 1;
+        s.buf = 0;
+        s.n_evals += 1;
+    }
+    __syncthreads();
+    // noise = np.random.dirichlet([ALPHA] * 4096) (:153)
+    WaveMT w;
+    wmt_load(w, np_mt + (size_t)i * MT_WORDS, mt_a, mt_b, lane);
+    double* g = gam + (size_t)i * 4096;
+    long long att;
+    const double acc = wave_dirichlet_gamma(w, cfg.alpha, 4096, g, &att, lane);
+    wmt_store(w, np_mt + (size_t)i * MT_WORDS, lane);
+    const double invacc = 1 / acc;
+    __syncthreads();
+    // policy = (1-eps)*policy [fp32] + eps*noise [fp64]; legal_probs in list order (:154-160)
+    const float keep = (float)(1.0 - cfg.eps);
+    const int n = s.nmoves;
+    const uint16_t* ml = moves + (size_t)i * MAXM;
+    for (int j = lane; j < n; j += 64) {
+        const int mv = ml[j];
+        const int idx = (mv & 63) * 64 + ((mv >> 6) & 63);
+        const float p32 = keep * lp[idx];
+        const double noise = g[idx] * invacc;
+        vals[j] = (double)p32 + cfg.eps * noise;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        uint32_t* py = py_mt + (size_t)i * MT_WORDS;
+        double total = 0.0;
+        for (int j = 0; j < n; ++j) total = total + vals[j];
+        int pick;
+        if (total == 0.0) {
+            pick = mt_randbelow_serial(py, n);  // random.choice (:164)
+        } else {  // random.choices(valid_moves, weights=normalized) (:166-167)
+            double c = 0.0;
+            for (int j = 0; j < n; ++j) {
+                c = c + vals[j] / total;
+                cum[j] = c;
+            }
+            const double tot = cum[n - 1] + 0.0;
+            const double x = mt_random_serial(py) * tot;
+            int lo = 0, hi = n - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (x < cum[mid]) hi = mid;
+                else lo = mid + 1;
+            }
+            pick = lo;
+        }
+        s_pick = pick;
+    }
+    __syncthreads();
+    const int mv = ml[s_pick];
+    int8_t* board = boards + (size_t)i * 64;
+    // record (encode_board(gs.board), move_index) before the move (:173-174)
+    const unsigned long long r = lane == 0 ? atomicAdd(&ctr->rec_count, 1ull) : 0ull;
+    const unsigned long long ridx = __shfl(r, 0);
+    const int8_t sq = board[lane];
+    last_board[(size_t)i * 64 + lane] = sq;
+    if ((long long)ridx < cfg.record_cap) {
+        rec[ridx].board[lane] = sq;
+        if (lane == 0) {
+            rec[ridx].game_id = s.game_id;
+            rec[ridx].ply = s.ply;
+            rec[ridx].move = (uint16_t)((mv & 63) * 64 + ((mv >> 6) & 63));
+            rec[ridx].pad = 0;
+        }
+    } else if (lane == 0) {
+        atomicOr(&ctr->error, 2);
+    }
+    __syncthreads();
+    if (lane == 0) {
+        make_move_board(board, s.wtm, s.wkr, s.wkc, s.bkr, s.bkc, s.flags, s.ep, mv);
+        s.ply += 1;
+        atomicAdd(&ctr->plies, 1ull);
+    }
+    __syncthreads();
+    const int8_t b2 = board[lane];
+    const bool non_king = b2 != 0 && b2 != 1 && b2 != 7;
+    const bool draw = __ballot(non_king) == 0ull;
+    if (lane == 0) {
+        // termination order: isDraw (:180), resign (:185), max_moves (:196)
+        const int wtm = s.wtm;
+        if (draw) {
+            s.end_kind = END_DRAW;
+        } else if (s.ply > 15 && (double)s.last_value < -0.7) {
+            s.end_kind = END_RESIGN;
+            s.outcome = wtm ? -1 : 1;
+            s.reason = 1;
+        } else if (cfg.max_moves > 0 && s.ply >= cfg.max_moves) {
+            s.end_kind = END_MAXED;
+        }
+        if (s.end_kind != END_NONE) s.status = ST_FINISHED;
+        s.consumed = 0;
+        slots[i] = s;
+    }
+}
+
+// ------------------------------------------------------------- finish ----
+__global__ __launch_bounds__(64) void k_finish(DevCfg cfg, Slot* slots, int8_t* boards, uint16_t* moves,
+                                               uint32_t* np_mt, uint32_t* py_mt, kv_game* games, Ctr* ctr) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cfg.slots) return;
+    Slot s = slots[i];
+    if (s.status == ST_ACTIVE) {
+        atomicAdd(&ctr->active, 1);
+        return;
+    }
+    if (s.status != ST_FINISHED) return;
+    int8_t* board = boards + (size_t)i * 64;
+    // outcome (:210-238)
+    if (s.end_kind == END_MAXED) {
+        s.outcome = 0;
+        s.reason = 0;
+    } else if (s.end_kind != END_RESIGN) {
+        Pos p = slot_pos(s, board);
+        MoveOut o{moves + (size_t)i * MAXM, 0, MAXM, 0};
+        const bool chk = in_check(p);
+        int n1 = -1;
+        if (chk) n1 = valid_moves(p, o);
+        if (chk && n1 == 0) {
+            s.outcome = p.wtm ? -1 : 1;
+            s.reason = 2;
+        } else if (valid_moves(p, o) == 0) {
+            s.outcome = 0;
+            s.reason = 3;
+        } else {
+            bool kings_only = true;
+            for (int q = 0; q < 64; ++q) {
+                const int c = pos_at(p, q);
+                if (c != 0 && c != 1 && c != 7) kings_only = false;
+            }
+            s.outcome = 0;
+            s.reason = kings_only ? 4 : 5;  // material branch: always 0 (see oracle/kv_oracle.c)
+        }
+        slot_store_pos(s, board, p);
+    }
+    // flush of a non-empty buffer (:202-208): one more forward call
+    if (s.buf > 0) {
+        s.n_evals += 1;
+        if (cfg.seed_mode == KV_SEED_SEQUENTIAL) s.need_flush = 1;
+    }
+    const unsigned long long gi = atomicAdd(&ctr->games_count, 1ull);
+    kv_game gm;
+    gm.game_id = s.game_id;
+    gm.plies = s.ply;
+    gm.outcome = s.outcome;
+    gm.reward = s.outcome == 1 ? 1.0f : (s.outcome == 0 ? 0.2f : -1.0f);
+    gm.reason = s.reason;
+    gm.n_evals = s.n_evals;
+    gm.pad = 0;
+    games[gi % (unsigned long long)cfg.games_cap] = gm;
+    s.status = ST_IDLE;
+    if (cfg.recycle) {
+        const unsigned long long k = atomicAdd(&ctr->next_game, 1ull);
+        if ((long long)k < cfg.n_games) {
+            start_game(cfg, s, board, np_mt + (size_t)i * MT_WORDS, py_mt + (size_t)i * MT_WORDS, (long long)k);
+            atomicAdd(&ctr->active, 1);
+        }
+    }
+    slots[i] = s;
+}
+
+// the flush rows of sequential mode: boards [slots, 2*slots) = last appended board
+__global__ void k_flush_rows(DevCfg cfg, const Slot* slots, const int8_t* last_board, int8_t* nn_boards) {
+    const int i = blockIdx.x, lane = threadIdx.x;
+    if (i >= cfg.slots) return;
+    nn_boards[(size_t)(cfg.slots + i) * 64 + lane] = slots[i].need_flush ? last_board[(size_t)i * 64 + lane] : 0;
+}
+
+}  // namespace kv
+
+// ---------------------------------------------------------------- host --
+struct kv_engine {
+    kv_config cfg;
+    kv::DevCfg dc;
+    kv_net* net = nullptr;
+    hipStream_t st = nullptr;
+    kv::Slot* slots = nullptr;
+    int8_t* boards = nullptr;  // [rows][64]: slot boards, then flush rows
+    uint16_t* moves = nullptr;
+    float* logits = nullptr;
+    float* values = nullptr;
+    float* last_probs = nullptr;
+    double* gam = nullptr;
+    uint32_t* np_mt = nullptr;
+    uint32_t* py_mt = nullptr;
+    kv_record* rec = nullptr;
+    kv_game* games = nullptr;
+    int8_t* last_board = nullptr;
+    kv::Ctr* ctr = nullptr;
+    kv::Ctr* ctr_host = nullptr;  // pinned
+    long long steps = 0;
+    double wall_ms = 0;
+    std::vector<hipEvent_t> ev;  // residual-conv section start/end per forward
+    int n_ev_used = 0;
+    double nn_res_ms = 0;
+    long long nn_res_launches = 0;
+    bool loaded = false;
+};
+
+static int eng_counters(kv_engine* e) {
+    KV_HIP(hipMemcpyAsync(e->ctr_host, e->ctr, sizeof(kv::Ctr), hipMemcpyDeviceToHost, e->st));
+    KV_HIP(hipStreamSynchronize(e->st));
+    if (e->ctr_host->error) {
+        kv::set_error("engine device error flags 0x%x (1: move list overflow, 2: record buffer full)",
+                      e->ctr_host->error);
+        return KV_EOVERFLOW;
+    }
+    return KV_OK;
+}
+
+static int eng_collect_timing(kv_engine* e) {
+    for (int k = 0; k + 1 < e->n_ev_used; k += 2) {
+        float ms = 0.f;
+        KV_HIP(hipEventSynchronize(e->ev[k + 1]));
+        KV_HIP(hipEventElapsedTime(&ms, e->ev[k], e->ev[k + 1]));
+        e->nn_res_ms += ms;
+        e->nn_res_launches += 10;
+    }
+    e->n_ev_used = 0;
+    return KV_OK;
+}
+
+extern "C" {
+
+int kv_create(const kv_config* cfg, kv_engine** out) {
+    KV_REQUIRE(cfg && out, KV_EINVAL, "kv_create: NULL argument");
+    KV_REQUIRE(cfg->slots > 0 && cfg->n_games >= 0, KV_EINVAL, "kv_create: slots must be > 0");
+    KV_REQUIRE(cfg->alpha > 0.0 && cfg->alpha < 1.0, KV_EINVAL,
+               "kv_create: DIR_NOISE_ALPHA must be in (0,1) (legacy gamma shape<1 branch), got %g", cfg->alpha);
+    KV_REQUIRE(cfg->batch >= 1, KV_EINVAL, "kv_create: SELFPLAY_BATCH_SIZE must be >= 1");
+    KV_REQUIRE(cfg->seed_mode == KV_SEED_PER_GAME || cfg->seed_mode == KV_SEED_SEQUENTIAL, KV_EINVAL,
+               "kv_create: bad seed_mode");
+    KV_REQUIRE(cfg->seed_mode != KV_SEED_SEQUENTIAL || cfg->slots == 1, KV_EINVAL,
+               "kv_create: sequential seeding plays games in order on one slot");
+    KV_REQUIRE(cfg->sims == 0, KV_EINVAL, "kv_create: MCTS mode (sims > 0) not available in this build");
+    KV_HIP(hipSetDevice(cfg->device));
+    kv_engine* e = new kv_engine();
+    e->cfg = *cfg;
+    if (e->cfg.game_id_stride <= 0) e->cfg.game_id_stride = 1;
+    if (e->cfg.record_cap <= 0) e->cfg.record_cap = 1 << 20;
+    kv::DevCfg& d = e->dc;
+    d.slots = cfg->slots;
+    d.n_games = cfg->n_games;
+    d.id_base = cfg->game_id_base;
+    d.id_stride = e->cfg.game_id_stride;
+    d.seed = cfg->seed;
+    d.seed_mode = cfg->seed_mode;
+    d.max_moves = cfg->max_moves;
+    d.batch = cfg->batch;
+    d.eps = cfg->eps;
+    d.alpha = cfg->alpha;
+    d.record_cap = e->cfg.record_cap;
+    d.recycle = cfg->recycle;
+    d.rows = cfg->seed_mode == KV_SEED_SEQUENTIAL ? 2 * cfg->slots : cfg->slots;
+    d.games_cap = std::max<long long>(1, std::min<long long>(cfg->n_games, 1 << 20));
+    const size_t S = (size_t)cfg->slots, R = (size_t)d.rows;
+    int rc = KV_OK;
+#define ALLOC(ptr, bytes)                                   \
+    do {                                                    \
+        hipError_t er_ = hipMalloc(&(ptr), (bytes));        \
+        if (er_ != hipSuccess) {                            \
+            kv::set_error("kv_create: hipMalloc %s (%zu B): %s", #ptr, (size_t)(bytes), hipGetErrorString(er_)); \
+            kv_destroy(e);                                  \
+            return KV_ENOMEM;                               \
+        }                                                   \
+    } while (0)
+    ALLOC(e->slots, S * sizeof(kv::Slot));
+    ALLOC(e->boards, R * 64);
+    ALLOC(e->moves, S * kv::MAXM * sizeof(uint16_t));
+    ALLOC(e->logits, R * 4096 * sizeof(float));
+    ALLOC(e->values, R * sizeof(float));
+    ALLOC(e->last_probs, S * 4096 * sizeof(float));
+    ALLOC(e->gam, S * 4096 * sizeof(double));
+    ALLOC(e->np_mt, S * kv::MT_WORDS * sizeof(uint32_t));
+    ALLOC(e->py_mt, S * kv::MT_WORDS * sizeof(uint32_t));
+    ALLOC(e->rec, (size_t)e->cfg.record_cap * sizeof(kv_record));
+    ALLOC(e->games, (size_t)d.games_cap * sizeof(kv_game));
+    ALLOC(e->last_board, S * 64);
+    ALLOC(e->ctr, sizeof(kv::Ctr));
+#undef ALLOC
+    if (hipHostMalloc(&e->ctr_host, sizeof(kv::Ctr)) != hipSuccess) {
+        kv_destroy(e);
+        kv::set_error("kv_create: hipHostMalloc failed");
+        return KV_ENOMEM;
+    }
+    if ((rc = kv_net_create(cfg->device, &e->net))) {
+        kv_destroy(e);
+        return rc;
+    }
+    if (hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) != hipSuccess) {
+        kv_destroy(e);
+        kv::set_error("kv_create: stream");
+        return KV_EHIP;
+    }
+    (void)hipMemsetAsync(e->boards, 0, R * 64, e->st);
+    (void)hipMemsetAsync(e->ctr, 0, sizeof(kv::Ctr), e->st);
+    (void)hipMemsetAsync(e->last_probs, 0, S * 4096 * sizeof(float), e->st);
+    kv::Ctr c0;
+    memset(&c0, 0, sizeof(c0));
+    c0.next_game = (unsigned long long)std::min<long long>(cfg->n_games, cfg->slots);
+    (void)hipMemcpyAsync(e->ctr, &c0, sizeof(c0), hipMemcpyHostToDevice, e->st);
+    hipLaunchKernelGGL(kv::k_init, dim3((cfg->slots + 63) / 64), dim3(64), 0, e->st, d, e->slots, e->boards,
+                       e->np_mt, e->py_mt, e->ctr);
+    KV_HIP(hipGetLastError());
+    KV_HIP(hipStreamSynchronize(e->st));
+    *out = e;
+    return KV_OK;
+}
+
+int kv_load_weights(kv_engine* e, const float* packed, size_t n_floats) {
+    KV_REQUIRE(e, KV_EINVAL, "kv_load_weights: NULL engine");
+    int rc = kv_net_load(e->net, packed, n_floats);
+    if (rc == KV_OK) e->loaded = true;
+    return rc;
+}
+
+int kv_set_max_moves(kv_engine* e, int max_moves) {
+    KV_REQUIRE(e, KV_EINVAL, "kv_set_max_moves: NULL");
+    e->cfg.max_moves = max_moves;
+    e->dc.max_moves = max_moves;
+    return KV_OK;
+}
+
+int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
+    KV_REQUIRE(e && e->loaded, KV_EINVAL, "kv_run: engine has no weights");
+    KV_HIP(hipSetDevice(e->cfg.device));
+    const auto t0 = std::chrono::steady_clock::now();
+    const int S = e->cfg.slots;
+    const int check_every = (S >= 64 && stop_after_games < 0) ? 4 : 1;
+    int rc = eng_counters(e);
+    if (rc) return rc;
+    long long done = 0;
+    while ((max_steps < 0 || done < max_steps) && e->ctr_host->active > 0 &&
+           (stop_after_games < 0 || (int64_t)e->ctr_host->games_count < stop_after_games)) {
+        hipLaunchKernelGGL(kv::k_movegen, dim3((S + 63) / 64), dim3(64), 0, e->st, e->dc, e->slots, e->boards,
+                           e->moves, e->ctr);
+        KV_HIP(hipGetLastError());
+        if (e->dc.rows > S)
+            hipLaunchKernelGGL(kv::k_flush_rows, dim3(S), dim3(64), 0, e->st, e->dc, e->slots, e->last_board,
+                               e->boards);
+        // residual-conv section timing (HIP events on the engine stream)
+        if ((size_t)e->n_ev_used + 2 > e->ev.size()) {
+            for (int k = 0; k < 2; ++k) {
+                hipEvent_t x;
+                KV_HIP(hipEventCreate(&x));
+                e->ev.push_back(x);
+            }
+        }
+        kv::net_set_res_events(e->net, e->ev[e->n_ev_used], e->ev[e->n_ev_used + 1]);
+        e->n_ev_used += 2;
+        if ((rc = kv::net_forward_boards_internal(e->net, e->boards, e->dc.rows, e->logits, e->values, e->st)))
+            return rc;
+        kv::net_set_res_events(e->net, nullptr, nullptr);
+        hipLaunchKernelGGL(kv::k_sample, dim3(S), dim3(64), 0, e->st, e->dc, e->slots, e->boards, e->moves,
+                           e->logits, e->values, e->last_probs, e->gam, e->np_mt, e->py_mt, e->rec, e->last_board,
+                           e->ctr);
+        KV_HIP(hipGetLastError());
+        KV_HIP(hipMemsetAsync(&e->ctr->active, 0, sizeof(int), e->st));
+        hipLaunchKernelGGL(kv::k_finish, dim3((S + 63) / 64), dim3(64), 0, e->st, e->dc, e->slots, e->boards,
+                           e->moves, e->np_mt, e->py_mt, e->games, e->ctr);
+        KV_HIP(hipGetLastError());
+        ++done;
+        ++e->steps;
+        if (done % check_every == 0 || (max_steps >= 0 && done >= max_steps)) {
+            if ((rc = eng_counters(e))) return rc;
+            if ((rc = eng_collect_timing(e))) return rc;
+        }
+    }
+    if ((rc = eng_counters(e))) return rc;
+    if ((rc = eng_collect_timing(e))) return rc;
+    e->wall_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return KV_OK;
+}
+
+int kv_reset_records(kv_engine* e) {
+    KV_REQUIRE(e, KV_EINVAL, "kv_reset_records: NULL");
+    KV_HIP(hipMemsetAsync(&e->ctr->rec_count, 0, sizeof(unsigned long long), e->st));
+    KV_HIP(hipStreamSynchronize(e->st));
+    return KV_OK;
+}
+
+int kv_sync(kv_engine* e) {
+    KV_REQUIRE(e, KV_EINVAL, "kv_sync: NULL");
+    KV_HIP(hipStreamSynchronize(e->st));
+    return KV_OK;
+}
+
+int kv_records(kv_engine* e, kv_record* out, size_t cap, size_t* n) {
+    KV_REQUIRE(e && n, KV_EINVAL, "kv_records: NULL argument");
+    int rc = eng_counters(e);
+    if (rc) return rc;
+    size_t cnt = (size_t)std::min<unsigned long long>(e->ctr_host->rec_count, (unsigned long long)e->cfg.record_cap);
+    *n = cnt;
+    if (!out) return KV_OK;
+    KV_REQUIRE(cap >= cnt, KV_EINVAL, "kv_records: buffer holds %zu, need %zu", cap, cnt);
+    KV_HIP(hipMemcpy(out, e->rec, cnt * sizeof(kv_record), hipMemcpyDeviceToHost));
+    std::stable_sort(out, out + cnt, [](const kv_record& a, const kv_record& b) {
+        return a.game_id != b.game_id ? a.game_id < b.game_id : a.ply < b.ply;
+    });
+    return KV_OK;
+}
+
+int kv_games(kv_engine* e, kv_game* out, size_t cap, size_t* n) {
+    KV_REQUIRE(e && n, KV_EINVAL, "kv_games: NULL argument");
+    int rc = eng_counters(e);
+    if (rc) return rc;
+    size_t cnt = (size_t)std::min<unsigned long long>(e->ctr_host->games_count, (unsigned long long)e->dc.games_cap);
+    *n = cnt;
+    if (!out) return KV_OK;
+    KV_REQUIRE(cap >= cnt, KV_EINVAL, "kv_games: buffer holds %zu, need %zu", cap, cnt);
+    KV_HIP(hipMemcpy(out, e->games, cnt * sizeof(kv_game), hipMemcpyDeviceToHost));
+    std::sort(out, out + cnt, [](const kv_game& a, const kv_game& b) { return a.game_id < b.game_id; });
+    return KV_OK;
+}
+
+int kv_stats_get(kv_engine* e, kv_stats* out) {
+    KV_REQUIRE(e && out, KV_EINVAL, "kv_stats_get: NULL argument");
+    int rc = eng_counters(e);
+    if (rc) return rc;
+    out->steps = e->steps;
+    out->plies = (int64_t)e->ctr_host->plies;
+    out->games_done = (int64_t)e->ctr_host->games_count;
+    out->nn_rows = (int64_t)e->ctr_host->nn_rows;
+    out->sims = (int64_t)e->ctr_host->sims;
+    out->records = (int64_t)e->ctr_host->rec_count;
+    out->res_conv_ms = e->nn_res_ms;
+    out->res_conv_launches = e->nn_res_launches;
+    out->step_ms = e->wall_ms;
+    return KV_OK;
+}
+
+void kv_destroy(kv_engine* e) {
+    if (!e) return;
+    (void)hipSetDevice(e->cfg.device);
+    if (e->st) (void)hipStreamSynchronize(e->st);
+    void* bufs[] = {e->slots, e->boards, e->moves, e->logits, e->values, e->last_probs, e->gam,
+                    e->np_mt, e->py_mt, e->rec, e->games, e->last_board, e->ctr};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    if (e->ctr_host) (void)hipHostFree(e->ctr_host);
+    for (auto x : e->ev) (void)hipEventDestroy(x);
+    if (e->net) kv_net_destroy(e->net);
+    if (e->st) (void)hipStreamDestroy(e->st);
+    delete e;
+}
+
+}  // extern "C"

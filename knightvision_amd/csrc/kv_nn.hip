@@ -370,10 +370,8 @@ struct kv_net {
     float* T = nullptr;
     float* pfeat = nullptr;
     bool timing = false;
-    hipEvent_t ev[24];
-    int n_ev = 0;
-    float conv_ms = 0.f;
-    int n_conv = 0;
+    hipEvent_t ev[3];
+    hipEvent_t res_a = nullptr, res_b = nullptr;  // engine hook: residual section
 };
 
 template <int CIN, int CK, bool RESID>
@@ -396,7 +394,7 @@ static int launch_conv(const float* in, const float* w, const float* sc, const f
 static int net_reserve(kv_net* net, int nb_pad) {
     if (nb_pad <= net->cap) return KV_OK;
     int cap = nb_pad < 64 ? 64 : nb_pad;
-    hipFree(net->x16); hipFree(net->X); hipFree(net->T); hipFree(net->pfeat);
+    (void)hipFree(net->x16); (void)hipFree(net->X); (void)hipFree(net->T); (void)hipFree(net->pfeat);
     net->x16 = net->X = net->T = net->pfeat = nullptr;
     net->cap = 0;
     KV_HIP(hipMalloc(&net->x16, (size_t)cap * 64 * 16 * 4));
@@ -421,6 +419,7 @@ static int net_tower(kv_net* net, int nb, int nb_pad, float* policy, float* valu
                                           nb_pad, st)))
         return rc;
     if (tm) KV_HIP(hipEventRecord(net->ev[1], st));
+    if (net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
     for (int r = 0; r < 5; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         if ((rc = launch_conv<512, 32, false>(net->X, W + o.w[l1], W + o.scale[l1], W + o.shift[l1], nullptr, net->T,
@@ -431,6 +430,7 @@ static int net_tower(kv_net* net, int nb, int nb_pad, float* policy, float* valu
             return rc;
     }
     if (tm) KV_HIP(hipEventRecord(net->ev[2], st));
+    if (net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
     hipLaunchKernelGGL(kv::heads_kernel, dim3(nb), dim3(256), 0, st, net->X, W + o.head_w, W + o.head_scale,
                        W + o.head_shift, W + o.vfc1_w, W + o.vfc1_b, W + o.vfc2_w, W + o.vfc2_b, net->pfeat, value);
     KV_HIP(hipGetLastError());
@@ -519,13 +519,13 @@ int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv) {
 
 void kv_net_destroy(kv_net* net) {
     if (!net) return;
-    hipSetDevice(net->device);
-    hipFree(net->w);
-    hipFree(net->x16);
-    hipFree(net->X);
-    hipFree(net->T);
-    hipFree(net->pfeat);
-    for (int i = 0; i < 3; ++i) hipEventDestroy(net->ev[i]);
+    (void)hipSetDevice(net->device);
+    (void)hipFree(net->w);
+    (void)hipFree(net->x16);
+    (void)hipFree(net->X);
+    (void)hipFree(net->T);
+    (void)hipFree(net->pfeat);
+    for (int i = 0; i < 3; ++i) (void)hipEventDestroy(net->ev[i]);
     delete net;
 }
 
@@ -536,5 +536,10 @@ namespace kv {
 int net_forward_boards_internal(kv_net* net, const int8_t* boards_dev, int B, float* policy, float* value,
                                 hipStream_t st) {
     return kv_net_forward_boards(net, boards_dev, B, policy, value, (void*)st);
+}
+int net_set_res_events(kv_net* net, hipEvent_t a, hipEvent_t b) {
+    net->res_a = a;
+    net->res_b = b;
+    return KV_OK;
 }
 }  // namespace kv
