@@ -1,0 +1,170 @@
+"""Benchmark of the self-play data-generation path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode mcts|ref] ...
+
+One step = one ply-step of every concurrent game slot on a GPU (sims > 0: the
+full PUCT search of every slot's current move -- `sims` network batches --
+then the move; ref: one network row per slot, then the reference's sampled
+move). Inputs are synthetic: build-defined random-init weights (seed 42,
+knightvision_amd.weights), games from the initial position, per-game seeds
+42 + global game id, slots recycled so every step is steady state.
+
+N > 1: launched by torch.distributed.run, one process per GPU; games are
+sharded by global id (weak scaling, no collective in the loop); the timed
+region is bracketed by barrier + synchronize and the max over ranks is used.
+After the timed region the ranks all-gather their experience records over
+RCCL (reported as gather_ms, not part of `value`).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+FLOP_PER_EVAL = 3175744512            # SURVEY.md 8d, ChessNet forward per position
+FLOP_RES_CONV_PER_BOARD = 301989888   # one 3x3 512->512 conv on 8x8 (2*64*512*4608)
+FP32_MFMA_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md, f32-input MFMA (dense)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--mode", choices=["mcts", "ref"], default=os.environ.get("KV_BENCH_MODE", "ref"))
+    ap.add_argument("--slots", type=int, default=256)
+    ap.add_argument("--sims", type=int, default=400)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds: float, sims: int):
+    """The oracle restatement (C rules + RNG + reference eval schedule) with the
+    reference's network run by torch on the host CPU, faithful one-eval-per-ply
+    (test infrastructure; never the measured product)."""
+    from oracle import oracle as O
+    from oracle import torch_ref
+    from knightvision_amd.weights import synthetic_state_dict
+    ev = torch_ref.make_eval_fn(synthetic_state_dict(42, "init"))
+    t0 = time.perf_counter()
+    plies = games = 0
+    seed = 42
+    while time.perf_counter() - t0 < seconds:
+        r = O.play_game(ev, O.MT(seed, "numpy"), O.MT(seed, "python"), O.Last(), max_moves=64, batch=16,
+                        softmax_fn=torch_ref.torch_softmax)
+        plies += r["plies"]
+        games += 1
+        seed += 1
+    dt = time.perf_counter() - t0
+    return dict(value=plies / dt, unit="plies/s", cores=torch.get_num_threads(), kind="port",
+                sample=f"{games} games x <=64 plies (per-game seeds 42+), oracle rules/RNG + torch-CPU "
+                       f"ChessNet fp32, batch-16 reference schedule, {dt:.1f}s")
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from knightvision_amd.engine import SelfPlayEngine
+    from knightvision_amd.weights import synthetic_state_dict
+    from knightvision_amd.distributed import gather_experience
+
+    mcts = args.mode == "mcts"
+    sims = args.sims if mcts else 0
+    steps = args.steps if args.steps is not None else (3 if mcts else 40)
+    warmup = args.warmup if args.warmup is not None else (1 if mcts else 8)
+    G = args.slots
+    eng = SelfPlayEngine(synthetic_state_dict(42, "init"), slots=G, n_games=1 << 40, seed=42, max_moves=None,
+                         batch=16, sims=sims, game_id_base=rank, game_id_stride=world,
+                         record_cap=max(1 << 16, G * (steps + warmup + 8)), device=local)
+    eng.run(warmup)
+    s0 = eng.stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.run(steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    s1 = eng.stats()
+    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    d = {k: s1[k] - s0[k] for k in ("plies", "games_done", "nn_rows", "sims", "res_conv_ms", "res_conv_launches")}
+    tot = torch.tensor([d["plies"], d["games_done"], d["nn_rows"], d["sims"]], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tot)
+    plies, games_done, nn_rows, sims_done = (float(x) for x in tot.tolist())
+
+    # experience gather (RCCL all-gather of packed records), outside `value`
+    recs, gms = eng.records(), eng.games()
+    torch.cuda.synchronize()
+    tg = time.perf_counter()
+    if world > 1:
+        recs_all, gms_all = gather_experience(recs, gms)
+    else:
+        recs_all, gms_all = recs, gms
+    gather_ms = (time.perf_counter() - tg) * 1e3
+    mean_len = float(gms_all["plies"].mean()) if len(gms_all) else float("nan")
+
+    # roofline of the dominant kernel (residual 3x3 conv), HIP events on the engine stream
+    launches = max(d["res_conv_launches"], 1)
+    rows_per_launch = (nn_rows / world) / max(steps, 1) if not mcts else G
+    conv_ms = d["res_conv_ms"] / launches
+    achieved = FLOP_RES_CONV_PER_BOARD * rows_per_launch / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
+    traffic = None
+    pmc = os.path.join(HERE, "profiles", "r01_pmc_resconv.json")
+    if os.path.exists(pmc):
+        traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+    eng.close()
+
+    if rank == 0:
+        if mcts:
+            metric, unit, value = "MCTS simulations/sec + self-play games/hour", "sims/s", sims_done / dt
+        else:
+            metric, unit, value = "self-play plies/sec + games/hour (reference move selection, sims=0)", \
+                "plies/s", plies / dt
+        games_per_hour = plies / dt * 3600.0 / mean_len if mean_len == mean_len and mean_len > 0 else None
+        out = {
+            "metric": metric, "value": value, "unit": unit, "n_gpus": world, "steps": steps, "warmup": warmup,
+            "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32", "data": "synthetic (random-init weights seed 42, self-play from the start position)",
+            "config": {"workload": f"{G} concurrent games/GPU, {'%d sims/move' % sims if mcts else 'reference sampled move (sims=0)'}, "
+                                   f"batch-{G} NN eval, faithful one-eval-per-position",
+                       "slots_per_gpu": G, "sims_per_move": sims, "nn_batch": G, "parallelism": f"games sharded x{world}"},
+            "plies_per_s": plies / dt, "games_per_hour": games_per_hour, "mean_plies_per_game": mean_len,
+            "games_completed": games_done, "nn_evals_per_s": nn_rows / dt,
+            "nn_tflops": nn_rows * FLOP_PER_EVAL / dt / 1e12, "gather_ms": gather_ms,
+            "records_gathered": int(len(recs_all)),
+            "roofline": {"bound": "mfma", "kernel": "conv3x3_kernel<512,32> (residual tower)",
+                         "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None,
+                         "traffic": traffic, "avg_launch_ms": conv_ms, "rows_per_launch": rows_per_launch},
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, sims)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -69,6 +69,7 @@ void kv_net_destroy(kv_net* net);
 
 #define KV_EVAL_FAITHFUL 0 /* every board evaluated once, as the reference does */
 #define KV_EVAL_LAZY 1     /* only the rows the schedule consumes are evaluated */
+#define KV_EVAL_HASH 2     /* TEST ONLY: uniform logits + hash value instead of the network */
 
 typedef struct {
     int device;

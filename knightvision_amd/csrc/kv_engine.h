@@ -1,0 +1,256 @@
+// Shared device state of the self-play engine (kv_engine.hip: reference
+// move selection; kv_mcts.hip: PUCT search).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "kv_common.h"
+#include "kv_movegen.h"
+#include "kv_rng.h"
+
+#pragma clang fp contract(off)
+
+namespace kv {
+
+int net_forward_boards_internal(kv_net* net, const int8_t* boards_dev, int B, float* policy, float* value,
+                                hipStream_t st);
+int net_set_res_events(kv_net* net, hipEvent_t a, hipEvent_t b);
+
+enum : int { ST_IDLE = 0, ST_ACTIVE = 1, ST_FINISHED = 2 };
+enum : int { END_NONE = 0, END_NOMOVES = 1, END_DRAW = 2, END_RESIGN = 3, END_MAXED = 4 };
+
+struct Slot {
+    long long game_id;
+    int status;
+    int ply;
+    int wtm, wkr, wkc, bkr, bkc, flags, ep;
+    int nmoves;
+    int buf;
+    int has_last;
+    float last_value;
+    int consumed;
+    int need_flush;
+    int n_evals;
+    int end_kind;
+    int outcome;
+    int reason;
+    int pad[11];
+};
+static_assert(sizeof(Slot) == 128, "slot is one cache line");
+
+struct Ctr {
+    unsigned long long rec_count;
+    unsigned long long games_count;
+    unsigned long long next_game;
+    unsigned long long plies;
+    unsigned long long nn_rows;
+    unsigned long long sims;
+    int active;
+    int error;
+};
+
+struct DevCfg {
+    int slots;
+    long long n_games;
+    long long id_base, id_stride;
+    unsigned long long seed;
+    int seed_mode;
+    int max_moves;
+    int batch;
+    double eps, alpha;
+    long long record_cap;
+    int recycle;
+    int rows;  // NN rows per step (slots, or 2*slots with flush rows)
+    long long games_cap;  // game-record ring capacity
+    int sims;             // 0: reference move selection; >0: PUCT search
+    int eval_mode;        // KV_EVAL_*
+};
+
+__device__ inline Pos slot_pos(const Slot& s, const int8_t* board) {
+    Pos p;
+    pos_from_board(p, board, s.wtm, s.wkr, s.wkc, s.bkr, s.bkc, s.flags, s.ep);
+    return p;
+}
+
+__device__ inline void slot_store_pos(Slot& s, int8_t* board, const Pos& p) {
+    pos_to_board(p, board);
+    s.wtm = p.wtm;
+    s.wkr = p.kr[0]; s.wkc = p.kc[0]; s.bkr = p.kr[1]; s.bkc = p.kc[1];
+    s.flags = p.flags;
+    s.ep = p.ep;
+}
+
+
+struct MctsSlot {  // per-slot search scratch (kv_mcts.hip)
+    int node_count;
+    int edge_count;
+    int path_len;
+    int leaf_edge;
+    int leaf_pending;  // 1: the leaf row is in this step's network batch
+    int leaf_n;
+    int leaf_wtm;
+    float leaf_value;  // terminal value (white perspective) when !leaf_pending
+    float root_value;
+    int root_wtm;
+    int overflow;
+    int pad[5];
+};
+
+struct Tree {  // per-slot SoA node / edge pools, slot i at i*ecap / i*ncap
+    uint16_t* e_move;
+    float* e_P;
+    int* e_N;
+    float* e_W;
+    int* e_child;
+    int* n_first;
+    int* n_cnt;
+    int* n_N;
+    int* path;        // [slot][ncap]
+    uint16_t* leaf_moves;  // [slot][MAXM]
+    MctsSlot* ms;
+    const float* sqrt_tab;  // (float)sqrt((double)n), n < ncap + 2
+    int ecap, ncap;
+    float c_puct;
+    int sims;
+};
+
+__device__ inline float wave_max(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
+    return v;
+}
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+    return v;
+}
+
+// torch.softmax over 4096 fp32 logits (self_play.py:150): max, exp(x-max),
+// sum, x * (1/sum)
+__device__ void wave_softmax_4096(const float* lg, float* out, int lane) {
+    float v[64];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        v[j] = lg[j * 64 + lane];
+        m = fmaxf(m, v[j]);
+    }
+    m = wave_max(m);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        v[j] = expf(v[j] - m);
+        s += v[j];
+    }
+    s = wave_sum(s);
+    const float inv = 1.0f / s;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) out[j * 64 + lane] = v[j] * inv;
+}
+
+
+// mixed legal weights of the reference (self_play.py:147-160) for a slot's
+// move list: (1-eps)*softmax [fp32] + eps*dirichlet [fp64], in list order.
+// Consumes the slot's numpy stream exactly as np.random.dirichlet does.
+__device__ inline void mixed_legal_weights(const DevCfg& cfg, const float* lp, const uint16_t* ml, int n,
+                                           double* gam_slot, uint32_t* np_state, uint32_t* mt_a, uint32_t* mt_b,
+                                           double* vals, int lane) {
+    WaveMT w;
+    wmt_load(w, np_state, mt_a, mt_b, lane);
+    long long att;
+    const double acc = wave_dirichlet_gamma(w, cfg.alpha, 4096, gam_slot, &att, lane);
+    wmt_store(w, np_state, lane);
+    const double invacc = 1 / acc;
+    __syncthreads();
+    const float keep = (float)(1.0 - cfg.eps);
+    for (int j = lane; j < n; j += 64) {
+        const int mv = ml[j];
+        const int idx = (mv & 63) * 64 + ((mv >> 6) & 63);
+        const float p32 = keep * lp[idx];
+        const double noise = gam_slot[idx] * invacc;
+        vals[j] = (double)p32 + cfg.eps * noise;
+    }
+    __syncthreads();
+}
+
+// random.choices(population, weights) / random.choice when the total is 0
+// (self_play.py:162-167, CPython random.py:506-541). Lane 0 only.
+__device__ inline int choose_weighted(const double* vals, double* cum, int n, uint32_t* py) {
+    double total = 0.0;
+    for (int j = 0; j < n; ++j) total = total + vals[j];
+    if (total == 0.0) return mt_randbelow_serial(py, n);
+    double c = 0.0;
+    for (int j = 0; j < n; ++j) {
+        c = c + vals[j] / total;
+        cum[j] = c;
+    }
+    const double tot = cum[n - 1] + 0.0;
+    const double x = mt_random_serial(py) * tot;
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (x < cum[mid]) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
+// record the position + move, makeMove, then the reference's termination
+// checks in order: isDraw (:180), resign (:185, `value` is the row the move
+// was chosen with), max_moves (:196). All lanes of the slot's wave.
+__device__ inline void commit_move(const DevCfg& cfg, Slot& s, int i, int mv, int8_t* boards, kv_record* rec,
+                                   int8_t* last_board, Ctr* ctr, int lane) {
+    int8_t* board = boards + (size_t)i * 64;
+    const unsigned long long r = lane == 0 ? atomicAdd(&ctr->rec_count, 1ull) : 0ull;
+    const unsigned long long ridx = __shfl(r, 0);
+    const int8_t sq = board[lane];
+    last_board[(size_t)i * 64 + lane] = sq;
+    if ((long long)ridx < cfg.record_cap) {
+        rec[ridx].board[lane] = sq;
+        if (lane == 0) {
+            rec[ridx].game_id = s.game_id;
+            rec[ridx].ply = s.ply;
+            rec[ridx].move = (uint16_t)((mv & 63) * 64 + ((mv >> 6) & 63));
+            rec[ridx].pad = 0;
+        }
+    } else if (lane == 0) {
+        atomicOr(&ctr->error, 2);
+    }
+    __syncthreads();
+    if (lane == 0) {
+        make_move_board(board, s.wtm, s.wkr, s.wkc, s.bkr, s.bkc, s.flags, s.ep, mv);
+        s.ply += 1;
+        atomicAdd(&ctr->plies, 1ull);
+    }
+    __syncthreads();
+    const int8_t b2 = board[lane];
+    const bool non_king = b2 != 0 && b2 != 1 && b2 != 7;
+    const bool draw = __ballot(non_king) == 0ull;
+    if (lane == 0) {
+        if (draw) {
+            s.end_kind = END_DRAW;
+        } else if (s.ply > 15 && (double)s.last_value < -0.7) {
+            s.end_kind = END_RESIGN;
+            s.outcome = s.wtm ? -1 : 1;
+            s.reason = 1;
+        } else if (cfg.max_moves > 0 && s.ply >= cfg.max_moves) {
+            s.end_kind = END_MAXED;
+        }
+        if (s.end_kind != END_NONE) s.status = ST_FINISHED;
+        s.consumed = 0;
+    }
+}
+
+// MCTS launches (kv_mcts.hip), all on `st`
+int mcts_root(const DevCfg& cfg, const Tree& t, Slot* slots, const uint16_t* moves, const float* logits,
+              const float* values, float* probs_scratch, double* gam, uint32_t* np_mt, hipStream_t st);
+int mcts_select(const DevCfg& cfg, const Tree& t, const Slot* slots, const int8_t* boards, int8_t* nn_boards,
+                Ctr* ctr, hipStream_t st);
+int mcts_backup(const DevCfg& cfg, const Tree& t, const Slot* slots, const float* logits, const float* values,
+                float* probs, Ctr* ctr, hipStream_t st);
+int mcts_choose(const DevCfg& cfg, const Tree& t, Slot* slots, int8_t* boards, uint32_t* py_mt, kv_record* rec,
+                int8_t* last_board, Ctr* ctr, hipStream_t st);
+int hash_eval(const int8_t* boards, int rows, float* logits, float* values, hipStream_t st);
+
+}  // namespace kv

@@ -27,76 +27,11 @@
 #include "kv_common.h"
 #include "kv_movegen.h"
 #include "kv_rng.h"
+#include "kv_engine.h"
 
 #pragma clang fp contract(off)
 
 namespace kv {
-
-int net_forward_boards_internal(kv_net* net, const int8_t* boards_dev, int B, float* policy, float* value,
-                                hipStream_t st);
-int net_set_res_events(kv_net* net, hipEvent_t a, hipEvent_t b);
-
-enum : int { ST_IDLE = 0, ST_ACTIVE = 1, ST_FINISHED = 2 };
-enum : int { END_NONE = 0, END_NOMOVES = 1, END_DRAW = 2, END_RESIGN = 3, END_MAXED = 4 };
-
-struct Slot {
-    long long game_id;
-    int status;
-    int ply;
-    int wtm, wkr, wkc, bkr, bkc, flags, ep;
-    int nmoves;
-    int buf;
-    int has_last;
-    float last_value;
-    int consumed;
-    int need_flush;
-    int n_evals;
-    int end_kind;
-    int outcome;
-    int reason;
-    int pad[11];
-};
-static_assert(sizeof(Slot) == 128, "slot is one cache line");
-
-struct Ctr {
-    unsigned long long rec_count;
-    unsigned long long games_count;
-    unsigned long long next_game;
-    unsigned long long plies;
-    unsigned long long nn_rows;
-    unsigned long long sims;
-    int active;
-    int error;
-};
-
-struct DevCfg {
-    int slots;
-    long long n_games;
-    long long id_base, id_stride;
-    unsigned long long seed;
-    int seed_mode;
-    int max_moves;
-    int batch;
-    double eps, alpha;
-    long long record_cap;
-    int recycle;
-    int rows;  // NN rows per step (slots, or 2*slots with flush rows)
-    long long games_cap;  // game-record ring capacity
-};
-
-__device__ inline Pos slot_pos(const Slot& s, const int8_t* board) {
-    Pos p;
-    pos_from_board(p, board, s.wtm, s.wkr, s.wkc, s.bkr, s.bkc, s.flags, s.ep);
-    return p;
-}
-
-__device__ inline void slot_store_pos(Slot& s, int8_t* board, const Pos& p) {
-    pos_to_board(p, board);
-    s.wtm = p.wtm;
-    s.wkr = p.kr[0]; s.wkc = p.kc[0]; s.bkr = p.kr[1]; s.bkc = p.kc[1];
-    s.flags = p.flags;
-    s.ep = p.ep;
-}
 
 __constant__ const int8_t kStart[64] = {9, 11, 10, 8, 7, 10, 11, 9, 12, 12, 12, 12, 12, 12, 12, 12,
                                         0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
@@ -176,40 +111,6 @@ __global__ __launch_bounds__(64) void k_movegen(DevCfg cfg, Slot* slots, int8_t*
 }
 
 // ------------------------------------------------------------- sample ----
-__device__ inline float wave_max(float v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
-    return v;
-}
-__device__ inline float wave_sum(float v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
-    return v;
-}
-
-// torch.softmax over 4096 fp32 logits (self_play.py:150): max, exp(x-max),
-// sum, x * (1/sum)
-__device__ void wave_softmax_4096(const float* lg, float* out, int lane) {
-    float v[64];
-    float m = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < 64; ++j) {
-        v[j] = lg[j * 64 + lane];
-        m = fmaxf(m, v[j]);
-    }
-    m = wave_max(m);
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < 64; ++j) {
-        v[j] = expf(v[j] - m);
-        s += v[j];
-    }
-    s = wave_sum(s);
-    const float inv = 1.0f / s;
-#pragma unroll
-    for (int j = 0; j < 64; ++j) out[j * 64 + lane] = v[j] * inv;
-}
-
 __global__ __launch_bounds__(64) void k_sample(DevCfg cfg, Slot* slots, int8_t* boards, const uint16_t* moves,
                                                const float* logits, const float* values, float* last_probs,
                                                double* gam, uint32_t* np_mt, uint32_t* py_mt, kv_record* rec,
@@ -228,7 +129,7 @@ __global__ __launch_bounds__(64) void k_sample(DevCfg cfg, Slot* slots, int8_t* 
         s.has_last = 1;
         s.need_flush = 0;
     }
-    if (s.consumed) {
+    if (s.consumed) {  // policy/value = _last_outputs[...][-1] (:147-150)
         wave_softmax_4096(logits + (size_t)i * 4096, lp, lane);
         s.last_value = values[i];
         s.has_last = 1;
@@ -236,97 +137,14 @@ __global__ __launch_bounds__(64) void k_sample(DevCfg cfg, Slot* slots, int8_t* 
         s.n_evals += 1;
     }
     __syncthreads();
-    // noise = np.random.dirichlet([ALPHA] * 4096) (:153)
-    WaveMT w;
-    wmt_load(w, np_mt + (size_t)i * MT_WORDS, mt_a, mt_b, lane);
-    double* g = gam + (size_t)i * 4096;
-    long long att;
-    const double acc = wave_dirichlet_gamma(w, cfg.alpha, 4096, g, &att, lane);
-    wmt_store(w, np_mt + (size_t)i * MT_WORDS, lane);
-    const double invacc = 1 / acc;
-    __syncthreads();
-    // policy = (1-eps)*policy [fp32] + eps*noise [fp64]; legal_probs in list order (:154-160)
-    const float keep = (float)(1.0 - cfg.eps);
     const int n = s.nmoves;
     const uint16_t* ml = moves + (size_t)i * MAXM;
-    for (int j = lane; j < n; j += 64) {
-        const int mv = ml[j];
-        const int idx = (mv & 63) * 64 + ((mv >> 6) & 63);
-        const float p32 = keep * lp[idx];
-        const double noise = g[idx] * invacc;
-        vals[j] = (double)p32 + cfg.eps * noise;
-    }
+    mixed_legal_weights(cfg, lp, ml, n, gam + (size_t)i * 4096, np_mt + (size_t)i * MT_WORDS, mt_a, mt_b, vals,
+                        lane);
+    if (lane == 0) s_pick = choose_weighted(vals, cum, n, py_mt + (size_t)i * MT_WORDS);
     __syncthreads();
-    if (lane == 0) {
-        uint32_t* py = py_mt + (size_t)i * MT_WORDS;
-        double total = 0.0;
-        for (int j = 0; j < n; ++j) total = total + vals[j];
-        int pick;
-        if (total == 0.0) {
-            pick = mt_randbelow_serial(py, n);  // random.choice (:164)
-        } else {  // random.choices(valid_moves, weights=normalized) (:166-167)
-            double c = 0.0;
-            for (int j = 0; j < n; ++j) {
-                c = c + vals[j] / total;
-                cum[j] = c;
-            }
-            const double tot = cum[n - 1] + 0.0;
-            const double x = mt_random_serial(py) * tot;
-            int lo = 0, hi = n - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (x < cum[mid]) hi = mid;
-                else lo = mid + 1;
-            }
-            pick = lo;
-        }
-        s_pick = pick;
-    }
-    __syncthreads();
-    const int mv = ml[s_pick];
-    int8_t* board = boards + (size_t)i * 64;
-    // record (encode_board(gs.board), move_index) before the move (:173-174)
-    const unsigned long long r = lane == 0 ? atomicAdd(&ctr->rec_count, 1ull) : 0ull;
-    const unsigned long long ridx = __shfl(r, 0);
-    const int8_t sq = board[lane];
-    last_board[(size_t)i * 64 + lane] = sq;
-    if ((long long)ridx < cfg.record_cap) {
-        rec[ridx].board[lane] = sq;
-        if (lane == 0) {
-            rec[ridx].game_id = s.game_id;
-            rec[ridx].ply = s.ply;
-            rec[ridx].move = (uint16_t)((mv & 63) * 64 + ((mv >> 6) & 63));
-            rec[ridx].pad = 0;
-        }
-    } else if (lane == 0) {
-        atomicOr(&ctr->error, 2);
-    }
-    __syncthreads();
-    if (lane == 0) {
-        make_move_board(board, s.wtm, s.wkr, s.wkc, s.bkr, s.bkc, s.flags, s.ep, mv);
-        s.ply += 1;
-        atomicAdd(&ctr->plies, 1ull);
-    }
-    __syncthreads();
-    const int8_t b2 = board[lane];
-    const bool non_king = b2 != 0 && b2 != 1 && b2 != 7;
-    const bool draw = __ballot(non_king) == 0ull;
-    if (lane == 0) {
-        // termination order: isDraw (:180), resign (:185), max_moves (:196)
-        const int wtm = s.wtm;
-        if (draw) {
-            s.end_kind = END_DRAW;
-        } else if (s.ply > 15 && (double)s.last_value < -0.7) {
-            s.end_kind = END_RESIGN;
-            s.outcome = wtm ? -1 : 1;
-            s.reason = 1;
-        } else if (cfg.max_moves > 0 && s.ply >= cfg.max_moves) {
-            s.end_kind = END_MAXED;
-        }
-        if (s.end_kind != END_NONE) s.status = ST_FINISHED;
-        s.consumed = 0;
-        slots[i] = s;
-    }
+    commit_move(cfg, s, i, ml[s_pick], boards, rec, last_board, ctr, lane);
+    if (lane == 0) slots[i] = s;
 }
 
 // ------------------------------------------------------------- finish ----
@@ -369,7 +187,7 @@ __global__ __launch_bounds__(64) void k_finish(DevCfg cfg, Slot* slots, int8_t* 
         slot_store_pos(s, board, p);
     }
     // flush of a non-empty buffer (:202-208): one more forward call
-    if (s.buf > 0) {
+    if (cfg.sims == 0 && s.buf > 0) {
         s.n_evals += 1;
         if (cfg.seed_mode == KV_SEED_SEQUENTIAL) s.need_flush = 1;
     }
@@ -430,6 +248,12 @@ struct kv_engine {
     double nn_res_ms = 0;
     long long nn_res_launches = 0;
     bool loaded = false;
+    // MCTS (sims > 0)
+    kv::Tree tree;
+    kv::MctsSlot* ms = nullptr;
+    int8_t* nn_boards = nullptr;
+    float* probs = nullptr;
+    float* sqrt_tab = nullptr;
 };
 
 static int eng_counters(kv_engine* e) {
@@ -467,7 +291,11 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
                "kv_create: bad seed_mode");
     KV_REQUIRE(cfg->seed_mode != KV_SEED_SEQUENTIAL || cfg->slots == 1, KV_EINVAL,
                "kv_create: sequential seeding plays games in order on one slot");
-    KV_REQUIRE(cfg->sims == 0, KV_EINVAL, "kv_create: MCTS mode (sims > 0) not available in this build");
+    KV_REQUIRE(cfg->sims >= 0 && cfg->sims <= 100000, KV_EINVAL, "kv_create: sims out of range");
+    KV_REQUIRE(cfg->sims == 0 || cfg->seed_mode == KV_SEED_PER_GAME, KV_EINVAL,
+               "kv_create: MCTS mode uses per-game seeding");
+    KV_REQUIRE(cfg->eval_mode == KV_EVAL_FAITHFUL || cfg->eval_mode == KV_EVAL_HASH, KV_EINVAL,
+               "kv_create: eval_mode %d not available", cfg->eval_mode);
     KV_HIP(hipSetDevice(cfg->device));
     kv_engine* e = new kv_engine();
     e->cfg = *cfg;
@@ -488,6 +316,8 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
     d.recycle = cfg->recycle;
     d.rows = cfg->seed_mode == KV_SEED_SEQUENTIAL ? 2 * cfg->slots : cfg->slots;
     d.games_cap = std::max<long long>(1, std::min<long long>(cfg->n_games, 1 << 20));
+    d.sims = cfg->sims;
+    d.eval_mode = cfg->eval_mode;
     const size_t S = (size_t)cfg->slots, R = (size_t)d.rows;
     int rc = KV_OK;
 #define ALLOC(ptr, bytes)                                   \
@@ -512,6 +342,38 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
     ALLOC(e->games, (size_t)d.games_cap * sizeof(kv_game));
     ALLOC(e->last_board, S * 64);
     ALLOC(e->ctr, sizeof(kv::Ctr));
+    if (cfg->sims > 0) {
+        kv::Tree& t = e->tree;
+        t.ncap = cfg->sims + 2;
+        t.ecap = 48 * (cfg->sims + 1) + kv::MAXM;
+        t.c_puct = cfg->c_puct > 0.f ? cfg->c_puct : 1.5f;
+        t.sims = cfg->sims;
+        const size_t E = S * (size_t)t.ecap, N = S * (size_t)t.ncap;
+        ALLOC(t.e_move, E * sizeof(uint16_t));
+        ALLOC(t.e_P, E * sizeof(float));
+        ALLOC(t.e_N, E * sizeof(int));
+        ALLOC(t.e_W, E * sizeof(float));
+        ALLOC(t.e_child, E * sizeof(int));
+        ALLOC(t.n_first, N * sizeof(int));
+        ALLOC(t.n_cnt, N * sizeof(int));
+        ALLOC(t.n_N, N * sizeof(int));
+        ALLOC(t.path, N * sizeof(int));
+        ALLOC(t.leaf_moves, S * kv::MAXM * sizeof(uint16_t));
+        ALLOC(e->ms, S * sizeof(kv::MctsSlot));
+        ALLOC(e->nn_boards, S * 64);
+        ALLOC(e->probs, S * 4096 * sizeof(float));
+        ALLOC(e->sqrt_tab, (size_t)(t.ncap + 2) * sizeof(float));
+        t.ms = e->ms;
+        std::vector<float> sq(t.ncap + 2);
+        for (int k = 0; k < t.ncap + 2; ++k) sq[k] = (float)sqrt((double)k);
+        if (hipMemcpy(e->sqrt_tab, sq.data(), sq.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+            kv_destroy(e);
+            kv::set_error("kv_create: sqrt table copy");
+            return KV_EHIP;
+        }
+        t.sqrt_tab = e->sqrt_tab;
+        (void)hipMemset(e->ms, 0, S * sizeof(kv::MctsSlot));
+    }
 #undef ALLOC
     if (hipHostMalloc(&e->ctr_host, sizeof(kv::Ctr)) != hipSuccess) {
         kv_destroy(e);
@@ -556,12 +418,31 @@ int kv_set_max_moves(kv_engine* e, int max_moves) {
     return KV_OK;
 }
 
+// one network pass over `rows` boards (or the hash test evaluator), with the
+// residual-tower section bracketed by HIP events for the roofline
+static int eng_eval(kv_engine* e, const int8_t* boards, int rows) {
+    if (e->dc.eval_mode == KV_EVAL_HASH) return kv::hash_eval(boards, rows, e->logits, e->values, e->st);
+    if ((size_t)e->n_ev_used + 2 > e->ev.size()) {
+        for (int k = 0; k < 2; ++k) {
+            hipEvent_t x;
+            KV_HIP(hipEventCreate(&x));
+            e->ev.push_back(x);
+        }
+    }
+    kv::net_set_res_events(e->net, e->ev[e->n_ev_used], e->ev[e->n_ev_used + 1]);
+    e->n_ev_used += 2;
+    const int rc = kv::net_forward_boards_internal(e->net, boards, rows, e->logits, e->values, e->st);
+    kv::net_set_res_events(e->net, nullptr, nullptr);
+    return rc;
+}
+
 int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
     KV_REQUIRE(e && e->loaded, KV_EINVAL, "kv_run: engine has no weights");
     KV_HIP(hipSetDevice(e->cfg.device));
     const auto t0 = std::chrono::steady_clock::now();
     const int S = e->cfg.slots;
-    const int check_every = (S >= 64 && stop_after_games < 0) ? 4 : 1;
+    const bool mcts = e->dc.sims > 0;
+    const int check_every = (S >= 64 && stop_after_games < 0 && !mcts) ? 4 : 1;
     int rc = eng_counters(e);
     if (rc) return rc;
     long long done = 0;
@@ -573,23 +454,27 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
         if (e->dc.rows > S)
             hipLaunchKernelGGL(kv::k_flush_rows, dim3(S), dim3(64), 0, e->st, e->dc, e->slots, e->last_board,
                                e->boards);
-        // residual-conv section timing (HIP events on the engine stream)
-        if ((size_t)e->n_ev_used + 2 > e->ev.size()) {
-            for (int k = 0; k < 2; ++k) {
-                hipEvent_t x;
-                KV_HIP(hipEventCreate(&x));
-                e->ev.push_back(x);
+        if ((rc = eng_eval(e, e->boards, e->dc.rows))) return rc;
+        if (!mcts) {
+            hipLaunchKernelGGL(kv::k_sample, dim3(S), dim3(64), 0, e->st, e->dc, e->slots, e->boards, e->moves,
+                               e->logits, e->values, e->last_probs, e->gam, e->np_mt, e->py_mt, e->rec,
+                               e->last_board, e->ctr);
+            KV_HIP(hipGetLastError());
+        } else {
+            const kv::Tree& t = e->tree;
+            if ((rc = kv::mcts_root(e->dc, t, e->slots, e->moves, e->logits, e->values, e->probs, e->gam, e->np_mt,
+                                    e->st)))
+                return rc;
+            for (int k = 0; k < e->dc.sims; ++k) {
+                if ((rc = kv::mcts_select(e->dc, t, e->slots, e->boards, e->nn_boards, e->ctr, e->st))) return rc;
+                if ((rc = eng_eval(e, e->nn_boards, S))) return rc;
+                if ((rc = kv::mcts_backup(e->dc, t, e->slots, e->logits, e->values, e->probs, e->ctr, e->st)))
+                    return rc;
             }
+            if ((rc = kv::mcts_choose(e->dc, t, e->slots, e->boards, e->py_mt, e->rec, e->last_board, e->ctr,
+                                      e->st)))
+                return rc;
         }
-        kv::net_set_res_events(e->net, e->ev[e->n_ev_used], e->ev[e->n_ev_used + 1]);
-        e->n_ev_used += 2;
-        if ((rc = kv::net_forward_boards_internal(e->net, e->boards, e->dc.rows, e->logits, e->values, e->st)))
-            return rc;
-        kv::net_set_res_events(e->net, nullptr, nullptr);
-        hipLaunchKernelGGL(kv::k_sample, dim3(S), dim3(64), 0, e->st, e->dc, e->slots, e->boards, e->moves,
-                           e->logits, e->values, e->last_probs, e->gam, e->np_mt, e->py_mt, e->rec, e->last_board,
-                           e->ctr);
-        KV_HIP(hipGetLastError());
         KV_HIP(hipMemsetAsync(&e->ctr->active, 0, sizeof(int), e->st));
         hipLaunchKernelGGL(kv::k_finish, dim3((S + 63) / 64), dim3(64), 0, e->st, e->dc, e->slots, e->boards,
                            e->moves, e->np_mt, e->py_mt, e->games, e->ctr);
@@ -668,8 +553,11 @@ void kv_destroy(kv_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->cfg.device);
     if (e->st) (void)hipStreamSynchronize(e->st);
+    kv::Tree& t = e->tree;
     void* bufs[] = {e->slots, e->boards, e->moves, e->logits, e->values, e->last_probs, e->gam,
-                    e->np_mt, e->py_mt, e->rec, e->games, e->last_board, e->ctr};
+                    e->np_mt, e->py_mt, e->rec, e->games, e->last_board, e->ctr,
+                    t.e_move, t.e_P, t.e_N, t.e_W, t.e_child, t.n_first, t.n_cnt, t.n_N, t.path,
+                    t.leaf_moves, e->ms, e->nn_boards, e->probs, e->sqrt_tab};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (e->ctr_host) (void)hipHostFree(e->ctr_host);

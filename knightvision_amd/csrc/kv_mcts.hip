@@ -1,0 +1,324 @@
+// PUCT Monte-Carlo tree search on MI355X (no reference counterpart: the
+// reference samples moves from the network policy, self_play.py:150-167; the
+// semantics below are build-defined and restated on the CPU in
+// oracle/kv_oracle.c kvo_mcts_*). One wavefront per concurrent game.
+//
+// Per move of each game slot:
+//   root   : network row of the position; priors = the reference's own mixed
+//            move distribution (softmax x (1-eps) + Dirichlet x eps over the
+//            legal list, normalised; self_play.py:147-166), so the numpy
+//            stream is consumed exactly as in the reference; node 0 created.
+//   sims x : select (PUCT from the root: Q + c_puct * P * sqrt(N_parent) /
+//            (1 + N_child), Q = W/N or 0, first maximum in move-list order) ->
+//            apply the path's moves to the slot's board -> leaf = first edge
+//            with no child: isDraw => value 0; no legal moves => mate (-1 for
+//            the side to move) or stalemate 0; else the leaf board joins this
+//            step's network batch (one row per slot) -> backup: priors =
+//            softmax restricted to the legal list and renormalised, node
+//            created, N += 1 and W += value from the mover's side along the
+//            path (the value head is white-perspective, self_play.py:253).
+//   choose : random.choices over the root visit counts on the CPython stream
+//            (tau = 1), then makeMove / record / termination as the reference.
+// Tree: structure-of-arrays node and edge pools per slot in HBM
+// (move, P, N, W, child per edge; first edge, edge count, N per node).
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "kv_engine.h"
+
+#pragma clang fp contract(off)
+
+namespace kv {
+
+__device__ inline void wave_argmax_first(float& best, int& idx) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const float ob = __shfl_xor(best, m);
+        const int oi = __shfl_xor(idx, m);
+        if (ob > best || (ob == best && oi < idx)) {
+            best = ob;
+            idx = oi;
+        }
+    }
+}
+
+// PUCT score; identical op order in kvo_mcts (oracle), no contraction
+__device__ inline float puct(float c_puct, float P, float sq, int N, float W) {
+    const float u = c_puct * P * sq / (float)(1 + N);
+    const float q = N > 0 ? W / (float)N : 0.0f;
+    return q + u;
+}
+
+__global__ __launch_bounds__(64) void k_mcts_root(DevCfg cfg, Tree t, Slot* slots, const uint16_t* moves,
+                                                  const float* logits, const float* values, float* probs,
+                                                  double* gam, uint32_t* np_mt) {
+    __shared__ uint32_t mt_a[MT_N], mt_b[MT_N];
+    __shared__ double vals[MAXM];
+    const int i = blockIdx.x, lane = threadIdx.x;
+    Slot s = slots[i];
+    if (s.status != ST_ACTIVE) return;
+    float* lp = probs + (size_t)i * 4096;
+    wave_softmax_4096(logits + (size_t)i * 4096, lp, lane);
+    __syncthreads();
+    const int n = s.nmoves;
+    const uint16_t* ml = moves + (size_t)i * MAXM;
+    mixed_legal_weights(cfg, lp, ml, n, gam + (size_t)i * 4096, np_mt + (size_t)i * MT_WORDS, mt_a, mt_b, vals,
+                        lane);
+    __shared__ double s_total;
+    if (lane == 0) {
+        double total = 0.0;
+        for (int j = 0; j < n; ++j) total = total + vals[j];
+        s_total = total;
+    }
+    __syncthreads();
+    const double total = s_total;
+    const size_t eb = (size_t)i * t.ecap, nb = (size_t)i * t.ncap;
+    for (int j = lane; j < n; j += 64) {
+        t.e_move[eb + j] = ml[j];
+        t.e_P[eb + j] = total == 0.0 ? 1.0f / (float)n : (float)(vals[j] / total);
+        t.e_N[eb + j] = 0;
+        t.e_W[eb + j] = 0.f;
+        t.e_child[eb + j] = -1;
+    }
+    if (lane == 0) {
+        t.n_first[nb] = 0;
+        t.n_cnt[nb] = n;
+        t.n_N[nb] = 1;
+        MctsSlot m = t.ms[i];
+        m.node_count = 1;
+        m.edge_count = n;
+        m.root_value = values[i];
+        m.root_wtm = s.wtm;
+        m.path_len = 0;
+        m.leaf_pending = 0;
+        m.pad[0] = 1;  // network rows consumed this move
+        t.ms[i] = m;
+        slots[i].last_value = values[i];
+    }
+}
+
+__global__ __launch_bounds__(64) void k_mcts_select(DevCfg cfg, Tree t, const Slot* slots, const int8_t* boards,
+                                                    int8_t* nn_boards, Ctr* ctr) {
+    __shared__ int8_t bd[64];
+    __shared__ int s_meta[8];  // wtm wkr wkc bkr bkc flags ep
+    const int i = blockIdx.x, lane = threadIdx.x;
+    const Slot s = slots[i];
+    if (s.status != ST_ACTIVE) return;
+    bd[lane] = boards[(size_t)i * 64 + lane];
+    if (lane == 0) {
+        s_meta[0] = s.wtm; s_meta[1] = s.wkr; s_meta[2] = s.wkc; s_meta[3] = s.bkr; s_meta[4] = s.bkc;
+        s_meta[5] = s.flags; s_meta[6] = s.ep;
+    }
+    __syncthreads();
+    const size_t eb = (size_t)i * t.ecap, nb = (size_t)i * t.ncap;
+    int* path = t.path + nb;
+    int node = 0, depth = 0, leaf = -1;
+    for (;;) {
+        const int first = t.n_first[nb + node], cnt = t.n_cnt[nb + node];
+        const float sq = t.sqrt_tab[t.n_N[nb + node]];
+        float best = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int j = lane; j < cnt; j += 64) {
+            const size_t e = eb + first + j;
+            const float sc = puct(t.c_puct, t.e_P[e], sq, t.e_N[e], t.e_W[e]);
+            if (sc > best) {  // lanes see their edges in increasing j: strict > keeps the first
+                best = sc;
+                bi = j;
+            }
+        }
+        wave_argmax_first(best, bi);
+        const int e = first + bi;
+        if (lane == 0) {
+            path[depth] = e;
+            make_move_board(bd, s_meta[0], s_meta[1], s_meta[2], s_meta[3], s_meta[4], s_meta[5], s_meta[6],
+                            t.e_move[eb + e]);
+        }
+        ++depth;
+        __syncthreads();
+        const int child = t.e_child[eb + e];
+        if (child < 0 || depth >= t.ncap) {
+            leaf = e;
+            break;
+        }
+        node = child;
+    }
+    if (lane == 0) {
+        MctsSlot m = t.ms[i];
+        m.path_len = depth;
+        m.leaf_edge = leaf;
+        m.leaf_pending = 0;
+        m.leaf_n = 0;
+        m.leaf_value = 0.f;
+        if (is_draw_board(bd)) {  // GameState.isDraw after the move ends the game (self_play.py:180)
+            m.leaf_value = 0.f;
+        } else {
+            Pos p;
+            pos_from_board(p, bd, s_meta[0], s_meta[1], s_meta[2], s_meta[3], s_meta[4], s_meta[5], s_meta[6]);
+            MoveOut o{t.leaf_moves + (size_t)i * MAXM, 0, MAXM, 0};
+            const int n = valid_moves(p, o);
+            if (o.overflow) atomicOr(&ctr->error, 1);
+            m.leaf_wtm = p.wtm;
+            if (n == 0) {
+                m.leaf_value = in_check(p) ? (p.wtm ? -1.f : 1.f) : 0.f;  // mate / stalemate
+            } else {
+                pos_to_board(p, bd);  // the board the reference would encode (after getValidMoves)
+                m.leaf_pending = 1;
+                m.leaf_n = n < MAXM ? n : MAXM;
+                atomicAdd(&ctr->nn_rows, 1ull);
+            }
+        }
+        t.ms[i] = m;
+    }
+    __syncthreads();
+    nn_boards[(size_t)i * 64 + lane] = bd[lane];
+}
+
+__global__ __launch_bounds__(64) void k_mcts_backup(DevCfg cfg, Tree t, const Slot* slots, const float* logits,
+                                                    const float* values, float* probs, Ctr* ctr) {
+    __shared__ float pri[MAXM];
+    const int i = blockIdx.x, lane = threadIdx.x;
+    const Slot s = slots[i];
+    if (s.status != ST_ACTIVE) return;
+    MctsSlot m = t.ms[i];
+    const size_t eb = (size_t)i * t.ecap, nb = (size_t)i * t.ncap;
+    float v = m.leaf_value;
+    if (m.leaf_pending) {
+        v = values[i];
+        float* lp = probs + (size_t)i * 4096;
+        wave_softmax_4096(logits + (size_t)i * 4096, lp, lane);
+        __syncthreads();
+        const uint16_t* lm = t.leaf_moves + (size_t)i * MAXM;
+        const int n = m.leaf_n;
+        for (int j = lane; j < n; j += 64) {
+            const int mv = lm[j];
+            pri[j] = lp[(mv & 63) * 64 + ((mv >> 6) & 63)];
+        }
+        __syncthreads();
+        __shared__ float s_sum;
+        if (lane == 0) {
+            float sum = 0.f;
+            for (int j = 0; j < n; ++j) sum = sum + pri[j];
+            s_sum = sum;
+        }
+        __syncthreads();
+        const float sum = s_sum;
+        const bool fits = m.edge_count + n <= t.ecap && m.node_count < t.ncap;
+        if (fits) {
+            const int first = m.edge_count;
+            for (int j = lane; j < n; j += 64) {
+                const size_t e = eb + first + j;
+                t.e_move[e] = lm[j];
+                t.e_P[e] = sum > 0.f ? pri[j] / sum : 1.0f / (float)n;
+                t.e_N[e] = 0;
+                t.e_W[e] = 0.f;
+                t.e_child[e] = -1;
+            }
+        }
+        if (lane == 0) {
+            if (fits) {
+                const int id = m.node_count;
+                t.n_first[nb + id] = m.edge_count;
+                t.n_cnt[nb + id] = n;
+                t.n_N[nb + id] = 0;
+                t.e_child[eb + m.leaf_edge] = id;
+                m.node_count += 1;
+                m.edge_count += n;
+            } else {
+                m.overflow += 1;
+            }
+            m.pad[0] += 1;
+        }
+    }
+    if (lane == 0) {
+        // backup along the path: the mover at depth d is the root side flipped d times
+        const int* path = t.path + nb;
+        int node = 0;
+        t.n_N[nb + node] += 1;
+        for (int d = 0; d < m.path_len; ++d) {
+            const size_t e = eb + path[d];
+            const bool white_moved = ((m.root_wtm != 0) ^ (d & 1)) != 0;
+            t.e_N[e] += 1;
+            t.e_W[e] = t.e_W[e] + (white_moved ? v : -v);
+            node = t.e_child[e];
+            if (node >= 0) t.n_N[nb + node] += 1;
+        }
+        t.ms[i] = m;
+        atomicAdd(&ctr->sims, 1ull);
+    }
+}
+
+__global__ __launch_bounds__(64) void k_mcts_choose(DevCfg cfg, Tree t, Slot* slots, int8_t* boards,
+                                                    uint32_t* py_mt, kv_record* rec, int8_t* last_board, Ctr* ctr) {
+    __shared__ double vals[MAXM];
+    __shared__ double cum[MAXM];
+    __shared__ int s_pick;
+    const int i = blockIdx.x, lane = threadIdx.x;
+    Slot s = slots[i];
+    if (s.status != ST_ACTIVE) return;
+    const MctsSlot m = t.ms[i];
+    const size_t eb = (size_t)i * t.ecap, nb = (size_t)i * t.ncap;
+    const int n = t.n_cnt[nb];
+    for (int j = lane; j < n; j += 64) vals[j] = (double)t.e_N[eb + j];
+    __syncthreads();
+    if (lane == 0) s_pick = choose_weighted(vals, cum, n, py_mt + (size_t)i * MT_WORDS);
+    __syncthreads();
+    s.last_value = m.root_value;  // resign test on the root's network value (:185)
+    s.n_evals += m.pad[0];
+    commit_move(cfg, s, i, t.e_move[eb + s_pick], boards, rec, last_board, ctr, lane);
+    if (lane == 0) slots[i] = s;
+}
+
+// Test evaluator (KV_EVAL_HASH): all logits 0 (uniform priors, exact in
+// float), value = dyadic hash of the 64 board codes. Lets the CPU restatement
+// reproduce every PUCT score bit for bit.
+__global__ void k_hash_eval(const int8_t* boards, int rows, float* logits, float* values) {
+    const int r = blockIdx.x, lane = threadIdx.x;
+    if (r >= rows) return;
+    for (int j = lane; j < 4096; j += 64) logits[(size_t)r * 4096 + j] = 0.f;
+    if (lane == 0) {
+        uint32_t h = 2166136261u;
+        for (int q = 0; q < 64; ++q) {
+            h ^= (uint8_t)boards[(size_t)r * 64 + q];
+            h *= 16777619u;
+        }
+        values[r] = (float)((int)(h % 129u) - 64) / 64.0f;
+    }
+}
+
+int mcts_root(const DevCfg& cfg, const Tree& t, Slot* slots, const uint16_t* moves, const float* logits,
+              const float* values, float* probs, double* gam, uint32_t* np_mt, hipStream_t st) {
+    hipLaunchKernelGGL(k_mcts_root, dim3(cfg.slots), dim3(64), 0, st, cfg, t, slots, moves, logits, values, probs,
+                       gam, np_mt);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+int mcts_select(const DevCfg& cfg, const Tree& t, const Slot* slots, const int8_t* boards, int8_t* nn_boards,
+                Ctr* ctr, hipStream_t st) {
+    hipLaunchKernelGGL(k_mcts_select, dim3(cfg.slots), dim3(64), 0, st, cfg, t, slots, boards, nn_boards, ctr);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+int mcts_backup(const DevCfg& cfg, const Tree& t, const Slot* slots, const float* logits, const float* values,
+                float* probs, Ctr* ctr, hipStream_t st) {
+    hipLaunchKernelGGL(k_mcts_backup, dim3(cfg.slots), dim3(64), 0, st, cfg, t, slots, logits, values, probs, ctr);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+int mcts_choose(const DevCfg& cfg, const Tree& t, Slot* slots, int8_t* boards, uint32_t* py_mt, kv_record* rec,
+                int8_t* last_board, Ctr* ctr, hipStream_t st) {
+    hipLaunchKernelGGL(k_mcts_choose, dim3(cfg.slots), dim3(64), 0, st, cfg, t, slots, boards, py_mt, rec,
+                       last_board, ctr);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+int hash_eval(const int8_t* boards, int rows, float* logits, float* values, hipStream_t st) {
+    hipLaunchKernelGGL(k_hash_eval, dim3(rows), dim3(64), 0, st, boards, rows, logits, values);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+}  // namespace kv

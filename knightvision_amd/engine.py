@@ -10,7 +10,7 @@ from . import _lib
 from .weights import pack_weights, state_dict_to_numpy
 
 SEED_PER_GAME, SEED_SEQUENTIAL = 0, 1
-EVAL_FAITHFUL, EVAL_LAZY = 0, 1
+EVAL_FAITHFUL, EVAL_LAZY, EVAL_HASH = 0, 1, 2
 
 RECORD_DTYPE = np.dtype([("game_id", "<i8"), ("ply", "<i4"), ("move", "<u2"), ("pad", "<u2"),
                          ("board", "i1", (64,))])

@@ -756,3 +756,196 @@ int kvo_play_game(const kvo_game_cfg* cfg, MT* np_mt, MT* py_mt, kvo_eval_fn cb,
 /* expose struct sizes so the ctypes wrapper can allocate opaque blobs */
 int kvo_sizeof_mt(void) { return (int)sizeof(MT); }
 int kvo_sizeof_last(void) { return (int)sizeof(kvo_last); }
+
+/* ----------------------------------------------------------- MCTS ------
+ * CPU restatement of the build-defined PUCT search of
+ * knightvision_amd/csrc/kv_mcts.hip (no reference counterpart). Same
+ * capacities, same fp32 operation order (-ffp-contract=off), same RNG use:
+ * the root priors are the reference's mixed legal weights (self_play.py
+ * :147-166) normalised, the move is random.choices over root visit counts.
+ * eval_cb == NULL selects the hash test evaluator (all logits 0, value =
+ * dyadic FNV-1a hash of the 64 board codes), which is exact on both sides. */
+typedef struct {
+    int sims;
+    float c_puct;
+    int max_moves;
+    double eps, alpha;
+} kvo_mcts_cfg;
+
+static void hash_eval_board(const int8_t* b, float* logits, float* value) {
+    uint32_t h = 2166136261u;
+    for (int q = 0; q < 64; ++q) { h ^= (uint8_t)b[q]; h *= 16777619u; }
+    for (int j = 0; j < 4096; ++j) logits[j] = 0.f;
+    *value = (float)((int)(h % 129u) - 64) / 64.0f;
+}
+
+static void eval_one(kvo_eval_fn cb, void* ctx, const GS* g, float* logits, float* value) {
+    if (!cb) { hash_eval_board(g->b, logits, value); return; }
+    int8_t vec[80];
+    float planes[768];
+    gs_to_vec(g, vec);
+    kvo_encode_board(vec, planes);
+    cb(ctx, planes, 1, logits, value);
+}
+
+static float puct_score(float c_puct, float P, float sq, int N, float W) {
+    const float u = c_puct * P * sq / (float)(1 + N);
+    const float q = N > 0 ? W / (float)N : 0.0f;
+    return q + u;
+}
+
+static int choose_weighted_c(MT* py, const double* w, int n) {
+    double total = 0.0;
+    for (int j = 0; j < n; ++j) total = total + w[j];
+    if (total == 0.0) return kvo_randbelow(py, n);
+    double* nw = (double*)malloc(sizeof(double) * (size_t)n);
+    for (int j = 0; j < n; ++j) nw[j] = w[j] / total;
+    int k = kvo_choices(py, nw, n);
+    free(nw);
+    return k;
+}
+
+static void softmax_any(kvo_softmax_fn smx, void* ctx, const float* lg, float* pr) {
+    if (smx) smx(ctx, lg, pr);
+    else kvo_softmax_f32(lg, 4096, pr);
+}
+
+/* plays one game; rec_moves[ply], visits[ply * maxm + j] = root visit counts
+ * in root move-list order (maxm entries per ply, -1 padded). */
+int kvo_mcts_play_game(const kvo_mcts_cfg* cfg, MT* np_mt, MT* py_mt, kvo_eval_fn cb, kvo_softmax_fn smx, void* ctx,
+                       uint16_t* rec_moves, int cap, int32_t* visits, int maxm, kvo_game_result* res) {
+    const int S = cfg->sims, ncap = S + 2, ecap = 48 * (S + 1) + 320;
+    float* sqt = (float*)malloc(sizeof(float) * (size_t)(ncap + 2));
+    for (int k = 0; k < ncap + 2; ++k) sqt[k] = (float)sqrt((double)k);
+    Mv* e_mv = (Mv*)malloc(sizeof(Mv) * (size_t)ecap);
+    float* e_P = (float*)malloc(sizeof(float) * (size_t)ecap);
+    int* e_N = (int*)malloc(sizeof(int) * (size_t)ecap);
+    float* e_W = (float*)malloc(sizeof(float) * (size_t)ecap);
+    int* e_child = (int*)malloc(sizeof(int) * (size_t)ecap);
+    int* n_first = (int*)malloc(sizeof(int) * (size_t)ncap);
+    int* n_cnt = (int*)malloc(sizeof(int) * (size_t)ncap);
+    int* n_N = (int*)malloc(sizeof(int) * (size_t)ncap);
+    int* path = (int*)malloc(sizeof(int) * (size_t)ncap);
+    float* logits = (float*)malloc(sizeof(float) * 4096);
+    float* probs = (float*)malloc(sizeof(float) * 4096);
+    double* noise = (double*)malloc(sizeof(double) * 4096);
+    double* w = (double*)malloc(sizeof(double) * MAXMV);
+    static ML ml, lm;
+    GS g;
+    gs_init(&g);
+    int move_count = 0, outcome = 0, reason = -1, maxed = 0, resigned = 0, evals = 0;
+    for (;;) {
+        valid_moves(&g, &ml);
+        if (ml.n == 0) break;
+        float root_value;
+        eval_one(cb, ctx, &g, logits, &root_value);
+        evals++;
+        softmax_any(smx, ctx, logits, probs);
+        kvo_dirichlet(np_mt, cfg->alpha, 4096, noise);
+        const float keep = (float)(1.0 - cfg->eps);
+        double total = 0.0;
+        for (int i = 0; i < ml.n; i++) {
+            int idx = (ml.m[i].fr * 8 + ml.m[i].fc) * 64 + ml.m[i].tr * 8 + ml.m[i].tc;
+            float p32 = keep * probs[idx];
+            w[i] = (double)p32 + cfg->eps * noise[idx];
+            total = total + w[i];
+        }
+        const int root_wtm = g.wtm;
+        int node_count = 1, edge_count = ml.n;
+        n_first[0] = 0; n_cnt[0] = ml.n; n_N[0] = 1;
+        for (int i = 0; i < ml.n; i++) {
+            e_mv[i] = ml.m[i];
+            e_P[i] = total == 0.0 ? 1.0f / (float)ml.n : (float)(w[i] / total);
+            e_N[i] = 0; e_W[i] = 0.f; e_child[i] = -1;
+        }
+        for (int s = 0; s < S; ++s) {
+            GS b = g;
+            int node = 0, depth = 0, leaf = -1;
+            for (;;) {
+                const int first = n_first[node], cnt = n_cnt[node];
+                const float sq = sqt[n_N[node]];
+                float best = -INFINITY;
+                int bi = 0;
+                for (int j = 0; j < cnt; ++j) {
+                    const float sc = puct_score(cfg->c_puct, e_P[first + j], sq, e_N[first + j], e_W[first + j]);
+                    if (sc > best) { best = sc; bi = j; }
+                }
+                const int e = first + bi;
+                path[depth++] = e;
+                make_move(&b, &e_mv[e]);
+                const int child = e_child[e];
+                if (child < 0 || depth >= ncap) { leaf = e; break; }
+                node = child;
+            }
+            float v = 0.f;
+            if (!is_draw(&b)) {
+                valid_moves(&b, &lm);
+                if (lm.n == 0) {
+                    v = in_check(&b) ? (b.wtm ? -1.f : 1.f) : 0.f;
+                } else {
+                    eval_one(cb, ctx, &b, logits, &v);
+                    evals++;
+                    softmax_any(smx, ctx, logits, probs);
+                    float sum = 0.f;
+                    for (int j = 0; j < lm.n; ++j) {
+                        int idx = (lm.m[j].fr * 8 + lm.m[j].fc) * 64 + lm.m[j].tr * 8 + lm.m[j].tc;
+                        sum = sum + probs[idx];
+                    }
+                    if (edge_count + lm.n <= ecap && node_count < ncap) {
+                        const int id = node_count++;
+                        n_first[id] = edge_count; n_cnt[id] = lm.n; n_N[id] = 0;
+                        for (int j = 0; j < lm.n; ++j) {
+                            int idx = (lm.m[j].fr * 8 + lm.m[j].fc) * 64 + lm.m[j].tr * 8 + lm.m[j].tc;
+                            const int e = edge_count + j;
+                            e_mv[e] = lm.m[j];
+                            e_P[e] = sum > 0.f ? probs[idx] / sum : 1.0f / (float)lm.n;
+                            e_N[e] = 0; e_W[e] = 0.f; e_child[e] = -1;
+                        }
+                        edge_count += lm.n;
+                        e_child[leaf] = id;
+                    }
+                }
+            }
+            n_N[0] += 1;
+            for (int d = 0; d < depth; ++d) {
+                const int e = path[d];
+                const int white_moved = ((root_wtm != 0) ^ (d & 1)) != 0;
+                e_N[e] += 1;
+                e_W[e] = e_W[e] + (white_moved ? v : -v);
+                const int nd = e_child[e];
+                if (nd >= 0) n_N[nd] += 1;
+            }
+        }
+        for (int i = 0; i < ml.n; ++i) w[i] = (double)e_N[i];
+        if (visits && move_count < cap)
+            for (int j = 0; j < maxm; ++j) visits[(size_t)move_count * maxm + j] = j < ml.n ? e_N[j] : -1;
+        const int pick = choose_weighted_c(py_mt, w, ml.n);
+        const Mv m = ml.m[pick];
+        if (move_count < cap) rec_moves[move_count] = (uint16_t)((m.fr * 8 + m.fc) * 64 + m.tr * 8 + m.tc);
+        make_move(&g, &m);
+        move_count++;
+        if (is_draw(&g)) break;
+        if (move_count > 15 && (double)root_value < -0.7) { outcome = g.wtm ? -1 : 1; reason = 1; resigned = 1; break; }
+        if (cfg->max_moves > 0 && move_count >= cfg->max_moves) { maxed = 1; break; }
+    }
+    if (maxed) { outcome = 0; reason = 0; }
+    else if (!resigned) {
+        int chk = in_check(&g);
+        int mate = 0;
+        if (chk) { valid_moves(&g, &ml); mate = ml.n == 0; }
+        if (mate) { outcome = g.wtm ? -1 : 1; reason = 2; }
+        else {
+            valid_moves(&g, &ml);
+            if (ml.n == 0) { outcome = 0; reason = 3; }
+            else { outcome = 0; reason = is_draw(&g) ? 4 : 5; }
+        }
+    }
+    res->plies = move_count;
+    res->outcome = outcome;
+    res->reward = outcome == 1 ? 1.0f : (outcome == 0 ? 0.2f : -1.0f);
+    res->reason = reason;
+    res->n_evals = evals;
+    free(sqt); free(e_mv); free(e_P); free(e_N); free(e_W); free(e_child); free(n_first); free(n_cnt); free(n_N);
+    free(path); free(logits); free(probs); free(noise); free(w);
+    return move_count;
+}

@@ -172,3 +172,42 @@ def play_game(eval_fn, np_mt: MT, py_mt: MT, last: Last, max_moves=None, batch=1
                             C.byref(res))
     return dict(moves=moves[:n].copy(), states=states[:n].copy(), plies=res.plies, outcome=res.outcome,
                 reward=float(res.reward), reason=res.reason, eval_sizes=sizes[:res.n_evals].copy())
+
+
+class MctsCfg(C.Structure):
+    _fields_ = [("sims", C.c_int), ("c_puct", C.c_float), ("max_moves", C.c_int), ("eps", C.c_double),
+                ("alpha", C.c_double)]
+
+
+def mcts_play_game(sims, np_mt: MT, py_mt: MT, eval_fn=None, max_moves=None, c_puct=1.5, eps=0.25, alpha=0.3,
+                   softmax_fn=None, cap=2048, maxm=320):
+    """Restated PUCT self-play game (build-defined semantics, kv_mcts.hip).
+    eval_fn None = hash test evaluator. Returns dict(moves, visits, ...)."""
+    L = lib()
+    if not hasattr(L.kvo_mcts_play_game, "_sig"):
+        L.kvo_mcts_play_game.argtypes = [C.POINTER(MctsCfg), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.POINTER(C.c_uint16), C.c_int, C.POINTER(C.c_int32), C.c_int,
+                                         C.POINTER(GameResult)]
+        L.kvo_mcts_play_game._sig = True
+    cb = None
+    if eval_fn is not None:
+        def _cb(ctx, planes, n, logits, values):
+            x = np.ctypeslib.as_array(planes, shape=(n, 12, 8, 8)).copy()
+            lg, vl = eval_fn(x)
+            np.ctypeslib.as_array(logits, shape=(n, 4096))[:] = lg
+            np.ctypeslib.as_array(values, shape=(n,))[:] = np.asarray(vl).reshape(n)
+        cb = EVAL_FN(_cb)
+    smx = None
+    if softmax_fn is not None:
+        def _sm(ctx, lg, pr):
+            np.ctypeslib.as_array(pr, shape=(4096,))[:] = softmax_fn(np.ctypeslib.as_array(lg, shape=(4096,)).copy())
+        smx = SOFTMAX_FN(_sm)
+    cfg = MctsCfg(sims, c_puct, max_moves if max_moves else 0, eps, alpha)
+    moves = np.zeros(cap, dtype=np.uint16)
+    visits = np.full((cap, maxm), -1, dtype=np.int32)
+    res = GameResult()
+    n = L.kvo_mcts_play_game(C.byref(cfg), np_mt.buf, py_mt.buf, C.cast(cb, C.c_void_p) if cb else None,
+                             C.cast(smx, C.c_void_p) if smx else None, None, _p(moves, C.c_uint16), cap,
+                             _p(visits, C.c_int32), maxm, C.byref(res))
+    return dict(moves=moves[:n].copy(), visits=visits[:n].copy(), plies=res.plies, outcome=res.outcome,
+                reward=float(res.reward), reason=res.reason, n_evals=res.n_evals)
