@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
-    ap.add_argument("--mode", choices=["mcts", "ref"], default=os.environ.get("KV_BENCH_MODE", "ref"))
+    ap.add_argument("--mode", choices=["mcts", "ref"], default=os.environ.get("KV_BENCH_MODE", "mcts"))
     ap.add_argument("--slots", type=int, default=256)
     ap.add_argument("--sims", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -58,6 +58,19 @@ def cpu_baseline(seconds: float, sims: int):
     t0 = time.perf_counter()
     plies = games = 0
     seed = 42
+    if sims > 0:
+        s_cpu = min(sims, 64)
+        done = 0
+        while time.perf_counter() - t0 < seconds:
+            r = O.mcts_play_game(s_cpu, O.MT(seed, "numpy"), O.MT(seed, "python"), ev, max_moves=2,
+                                 softmax_fn=torch_ref.torch_softmax)
+            done += r["plies"] * s_cpu
+            games += 1
+            seed += 1
+        dt = time.perf_counter() - t0
+        return dict(value=done / dt, unit="sims/s", cores=torch.get_num_threads(), kind="port",
+                    sample=f"{games} games x 2 moves x {s_cpu} sims (per-game seeds 42+), oracle PUCT restatement "
+                           f"+ torch-CPU ChessNet fp32, one leaf per network call, {dt:.1f}s")
     while time.perf_counter() - t0 < seconds:
         r = O.play_game(ev, O.MT(seed, "numpy"), O.MT(seed, "python"), O.Last(), max_moves=64, batch=16,
                         softmax_fn=torch_ref.torch_softmax)
@@ -141,7 +154,13 @@ def main():
         else:
             metric, unit, value = "self-play plies/sec + games/hour (reference move selection, sims=0)", \
                 "plies/s", plies / dt
-        games_per_hour = plies / dt * 3600.0 / mean_len if mean_len == mean_len and mean_len > 0 else None
+        # games/hour: plies/s over the mean game length -- measured when >= 20 games completed in the
+        # run, else the reference's measured mean of 371 plies/game (random-init weights)
+        if len(gms_all) >= 20:
+            basis, glen = f"measured mean over {len(gms_all)} games", mean_len
+        else:
+            basis, glen = "reference mean game length 371 plies (SURVEY.md 6)", 371.0
+        games_per_hour = plies / dt * 3600.0 / glen
         out = {
             "metric": metric, "value": value, "unit": unit, "n_gpus": world, "steps": steps, "warmup": warmup,
             "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -149,7 +168,8 @@ def main():
             "config": {"workload": f"{G} concurrent games/GPU, {'%d sims/move' % sims if mcts else 'reference sampled move (sims=0)'}, "
                                    f"batch-{G} NN eval, faithful one-eval-per-position",
                        "slots_per_gpu": G, "sims_per_move": sims, "nn_batch": G, "parallelism": f"games sharded x{world}"},
-            "plies_per_s": plies / dt, "games_per_hour": games_per_hour, "mean_plies_per_game": mean_len,
+            "plies_per_s": plies / dt, "games_per_hour": games_per_hour, "games_per_hour_basis": basis,
+            "mean_plies_per_game": mean_len if mean_len == mean_len else None,
             "games_completed": games_done, "nn_evals_per_s": nn_rows / dt,
             "nn_tflops": nn_rows * FLOP_PER_EVAL / dt / 1e12, "gather_ms": gather_ms,
             "records_gathered": int(len(recs_all)),

@@ -1,0 +1,63 @@
+"""World-size-2 gloo test of the multi-GPU path's only collective: the
+end-of-iteration experience gather (knightvision_amd.distributed), and of the
+game-id sharding (rank r plays ids r, r+W, ...)."""
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_q):
+    import torch.distributed as dist
+    from knightvision_amd.distributed import gather_experience
+    from knightvision_amd.engine import GAME_DTYPE, RECORD_DTYPE
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ids = list(range(rank, 10, world))  # sharded global ids
+    rng = np.random.default_rng(rank)
+    recs = []
+    games = np.zeros(len(ids), dtype=GAME_DTYPE)
+    for k, gid in enumerate(ids):
+        n = 3 + gid
+        r = np.zeros(n, dtype=RECORD_DTYPE)
+        r["game_id"] = gid
+        r["ply"] = np.arange(n)[::-1]  # out of order on purpose
+        r["move"] = gid * 100 + np.arange(n)[::-1]
+        r["board"] = rng.integers(0, 13, size=(n, 64))
+        recs.append(r)
+        games[k]["game_id"] = gid
+        games[k]["plies"] = n
+    recs = np.concatenate(recs)
+    all_r, all_g = gather_experience(recs, games)
+    out_q.put((rank, all_r["game_id"].tolist(), all_r["ply"].tolist(), all_r["move"].tolist(),
+               all_g["game_id"].tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_experience_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want_ids = [g for g in range(10) for _ in range(3 + g)]
+    want_ply = [p for g in range(10) for p in range(3 + g)]
+    for rank, ids, ply, move, gids in res:
+        assert ids == want_ids and ply == want_ply
+        assert move == [g * 100 + p for g in range(10) for p in range(3 + g)]
+        assert gids == list(range(10))
