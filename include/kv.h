@@ -57,6 +57,14 @@ int kv_net_forward_boards(kv_net* net, const int8_t* boards_dev, int B, float* p
 /* per-launch timing of the last forward (HIP events on `stream`): ms of the
  * residual conv launches summed, and count of those launches. */
 int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv);
+/* Arithmetic of the 3x3 convs with Cin 256/512 (the stem conv is always fp32):
+ * KV_PREC_FP32   f32-input MFMA, exact fp32 products (default; the parity mode)
+ * KV_PREC_BF16X3 each fp32 operand split into bf16 hi + lo, hi*hi + hi*lo +
+ *                lo*hi on bf16 MFMA with fp32 accumulation (logits within
+ *                1e-4 of the reference; not bit-exact to fp32) */
+#define KV_PREC_FP32 0
+#define KV_PREC_BF16X3 1
+int kv_net_set_precision(kv_net* net, int precision);
 int kv_net_set_timing(kv_net* net, int enable);
 void kv_net_destroy(kv_net* net);
 
@@ -88,6 +96,7 @@ typedef struct {
     int eval_mode;        /* KV_EVAL_* */
     int64_t record_cap;   /* record buffer capacity */
     int recycle;          /* 1: a finished slot starts the next game id */
+    int precision;        /* KV_PREC_* of the network convs */
 } kv_config;
 
 typedef struct {

@@ -380,7 +380,7 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
         kv::set_error("kv_create: hipHostMalloc failed");
         return KV_ENOMEM;
     }
-    if ((rc = kv_net_create(cfg->device, &e->net))) {
+    if ((rc = kv_net_create(cfg->device, &e->net)) || (rc = kv_net_set_precision(e->net, cfg->precision))) {
         kv_destroy(e);
         return rc;
     }

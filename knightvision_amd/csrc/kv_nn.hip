@@ -229,6 +229,194 @@ __global__ __launch_bounds__(512) void conv3x3_kernel(const float* __restrict__ 
     }
 }
 
+// ------------------------------------------------- bf16x3 conv kernel --
+// The same implicit GEMM with every fp32 operand split as x = hi + lo (two
+// bf16, hi = RNE(x), lo = RNE(x - hi)) and the product taken as
+// hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_bf16 with fp32 accumulation:
+// the dropped lo*lo term and the 16-bit mantissa of hi+lo keep the conv at
+// ~1e-5 relative error (logits within 3e-5 of the reference on the peaked
+// weight set; tolerance 1e-4). Three bf16 MFMAs cost 3/16 of one fp32 MFMA.
+// Workgroup: 4 boards x 128 output channels, 8 waves = 4 boards x 2 column
+// halves, 64x64 per wave (2x2 tiles). Weights are pre-split on the device at
+// load time ([Cout][9][Cin] bf16 hi and lo); activations stay fp32 in HBM and
+// are split while staging the halo into LDS. Strides (bytes): halo pixel 64,
+// halo row 656, weight row 80 -- conflict-free ds_read_b128 for every tap.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ inline unsigned bf16_rne(float x) {
+    const unsigned u = __float_as_uint(x);
+    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+
+__device__ inline void split2(float a, float b, unsigned& hi, unsigned& lo) {
+    const unsigned ha = bf16_rne(a), hb = bf16_rne(b);
+    const float ra = a - __uint_as_float(ha << 16), rb = b - __uint_as_float(hb << 16);
+    hi = ha | (hb << 16);
+    lo = bf16_rne(ra) | (bf16_rne(rb) << 16);
+}
+
+template <int CIN>
+struct Bf3Lds {
+    static constexpr int PSA = 64, RSA = 656, BOARDA = 10 * RSA;  // bytes
+    static constexpr int APART = 4 * BOARDA;                       // one of hi / lo
+    static constexpr int ABUF = 2 * APART;                         // hi + lo
+    static constexpr int PSB = 80, BPART = 128 * PSB, BBUF = 2 * BPART;
+    static constexpr int BYTES = 2 * ABUF + 2 * BBUF;
+};
+
+template <int CIN, bool RESID>
+__global__ __launch_bounds__(512) void conv3x3_bf16x3_kernel(const float* __restrict__ in,
+                                                             const uint16_t* __restrict__ whi,
+                                                             const uint16_t* __restrict__ wlo,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift, const float* resid,
+                                                             float* out, int cout) {
+    using G = Bf3Lds<CIN>;
+    constexpr int PSA = G::PSA, RSA = G::RSA, BOARDA = G::BOARDA, APART = G::APART, ABUF = G::ABUF;
+    constexpr int PSB = G::PSB, BPART = G::BPART, BBUF = G::BBUF;
+    constexpr int CK = 32, NCH = CIN / CK, NK = 9 * NCH;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wb = wave >> 1;  // board inside the tile
+    const int wn = wave & 1;   // 64-column half
+    const int n_base = blockIdx.x * 128;
+    const int b0 = blockIdx.y * 4;
+
+    for (int i = tid * 16; i < 2 * ABUF; i += 512 * 16) *(u32x4*)(lds + i) = u32x4{0u, 0u, 0u, 0u};
+
+    // staging: A = 4 boards x 64 px x 32 cin fp32 (4 float4 / thread), B = 128 n x 32 k (hi + lo 16 B / thread)
+    f32x4 ra[4];
+    u32x4 rbh, rbl;
+    auto loadA = [&](int ch) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int idx = tid + q * 512;  // 2048 float4
+            const int pix = idx >> 3, kq = idx & 7;
+            ra[q] = *(const f32x4*)(in + ((size_t)(b0 + (pix >> 6)) * 64 + (pix & 63)) * CIN + ch * CK + kq * 4);
+        }
+    };
+    auto storeA = [&](int buf) {
+        unsigned char* Ah = lds + buf * ABUF;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int idx = tid + q * 512;
+            const int pix = idx >> 3, kq = idx & 7;
+            const int p = pix & 63;
+            const int off = (pix >> 6) * BOARDA + ((p >> 3) + 1) * RSA + ((p & 7) + 1) * PSA + kq * 8;
+            unsigned h0, l0, h1, l1;
+            split2(ra[q][0], ra[q][1], h0, l0);
+            split2(ra[q][2], ra[q][3], h1, l1);
+            *(u32x2*)(Ah + off) = u32x2{h0, h1};
+            *(u32x2*)(Ah + APART + off) = u32x2{l0, l1};
+        }
+    };
+    auto loadB = [&](int kt) {
+        const int tap = kt % 9, ch = kt / 9;
+        const int n = tid >> 2, kq = tid & 3;
+        const size_t o = ((size_t)(n_base + n) * 9 + tap) * CIN + ch * CK + kq * 8;
+        rbh = *(const u32x4*)(whi + o);
+        rbl = *(const u32x4*)(wlo + o);
+    };
+    auto storeB = [&](int buf) {
+        unsigned char* Bh = lds + 2 * ABUF + buf * BBUF;
+        const int n = tid >> 2, kq = tid & 3;
+        *(u32x4*)(Bh + n * PSB + kq * 16) = rbh;
+        *(u32x4*)(Bh + BPART + n * PSB + kq * 16) = rbl;
+    };
+
+    const int h = lane >> 5, li = lane & 31;
+    int aoff[2], boff[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+        const int p = mt * 32 + li;
+        aoff[mt] = wb * BOARDA + ((p >> 3) + 1) * RSA + ((p & 7) + 1) * PSA + 16 * h;
+    }
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) boff[nt] = (wn * 64 + nt * 32 + li) * PSB + 16 * h;
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    __syncthreads();
+    loadA(0);
+    loadB(0);
+    storeA(0);
+    storeB(0);
+    __syncthreads();
+
+    for (int kt = 0; kt < NK; ++kt) {
+        const int tap = kt % 9, ch = kt / 9;
+        const bool nextB = kt + 1 < NK;
+        const bool nextA = (tap == 8) && (ch + 1 < NCH);
+        if (nextB) loadB(kt + 1);
+        if (nextA) loadA(ch + 1);
+        const unsigned char* Ah = lds + (ch & 1) * ABUF;
+        const unsigned char* Bh = lds + 2 * ABUF + (kt & 1) * BBUF;
+        const int toff = (tap / 3 - 1) * RSA + (tap % 3 - 1) * PSA;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                ah[mt] = *(const bf16x8*)(Ah + aoff[mt] + toff + 32 * s);
+                al[mt] = *(const bf16x8*)(Ah + APART + aoff[mt] + toff + 32 * s);
+            }
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                bh[nt] = *(const bf16x8*)(Bh + boff[nt] + 32 * s);
+                bl[nt] = *(const bf16x8*)(Bh + BPART + boff[nt] + 32 * s);
+            }
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) {
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
+                }
+        }
+        if (nextB) storeB((kt + 1) & 1);
+        if (nextA) storeA((ch + 1) & 1);
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        const int n = n_base + wn * 64 + nt * 32 + li;
+        const float sc = scale[n], sh = shift[n];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int pix = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const size_t idx = ((size_t)(b0 + wb) * 64 + pix) * cout + n;
+                float v = acc[mt][nt][r] * sc + sh;
+                if (RESID) v += resid[idx];
+                out[idx] = v > 0.f ? v : 0.f;
+            }
+        }
+    }
+}
+
+// fp32 weights -> bf16 hi / lo (RNE), elementwise
+__global__ void split_weights_kernel(const float* __restrict__ w, size_t n, uint16_t* __restrict__ hi,
+                                     uint16_t* __restrict__ lo) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = w[i];
+    const unsigned hb = bf16_rne(x);
+    hi[i] = (uint16_t)hb;
+    lo[i] = (uint16_t)bf16_rne(x - __uint_as_float(hb << 16));
+}
+
 // ------------------------------------------------------------- heads --
 // policy_conv/value_conv (1x1, 512->2 / 512->1) + BN + ReLU, NCHW flatten
 // (c*64+sq, ai/model.py:65), value_fc1 + ReLU, value_fc2 + tanh (:70-73).
@@ -372,7 +560,27 @@ struct kv_net {
     bool timing = false;
     hipEvent_t ev[3];
     hipEvent_t res_a = nullptr, res_b = nullptr;  // engine hook: residual section
+    int precision = KV_PREC_FP32;
+    uint16_t* whi = nullptr;  // bf16x3: split conv weights, layers 1..11, same offsets as w
+    uint16_t* wlo = nullptr;
 };
+
+template <int CIN, bool RESID>
+static int launch_conv_bf3(const float* in, const uint16_t* whi, const uint16_t* wlo, const float* sc,
+                           const float* sh, const float* resid, float* out, int cout, int nb_pad, hipStream_t st) {
+    using G = kv::Bf3Lds<CIN>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        KV_HIP(hipFuncSetAttribute((const void*)kv::conv3x3_bf16x3_kernel<CIN, RESID>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::BYTES));
+        attr_set = true;
+    }
+    dim3 grid(cout / 128, nb_pad / 4);
+    hipLaunchKernelGGL((kv::conv3x3_bf16x3_kernel<CIN, RESID>), grid, dim3(512), G::BYTES, st, in, whi, wlo, sc, sh,
+                       resid, out, cout);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
 
 template <int CIN, int CK, bool RESID>
 static int launch_conv(const float* in, const float* w, const float* sc, const float* sh, const float* resid,
@@ -415,12 +623,27 @@ static int net_tower(kv_net* net, int nb, int nb_pad, float* policy, float* valu
     if ((rc = launch_conv<16, 16, false>(net->x16, W + o.w[0], W + o.scale[0], W + o.shift[0], nullptr, net->T, 256,
                                          nb_pad, st)))
         return rc;
-    if ((rc = launch_conv<256, 32, false>(net->T, W + o.w[1], W + o.scale[1], W + o.shift[1], nullptr, net->X, 512,
-                                          nb_pad, st)))
+    const bool bf3 = net->precision == KV_PREC_BF16X3;
+    if (bf3) {
+        if ((rc = launch_conv_bf3<256, false>(net->T, net->whi + o.w[1], net->wlo + o.w[1], W + o.scale[1],
+                                              W + o.shift[1], nullptr, net->X, 512, nb_pad, st)))
+            return rc;
+    } else if ((rc = launch_conv<256, 32, false>(net->T, W + o.w[1], W + o.scale[1], W + o.shift[1], nullptr, net->X,
+                                                 512, nb_pad, st))) {
         return rc;
+    }
     if (tm) KV_HIP(hipEventRecord(net->ev[1], st));
     if (net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-    for (int r = 0; r < 5; ++r) {
+    for (int r = 0; r < 5 && bf3; ++r) {
+        const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
+        if ((rc = launch_conv_bf3<512, false>(net->X, net->whi + o.w[l1], net->wlo + o.w[l1], W + o.scale[l1],
+                                              W + o.shift[l1], nullptr, net->T, 512, nb_pad, st)))
+            return rc;
+        if ((rc = launch_conv_bf3<512, true>(net->T, net->whi + o.w[l2], net->wlo + o.w[l2], W + o.scale[l2],
+                                             W + o.shift[l2], net->X, net->X, 512, nb_pad, st)))
+            return rc;
+    }
+    for (int r = 0; r < 5 && !bf3; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         if ((rc = launch_conv<512, 32, false>(net->X, W + o.w[l1], W + o.scale[l1], W + o.shift[l1], nullptr, net->T,
                                               512, nb_pad, st)))
@@ -470,7 +693,26 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
                n_floats);
     KV_HIP(hipSetDevice(net->device));
     KV_HIP(hipMemcpy(net->w, packed, n_floats * sizeof(float), hipMemcpyHostToDevice));
+    if (!net->whi) {
+        KV_HIP(hipMalloc(&net->whi, net->off.total * sizeof(uint16_t)));
+        KV_HIP(hipMalloc(&net->wlo, net->off.total * sizeof(uint16_t)));
+    }
+    for (int l = 1; l < 12; ++l) {  // the 11 convs with Cin 256 / 512
+        const size_t n = (size_t)kv::kConv[l].cout * 9 * kv::kConv[l].cin_pad;
+        hipLaunchKernelGGL(kv::split_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0,
+                           net->w + net->off.w[l], n, net->whi + net->off.w[l], net->wlo + net->off.w[l]);
+        KV_HIP(hipGetLastError());
+    }
+    KV_HIP(hipDeviceSynchronize());
     net->loaded = true;
+    return KV_OK;
+}
+
+int kv_net_set_precision(kv_net* net, int precision) {
+    KV_REQUIRE(net, KV_EINVAL, "kv_net_set_precision: NULL");
+    KV_REQUIRE(precision == KV_PREC_FP32 || precision == KV_PREC_BF16X3, KV_EINVAL,
+               "kv_net_set_precision: unknown precision %d", precision);
+    net->precision = precision;
     return KV_OK;
 }
 
@@ -478,7 +720,7 @@ int kv_net_forward(kv_net* net, const float* planes_dev, int B, float* policy_de
     KV_REQUIRE(net && net->loaded, KV_EINVAL, "kv_net_forward: net not loaded");
     KV_REQUIRE(B > 0 && planes_dev && policy_dev && value_dev, KV_EINVAL, "kv_net_forward: bad arguments (B=%d)", B);
     hipStream_t st = (hipStream_t)stream;
-    const int nb_pad = (B + 1) & ~1;
+    const int nb_pad = (B + 3) & ~3;
     int rc = net_reserve(net, nb_pad);
     if (rc) return rc;
     hipLaunchKernelGGL(kv::planes_to_nhwc16_kernel, dim3((nb_pad * 64 + 255) / 256), dim3(256), 0, st, planes_dev, B,
@@ -492,7 +734,7 @@ int kv_net_forward_boards(kv_net* net, const int8_t* boards_dev, int B, float* p
     KV_REQUIRE(net && net->loaded, KV_EINVAL, "kv_net_forward_boards: net not loaded");
     KV_REQUIRE(B > 0 && boards_dev && policy_dev && value_dev, KV_EINVAL, "kv_net_forward_boards: bad arguments");
     hipStream_t st = (hipStream_t)stream;
-    const int nb_pad = (B + 1) & ~1;
+    const int nb_pad = (B + 3) & ~3;
     int rc = net_reserve(net, nb_pad);
     if (rc) return rc;
     hipLaunchKernelGGL(kv::encode_boards_kernel, dim3((nb_pad * 64 + 255) / 256), dim3(256), 0, st, boards_dev, B,
@@ -521,6 +763,8 @@ void kv_net_destroy(kv_net* net) {
     if (!net) return;
     (void)hipSetDevice(net->device);
     (void)hipFree(net->w);
+    (void)hipFree(net->whi);
+    (void)hipFree(net->wlo);
     (void)hipFree(net->x16);
     (void)hipFree(net->X);
     (void)hipFree(net->T);

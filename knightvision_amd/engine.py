@@ -34,14 +34,15 @@ def packed_from(weights) -> np.ndarray:
 class SelfPlayEngine:
     def __init__(self, weights, *, slots=256, n_games=256, seed=42, seed_mode=SEED_PER_GAME, max_moves=None,
                  batch=16, eps=0.25, alpha=0.3, sims=0, c_puct=1.5, eval_mode=EVAL_FAITHFUL, record_cap=None,
-                 recycle=True, device=0, game_id_base=0, game_id_stride=1):
+                 recycle=True, device=0, game_id_base=0, game_id_stride=1, precision="fp32"):
         L = _lib.lib()
         if record_cap is None:
             record_cap = max(1 << 16, min(1 << 26, int(n_games) * 400))
         cfg = _lib.Config(device=device, slots=slots, n_games=n_games, game_id_base=game_id_base,
                           game_id_stride=game_id_stride, seed=seed, seed_mode=seed_mode,
                           max_moves=max_moves if max_moves else 0, batch=batch, eps=eps, alpha=alpha, sims=sims,
-                          c_puct=c_puct, eval_mode=eval_mode, record_cap=record_cap, recycle=1 if recycle else 0)
+                          c_puct=c_puct, eval_mode=eval_mode, record_cap=record_cap, recycle=1 if recycle else 0,
+                          precision={"fp32": 0, "bf16x3": 1}[precision])
         h = C.c_void_p()
         _lib.check(L.kv_create(C.byref(cfg), C.byref(h)), "kv_create")
         self.h = h

@@ -131,15 +131,16 @@ GROUPS = {"pg_init_mm80": ("init", 80, 16), "pg_peaked_mm80": ("peaked", 80, 16)
           "pg_init_b1_mm60": ("init", 60, 1), "pg_init_full": ("init", None, 16)}
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 @pytest.mark.parametrize("group", list(GROUPS))
-def test_engine_games_match_reference(golden_dir, group):
+def test_engine_games_match_reference(golden_dir, group, precision):
     from knightvision_amd.engine import SelfPlayEngine, records_by_game
     variant, mm, batch = GROUPS[group]
     gold = _golden_games(golden_dir, group)
     n = len(gold)
     slots = max(1, n // 2)  # fewer slots than games: exercises slot recycling
     with SelfPlayEngine(synthetic_state_dict(42, variant), slots=slots, n_games=n, seed=gold[0]["seed"],
-                        max_moves=mm, batch=batch) as eng:
+                        max_moves=mm, batch=batch, precision=precision) as eng:
         eng.run()
         recs, games = eng.records(), eng.games()
     by = records_by_game(recs, games)
@@ -151,7 +152,7 @@ def test_engine_games_match_reference(golden_dir, group):
         if r == "exact":
             assert reward == pytest.approx(g["reward"])
             assert int(games[k]["n_evals"]) == g["n_evals"]
-    print(group, res)
+    print(precision, group, res)
     assert sum(r == "exact" for r in res) >= n - max(1, n // 8)
 
 

@@ -13,35 +13,37 @@ pytestmark = pytest.mark.gpu
 TOL_P, TOL_V = 1e-4, 1e-5
 
 
-def _net(variant):
+def _net(variant, precision="fp32"):
     from knightvision_amd.model import ChessNet
-    m = ChessNet()
+    m = ChessNet(precision=precision)
     sd = synthetic_state_dict(42, variant)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
     return m.eval()
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 @pytest.mark.parametrize("variant", ["init", "bn", "peaked"])
-def test_forward_matches_reference_golden(golden_dir, variant):
+def test_forward_matches_reference_golden(golden_dir, variant, precision):
     g = np.load(os.path.join(golden_dir, "nn.npz"))
-    m = _net(variant)
+    m = _net(variant, precision)
     p, v = m(torch.from_numpy(g["planes"]).cuda())
     torch.cuda.synchronize()
     dp = np.abs(p.cpu().numpy() - g[f"policy_{variant}"]).max()
     dv = np.abs(v.cpu().numpy() - g[f"value_{variant}"]).max()
-    print(variant, "max |dpolicy|", dp, "max |dvalue|", dv)
+    print(precision, variant, "max |dpolicy|", dp, "max |dvalue|", dv)
     assert dp <= TOL_P and dv <= TOL_V
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 @pytest.mark.parametrize("B", [1, 2, 3, 31, 64, 257])
-def test_forward_batch_sizes_vs_torch(B):
+def test_forward_batch_sizes_vs_torch(B, precision):
     from oracle import torch_ref
     rng = np.random.default_rng(B)
     codes = rng.integers(0, 13, size=(B, 64)) * (rng.random((B, 64)) < 0.4)
     from knightvision_amd.ai import codes_to_planes
     planes = codes_to_planes(codes)
     sd = synthetic_state_dict(42, "bn")
-    m = _net("bn")
+    m = _net("bn", precision)
     p, v = m(torch.from_numpy(planes).cuda())
     rp, rv = torch_ref.forward(sd, planes)
     dp = np.abs(p.cpu().numpy() - rp.numpy()).max()
@@ -53,13 +55,14 @@ def test_forward_batch_sizes_vs_torch(B):
     assert np.abs(vb.cpu().numpy() - v.cpu().numpy()).max() == 0.0
 
 
-def test_batch_invariance():
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+def test_batch_invariance(precision):
     """A board's outputs do not depend on the batch it is evaluated in."""
     from knightvision_amd.ai import codes_to_planes
     rng = np.random.default_rng(7)
     codes = rng.integers(0, 13, size=(40, 64)) * (rng.random((40, 64)) < 0.4)
     planes = torch.from_numpy(codes_to_planes(codes)).cuda()
-    m = _net("peaked")
+    m = _net("peaked", precision)
     p_all, v_all = m(planes)
     for i in (0, 17, 39):
         p1, v1 = m(planes[i:i + 1])
