@@ -178,16 +178,17 @@ __global__ __launch_bounds__(512) void conv3x3_kernel(const float* __restrict__ 
     __syncthreads();  // halo zeroed before the first interior store
     loadA(0);
     loadB(0);
-    storeA(A0);
-    storeB(B0);
-    __syncthreads();
-
+    // One barrier per k-tile. Tile kt is stored from registers at the top of
+    // iteration kt (its buffer was last read at kt-2, behind kt-1's barrier)
+    // and the loads for kt+1 are issued right after, so they have the whole
+    // compute of kt to land; A chunks are loaded a chunk ahead the same way.
     for (int kt = 0; kt < NK; ++kt) {
         const int tap = kt % 9, ch = kt / 9;
-        const bool nextB = kt + 1 < NK;
-        const bool nextA = (tap == 8) && (ch + 1 < NCH);
-        if (nextB) loadB(kt + 1);
-        if (nextA) loadA(ch + 1);
+        if (tap == 0) storeA((ch & 1) ? A1 : A0);
+        storeB((kt & 1) ? B1 : B0);
+        if (kt + 1 < NK) loadB(kt + 1);
+        if (tap == 0 && ch + 1 < NCH) loadA(ch + 1);
+        __syncthreads();
         const float* Ab = (ch & 1) ? A1 : A0;
         const float* Bb = (kt & 1) ? B1 : B0;
         const int toff = (tap / 3 - 1) * RS + (tap % 3 - 1) * PS;
@@ -205,9 +206,6 @@ __global__ __launch_bounds__(512) void conv3x3_kernel(const float* __restrict__ 
                 acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[j], v1[j], acc[1][1], 0, 0, 0);
             }
         }
-        if (nextB) storeB((kt & 1) ? B0 : B1);
-        if (nextA) storeA((ch & 1) ? A0 : A1);
-        __syncthreads();
     }
 
     // epilogue: D[row][col], row = (r&3) + 8*(r>>2) + 4*h, col = li
@@ -348,16 +346,13 @@ __global__ __launch_bounds__(512) void conv3x3_bf16x3_kernel(const float* __rest
     __syncthreads();
     loadA(0);
     loadB(0);
-    storeA(0);
-    storeB(0);
-    __syncthreads();
-
-    for (int kt = 0; kt < NK; ++kt) {
+    for (int kt = 0; kt < NK; ++kt) {  // one barrier per k-tile, as in conv3x3_kernel
         const int tap = kt % 9, ch = kt / 9;
-        const bool nextB = kt + 1 < NK;
-        const bool nextA = (tap == 8) && (ch + 1 < NCH);
-        if (nextB) loadB(kt + 1);
-        if (nextA) loadA(ch + 1);
+        if (tap == 0) storeA(ch & 1);
+        storeB(kt & 1);
+        if (kt + 1 < NK) loadB(kt + 1);
+        if (tap == 0 && ch + 1 < NCH) loadA(ch + 1);
+        __syncthreads();
         const unsigned char* Ah = lds + (ch & 1) * ABUF;
         const unsigned char* Bh = lds + 2 * ABUF + (kt & 1) * BBUF;
         const int toff = (tap / 3 - 1) * RSA + (tap % 3 - 1) * PSA;
@@ -383,9 +378,6 @@ __global__ __launch_bounds__(512) void conv3x3_bf16x3_kernel(const float* __rest
                     acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
                 }
         }
-        if (nextB) storeB((kt + 1) & 1);
-        if (nextA) storeA((ch + 1) & 1);
-        __syncthreads();
     }
 
 #pragma unroll

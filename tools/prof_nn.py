@@ -10,7 +10,7 @@ from knightvision_amd.model import ChessNet  # noqa: E402
 from knightvision_amd.weights import synthetic_state_dict  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-m = ChessNet()
+m = ChessNet(precision=os.environ.get("KV_PREC", "fp32"))
 m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(42, "init").items()})
 m.eval()
 net = m.kv_net(0)
