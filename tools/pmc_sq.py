@@ -6,6 +6,8 @@ from collections import defaultdict
 
 acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(sys.argv[1], recursive=True):
+    if "counter_collection" not in f:
+        continue
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
         if "conv3x3" not in k:
