@@ -95,7 +95,7 @@ template <int CIN, int CK, bool RESID>
 __global__ __launch_bounds__(512) void conv3x3_kernel(const float* __restrict__ in, const float* __restrict__ wt,
                                                       const float* __restrict__ scale,
                                                       const float* __restrict__ shift,
-                                                      const float* resid, float* out, int cout) {
+                                                      const float* resid, float* out, int cout, int kt_per) {
     using G = ConvLds<CIN, CK>;
     constexpr int PS = G::PS, RS = G::RS, BOARD = G::BOARD, ABUF = G::ABUF, BBUF = G::BBUF;
     constexpr int NCH = CIN / CK;
@@ -117,6 +117,10 @@ __global__ __launch_bounds__(512) void conv3x3_kernel(const float* __restrict__ 
     const int wn = wave & 3;   // 64-column group
     const int n_base = blockIdx.x * 256;
     const int b0 = blockIdx.y * 2;
+    // split-K (small batches): this workgroup owns k-tiles [kt0, kt1) and
+    // writes its raw partial sums to slab blockIdx.z (reduced in fixed order)
+    const int kt0 = kt_per > 0 ? (int)blockIdx.z * kt_per : 0;
+    const int kt1 = kt_per > 0 ? min(NK, kt0 + kt_per) : NK;
 
     for (int i = tid * 4; i < 2 * ABUF; i += 512 * 4) *(f32x4*)(smem + i) = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -176,18 +180,19 @@ __global__ __launch_bounds__(512) void conv3x3_kernel(const float* __restrict__ 
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     __syncthreads();  // halo zeroed before the first interior store
-    loadA(0);
-    loadB(0);
+    loadA(kt0 / 9);
+    loadB(kt0);
     // One barrier per k-tile. Tile kt is stored from registers at the top of
     // iteration kt (its buffer was last read at kt-2, behind kt-1's barrier)
     // and the loads for kt+1 are issued right after, so they have the whole
     // compute of kt to land; A chunks are loaded a chunk ahead the same way.
-    for (int kt = 0; kt < NK; ++kt) {
+    for (int kt = kt0; kt < kt1; ++kt) {
         const int tap = kt % 9, ch = kt / 9;
-        if (tap == 0) storeA((ch & 1) ? A1 : A0);
+        const bool chunk_start = tap == 0 || kt == kt0;
+        if (chunk_start) storeA((ch & 1) ? A1 : A0);
         storeB((kt & 1) ? B1 : B0);
-        if (kt + 1 < NK) loadB(kt + 1);
-        if (tap == 0 && ch + 1 < NCH) loadA(ch + 1);
+        if (kt + 1 < kt1) loadB(kt + 1);
+        if (chunk_start && (ch + 1) * 9 < kt1) loadA(ch + 1);
         __syncthreads();
         const float* Ab = (ch & 1) ? A1 : A0;
         const float* Bb = (kt & 1) ? B1 : B0;
@@ -209,6 +214,19 @@ __global__ __launch_bounds__(512) void conv3x3_kernel(const float* __restrict__ 
     }
 
     // epilogue: D[row][col], row = (r&3) + 8*(r>>2) + 4*h, col = li
+    if (kt_per > 0) {
+        float* slab = out + (size_t)blockIdx.z * gridDim.y * 128 * cout;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int pix = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    slab[((size_t)(b0 + wm) * 64 + pix) * cout + n_base + wn * 64 + nt * 32 + li] = acc[mt][nt][r];
+                }
+        return;
+    }
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
         const int n = n_base + wn * 64 + nt * 32 + li;
@@ -270,7 +288,7 @@ __global__ __launch_bounds__(512) void conv3x3_bf16x3_kernel(const float* __rest
                                                              const uint16_t* __restrict__ wlo,
                                                              const float* __restrict__ scale,
                                                              const float* __restrict__ shift, const float* resid,
-                                                             float* out, int cout) {
+                                                             float* out, int cout, int kt_per) {
     using G = Bf3Lds<CIN>;
     constexpr int PSA = G::PSA, RSA = G::RSA, BOARDA = G::BOARDA, APART = G::APART, ABUF = G::ABUF;
     constexpr int PSB = G::PSB, BPART = G::BPART, BBUF = G::BBUF;
@@ -282,6 +300,8 @@ __global__ __launch_bounds__(512) void conv3x3_bf16x3_kernel(const float* __rest
     const int wn = wave & 1;   // 64-column half
     const int n_base = blockIdx.x * 128;
     const int b0 = blockIdx.y * 4;
+    const int kt0 = kt_per > 0 ? (int)blockIdx.z * kt_per : 0;  // split-K, as in conv3x3_kernel
+    const int kt1 = kt_per > 0 ? min(NK, kt0 + kt_per) : NK;
 
     for (int i = tid * 16; i < 2 * ABUF; i += 512 * 16) *(u32x4*)(lds + i) = u32x4{0u, 0u, 0u, 0u};
 
@@ -344,14 +364,15 @@ __global__ __launch_bounds__(512) void conv3x3_bf16x3_kernel(const float* __rest
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     __syncthreads();
-    loadA(0);
-    loadB(0);
-    for (int kt = 0; kt < NK; ++kt) {  // one barrier per k-tile, as in conv3x3_kernel
+    loadA(kt0 / 9);
+    loadB(kt0);
+    for (int kt = kt0; kt < kt1; ++kt) {  // one barrier per k-tile, as in conv3x3_kernel
         const int tap = kt % 9, ch = kt / 9;
-        if (tap == 0) storeA(ch & 1);
+        const bool chunk_start = tap == 0 || kt == kt0;
+        if (chunk_start) storeA(ch & 1);
         storeB(kt & 1);
-        if (kt + 1 < NK) loadB(kt + 1);
-        if (tap == 0 && ch + 1 < NCH) loadA(ch + 1);
+        if (kt + 1 < kt1) loadB(kt + 1);
+        if (chunk_start && (ch + 1) * 9 < kt1) loadA(ch + 1);
         __syncthreads();
         const unsigned char* Ah = lds + (ch & 1) * ABUF;
         const unsigned char* Bh = lds + 2 * ABUF + (kt & 1) * BBUF;
@@ -380,6 +401,19 @@ __global__ __launch_bounds__(512) void conv3x3_bf16x3_kernel(const float* __rest
         }
     }
 
+    if (kt_per > 0) {
+        float* slab = out + (size_t)blockIdx.z * gridDim.y * 256 * cout;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int pix = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    slab[((size_t)(b0 + wb) * 64 + pix) * cout + n_base + wn * 64 + nt * 32 + li] = acc[mt][nt][r];
+                }
+        return;
+    }
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
         const int n = n_base + wn * 64 + nt * 32 + li;
@@ -407,6 +441,23 @@ __global__ void split_weights_kernel(const float* __restrict__ w, size_t n, uint
     const unsigned hb = bf16_rne(x);
     hi[i] = (uint16_t)hb;
     lo[i] = (uint16_t)bf16_rne(x - __uint_as_float(hb << 16));
+}
+
+// split-K combine: fixed-order sum of the slabs + folded BN (+ residual) + ReLU
+__global__ void splitk_reduce_kernel(const float* __restrict__ slab, int splits, size_t n4, int cout,
+                                     const float* __restrict__ scale, const float* __restrict__ shift,
+                                     const float* resid, float* out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // float4 index
+    if (i >= n4) return;
+    f32x4 v = ((const f32x4*)slab)[i];
+    for (int s = 1; s < splits; ++s) v += ((const f32x4*)slab)[(size_t)s * n4 + i];
+    const int c = (int)((i * 4) % (size_t)cout);
+    const f32x4 sc = *(const f32x4*)(scale + c), sh = *(const f32x4*)(shift + c);
+    f32x4 o = v * sc + sh;
+    if (resid) o += ((const f32x4*)resid)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = o[e] > 0.f ? o[e] : 0.f;
+    ((f32x4*)out)[i] = o;
 }
 
 // ------------------------------------------------------------- heads --
@@ -555,38 +606,79 @@ struct kv_net {
     int precision = KV_PREC_FP32;
     uint16_t* whi = nullptr;  // bf16x3: split conv weights, layers 1..11, same offsets as w
     uint16_t* wlo = nullptr;
+    float* slab = nullptr;  // split-K partial sums (small batches)
 };
+
+// Small batches (<= 16 boards: the sequential reference path, batch-16
+// schedules) have far fewer output tiles than CUs: split K into groups of 3
+// k-tiles over workgroups and sum the partial slabs in a fixed order. The
+// split is a function of the size class only, so results are bit-identical
+// for every batch inside a class (<= 16 boards, or > 16 boards).
+constexpr int kSplitMaxBoards = 16, kSplitKt = 3;
+static int split_kt(int nb_pad) { return nb_pad <= kSplitMaxBoards ? kSplitKt : 0; }
+
+static int launch_reduce(const float* slab, int splits, int rows, int cout, const float* sc, const float* sh,
+                         const float* resid, float* out, hipStream_t st) {
+    const size_t n4 = (size_t)rows * cout / 4;
+    hipLaunchKernelGGL(kv::splitk_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, slab, splits,
+                       n4, cout, sc, sh, resid, out);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
 
 template <int CIN, bool RESID>
 static int launch_conv_bf3(const float* in, const uint16_t* whi, const uint16_t* wlo, const float* sc,
-                           const float* sh, const float* resid, float* out, int cout, int nb_pad, hipStream_t st) {
+                           const float* sh, const float* resid, float* out, int cout, int nb_pad, float* slab,
+                           hipStream_t st) {
     using G = kv::Bf3Lds<CIN>;
     static bool attr_set = false;
     if (!attr_set) {
         KV_HIP(hipFuncSetAttribute((const void*)kv::conv3x3_bf16x3_kernel<CIN, RESID>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::BYTES));
+        KV_HIP(hipFuncSetAttribute((const void*)kv::conv3x3_bf16x3_kernel<CIN, false>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::BYTES));
         attr_set = true;
+    }
+    const int nk = 9 * (CIN / 32);
+    const int kt_per = slab ? split_kt(nb_pad) : 0;
+    if (kt_per) {
+        const int splits = (nk + kt_per - 1) / kt_per;
+        hipLaunchKernelGGL((kv::conv3x3_bf16x3_kernel<CIN, false>), dim3(cout / 128, nb_pad / 4, splits), dim3(512),
+                           G::BYTES, st, in, whi, wlo, sc, sh, nullptr, slab, cout, kt_per);
+        KV_HIP(hipGetLastError());
+        return launch_reduce(slab, splits, nb_pad * 64, cout, sc, sh, RESID ? resid : nullptr, out, st);
     }
     dim3 grid(cout / 128, nb_pad / 4);
     hipLaunchKernelGGL((kv::conv3x3_bf16x3_kernel<CIN, RESID>), grid, dim3(512), G::BYTES, st, in, whi, wlo, sc, sh,
-                       resid, out, cout);
+                       resid, out, cout, 0);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
 
 template <int CIN, int CK, bool RESID>
 static int launch_conv(const float* in, const float* w, const float* sc, const float* sh, const float* resid,
-                       float* out, int cout, int nb_pad, hipStream_t st) {
+                       float* out, int cout, int nb_pad, float* slab, hipStream_t st) {
     using G = kv::ConvLds<CIN, CK>;
     static bool attr_set = false;
     if (!attr_set) {
         KV_HIP(hipFuncSetAttribute((const void*)kv::conv3x3_kernel<CIN, CK, RESID>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::BYTES));
+        KV_HIP(hipFuncSetAttribute((const void*)kv::conv3x3_kernel<CIN, CK, false>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::BYTES));
         attr_set = true;
+    }
+    const int nk = 9 * (CIN / CK);
+    const int kt_per = slab ? split_kt(nb_pad) : 0;
+    if (kt_per) {
+        const int splits = (nk + kt_per - 1) / kt_per;
+        hipLaunchKernelGGL((kv::conv3x3_kernel<CIN, CK, false>), dim3(cout / 256, nb_pad / 2, splits), dim3(512),
+                           G::BYTES, st, in, w, sc, sh, nullptr, slab, cout, kt_per);
+        KV_HIP(hipGetLastError());
+        return launch_reduce(slab, splits, nb_pad * 64, cout, sc, sh, RESID ? resid : nullptr, out, st);
     }
     dim3 grid(cout / 256, nb_pad / 2);
     hipLaunchKernelGGL((kv::conv3x3_kernel<CIN, CK, RESID>), grid, dim3(512), G::BYTES, st, in, w, sc, sh, resid,
-                       out, cout);
+                       out, cout, 0);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -601,6 +693,8 @@ static int net_reserve(kv_net* net, int nb_pad) {
     KV_HIP(hipMalloc(&net->X, (size_t)cap * 64 * 512 * 4));
     KV_HIP(hipMalloc(&net->T, (size_t)cap * 64 * 512 * 4));
     KV_HIP(hipMalloc(&net->pfeat, (size_t)cap * 128 * 4));
+    if (!net->slab)  // 48 splits x 16 boards x 64 px x 512 channels
+        KV_HIP(hipMalloc(&net->slab, (size_t)(144 / kSplitKt) * kSplitMaxBoards * 64 * 512 * 4));
     net->cap = cap;
     return KV_OK;
 }
@@ -613,15 +707,15 @@ static int net_tower(kv_net* net, int nb, int nb_pad, float* policy, float* valu
     const bool tm = net->timing;
     if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
     if ((rc = launch_conv<16, 16, false>(net->x16, W + o.w[0], W + o.scale[0], W + o.shift[0], nullptr, net->T, 256,
-                                         nb_pad, st)))
+                                         nb_pad, nullptr, st)))
         return rc;
     const bool bf3 = net->precision == KV_PREC_BF16X3;
     if (bf3) {
         if ((rc = launch_conv_bf3<256, false>(net->T, net->whi + o.w[1], net->wlo + o.w[1], W + o.scale[1],
-                                              W + o.shift[1], nullptr, net->X, 512, nb_pad, st)))
+                                              W + o.shift[1], nullptr, net->X, 512, nb_pad, net->slab, st)))
             return rc;
     } else if ((rc = launch_conv<256, 32, false>(net->T, W + o.w[1], W + o.scale[1], W + o.shift[1], nullptr, net->X,
-                                                 512, nb_pad, st))) {
+                                                 512, nb_pad, net->slab, st))) {
         return rc;
     }
     if (tm) KV_HIP(hipEventRecord(net->ev[1], st));
@@ -629,19 +723,19 @@ static int net_tower(kv_net* net, int nb, int nb_pad, float* policy, float* valu
     for (int r = 0; r < 5 && bf3; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         if ((rc = launch_conv_bf3<512, false>(net->X, net->whi + o.w[l1], net->wlo + o.w[l1], W + o.scale[l1],
-                                              W + o.shift[l1], nullptr, net->T, 512, nb_pad, st)))
+                                              W + o.shift[l1], nullptr, net->T, 512, nb_pad, net->slab, st)))
             return rc;
         if ((rc = launch_conv_bf3<512, true>(net->T, net->whi + o.w[l2], net->wlo + o.w[l2], W + o.scale[l2],
-                                             W + o.shift[l2], net->X, net->X, 512, nb_pad, st)))
+                                             W + o.shift[l2], net->X, net->X, 512, nb_pad, net->slab, st)))
             return rc;
     }
     for (int r = 0; r < 5 && !bf3; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         if ((rc = launch_conv<512, 32, false>(net->X, W + o.w[l1], W + o.scale[l1], W + o.shift[l1], nullptr, net->T,
-                                              512, nb_pad, st)))
+                                              512, nb_pad, net->slab, st)))
             return rc;
         if ((rc = launch_conv<512, 32, true>(net->T, W + o.w[l2], W + o.scale[l2], W + o.shift[l2], net->X, net->X,
-                                             512, nb_pad, st)))
+                                             512, nb_pad, net->slab, st)))
             return rc;
     }
     if (tm) KV_HIP(hipEventRecord(net->ev[2], st));
@@ -757,6 +851,7 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->w);
     (void)hipFree(net->whi);
     (void)hipFree(net->wlo);
+    (void)hipFree(net->slab);
     (void)hipFree(net->x16);
     (void)hipFree(net->X);
     (void)hipFree(net->T);

@@ -57,13 +57,19 @@ def test_forward_batch_sizes_vs_torch(B, precision):
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 def test_batch_invariance(precision):
-    """A board's outputs do not depend on the batch it is evaluated in."""
+    """A board's outputs do not depend on the batch it is evaluated in, within a
+    batch-size class (<= 16 boards: split-K kernels; > 16: whole-K kernels);
+    across the two classes only the fp32 summation order differs."""
     from knightvision_amd.ai import codes_to_planes
     rng = np.random.default_rng(7)
     codes = rng.integers(0, 13, size=(40, 64)) * (rng.random((40, 64)) < 0.4)
     planes = torch.from_numpy(codes_to_planes(codes)).cuda()
     m = _net("peaked", precision)
-    p_all, v_all = m(planes)
-    for i in (0, 17, 39):
+    p_all, v_all = m(planes)  # 40 boards: whole-K class
+    p_20, v_20 = m(planes[20:])
+    assert torch.equal(p_20, p_all[20:]) and torch.equal(v_20, v_all[20:])
+    p_16, v_16 = m(planes[:16])  # split-K class
+    for i in (0, 5, 15):
         p1, v1 = m(planes[i:i + 1])
-        assert torch.equal(p1[0], p_all[i]) and torch.equal(v1[0], v_all[i])
+        assert torch.equal(p1[0], p_16[i]) and torch.equal(v1[0], v_16[i])
+    assert float((p_16 - p_all[:16]).abs().max()) < 1e-4
