@@ -15,19 +15,10 @@
 
 namespace kv {
 
-__device__ inline Pos pos_from_vec(const int8_t* v) {
-    Pos p;
-    pos_from_board(p, v, v[64], v[65], v[66], v[67], v[68],
-                   (v[69] ? F_WKM : 0) | (v[70] ? F_BKM : 0) | (v[71] ? F_WRK : 0) | (v[72] ? F_WRQ : 0) |
-                       (v[73] ? F_BRK : 0) | (v[74] ? F_BRQ : 0),
-                   v[75] < 0 ? -1 : v[75] * 8 + v[76]);
-    return p;
-}
-
 __device__ inline void pos_to_vec(const Pos& p, int8_t* v) {
     pos_to_board(p, v);
     v[64] = (int8_t)p.wtm;
-    v[65] = p.kr[0]; v[66] = p.kc[0]; v[67] = p.kr[1]; v[68] = p.kc[1];
+    v[65] = p.wkr; v[66] = p.wkc; v[67] = p.bkr; v[68] = p.bkc;
     v[69] = (p.flags & F_WKM) ? 1 : 0; v[70] = (p.flags & F_BKM) ? 1 : 0;
     v[71] = (p.flags & F_WRK) ? 1 : 0; v[72] = (p.flags & F_WRQ) ? 1 : 0;
     v[73] = (p.flags & F_BRK) ? 1 : 0; v[74] = (p.flags & F_BRQ) ? 1 : 0;
@@ -36,32 +27,45 @@ __device__ inline void pos_to_vec(const Pos& p, int8_t* v) {
     v[77] = v[78] = v[79] = 0;
 }
 
-__global__ void k_dev_valid(const int8_t* states, int n, uint16_t* moves, int cap, int* nmoves, int8_t* after,
-                            uint8_t* chk) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    Pos p = pos_from_vec(states + (size_t)i * 80);
-    MoveOut o{moves + (size_t)i * cap, 0, cap, 0};
-    const int m = valid_moves(p, o);
-    nmoves[i] = o.overflow ? -m : m;
-    pos_to_vec(p, after + (size_t)i * 80);
-    chk[i] = in_check(p) ? 1 : 0;
+__device__ inline Pos wave_pos_from_vec(const int8_t* v, int lane) {
+    return wave_pos(v[lane], v[64], v[65], v[66], v[67], v[68],
+                    (v[69] ? F_WKM : 0) | (v[70] ? F_BKM : 0) | (v[71] ? F_WRK : 0) | (v[72] ? F_WRQ : 0) |
+                        (v[73] ? F_BRK : 0) | (v[74] ? F_BRQ : 0),
+                    v[75] < 0 ? -1 : v[75] * 8 + v[76]);
 }
 
-__global__ void k_dev_make(int8_t* states, const int* index, int n, uint16_t* scratch, int* status) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// one wave per position, exactly as the engine runs the generator
+__global__ __launch_bounds__(64) void k_dev_valid(const int8_t* states, int n, uint16_t* moves, int cap,
+                                                  int* nmoves, int8_t* after, uint8_t* chk) {
+    const int i = blockIdx.x, lane = threadIdx.x;
+    if (i >= n) return;
+    Pos p = wave_pos_from_vec(states + (size_t)i * 80, lane);
+    const int m = wave_valid_moves(p, moves + (size_t)i * cap, cap, lane);
+    const bool c = in_check(p);
+    if (lane == 0) {
+        nmoves[i] = m > cap ? -m : m;
+        pos_to_vec(p, after + (size_t)i * 80);
+        chk[i] = c ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_dev_make(int8_t* states, const int* index, int n, uint16_t* scratch,
+                                                 int* status) {
+    const int i = blockIdx.x, lane = threadIdx.x;
     if (i >= n) return;
     int8_t* v = states + (size_t)i * 80;
-    Pos p = pos_from_vec(v);
-    MoveOut o{scratch + (size_t)i * MAXM, 0, MAXM, 0};
-    const int m = valid_moves(p, o);
+    Pos p = wave_pos_from_vec(v, lane);
+    uint16_t* ml = scratch + (size_t)i * MAXM;
+    const int m = wave_valid_moves(p, ml, MAXM, lane);
+    __syncthreads();
+    if (lane != 0) return;
     if (index[i] < 0 || index[i] >= m || index[i] >= MAXM) {
         status[i] = -1;
         return;
     }
     pos_to_vec(p, v);
-    int wtm = p.wtm, wkr = p.kr[0], wkc = p.kc[0], bkr = p.kr[1], bkc = p.kc[1], fl = p.flags, ep = p.ep;
-    make_move_board(v, wtm, wkr, wkc, bkr, bkc, fl, ep, o.m[index[i]]);
+    int wtm = p.wtm, wkr = p.wkr, wkc = p.wkc, bkr = p.bkr, bkc = p.bkc, fl = p.flags, ep = p.ep;
+    make_move_board(v, wtm, wkr, wkc, bkr, bkc, fl, ep, ml[index[i]]);
     Pos q;
     pos_from_board(q, v, wtm, wkr, wkc, bkr, bkc, fl, ep);
     pos_to_vec(q, v);
@@ -128,7 +132,7 @@ int kv_dev_valid_moves(int device, const int8_t* states, int n, uint16_t* moves_
     KV_HIP(nm.alloc(n));
     KV_HIP(c.alloc(n));
     KV_HIP(hipMemcpy(s.p, states, (size_t)n * 80, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(kv::k_dev_valid, dim3((n + 63) / 64), dim3(64), 0, 0, s.p, n, m.p, cap, nm.p, a.p, c.p);
+    hipLaunchKernelGGL(kv::k_dev_valid, dim3(n), dim3(64), 0, 0, s.p, n, m.p, cap, nm.p, a.p, c.p);
     KV_HIP(hipGetLastError());
     KV_HIP(hipDeviceSynchronize());
     KV_HIP(hipMemcpy(moves_out, m.p, (size_t)n * cap * sizeof(uint16_t), hipMemcpyDeviceToHost));
@@ -150,7 +154,7 @@ int kv_dev_make_move(int device, int8_t* states, const int* index, int n) {
     KV_HIP(scr.alloc((size_t)n * kv::MAXM));
     KV_HIP(hipMemcpy(s.p, states, (size_t)n * 80, hipMemcpyHostToDevice));
     KV_HIP(hipMemcpy(ix.p, index, (size_t)n * sizeof(int), hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(kv::k_dev_make, dim3((n + 63) / 64), dim3(64), 0, 0, s.p, ix.p, n, scr.p, stt.p);
+    hipLaunchKernelGGL(kv::k_dev_make, dim3(n), dim3(64), 0, 0, s.p, ix.p, n, scr.p, stt.p);
     KV_HIP(hipGetLastError());
     KV_HIP(hipDeviceSynchronize());
     std::vector<int> st(n);

@@ -76,7 +76,7 @@ __device__ inline Pos slot_pos(const Slot& s, const int8_t* board) {
 __device__ inline void slot_store_pos(Slot& s, int8_t* board, const Pos& p) {
     pos_to_board(p, board);
     s.wtm = p.wtm;
-    s.wkr = p.kr[0]; s.wkc = p.kc[0]; s.bkr = p.kr[1]; s.bkc = p.kc[1];
+    s.wkr = p.wkr; s.wkc = p.wkc; s.bkr = p.bkr; s.bkc = p.bkc;
     s.flags = p.flags;
     s.ep = p.ep;
 }

@@ -2,8 +2,8 @@
 // :111-255 / self_play :258-291 for `slots` concurrent games per GPU.
 //
 // One ply-step of every live game slot is four launches on one stream:
-//   k_movegen  one lane per slot: reference-exact legal list (kv_movegen.h),
-//              game-over detection, SELFPLAY_BATCH_SIZE schedule bookkeeping
+//   k_movegen  one wave per slot, lane = square: reference-exact legal list
+//              (kv_movegen.h wave_valid_moves), game-over detection, SELFPLAY_BATCH_SIZE schedule bookkeeping
 //   NN         ChessNet over the slots' boards (kv_nn.hip) -- every board is
 //              evaluated once, as the reference does (faithful), or only the
 //              rows the schedule consumes (lazy)
@@ -12,7 +12,7 @@
 //              0.75/0.25 mix in the reference's fp32/fp64 order, CPython
 //              random.choices on the slot's second stream, makeMove, record,
 //              termination (draw / resign / max_moves)
-//   k_finish   one lane per slot: outcome + reward exactly as :210-250, game
+//   k_finish   one wave per finished slot: outcome + reward exactly as :210-250, game
 //              record, then the slot starts the next game id (recycling)
 // The host only launches and, every few steps, reads one counter.
 #include <hip/hip_runtime.h>
@@ -85,16 +85,19 @@ __global__ void k_init(DevCfg cfg, Slot* slots, int8_t* boards, uint32_t* np_mt,
 // ------------------------------------------------------------ movegen ----
 __global__ __launch_bounds__(64) void k_movegen(DevCfg cfg, Slot* slots, int8_t* boards, uint16_t* moves,
                                                 Ctr* ctr) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= cfg.slots) return;
+    const int i = blockIdx.x, lane = threadIdx.x;
     Slot s = slots[i];
     if (s.status != ST_ACTIVE) return;
     int8_t* board = boards + (size_t)i * 64;
-    Pos p = slot_pos(s, board);
-    MoveOut o{moves + (size_t)i * MAXM, 0, MAXM, 0};
-    const int n = valid_moves(p, o);
-    if (o.overflow) atomicOr(&ctr->error, 1);
-    slot_store_pos(s, board, p);  // the reference may mutate the board (stale king, double check)
+    Pos p = wave_pos(board[lane], s.wtm, s.wkr, s.wkc, s.bkr, s.bkc, s.flags, s.ep);
+    const int n = wave_valid_moves(p, moves + (size_t)i * MAXM, MAXM, lane);
+    board[lane] = (int8_t)pos_at(p, lane);  // the reference may mutate the board (stale king, double check)
+    if (lane != 0) return;
+    if (n > MAXM) atomicOr(&ctr->error, 1);
+    s.wtm = p.wtm;
+    s.wkr = p.wkr; s.wkc = p.wkc; s.bkr = p.bkr; s.bkc = p.bkc;
+    s.flags = p.flags;
+    s.ep = p.ep;
     s.nmoves = n < MAXM ? n : MAXM;
     if (n == 0) {
         s.end_kind = END_NOMOVES;
@@ -150,11 +153,10 @@ __global__ __launch_bounds__(64) void k_sample(DevCfg cfg, Slot* slots, int8_t* 
 // ------------------------------------------------------------- finish ----
 __global__ __launch_bounds__(64) void k_finish(DevCfg cfg, Slot* slots, int8_t* boards, uint16_t* moves,
                                                uint32_t* np_mt, uint32_t* py_mt, kv_game* games, Ctr* ctr) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= cfg.slots) return;
+    const int i = blockIdx.x, lane = threadIdx.x;
     Slot s = slots[i];
     if (s.status == ST_ACTIVE) {
-        atomicAdd(&ctr->active, 1);
+        if (lane == 0) atomicAdd(&ctr->active, 1);
         return;
     }
     if (s.status != ST_FINISHED) return;
@@ -164,28 +166,30 @@ __global__ __launch_bounds__(64) void k_finish(DevCfg cfg, Slot* slots, int8_t* 
         s.outcome = 0;
         s.reason = 0;
     } else if (s.end_kind != END_RESIGN) {
-        Pos p = slot_pos(s, board);
-        MoveOut o{moves + (size_t)i * MAXM, 0, MAXM, 0};
+        Pos p = wave_pos(board[lane], s.wtm, s.wkr, s.wkc, s.bkr, s.bkc, s.flags, s.ep);
+        uint16_t* ml = moves + (size_t)i * MAXM;
         const bool chk = in_check(p);
         int n1 = -1;
-        if (chk) n1 = valid_moves(p, o);
+        if (chk) n1 = wave_valid_moves(p, ml, MAXM, lane);
         if (chk && n1 == 0) {
             s.outcome = p.wtm ? -1 : 1;
             s.reason = 2;
-        } else if (valid_moves(p, o) == 0) {
+        } else if (wave_valid_moves(p, ml, MAXM, lane) == 0) {
             s.outcome = 0;
             s.reason = 3;
         } else {
-            bool kings_only = true;
-            for (int q = 0; q < 64; ++q) {
-                const int c = pos_at(p, q);
-                if (c != 0 && c != 1 && c != 7) kings_only = false;
-            }
+            const bool kings_only = (p.w | p.b) == p.K;
             s.outcome = 0;
             s.reason = kings_only ? 4 : 5;  // material branch: always 0 (see oracle/kv_oracle.c)
         }
-        slot_store_pos(s, board, p);
+        board[lane] = (int8_t)pos_at(p, lane);
+        s.wtm = p.wtm;
+        s.wkr = p.wkr; s.wkc = p.wkc; s.bkr = p.bkr; s.bkc = p.bkc;
+        s.flags = p.flags;
+        s.ep = p.ep;
     }
+    __syncthreads();
+    if (lane != 0) return;
     // flush of a non-empty buffer (:202-208): one more forward call
     if (cfg.sims == 0 && s.buf > 0) {
         s.n_evals += 1;
@@ -448,7 +452,7 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
     long long done = 0;
     while ((max_steps < 0 || done < max_steps) && e->ctr_host->active > 0 &&
            (stop_after_games < 0 || (int64_t)e->ctr_host->games_count < stop_after_games)) {
-        hipLaunchKernelGGL(kv::k_movegen, dim3((S + 63) / 64), dim3(64), 0, e->st, e->dc, e->slots, e->boards,
+        hipLaunchKernelGGL(kv::k_movegen, dim3(S), dim3(64), 0, e->st, e->dc, e->slots, e->boards,
                            e->moves, e->ctr);
         KV_HIP(hipGetLastError());
         if (e->dc.rows > S)
@@ -476,7 +480,7 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
                 return rc;
         }
         KV_HIP(hipMemsetAsync(&e->ctr->active, 0, sizeof(int), e->st));
-        hipLaunchKernelGGL(kv::k_finish, dim3((S + 63) / 64), dim3(64), 0, e->st, e->dc, e->slots, e->boards,
+        hipLaunchKernelGGL(kv::k_finish, dim3(S), dim3(64), 0, e->st, e->dc, e->slots, e->boards,
                            e->moves, e->np_mt, e->py_mt, e->games, e->ctr);
         KV_HIP(hipGetLastError());
         ++done;

@@ -142,33 +142,31 @@ __global__ __launch_bounds__(64) void k_mcts_select(DevCfg cfg, Tree t, const Sl
         }
         node = child;
     }
-    if (lane == 0) {
-        MctsSlot m = t.ms[i];
-        m.path_len = depth;
-        m.leaf_edge = leaf;
-        m.leaf_pending = 0;
-        m.leaf_n = 0;
+    MctsSlot m = t.ms[i];
+    m.path_len = depth;
+    m.leaf_edge = leaf;
+    m.leaf_pending = 0;
+    m.leaf_n = 0;
+    m.leaf_value = 0.f;
+    const int8_t code = bd[lane];
+    if (__ballot(code != 0 && code != 1 && code != 7) == 0ull) {
+        // GameState.isDraw after the move ends the game (self_play.py:180)
         m.leaf_value = 0.f;
-        if (is_draw_board(bd)) {  // GameState.isDraw after the move ends the game (self_play.py:180)
-            m.leaf_value = 0.f;
+    } else {
+        Pos p = wave_pos(code, s_meta[0], s_meta[1], s_meta[2], s_meta[3], s_meta[4], s_meta[5], s_meta[6]);
+        const int n = wave_valid_moves(p, t.leaf_moves + (size_t)i * MAXM, MAXM, lane);
+        if (n > MAXM && lane == 0) atomicOr(&ctr->error, 1);
+        m.leaf_wtm = p.wtm;
+        if (n == 0) {
+            m.leaf_value = in_check(p) ? (p.wtm ? -1.f : 1.f) : 0.f;  // mate / stalemate
         } else {
-            Pos p;
-            pos_from_board(p, bd, s_meta[0], s_meta[1], s_meta[2], s_meta[3], s_meta[4], s_meta[5], s_meta[6]);
-            MoveOut o{t.leaf_moves + (size_t)i * MAXM, 0, MAXM, 0};
-            const int n = valid_moves(p, o);
-            if (o.overflow) atomicOr(&ctr->error, 1);
-            m.leaf_wtm = p.wtm;
-            if (n == 0) {
-                m.leaf_value = in_check(p) ? (p.wtm ? -1.f : 1.f) : 0.f;  // mate / stalemate
-            } else {
-                pos_to_board(p, bd);  // the board the reference would encode (after getValidMoves)
-                m.leaf_pending = 1;
-                m.leaf_n = n < MAXM ? n : MAXM;
-                atomicAdd(&ctr->nn_rows, 1ull);
-            }
+            bd[lane] = (int8_t)pos_at(p, lane);  // the board the reference would encode (after getValidMoves)
+            m.leaf_pending = 1;
+            m.leaf_n = n < MAXM ? n : MAXM;
+            if (lane == 0) atomicAdd(&ctr->nn_rows, 1ull);
         }
-        t.ms[i] = m;
     }
+    if (lane == 0) t.ms[i] = m;
     __syncthreads();
     nn_boards[(size_t)i * 64 + lane] = bd[lane];
 }
