@@ -31,6 +31,7 @@ sys.path.insert(0, HERE)
 
 FLOP_PER_EVAL = 3175744512            # SURVEY.md 8d, ChessNet forward per position
 FLOP_RES_CONV_PER_BOARD = 301989888   # one 3x3 512->512 conv on 8x8 (2*64*512*4608)
+FLOP_WINO_GEMM_PER_BOARD = 75497472   # its Winograd F(4x4,3x3) GEMMs: 2 * 4 tiles * 36 * 512 * 512
 FP32_MFMA_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md, f32-input MFMA (dense)
 
 
@@ -43,6 +44,10 @@ def parse():
     ap.add_argument("--slots", type=int, default=256)
     ap.add_argument("--sims", type=int, default=400)
     ap.add_argument("--precision", choices=["fp32", "bf16x3"], default="fp32")
+    ap.add_argument("--algo", choices=["auto", "direct", "winograd"], default="auto",
+                    help="conv algorithm of the fp32 tower (auto: Winograd F(4x4,3x3) above 16 boards)")
+    ap.add_argument("--compare-direct", type=int, default=1,
+                    help="also measure the fp32 direct implicit-GEMM convs (reported under 'fp32_direct')")
     ap.add_argument("--alt-precision", default="bf16x3",
                     help="also measure this network precision (reported under 'alt_precision'; '' to skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -105,10 +110,11 @@ def main():
     warmup = args.warmup if args.warmup is not None else (1 if mcts else 8)
     G = args.slots
 
-    def measure(precision):
+    def measure(precision, algo="auto"):
         eng = SelfPlayEngine(synthetic_state_dict(42, "init"), slots=G, n_games=1 << 40, seed=42, max_moves=None,
                              batch=16, sims=sims, game_id_base=rank, game_id_stride=world,
-                             record_cap=max(1 << 16, G * (steps + warmup + 8)), device=local, precision=precision)
+                             record_cap=max(1 << 16, G * (steps + warmup + 8)), device=local, precision=precision,
+                             algo=algo)
         eng.run(warmup)
         s0 = eng.stats()
         if world > 1:
@@ -135,14 +141,17 @@ def main():
         launches = max(d["res_conv_launches"], 1)
         conv_ms = d["res_conv_ms"] / launches
         return dict(dt=dt, plies=plies, games_done=games_done, nn_rows=nn_rows, sims=sims_done, conv_ms=conv_ms,
-                    recs=recs, gms=gms)
+                    recs=recs, gms=gms, dom_flop=s1["dom_flop"], dom_algo=s1["dom_algo"])
 
-    m = measure(args.precision)
+    m = measure(args.precision, args.algo)
     dt, plies, games_done, nn_rows, sims_done, conv_ms = (m[k] for k in ("dt", "plies", "games_done", "nn_rows",
                                                                           "sims", "conv_ms"))
     alt = None
     if args.alt_precision and args.alt_precision != args.precision:
         alt = measure(args.alt_precision)
+    direct = None
+    if args.compare_direct and args.precision == "fp32" and m["dom_algo"] == 2:
+        direct = measure("fp32", "direct")
 
     # experience gather (RCCL all-gather of packed records), outside `value`
     recs, gms = m["recs"], m["gms"]
@@ -155,13 +164,18 @@ def main():
     gather_ms = (time.perf_counter() - tg) * 1e3
     mean_len = float(gms_all["plies"].mean()) if len(gms_all) else float("nan")
 
-    # roofline of the dominant kernel (residual 3x3 conv), HIP events on the engine stream
-    rows_per_launch = G
-    achieved = FLOP_RES_CONV_PER_BOARD * rows_per_launch / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
+    # roofline of the dominant kernel, timed with HIP events on the engine stream: the residual-tower
+    # Winograd GEMM launch (36 x [4*boards x 512 x 512]) or, for the direct algorithm, the residual conv
+    wino = m["dom_algo"] == 2
+    flop_alg = (FLOP_WINO_GEMM_PER_BOARD if wino else FLOP_RES_CONV_PER_BOARD) * G
+    achieved = flop_alg / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
+    kname = "wino_gemm_kernel<512,4,1,2>" if wino else "conv3x3_kernel<512,32>"
     traffic = None
-    pmc = os.path.join(HERE, "profiles", "r01_pmc_resconv.json")
+    pmc = os.path.join(HERE, "profiles", "r01_pmc_wino_gemm.json" if wino else "r01_pmc_resconv.json")
     if os.path.exists(pmc):
-        traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        pj = json.load(open(pmc))
+        if pj.get("batch") == G and pj.get("kernel", "").split("<")[0] == kname.split("<")[0]:
+            traffic = pj.get("hbm_bytes_per_launch")
 
     if rank == 0:
         if mcts:
@@ -188,12 +202,24 @@ def main():
             "games_completed": games_done, "nn_evals_per_s": nn_rows / dt,
             "nn_tflops": nn_rows * FLOP_PER_EVAL / dt / 1e12, "gather_ms": gather_ms,
             "records_gathered": int(len(recs_all)),
-            "roofline": {"bound": "mfma", "kernel": "conv3x3_kernel<512,32> (residual tower)",
+            "roofline": {"bound": "mfma",
+                         "kernel": kname + (" (residual-tower Winograd F(4x4,3x3) GEMMs)" if wino
+                                            else " (residual-tower 3x3 conv, implicit GEMM)"),
                          "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None,
-                         "traffic": traffic, "avg_launch_ms": conv_ms, "rows_per_launch": rows_per_launch,
-                         "flop_per_launch": FLOP_RES_CONV_PER_BOARD * rows_per_launch},
+                         "traffic": traffic, "avg_launch_ms": conv_ms, "boards_per_launch": G,
+                         "flop_per_launch": flop_alg, "mfma_flop_per_launch_incl_padding": m["dom_flop"],
+                         "direct_conv_equiv_tflops": (FLOP_RES_CONV_PER_BOARD * G / (conv_ms * 1e-3) / 1e12
+                                                      if conv_ms > 0 else None)},
         }
+        if direct is not None:
+            d_ach = (FLOP_RES_CONV_PER_BOARD * G / (direct["conv_ms"] * 1e-3) / 1e12) if direct["conv_ms"] > 0 else None
+            out["fp32_direct"] = {
+                "note": "same fp32 network with the direct implicit-GEMM convs (exact fp32 products, 9 taps)",
+                "value": (direct["sims"] if mcts else direct["plies"]) / direct["dt"], "unit": unit,
+                "ms_per_step": direct["dt"] * 1e3 / steps,
+                "res_conv_avg_launch_ms": direct["conv_ms"], "res_conv_tflops": d_ach,
+                "res_conv_frac": (d_ach / FP32_MFMA_PEAK_TFLOPS) if d_ach else None}
         if alt is not None:
             a_ach = (FLOP_RES_CONV_PER_BOARD * G / (alt["conv_ms"] * 1e-3) / 1e12) if alt["conv_ms"] > 0 else None
             out["alt_precision"] = {

@@ -65,6 +65,16 @@ int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv);
 #define KV_PREC_FP32 0
 #define KV_PREC_BF16X3 1
 int kv_net_set_precision(kv_net* net, int precision);
+/* Algorithm of the fp32 3x3 convs with Cin 256/512:
+ * KV_ALGO_AUTO      Winograd for batches > 16 boards, direct (split-K) below
+ * KV_ALGO_DIRECT    implicit GEMM over the 9 taps (exact fp32 products)
+ * KV_ALGO_WINOGRAD  F(4x4,3x3): 36 GEMMs of 4 tiles x Cin x Cout per board, 4x
+ *                   fewer FLOPs, fp32 transforms (logits within 1e-4)
+ * Results are batch-invariant inside a class (<= 16 boards, > 16 boards). */
+#define KV_ALGO_AUTO 0
+#define KV_ALGO_DIRECT 1
+#define KV_ALGO_WINOGRAD 2
+int kv_net_set_algo(kv_net* net, int algo);
 int kv_net_set_timing(kv_net* net, int enable);
 void kv_net_destroy(kv_net* net);
 
@@ -97,6 +107,7 @@ typedef struct {
     int64_t record_cap;   /* record buffer capacity */
     int recycle;          /* 1: a finished slot starts the next game id */
     int precision;        /* KV_PREC_* of the network convs */
+    int algo;             /* KV_ALGO_* of the network convs */
 } kv_config;
 
 typedef struct {
@@ -124,9 +135,13 @@ typedef struct {
     int64_t nn_rows;      /* boards evaluated by the network */
     int64_t sims;         /* MCTS backups completed */
     int64_t records;
-    double res_conv_ms;   /* device time of the residual-tower conv launches (HIP events) */
+    double res_conv_ms;   /* device time of the measured dominant-kernel launches (HIP events):
+                             direct: the 10 residual convs of each forward; Winograd: one
+                             residual GEMM launch per forward */
     int64_t res_conv_launches;
     double step_ms;       /* wall time inside kv_run */
+    double dom_flop;      /* MFMA FLOPs of one measured launch (padded rows included) */
+    int64_t dom_algo;     /* KV_ALGO_DIRECT or KV_ALGO_WINOGRAD for those launches */
 } kv_stats;
 
 typedef struct kv_engine kv_engine;

@@ -20,7 +20,7 @@ class Config(C.Structure):
                 ("game_id_stride", C.c_int64), ("seed", C.c_uint64), ("seed_mode", C.c_int),
                 ("max_moves", C.c_int), ("batch", C.c_int), ("eps", C.c_double), ("alpha", C.c_double),
                 ("sims", C.c_int), ("c_puct", C.c_float), ("eval_mode", C.c_int), ("record_cap", C.c_int64),
-                ("recycle", C.c_int), ("precision", C.c_int)]
+                ("recycle", C.c_int), ("precision", C.c_int), ("algo", C.c_int)]
 
 
 class Record(C.Structure):
@@ -36,7 +36,8 @@ class Game(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("steps", C.c_int64), ("plies", C.c_int64), ("games_done", C.c_int64), ("nn_rows", C.c_int64),
                 ("sims", C.c_int64), ("records", C.c_int64), ("res_conv_ms", C.c_double),
-                ("res_conv_launches", C.c_int64), ("step_ms", C.c_double)]
+                ("res_conv_launches", C.c_int64), ("step_ms", C.c_double), ("dom_flop", C.c_double),
+                ("dom_algo", C.c_int64)]
 
 
 assert C.sizeof(Record) == 80 and C.sizeof(Game) == 32
@@ -57,6 +58,7 @@ def _declare(L):
         "kv_net_last_timing": ([vp, P(C.c_float), P(i)], i),
         "kv_net_destroy": ([vp], None),
         "kv_net_set_precision": ([vp, i], i),
+        "kv_net_set_algo": ([vp, i], i),
         "kv_create": ([P(Config), P(vp)], i),
         "kv_load_weights": ([vp, P(C.c_float), sz], i),
         "kv_run": ([vp, i64, i64], i),
@@ -82,7 +84,8 @@ def _declare(L):
 
 
 EXPORTED = ["kv_last_error", "kv_version", "kv_net_packed_size", "kv_net_create", "kv_net_load", "kv_net_forward",
-            "kv_net_forward_boards", "kv_net_set_timing", "kv_net_last_timing", "kv_net_destroy", "kv_net_set_precision", "kv_create",
+            "kv_net_forward_boards", "kv_net_set_timing", "kv_net_last_timing", "kv_net_destroy", "kv_net_set_precision", "kv_net_set_algo",
+            "kv_create",
             "kv_load_weights", "kv_run", "kv_set_max_moves", "kv_records", "kv_games", "kv_stats_get", "kv_sync", "kv_reset_records", "kv_destroy",
             "kv_dev_valid_moves", "kv_dev_make_move", "kv_dev_dirichlet", "kv_dev_py_random"]
 

@@ -251,6 +251,8 @@ struct kv_engine {
     int n_ev_used = 0;
     double nn_res_ms = 0;
     long long nn_res_launches = 0;
+    int dom_algo = KV_ALGO_DIRECT, dom_launches = 10;  // what each event pair brackets
+    double dom_flop = 0;
     bool loaded = false;
     // MCTS (sims > 0)
     kv::Tree tree;
@@ -277,7 +279,7 @@ static int eng_collect_timing(kv_engine* e) {
         KV_HIP(hipEventSynchronize(e->ev[k + 1]));
         KV_HIP(hipEventElapsedTime(&ms, e->ev[k], e->ev[k + 1]));
         e->nn_res_ms += ms;
-        e->nn_res_launches += 10;
+        e->nn_res_launches += e->dom_launches;
     }
     e->n_ev_used = 0;
     return KV_OK;
@@ -384,7 +386,8 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
         kv::set_error("kv_create: hipHostMalloc failed");
         return KV_ENOMEM;
     }
-    if ((rc = kv_net_create(cfg->device, &e->net)) || (rc = kv_net_set_precision(e->net, cfg->precision))) {
+    if ((rc = kv_net_create(cfg->device, &e->net)) || (rc = kv_net_set_precision(e->net, cfg->precision)) ||
+        (rc = kv_net_set_algo(e->net, cfg->algo))) {
         kv_destroy(e);
         return rc;
     }
@@ -437,6 +440,7 @@ static int eng_eval(kv_engine* e, const int8_t* boards, int rows) {
     e->n_ev_used += 2;
     const int rc = kv::net_forward_boards_internal(e->net, boards, rows, e->logits, e->values, e->st);
     kv::net_set_res_events(e->net, nullptr, nullptr);
+    kv::net_dom_info(e->net, &e->dom_algo, &e->dom_launches, &e->dom_flop);
     return rc;
 }
 
@@ -550,6 +554,8 @@ int kv_stats_get(kv_engine* e, kv_stats* out) {
     out->res_conv_ms = e->nn_res_ms;
     out->res_conv_launches = e->nn_res_launches;
     out->step_ms = e->wall_ms;
+    out->dom_flop = e->dom_flop;
+    out->dom_algo = e->dom_algo;
     return KV_OK;
 }
 

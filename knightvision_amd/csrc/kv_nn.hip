@@ -19,6 +19,7 @@
 #include <string.h>
 
 #include "kv_common.h"
+#include "kv_wino.h"
 
 namespace kv {
 
@@ -607,6 +608,15 @@ struct kv_net {
     uint16_t* whi = nullptr;  // bf16x3: split conv weights, layers 1..11, same offsets as w
     uint16_t* wlo = nullptr;
     float* slab = nullptr;  // split-K partial sums (small batches)
+    int algo = KV_ALGO_AUTO;
+    float* U = nullptr;     // Winograd weights [36][Cout][Cin] of convs 1..11
+    size_t uoff[12] = {};
+    float* V = nullptr;     // Winograd workspaces [36][cap*4][512]
+    float* Mw = nullptr;
+    // the dominant kernel bracketed by res_a/res_b in the last forward
+    int dom_algo = KV_ALGO_DIRECT;
+    int dom_launches = 10;
+    double dom_flop = 0;
 };
 
 // Small batches (<= 16 boards: the sequential reference path, batch-16
@@ -683,19 +693,115 @@ static int launch_conv(const float* in, const float* w, const float* sc, const f
     return KV_OK;
 }
 
+// Winograd for the fp32 tower when the batch is past the split-K class
+static bool use_wino(const kv_net* net, int B) {
+    if (net->precision != KV_PREC_FP32) return false;
+    if (net->algo == KV_ALGO_WINOGRAD) return true;
+    return net->algo == KV_ALGO_AUTO && B > kSplitMaxBoards;
+}
+
+// padded batch: a multiple of 4 boards (direct tiles) or 32 (128-row GEMM tiles)
+static int net_pad(const kv_net* net, int B) { return use_wino(net, B) ? (B + 31) & ~31 : (B + 3) & ~3; }
+
 static int net_reserve(kv_net* net, int nb_pad) {
     if (nb_pad <= net->cap) return KV_OK;
     int cap = nb_pad < 64 ? 64 : nb_pad;
     (void)hipFree(net->x16); (void)hipFree(net->X); (void)hipFree(net->T); (void)hipFree(net->pfeat);
-    net->x16 = net->X = net->T = net->pfeat = nullptr;
+    (void)hipFree(net->V); (void)hipFree(net->Mw);
+    net->x16 = net->X = net->T = net->pfeat = net->V = net->Mw = nullptr;
     net->cap = 0;
     KV_HIP(hipMalloc(&net->x16, (size_t)cap * 64 * 16 * 4));
     KV_HIP(hipMalloc(&net->X, (size_t)cap * 64 * 512 * 4));
     KV_HIP(hipMalloc(&net->T, (size_t)cap * 64 * 512 * 4));
     KV_HIP(hipMalloc(&net->pfeat, (size_t)cap * 128 * 4));
+    KV_HIP(hipMalloc(&net->V, (size_t)kv::WN_XI * cap * 4 * 512 * 4));
+    KV_HIP(hipMalloc(&net->Mw, (size_t)kv::WN_XI * cap * 4 * 512 * 4));
     if (!net->slab)  // 48 splits x 16 boards x 64 px x 512 channels
         KV_HIP(hipMalloc(&net->slab, (size_t)(144 / kSplitKt) * kSplitMaxBoards * 64 * 512 * 4));
     net->cap = cap;
+    return KV_OK;
+}
+
+static int net_heads(kv_net* net, int nb, float* policy, float* value, hipStream_t st);
+
+template <int K, int WR, int MT, int NT>
+static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows, hipStream_t st) {
+    using T = kv::WinoTile<WR, MT, NT>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        KV_HIP(hipFuncSetAttribute((const void*)kv::wino_gemm_kernel<K, WR, MT, NT>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::BYTES));
+        attr_set = true;
+    }
+    KV_REQUIRE(rows % T::WM == 0, KV_EINVAL, "wino gemm: rows %d not a multiple of %d", rows, T::WM);
+    hipLaunchKernelGGL((kv::wino_gemm_kernel<K, WR, MT, NT>), dim3(512 / T::WN, rows / T::WM, kv::WN_XI), dim3(512),
+                       T::BYTES, st, V, U, M, rows, 512);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+static int wino_tile_choice() {
+    static int c = -1;
+    if (c < 0) {
+        const char* e = getenv("KV_WINO_TILE");
+        c = e ? atoi(e) : 0;
+    }
+    return c;
+}
+
+template <int K>
+static int launch_wino_gemm(const float* V, const float* U, float* M, int rows, hipStream_t st) {
+    switch (wino_tile_choice()) {
+        case 1: return launch_wino_gemm_t<K, 2, 1, 2>(V, U, M, rows, st);  // 64 x 256
+        case 2: return launch_wino_gemm_t<K, 1, 2, 1>(V, U, M, rows, st);  // 64 x 256
+        case 4: return launch_wino_gemm_t<K, 2, 2, 1>(V, U, M, rows, st);  // 128 x 128
+        case 5: return launch_wino_gemm_t<K, 2, 2, 2>(V, U, M, rows, st);  // 128 x 256
+        default: return launch_wino_gemm_t<K, 4, 1, 2>(V, U, M, rows, st);  // 128 x 128, 2 workgroups / CU
+    }
+}
+
+template <bool RESID, bool WRITE_Y, bool NEXT_V>
+static int launch_wino_out(const float* M, int nb_pad, const float* sc, const float* sh, const float* resid, float* Y,
+                           float* Vn, hipStream_t st) {
+    hipLaunchKernelGGL((kv::wino_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 64, nb_pad), dim3(256), 0, st, M,
+                       nb_pad * 4, sc, sh, resid, Y, Vn);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+// Winograd tower: conv2 and the 5 residual blocks (conv1 output in net->T)
+static int net_tower_wino(kv_net* net, int nb_pad, hipStream_t st) {
+    const float* W = net->w;
+    const kv::PackOffsets& o = net->off;
+    const int rows = nb_pad * 4;
+    int rc;
+    hipLaunchKernelGGL(kv::wino_in_kernel<256>, dim3(256 / 64, nb_pad), dim3(256), 0, st, net->T, rows, net->V);
+    KV_HIP(hipGetLastError());
+    if ((rc = launch_wino_gemm<256>(net->V, net->U + net->uoff[1], net->Mw, rows, st))) return rc;
+    if ((rc = launch_wino_out<false, true, true>(net->Mw, nb_pad, W + o.scale[1], W + o.shift[1], nullptr, net->X,
+                                                 net->V, st)))
+        return rc;
+    if (net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
+    for (int r = 0; r < 5; ++r) {
+        const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
+        const bool mark = r == 2;  // one representative residual GEMM for the engine's timing hook
+        if (mark && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
+        if ((rc = launch_wino_gemm<512>(net->V, net->U + net->uoff[l1], net->Mw, rows, st))) return rc;
+        if (mark && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
+        if ((rc = launch_wino_out<false, false, true>(net->Mw, nb_pad, W + o.scale[l1], W + o.shift[l1], nullptr,
+                                                      nullptr, net->V, st)))
+            return rc;
+        if ((rc = launch_wino_gemm<512>(net->V, net->U + net->uoff[l2], net->Mw, rows, st))) return rc;
+        rc = r < 4 ? launch_wino_out<true, true, true>(net->Mw, nb_pad, W + o.scale[l2], W + o.shift[l2], net->X,
+                                                       net->X, net->V, st)
+                   : launch_wino_out<true, true, false>(net->Mw, nb_pad, W + o.scale[l2], W + o.shift[l2], net->X,
+                                                        net->X, nullptr, st);
+        if (rc) return rc;
+    }
+    if (net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
+    net->dom_algo = KV_ALGO_WINOGRAD;
+    net->dom_launches = 1;
+    net->dom_flop = 2.0 * kv::WN_XI * rows * 512.0 * 512.0;
     return KV_OK;
 }
 
@@ -705,6 +811,14 @@ static int net_tower(kv_net* net, int nb, int nb_pad, float* policy, float* valu
     const kv::PackOffsets& o = net->off;
     int rc;
     const bool tm = net->timing;
+    if (use_wino(net, nb)) {
+        if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
+        if ((rc = launch_conv<16, 16, false>(net->x16, W + o.w[0], W + o.scale[0], W + o.shift[0], nullptr, net->T,
+                                             256, nb_pad, nullptr, st)))
+            return rc;
+        if ((rc = net_tower_wino(net, nb_pad, st))) return rc;
+        return net_heads(net, nb, policy, value, st);
+    }
     if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
     if ((rc = launch_conv<16, 16, false>(net->x16, W + o.w[0], W + o.scale[0], W + o.shift[0], nullptr, net->T, 256,
                                          nb_pad, nullptr, st)))
@@ -740,6 +854,15 @@ static int net_tower(kv_net* net, int nb, int nb_pad, float* policy, float* valu
     }
     if (tm) KV_HIP(hipEventRecord(net->ev[2], st));
     if (net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
+    net->dom_algo = KV_ALGO_DIRECT;
+    net->dom_launches = 10;
+    net->dom_flop = (double)nb_pad * 64 * 512 * 4608 * 2;
+    return net_heads(net, nb, policy, value, st);
+}
+
+static int net_heads(kv_net* net, int nb, float* policy, float* value, hipStream_t st) {
+    const float* W = net->w;
+    const kv::PackOffsets& o = net->off;
     hipLaunchKernelGGL(kv::heads_kernel, dim3(nb), dim3(256), 0, st, net->X, W + o.head_w, W + o.head_scale,
                        W + o.head_shift, W + o.vfc1_w, W + o.vfc1_b, W + o.vfc2_w, W + o.vfc2_b, net->pfeat, value);
     KV_HIP(hipGetLastError());
@@ -789,8 +912,30 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
                            net->w + net->off.w[l], n, net->whi + net->off.w[l], net->wlo + net->off.w[l]);
         KV_HIP(hipGetLastError());
     }
+    if (!net->U) {
+        size_t tot = 0;
+        for (int l = 1; l < 12; ++l) {
+            net->uoff[l] = tot;
+            tot += (size_t)kv::WN_XI * kv::kConv[l].cout * kv::kConv[l].cin;
+        }
+        KV_HIP(hipMalloc(&net->U, tot * sizeof(float)));
+    }
+    for (int l = 1; l < 12; ++l) {
+        const size_t n = (size_t)kv::kConv[l].cout * kv::kConv[l].cin;
+        hipLaunchKernelGGL(kv::wino_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0,
+                           net->w + net->off.w[l], kv::kConv[l].cout, kv::kConv[l].cin, net->U + net->uoff[l]);
+        KV_HIP(hipGetLastError());
+    }
     KV_HIP(hipDeviceSynchronize());
     net->loaded = true;
+    return KV_OK;
+}
+
+int kv_net_set_algo(kv_net* net, int algo) {
+    KV_REQUIRE(net, KV_EINVAL, "kv_net_set_algo: NULL");
+    KV_REQUIRE(algo == KV_ALGO_AUTO || algo == KV_ALGO_DIRECT || algo == KV_ALGO_WINOGRAD, KV_EINVAL,
+               "kv_net_set_algo: unknown algo %d", algo);
+    net->algo = algo;
     return KV_OK;
 }
 
@@ -806,7 +951,7 @@ int kv_net_forward(kv_net* net, const float* planes_dev, int B, float* policy_de
     KV_REQUIRE(net && net->loaded, KV_EINVAL, "kv_net_forward: net not loaded");
     KV_REQUIRE(B > 0 && planes_dev && policy_dev && value_dev, KV_EINVAL, "kv_net_forward: bad arguments (B=%d)", B);
     hipStream_t st = (hipStream_t)stream;
-    const int nb_pad = (B + 3) & ~3;
+    const int nb_pad = net_pad(net, B);
     int rc = net_reserve(net, nb_pad);
     if (rc) return rc;
     hipLaunchKernelGGL(kv::planes_to_nhwc16_kernel, dim3((nb_pad * 64 + 255) / 256), dim3(256), 0, st, planes_dev, B,
@@ -820,7 +965,7 @@ int kv_net_forward_boards(kv_net* net, const int8_t* boards_dev, int B, float* p
     KV_REQUIRE(net && net->loaded, KV_EINVAL, "kv_net_forward_boards: net not loaded");
     KV_REQUIRE(B > 0 && boards_dev && policy_dev && value_dev, KV_EINVAL, "kv_net_forward_boards: bad arguments");
     hipStream_t st = (hipStream_t)stream;
-    const int nb_pad = (B + 3) & ~3;
+    const int nb_pad = net_pad(net, B);
     int rc = net_reserve(net, nb_pad);
     if (rc) return rc;
     hipLaunchKernelGGL(kv::encode_boards_kernel, dim3((nb_pad * 64 + 255) / 256), dim3(256), 0, st, boards_dev, B,
@@ -841,7 +986,7 @@ int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv) {
     float ms = 0.f;
     KV_HIP(hipEventElapsedTime(&ms, net->ev[1], net->ev[2]));
     if (conv_ms) *conv_ms = ms;
-    if (n_conv) *n_conv = 10;
+    if (n_conv) *n_conv = 10;  // convs of the residual section (Winograd: GEMMs + transforms)
     return KV_OK;
 }
 
@@ -856,6 +1001,9 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->X);
     (void)hipFree(net->T);
     (void)hipFree(net->pfeat);
+    (void)hipFree(net->U);
+    (void)hipFree(net->V);
+    (void)hipFree(net->Mw);
     for (int i = 0; i < 3; ++i) (void)hipEventDestroy(net->ev[i]);
     delete net;
 }
@@ -873,4 +1021,10 @@ int net_set_res_events(kv_net* net, hipEvent_t a, hipEvent_t b) {
     net->res_b = b;
     return KV_OK;
 }
+void net_dom_info(const kv_net* net, int* algo, int* launches, double* flop) {
+    *algo = net->dom_algo;
+    *launches = net->dom_launches;
+    *flop = net->dom_flop;
+}
+int net_set_algo_internal(kv_net* net, int algo) { return kv_net_set_algo(net, algo); }
 }  // namespace kv

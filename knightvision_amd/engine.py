@@ -31,10 +31,14 @@ def packed_from(weights) -> np.ndarray:
     return pack_weights(state_dict_to_numpy(weights))[0]
 
 
+ALGOS = {"auto": 0, "direct": 1, "winograd": 2}
+
+
 class SelfPlayEngine:
     def __init__(self, weights, *, slots=256, n_games=256, seed=42, seed_mode=SEED_PER_GAME, max_moves=None,
                  batch=16, eps=0.25, alpha=0.3, sims=0, c_puct=1.5, eval_mode=EVAL_FAITHFUL, record_cap=None,
-                 recycle=True, device=0, game_id_base=0, game_id_stride=1, precision="fp32"):
+                 recycle=True, device=0, game_id_base=0, game_id_stride=1, precision="fp32",
+                 algo="auto"):
         L = _lib.lib()
         if record_cap is None:
             record_cap = max(1 << 16, min(1 << 26, int(n_games) * 400))
@@ -42,7 +46,7 @@ class SelfPlayEngine:
                           game_id_stride=game_id_stride, seed=seed, seed_mode=seed_mode,
                           max_moves=max_moves if max_moves else 0, batch=batch, eps=eps, alpha=alpha, sims=sims,
                           c_puct=c_puct, eval_mode=eval_mode, record_cap=record_cap, recycle=1 if recycle else 0,
-                          precision={"fp32": 0, "bf16x3": 1}[precision])
+                          precision={"fp32": 0, "bf16x3": 1}[precision], algo=ALGOS[algo])
         h = C.c_void_p()
         _lib.check(L.kv_create(C.byref(cfg), C.byref(h)), "kv_create")
         self.h = h

@@ -21,6 +21,7 @@ from .weights import pack_weights, state_dict_to_numpy
 
 
 PRECISIONS = {"fp32": 0, "bf16x3": 1}
+ALGOS = {"auto": 0, "direct": 1, "winograd": 2}
 
 
 class ResidualBlock(nn.Module):
@@ -37,7 +38,7 @@ class ResidualBlock(nn.Module):
 class KVNet:
     """Owner of one kv_net (device weights + workspace) on one GPU."""
 
-    def __init__(self, device_index: int, packed: np.ndarray, precision: str = "fp32"):
+    def __init__(self, device_index: int, packed: np.ndarray, precision: str = "fp32", algo: str = "auto"):
         L = _lib.lib()
         if packed.size != L.kv_net_packed_size():
             raise _lib.KVError(f"packed weights have {packed.size} floats, library expects {L.kv_net_packed_size()}")
@@ -46,6 +47,7 @@ class KVNet:
         _lib.check(L.kv_net_create(device_index, C.byref(h)), "kv_net_create")
         self.h = h
         _lib.check(L.kv_net_set_precision(self.h, PRECISIONS[precision]), "kv_net_set_precision")
+        _lib.check(L.kv_net_set_algo(self.h, ALGOS[algo]), "kv_net_set_algo")
         p = np.ascontiguousarray(packed, dtype=np.float32)
         _lib.check(L.kv_net_load(self.h, p.ctypes.data_as(C.POINTER(C.c_float)), p.size), "kv_net_load")
 
@@ -86,12 +88,15 @@ class KVNet:
 class ChessNet(nn.Module):
     """ai/model.py:27-77 ChessNet with the HIP forward."""
 
-    def __init__(self, verbose: bool = False, precision: str = "fp32"):
+    def __init__(self, verbose: bool = False, precision: str = "fp32", algo: str = "auto"):
         super().__init__()
         self.verbose = verbose
         if precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {list(PRECISIONS)}")
+        if algo not in ALGOS:
+            raise ValueError(f"algo must be one of {list(ALGOS)}")
         self.precision = precision
+        self.algo = algo
         self.conv1 = nn.Conv2d(12, 256, kernel_size=3, padding=1)
         self.bn1 = nn.BatchNorm2d(256)
         self.conv2 = nn.Conv2d(256, 512, kernel_size=3, padding=1)
@@ -109,7 +114,7 @@ class ChessNet(nn.Module):
 
     # -- packed device weights ------------------------------------------------
     def _version_key(self, device_index):
-        return (device_index, self.precision) + tuple(t._version for t in self.state_dict().values())
+        return (device_index, self.precision, self.algo) + tuple(t._version for t in self.state_dict().values())
 
     def packed_weights(self) -> np.ndarray:
         return pack_weights(state_dict_to_numpy(self.state_dict()))[0]
@@ -119,7 +124,7 @@ class ChessNet(nn.Module):
         if self._kv is None or self._kv_key != key:
             if self._kv is not None:
                 self._kv.close()
-            self._kv = KVNet(device_index, self.packed_weights(), self.precision)
+            self._kv = KVNet(device_index, self.packed_weights(), self.precision, self.algo)
             self._kv_key = key
         return self._kv
 

@@ -13,37 +13,41 @@ pytestmark = pytest.mark.gpu
 TOL_P, TOL_V = 1e-4, 1e-5
 
 
-def _net(variant, precision="fp32"):
+# (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x4,3x3) / bf16x3 direct
+MODES = [("fp32", "direct"), ("fp32", "winograd"), ("bf16x3", "auto")]
+
+
+def _net(variant, precision="fp32", algo="auto"):
     from knightvision_amd.model import ChessNet
-    m = ChessNet(precision=precision)
+    m = ChessNet(precision=precision, algo=algo)
     sd = synthetic_state_dict(42, variant)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
     return m.eval()
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("precision,algo", MODES)
 @pytest.mark.parametrize("variant", ["init", "bn", "peaked"])
-def test_forward_matches_reference_golden(golden_dir, variant, precision):
+def test_forward_matches_reference_golden(golden_dir, variant, precision, algo):
     g = np.load(os.path.join(golden_dir, "nn.npz"))
-    m = _net(variant, precision)
+    m = _net(variant, precision, algo)
     p, v = m(torch.from_numpy(g["planes"]).cuda())
     torch.cuda.synchronize()
     dp = np.abs(p.cpu().numpy() - g[f"policy_{variant}"]).max()
     dv = np.abs(v.cpu().numpy() - g[f"value_{variant}"]).max()
-    print(precision, variant, "max |dpolicy|", dp, "max |dvalue|", dv)
+    print(precision, algo, variant, "max |dpolicy|", dp, "max |dvalue|", dv)
     assert dp <= TOL_P and dv <= TOL_V
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("precision,algo", MODES)
 @pytest.mark.parametrize("B", [1, 2, 3, 31, 64, 257])
-def test_forward_batch_sizes_vs_torch(B, precision):
+def test_forward_batch_sizes_vs_torch(B, precision, algo):
     from oracle import torch_ref
     rng = np.random.default_rng(B)
     codes = rng.integers(0, 13, size=(B, 64)) * (rng.random((B, 64)) < 0.4)
     from knightvision_amd.ai import codes_to_planes
     planes = codes_to_planes(codes)
     sd = synthetic_state_dict(42, "bn")
-    m = _net("bn", precision)
+    m = _net("bn", precision, algo)
     p, v = m(torch.from_numpy(planes).cuda())
     rp, rv = torch_ref.forward(sd, planes)
     dp = np.abs(p.cpu().numpy() - rp.numpy()).max()
@@ -58,8 +62,9 @@ def test_forward_batch_sizes_vs_torch(B, precision):
 @pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 def test_batch_invariance(precision):
     """A board's outputs do not depend on the batch it is evaluated in, within a
-    batch-size class (<= 16 boards: split-K kernels; > 16: whole-K kernels);
-    across the two classes only the fp32 summation order differs."""
+    batch-size class (<= 16 boards: split-K direct kernels; > 16: whole-K
+    kernels, Winograd for fp32); across the two classes only the rounding
+    differs (fp32 summation order / Winograd transforms)."""
     from knightvision_amd.ai import codes_to_planes
     rng = np.random.default_rng(7)
     codes = rng.integers(0, 13, size=(40, 64)) * (rng.random((40, 64)) < 0.4)

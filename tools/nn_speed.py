@@ -12,7 +12,8 @@ from knightvision_amd.weights import synthetic_state_dict
 
 FLOP = 3175744512
 prec = os.environ.get("KV_PREC", "fp32")
-m = ChessNet(precision=prec)
+algo = os.environ.get("KV_ALGO", "auto")
+m = ChessNet(precision=prec, algo=algo)
 m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(42, "bn").items()})
 m.eval()
 net = m.kv_net(0)
@@ -29,4 +30,4 @@ for B in [int(a) for a in (sys.argv[1:] or ["256", "1024", "2048"])]:
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / n
-    print(f"{prec} B={B} forward {ms:.3f} ms  {B/ms*1e3:.0f} boards/s  {B*FLOP/ms/1e9:.1f} TFLOP/s", flush=True)
+    print(f"{prec}/{algo} B={B} forward {ms:.3f} ms  {B/ms*1e3:.0f} boards/s  {B*FLOP/ms/1e9:.1f} TFLOP/s", flush=True)

@@ -1,29 +1,51 @@
-"""Summarise rocprofv3 PMC csv passes for the residual conv: HBM bytes per
-launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts half of
-a wide coalesced read, MI355X_MICROARCH.md HBM section)."""
+"""Summarise rocprofv3 PMC csv passes for one kernel: HBM bytes per launch =
+(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts half of a wide
+coalesced read, MI355X_MICROARCH.md HBM section).
+
+    python tools/pmc_summary.py FETCH_GLOB WRITE_GLOB BATCH [resconv|wino_gemm]
+"""
 import csv
 import glob
 import json
 import sys
 
+KERNELS = {
+    "resconv": ("conv3x3_kernel<512,32", "conv3x3_kernel<512,32,*>"),
+    "wino_gemm": ("wino_gemm_kernel<512,", "wino_gemm_kernel<512,4,1,2>"),
+}
 
-def load(pattern, counter):
+
+def load(pattern, counter, sub):
     vals = []
     for f in glob.glob(pattern, recursive=True):
         for r in csv.DictReader(open(f)):
-            if r.get("Counter_Name") == counter and "conv3x3_kernel<512, 32" in r.get("Kernel_Name", ""):
+            if r.get("Counter_Name") == counter and sub in r.get("Kernel_Name", "").replace(" ", ""):
                 vals.append(float(r["Counter_Value"]))
     return vals
 
 
-fetch = load(sys.argv[1], "FETCH_SIZE")
-write = load(sys.argv[2], "WRITE_SIZE")
-B = int(sys.argv[3])
-f = sum(fetch) / max(len(fetch), 1)
-w = sum(write) / max(len(write), 1)
-alg = B * 64 * 512 * 4 * 2 + 512 * 9 * 512 * 4  # activations in + out, weights once
-out = {"kernel": "conv3x3_kernel<512,32,*>", "batch": B, "launches_fetch": len(fetch), "launches_write": len(write),
-       "FETCH_SIZE_kB_avg": f, "WRITE_SIZE_kB_avg": w, "hbm_bytes_per_launch": (2 * f + w) * 1024,
-       "algorithmic_min_bytes_per_launch": alg,
-       "note": "hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024 per MI355X_MICROARCH.md; FETCH/WRITE from separate --pmc passes"}
-print(json.dumps(out, indent=1))
+def algorithmic_bytes(kind, B):
+    if kind == "resconv":  # activations in + out, weights once
+        return B * 64 * 512 * 4 * 2 + 512 * 9 * 512 * 4
+    rows = 4 * B  # V read + M write over the 36 GEMMs, U once
+    return 36 * rows * 512 * 4 * 2 + 36 * 512 * 512 * 4
+
+
+def main():
+    B = int(sys.argv[3])
+    kind = sys.argv[4] if len(sys.argv) > 4 else "resconv"
+    sub, name = KERNELS[kind]
+    fetch = load(sys.argv[1], "FETCH_SIZE", sub)
+    write = load(sys.argv[2], "WRITE_SIZE", sub)
+    f = sum(fetch) / max(len(fetch), 1)
+    w = sum(write) / max(len(write), 1)
+    out = {"kernel": name, "batch": B, "launches_fetch": len(fetch), "launches_write": len(write),
+           "FETCH_SIZE_kB_avg": f, "WRITE_SIZE_kB_avg": w, "hbm_bytes_per_launch": (2 * f + w) * 1024,
+           "algorithmic_min_bytes_per_launch": algorithmic_bytes(kind, B),
+           "note": "hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024 per MI355X_MICROARCH.md; FETCH/WRITE from separate "
+                   "--pmc passes"}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
