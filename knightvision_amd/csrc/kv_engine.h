@@ -150,6 +150,24 @@ __device__ void wave_softmax_4096(const float* lg, float* out, int lane) {
     for (int j = 0; j < 64; ++j) out[j * 64 + lane] = v[j] * inv;
 }
 
+// max and 1/sum of the same softmax, without writing it out: entry i of the
+// softmax is then expf(lg[i] - m) * inv, bit for bit (same sum order)
+__device__ inline void wave_softmax_4096_stats(const float* lg, int lane, float& m_out, float& inv_out) {
+    float v[64];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        v[j] = lg[j * 64 + lane];
+        m = fmaxf(m, v[j]);
+    }
+    m = wave_max(m);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) s += expf(v[j] - m);
+    s = wave_sum(s);
+    m_out = m;
+    inv_out = 1.0f / s;
+}
 
 // mixed legal weights of the reference (self_play.py:147-160) for a slot's
 // move list: (1-eps)*softmax [fp32] + eps*dirichlet [fp64], in list order.

@@ -182,14 +182,14 @@ __global__ __launch_bounds__(64) void k_mcts_backup(DevCfg cfg, Tree t, const Sl
     float v = m.leaf_value;
     if (m.leaf_pending) {
         v = values[i];
-        float* lp = probs + (size_t)i * 4096;
-        wave_softmax_4096(logits + (size_t)i * 4096, lp, lane);
-        __syncthreads();
+        const float* lg = logits + (size_t)i * 4096;
+        float sm_max, sm_inv;  // softmax entries of the legal moves only (no 16 KB round trip)
+        wave_softmax_4096_stats(lg, lane, sm_max, sm_inv);
         const uint16_t* lm = t.leaf_moves + (size_t)i * MAXM;
         const int n = m.leaf_n;
         for (int j = lane; j < n; j += 64) {
             const int mv = lm[j];
-            pri[j] = lp[(mv & 63) * 64 + ((mv >> 6) & 63)];
+            pri[j] = expf(lg[(mv & 63) * 64 + ((mv >> 6) & 63)] - sm_max) * sm_inv;
         }
         __syncthreads();
         __shared__ float s_sum;

@@ -734,7 +734,8 @@ static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows
         attr_set = true;
     }
     KV_REQUIRE(rows % T::WM == 0, KV_EINVAL, "wino gemm: rows %d not a multiple of %d", rows, T::WM);
-    hipLaunchKernelGGL((kv::wino_gemm_kernel<K, WR, MT, NT>), dim3(512 / T::WN, rows / T::WM, kv::WN_XI), dim3(512),
+    KV_REQUIRE((kv::WN_XI * (rows / T::WM) * (512 / T::WN)) % 8 == 0, KV_EINVAL, "wino gemm: tile count");
+    hipLaunchKernelGGL((kv::wino_gemm_kernel<K, WR, MT, NT>), dim3(kv::WN_XI * (rows / T::WM) * (512 / T::WN)), dim3(512),
                        T::BYTES, st, V, U, M, rows, 512);
     KV_HIP(hipGetLastError());
     return KV_OK;

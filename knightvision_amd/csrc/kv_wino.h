@@ -201,9 +201,16 @@ __global__ __launch_bounds__(512) void wino_gemm_kernel(const float* __restrict_
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WC, wn = wave % WC;
-    const int xi = blockIdx.z;
-    const int n_base = blockIdx.x * WN;
-    const int r_base = blockIdx.y * WM;
+    // XCD-aware tile order: blocks b and b+8 share an XCD (round-robin
+    // dealing), so each group of 8 gets a contiguous run of the xi-major tile
+    // order -- the 4 column tiles of a row panel and the row panels of one xi
+    // run on one XCD and re-read V / U from its L2 instead of HBM.
+    const int CT = cout / WN, RT = rows / WM;
+    const int nwg = WN_XI * RT * CT;  // a multiple of 8 (36 * 4 * RT)
+    const int idx = (int)(blockIdx.x & 7) * (nwg >> 3) + (int)(blockIdx.x >> 3);
+    const int xi = idx / (CT * RT);
+    const int n_base = (idx % CT) * WN;
+    const int r_base = ((idx / CT) % RT) * WM;
     const float* Va = V + ((size_t)xi * rows + r_base) * K;
     const float* Ub = U + ((size_t)xi * cout + n_base) * K;
 

@@ -1,4 +1,8 @@
-"""Average SQ / GRBM counters per dispatch for the conv kernels of a rocprofv3 --pmc csv."""
+"""Average SQ / GRBM counters per dispatch for the kernels of a rocprofv3 --pmc csv
+whose names contain one of the given substrings (default: conv3x3).
+
+    python tools/pmc_sq.py CSV_GLOB [substring ...]
+"""
 import csv
 import glob
 import sys
@@ -10,7 +14,7 @@ for f in glob.glob(sys.argv[1], recursive=True):
         continue
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "conv3x3" not in k:
+        if not any(s in k for s in (sys.argv[2:] or ["conv3x3"])):
             continue
         short = k.split("(")[0].replace("void kv::", "")
         acc[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
