@@ -180,7 +180,7 @@ struct WinoTile {
 };
 
 template <int K, int WR, int MT, int NT>
-__global__ __launch_bounds__(512) void wino_gemm_kernel(const float* __restrict__ V, const float* __restrict__ U,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void wino_gemm_kernel(const float* __restrict__ V, const float* __restrict__ U,
                                                         float* __restrict__ M, int rows, int cout) {
     using T = WinoTile<WR, MT, NT>;
     constexpr int WM = T::WM, WN = T::WN, WC = T::WC;
@@ -272,20 +272,29 @@ __global__ __launch_bounds__(512) void wino_gemm_kernel(const float* __restrict_
             loadB(kt + 1);
         }
         __syncthreads();
+        // fragments for step s+1 are read from LDS while step s's MFMAs run
+        f32x4 a[2][MT], b[2][NT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) a[0][mt] = *(const f32x4*)(Ab + aoff[mt]);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) b[0][nt] = *(const f32x4*)(Bb + boff[nt]);
 #pragma unroll
         for (int s = 0; s < CK / 8; ++s) {
-            f32x4 a[MT], b[NT];
+            const int cb = s & 1, nb = cb ^ 1;
+            if (s + 1 < CK / 8) {
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt) a[mt] = *(const f32x4*)(Ab + aoff[mt] + 8 * s);
+                for (int mt = 0; mt < MT; ++mt) a[nb][mt] = *(const f32x4*)(Ab + aoff[mt] + 8 * (s + 1));
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt) b[nt] = *(const f32x4*)(Bb + boff[nt] + 8 * s);
+                for (int nt = 0; nt < NT; ++nt) b[nb][nt] = *(const f32x4*)(Bb + boff[nt] + 8 * (s + 1));
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt)
-                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mt][j], b[nt][j], acc[mt][nt], 0, 0, 0);
+                        acc[mt][nt] =
+                            __builtin_amdgcn_mfma_f32_32x32x2f32(a[cb][mt][j], b[cb][nt][j], acc[mt][nt], 0, 0, 0);
         }
     }
 
