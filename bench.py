@@ -167,14 +167,18 @@ def main():
     # roofline of the dominant kernel, timed with HIP events on the engine stream: the residual-tower
     # Winograd GEMM launch (36 x [4*boards x 512 x 512]) or, for the direct algorithm, the residual conv
     wino = m["dom_algo"] == 2
-    flop_alg = (FLOP_WINO_GEMM_PER_BOARD if wino else FLOP_RES_CONV_PER_BOARD) * G
+    # boards one measured launch covers (the Winograd tower may run the batch as two halves on two streams);
+    # padding rows are not algorithmic work
+    per_board = FLOP_WINO_GEMM_PER_BOARD if wino else FLOP_RES_CONV_PER_BOARD
+    bpl = min(G, int(round(m["dom_flop"] / per_board))) if m["dom_flop"] else G
+    flop_alg = per_board * bpl
     achieved = flop_alg / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
     kname = "wino_gemm_kernel<512,4,1,2>" if wino else "conv3x3_kernel<512,32>"
     traffic = None
     pmc = os.path.join(HERE, "profiles", "r01_pmc_wino_gemm.json" if wino else "r01_pmc_resconv.json")
     if os.path.exists(pmc):
         pj = json.load(open(pmc))
-        if pj.get("batch") == G and pj.get("kernel", "").split("<")[0] == kname.split("<")[0]:
+        if pj.get("batch") == bpl and pj.get("kernel", "").split("<")[0] == kname.split("<")[0]:
             traffic = pj.get("hbm_bytes_per_launch")
 
     if rank == 0:
@@ -207,9 +211,9 @@ def main():
                                             else " (residual-tower 3x3 conv, implicit GEMM)"),
                          "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None,
-                         "traffic": traffic, "avg_launch_ms": conv_ms, "boards_per_launch": G,
+                         "traffic": traffic, "avg_launch_ms": conv_ms, "boards_per_launch": bpl,
                          "flop_per_launch": flop_alg, "mfma_flop_per_launch_incl_padding": m["dom_flop"],
-                         "direct_conv_equiv_tflops": (FLOP_RES_CONV_PER_BOARD * G / (conv_ms * 1e-3) / 1e12
+                         "direct_conv_equiv_tflops": (FLOP_RES_CONV_PER_BOARD * bpl / (conv_ms * 1e-3) / 1e12
                                                       if conv_ms > 0 else None)},
         }
         if direct is not None:

@@ -612,8 +612,11 @@ struct kv_net {
     float* U = nullptr;     // Winograd weights [36][Cout][Cin] of convs 1..11
     size_t uoff[12] = {};
     float* V = nullptr;     // Winograd workspaces [36][cap*4][512]
+    float* V256 = nullptr;  // conv2's input transform [36][cap*4][256]
     float* Mw = nullptr;
     // the dominant kernel bracketed by res_a/res_b in the last forward
+    hipStream_t s2 = nullptr;  // second stream of the split Winograd tower
+    hipEvent_t sev[3] = {};
     int dom_algo = KV_ALGO_DIRECT;
     int dom_launches = 10;
     double dom_flop = 0;
@@ -707,8 +710,8 @@ static int net_reserve(kv_net* net, int nb_pad) {
     if (nb_pad <= net->cap) return KV_OK;
     int cap = nb_pad < 64 ? 64 : nb_pad;
     (void)hipFree(net->x16); (void)hipFree(net->X); (void)hipFree(net->T); (void)hipFree(net->pfeat);
-    (void)hipFree(net->V); (void)hipFree(net->Mw);
-    net->x16 = net->X = net->T = net->pfeat = net->V = net->Mw = nullptr;
+    (void)hipFree(net->V); (void)hipFree(net->Mw); (void)hipFree(net->V256);
+    net->x16 = net->X = net->T = net->pfeat = net->V = net->Mw = net->V256 = nullptr;
     net->cap = 0;
     KV_HIP(hipMalloc(&net->x16, (size_t)cap * 64 * 16 * 4));
     KV_HIP(hipMalloc(&net->X, (size_t)cap * 64 * 512 * 4));
@@ -716,6 +719,7 @@ static int net_reserve(kv_net* net, int nb_pad) {
     KV_HIP(hipMalloc(&net->pfeat, (size_t)cap * 128 * 4));
     KV_HIP(hipMalloc(&net->V, (size_t)kv::WN_XI * cap * 4 * 512 * 4));
     KV_HIP(hipMalloc(&net->Mw, (size_t)kv::WN_XI * cap * 4 * 512 * 4));
+    KV_HIP(hipMalloc(&net->V256, (size_t)kv::WN_XI * cap * 4 * 256 * 4));
     if (!net->slab)  // 48 splits x 16 boards x 64 px x 512 channels
         KV_HIP(hipMalloc(&net->slab, (size_t)(144 / kSplitKt) * kSplitMaxBoards * 64 * 512 * 4));
     net->cap = cap;
@@ -725,7 +729,7 @@ static int net_reserve(kv_net* net, int nb_pad) {
 static int net_heads(kv_net* net, int nb, float* policy, float* value, hipStream_t st);
 
 template <int K, int WR, int MT, int NT>
-static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows, hipStream_t st) {
+static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
     using T = kv::WinoTile<WR, MT, NT>;
     static bool attr_set = false;
     if (!attr_set) {
@@ -736,7 +740,7 @@ static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows
     KV_REQUIRE(rows % T::WM == 0, KV_EINVAL, "wino gemm: rows %d not a multiple of %d", rows, T::WM);
     KV_REQUIRE((kv::WN_XI * (rows / T::WM) * (512 / T::WN)) % 8 == 0, KV_EINVAL, "wino gemm: tile count");
     hipLaunchKernelGGL((kv::wino_gemm_kernel<K, WR, MT, NT>), dim3(kv::WN_XI * (rows / T::WM) * (512 / T::WN)), dim3(512),
-                       T::BYTES, st, V, U, M, rows, 512);
+                       T::BYTES, st, V, U, M, rows, 512, stride);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -751,58 +755,100 @@ static int wino_tile_choice() {
 }
 
 template <int K>
-static int launch_wino_gemm(const float* V, const float* U, float* M, int rows, hipStream_t st) {
+static int launch_wino_gemm(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
     switch (wino_tile_choice()) {
-        case 1: return launch_wino_gemm_t<K, 2, 1, 2>(V, U, M, rows, st);  // 64 x 256
-        case 2: return launch_wino_gemm_t<K, 1, 2, 1>(V, U, M, rows, st);  // 64 x 256
-        case 4: return launch_wino_gemm_t<K, 2, 2, 1>(V, U, M, rows, st);  // 128 x 128
-        case 5: return launch_wino_gemm_t<K, 2, 2, 2>(V, U, M, rows, st);  // 128 x 256
-        default: return launch_wino_gemm_t<K, 4, 1, 2>(V, U, M, rows, st);  // 128 x 128, 2 workgroups / CU
+        case 1: return launch_wino_gemm_t<K, 2, 1, 2>(V, U, M, rows, stride, st);  // 64 x 256
+        case 2: return launch_wino_gemm_t<K, 1, 2, 1>(V, U, M, rows, stride, st);  // 64 x 256
+        case 4: return launch_wino_gemm_t<K, 2, 2, 1>(V, U, M, rows, stride, st);  // 128 x 128
+        case 5: return launch_wino_gemm_t<K, 2, 2, 2>(V, U, M, rows, stride, st);  // 128 x 256
+        default: return launch_wino_gemm_t<K, 4, 1, 2>(V, U, M, rows, stride, st);  // 128 x 128, 2 workgroups / CU
     }
 }
 
+// boards [b0, b0 + nb) of a batch whose V / M slabs hold `stride` rows
 template <bool RESID, bool WRITE_Y, bool NEXT_V>
-static int launch_wino_out(const float* M, int nb_pad, const float* sc, const float* sh, const float* resid, float* Y,
-                           float* Vn, hipStream_t st) {
-    hipLaunchKernelGGL((kv::wino_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 64, nb_pad), dim3(256), 0, st, M,
-                       nb_pad * 4, sc, sh, resid, Y, Vn);
+static int launch_wino_out(const float* M, int b0, int nb, int stride, const float* sc, const float* sh,
+                           const float* resid, float* Y, float* Vn, hipStream_t st) {
+    const size_t ro = (size_t)b0 * 4 * 512, po = (size_t)b0 * 64 * 512;
+    hipLaunchKernelGGL((kv::wino_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 64, nb), dim3(256), 0, st, M + ro,
+                       stride, sc, sh, resid ? resid + po : nullptr, Y ? Y + po : nullptr, Vn ? Vn + ro : nullptr);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
 
-// Winograd tower: conv2 and the 5 residual blocks (conv1 output in net->T)
-static int net_tower_wino(kv_net* net, int nb_pad, hipStream_t st) {
+static int wino_streams() {
+    static int c = -1;
+    if (c < 0) {
+        const char* e = getenv("KV_WINO_STREAMS");
+        c = e ? atoi(e) : 1;
+    }
+    return c;
+}
+
+// conv2 + the 5 residual blocks for boards [b0, b0 + nb) on stream st
+static int wino_blocks(kv_net* net, int b0, int nb, int stride, bool mark, hipStream_t st, hipEvent_t after_first) {
     const float* W = net->w;
     const kv::PackOffsets& o = net->off;
-    const int rows = nb_pad * 4;
+    const size_t ro = (size_t)b0 * 4 * 512, ro256 = (size_t)b0 * 4 * 256;
+    const int rows = nb * 4;
+    float* V = net->V;
+    float* M = net->Mw;
     int rc;
-    hipLaunchKernelGGL(kv::wino_in_kernel<256>, dim3(256 / 64, nb_pad), dim3(256), 0, st, net->T, rows, net->V);
-    KV_HIP(hipGetLastError());
-    if ((rc = launch_wino_gemm<256>(net->V, net->U + net->uoff[1], net->Mw, rows, st))) return rc;
-    if ((rc = launch_wino_out<false, true, true>(net->Mw, nb_pad, W + o.scale[1], W + o.shift[1], nullptr, net->X,
-                                                 net->V, st)))
+    if ((rc = launch_wino_gemm<256>(net->V256 + ro256, net->U + net->uoff[1], M + ro, rows, stride, st))) return rc;
+    if (after_first) KV_HIP(hipEventRecord(after_first, st));
+    if ((rc = launch_wino_out<false, true, true>(M, b0, nb, stride, W + o.scale[1], W + o.shift[1], nullptr, net->X,
+                                                 V, st)))
         return rc;
-    if (net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
+    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
     for (int r = 0; r < 5; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
-        const bool mark = r == 2;  // one representative residual GEMM for the engine's timing hook
-        if (mark && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-        if ((rc = launch_wino_gemm<512>(net->V, net->U + net->uoff[l1], net->Mw, rows, st))) return rc;
-        if (mark && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
-        if ((rc = launch_wino_out<false, false, true>(net->Mw, nb_pad, W + o.scale[l1], W + o.shift[l1], nullptr,
-                                                      nullptr, net->V, st)))
+        const bool m = mark && r == 2;  // one representative residual GEMM for the engine's timing hook
+        if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
+        if ((rc = launch_wino_gemm<512>(V + ro, net->U + net->uoff[l1], M + ro, rows, stride, st))) return rc;
+        if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
+        if ((rc = launch_wino_out<false, false, true>(M, b0, nb, stride, W + o.scale[l1], W + o.shift[l1], nullptr,
+                                                      nullptr, V, st)))
             return rc;
-        if ((rc = launch_wino_gemm<512>(net->V, net->U + net->uoff[l2], net->Mw, rows, st))) return rc;
-        rc = r < 4 ? launch_wino_out<true, true, true>(net->Mw, nb_pad, W + o.scale[l2], W + o.shift[l2], net->X,
-                                                       net->X, net->V, st)
-                   : launch_wino_out<true, true, false>(net->Mw, nb_pad, W + o.scale[l2], W + o.shift[l2], net->X,
+        if ((rc = launch_wino_gemm<512>(V + ro, net->U + net->uoff[l2], M + ro, rows, stride, st))) return rc;
+        rc = r < 4 ? launch_wino_out<true, true, true>(M, b0, nb, stride, W + o.scale[l2], W + o.shift[l2], net->X,
+                                                       net->X, V, st)
+                   : launch_wino_out<true, true, false>(M, b0, nb, stride, W + o.scale[l2], W + o.shift[l2], net->X,
                                                         net->X, nullptr, st);
         if (rc) return rc;
     }
-    if (net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
+    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
+    return KV_OK;
+}
+
+// Winograd tower: conv2 and the 5 residual blocks (conv1 output in net->T).
+// With KV_WINO_STREAMS=2/3 and >= 64 boards the batch is split in two halves
+// that run on two streams (3: the second half starts one GEMM later), so one
+// half's memory-bound transforms overlap the other half's GEMMs.
+static int net_tower_wino(kv_net* net, int nb_pad, hipStream_t st) {
+    const int rows = nb_pad * 4;
+    int rc;
+    hipLaunchKernelGGL(kv::wino_in_kernel<256>, dim3(256 / 64, nb_pad), dim3(256), 0, st, net->T, rows, net->V256);
+    KV_HIP(hipGetLastError());
+    const int ns = wino_streams();
+    if (ns >= 2 && nb_pad % 64 == 0) {
+        if (!net->s2) {
+            KV_HIP(hipStreamCreateWithFlags(&net->s2, hipStreamNonBlocking));
+            for (int i = 0; i < 3; ++i) KV_HIP(hipEventCreateWithFlags(&net->sev[i], hipEventDisableTiming));
+        }
+        const int half = nb_pad / 2;
+        KV_HIP(hipEventRecord(net->sev[0], st));
+        if ((rc = wino_blocks(net, 0, half, rows, true, st, ns >= 3 ? net->sev[1] : nullptr))) return rc;
+        KV_HIP(hipStreamWaitEvent(net->s2, ns >= 3 ? net->sev[1] : net->sev[0], 0));
+        if ((rc = wino_blocks(net, half, half, rows, false, net->s2, nullptr))) return rc;
+        KV_HIP(hipEventRecord(net->sev[2], net->s2));
+        KV_HIP(hipStreamWaitEvent(st, net->sev[2], 0));
+        net->dom_flop = 2.0 * kv::WN_XI * (half * 4) * 512.0 * 512.0;
+    } else {
+        if ((rc = wino_blocks(net, 0, nb_pad, rows, true, st, nullptr))) return rc;
+        net->dom_flop = 2.0 * kv::WN_XI * rows * 512.0 * 512.0;
+    }
     net->dom_algo = KV_ALGO_WINOGRAD;
     net->dom_launches = 1;
-    net->dom_flop = 2.0 * kv::WN_XI * rows * 512.0 * 512.0;
     return KV_OK;
 }
 
@@ -1005,7 +1051,12 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->U);
     (void)hipFree(net->V);
     (void)hipFree(net->Mw);
+    (void)hipFree(net->V256);
     for (int i = 0; i < 3; ++i) (void)hipEventDestroy(net->ev[i]);
+    if (net->s2) {
+        for (int i = 0; i < 3; ++i) (void)hipEventDestroy(net->sev[i]);
+        (void)hipStreamDestroy(net->s2);
+    }
     delete net;
 }
 

@@ -166,7 +166,8 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
     wino_input_tile(d, Vn, base, xs);
 }
 
-// The 36 GEMMs M[xi] = V[xi] x U[xi]^T on v_mfma_f32_32x32x2_f32.
+// The 36 GEMMs M[xi] = V[xi] x U[xi]^T on v_mfma_f32_32x32x2_f32, over `rows`
+// rows of V / M whose xi slabs are `stride` rows apart (a batch slice).
 // Workgroup: WM x WN outputs of one xi; 8 waves in a WR x (8/WR) grid, each
 // (MT*32) x (NT*32). K (= Cin) streams through LDS in k-tiles of 32
 // (double-buffered A [WM][32] and B [WN][32], row stride 36 floats:
@@ -181,7 +182,7 @@ struct WinoTile {
 
 template <int K, int WR, int MT, int NT>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void wino_gemm_kernel(const float* __restrict__ V, const float* __restrict__ U,
-                                                        float* __restrict__ M, int rows, int cout) {
+                                                        float* __restrict__ M, int rows, int cout, int stride) {
     using T = WinoTile<WR, MT, NT>;
     constexpr int WM = T::WM, WN = T::WN, WC = T::WC;
     constexpr int CK = 32, PS = 36;
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const int xi = idx / (CT * RT);
     const int n_base = (idx % CT) * WN;
     const int r_base = ((idx / CT) % RT) * WM;
-    const float* Va = V + ((size_t)xi * rows + r_base) * K;
+    const float* Va = V + ((size_t)xi * stride + r_base) * K;
     const float* Ub = U + ((size_t)xi * cout + n_base) * K;
 
     f32x4 ra[A_F4];
@@ -299,7 +300,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     }
 
     // D[row][col]: row = (r&3) + 8*(r>>2) + 4*h inside the 32-row tile, col = li
-    float* Mo = M + ((size_t)xi * rows + r_base + wm * MT * 32) * cout + n_base + wn * NT * 32 + li;
+    float* Mo = M + ((size_t)xi * stride + r_base + wm * MT * 32) * cout + n_base + wn * NT * 32 + li;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
