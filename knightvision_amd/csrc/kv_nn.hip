@@ -728,44 +728,33 @@ static int net_reserve(kv_net* net, int nb_pad) {
 
 static int net_heads(kv_net* net, int nb, float* policy, float* value, hipStream_t st);
 
-template <int K, int WR, int MT, int NT>
+// LDS_PAD: dynamic LDS requested beyond the tiles' need, to cap workgroups per CU
+template <int K, int WR, int WC, int MT, int NT, int LDS_PAD = 0>
 static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
-    using T = kv::WinoTile<WR, MT, NT>;
+    using T = kv::WinoTile<WR, WC, MT, NT>;
+    constexpr size_t bytes = T::BYTES + LDS_PAD;
     static bool attr_set = false;
     if (!attr_set) {
-        KV_HIP(hipFuncSetAttribute((const void*)kv::wino_gemm_kernel<K, WR, MT, NT>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::BYTES));
+        KV_HIP(hipFuncSetAttribute((const void*)kv::wino_gemm_kernel<K, WR, WC, MT, NT>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
         attr_set = true;
     }
-    KV_REQUIRE(rows % T::WM == 0, KV_EINVAL, "wino gemm: rows %d not a multiple of %d", rows, T::WM);
-    KV_REQUIRE((kv::WN_XI * (rows / T::WM) * (512 / T::WN)) % 8 == 0, KV_EINVAL, "wino gemm: tile count");
-    hipLaunchKernelGGL((kv::wino_gemm_kernel<K, WR, MT, NT>), dim3(kv::WN_XI * (rows / T::WM) * (512 / T::WN)), dim3(512),
-                       T::BYTES, st, V, U, M, rows, 512, stride);
+    const int nwg = kv::WN_XI * (rows / T::WM) * (512 / T::WN);
+    KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0, KV_EINVAL, "wino gemm: rows %d vs tile %d", rows, T::WM);
+    hipLaunchKernelGGL((kv::wino_gemm_kernel<K, WR, WC, MT, NT>), dim3(nwg), dim3(T::THREADS), bytes, st, V, U, M,
+                       rows, 512, stride);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
 
-static int wino_tile_choice() {
-    static int c = -1;
-    if (c < 0) {
-        const char* e = getenv("KV_WINO_TILE");
-        c = e ? atoi(e) : 0;
-    }
-    return c;
-}
-
+// 128 tiles x 128 channels per workgroup, 8 waves of 32x64, 74 KB LDS -> 2
+// workgroups per CU. Measured against 64x64, 64x128, 128x64 (1 or 2 per CU)
+// and 128x256 tiles at 256 and 2048 boards: fastest or within noise at both.
 template <int K>
 static int launch_wino_gemm(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
-    switch (wino_tile_choice()) {
-        case 1: return launch_wino_gemm_t<K, 2, 1, 2>(V, U, M, rows, stride, st);  // 64 x 256
-        case 2: return launch_wino_gemm_t<K, 1, 2, 1>(V, U, M, rows, stride, st);  // 64 x 256
-        case 4: return launch_wino_gemm_t<K, 2, 2, 1>(V, U, M, rows, stride, st);  // 128 x 128
-        case 5: return launch_wino_gemm_t<K, 2, 2, 2>(V, U, M, rows, stride, st);  // 128 x 256
-        default: return launch_wino_gemm_t<K, 4, 1, 2>(V, U, M, rows, stride, st);  // 128 x 128, 2 workgroups / CU
-    }
+    return launch_wino_gemm_t<K, 4, 2, 1, 2>(V, U, M, rows, stride, st);
 }
 
-// boards [b0, b0 + nb) of a batch whose V / M slabs hold `stride` rows
 template <bool RESID, bool WRITE_Y, bool NEXT_V>
 static int launch_wino_out(const float* M, int b0, int nb, int stride, const float* sc, const float* sh,
                            const float* resid, float* Y, float* Vn, hipStream_t st) {

@@ -173,25 +173,27 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
 // (double-buffered A [WM][32] and B [WN][32], row stride 36 floats:
 // conflict-free ds_read_b128), one barrier per k-tile, the next k-tile's
 // global loads issued before the current tile's MFMAs.
-template <int WR, int MT, int NT>
+template <int WR, int WC, int MT, int NT>
 struct WinoTile {
-    static constexpr int WC = 8 / WR;
+    static constexpr int THREADS = WR * WC * 64;
     static constexpr int WM = WR * MT * 32, WN = WC * NT * 32;
     static constexpr size_t BYTES = (size_t)(2 * WM * 36 + 2 * WN * 36) * 4;
 };
 
-template <int K, int WR, int MT, int NT>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void wino_gemm_kernel(const float* __restrict__ V, const float* __restrict__ U,
-                                                        float* __restrict__ M, int rows, int cout, int stride) {
-    using T = WinoTile<WR, MT, NT>;
-    constexpr int WM = T::WM, WN = T::WN, WC = T::WC;
+template <int K, int WR, int WC, int MT, int NT>
+__global__ __launch_bounds__(WR * WC * 64) void wino_gemm_kernel(const float* __restrict__ V,
+                                                                   const float* __restrict__ U,
+                                                                   float* __restrict__ M, int rows, int cout,
+                                                                   int stride) {
+    using T = WinoTile<WR, WC, MT, NT>;
+    constexpr int WM = T::WM, WN = T::WN, TH = T::THREADS;
     constexpr int CK = 32, PS = 36;
     constexpr int NK = K / CK;
     constexpr int KQ = CK / 4;
-    constexpr int A_F4 = (WM * KQ) / 512;
-    constexpr int B_F4 = (WN * KQ) / 512;
+    constexpr int A_F4 = (WM * KQ) / TH;
+    constexpr int B_F4 = (WN * KQ) / TH;
     constexpr int ABUF = WM * PS, BBUF = WN * PS;
-    static_assert(A_F4 >= 1 && B_F4 >= 1 && (WM * KQ) % 512 == 0 && (WN * KQ) % 512 == 0, "tile shape");
+    static_assert(A_F4 >= 1 && B_F4 >= 1 && (WM * KQ) % TH == 0 && (WN * KQ) % TH == 0, "tile shape");
 
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* const A0 = smem;
@@ -220,28 +222,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     auto loadA = [&](int kt) {
 #pragma unroll
         for (int q = 0; q < A_F4; ++q) {
-            const int idx = tid + q * 512;
+            const int idx = tid + q * TH;
             ra[q] = *(const f32x4*)(Va + (size_t)(idx / KQ) * K + kt * CK + (idx % KQ) * 4);
         }
     };
     auto storeA = [&](float* Ab) {
 #pragma unroll
         for (int q = 0; q < A_F4; ++q) {
-            const int idx = tid + q * 512;
+            const int idx = tid + q * TH;
             *(f32x4*)(Ab + (idx / KQ) * PS + (idx % KQ) * 4) = ra[q];
         }
     };
     auto loadB = [&](int kt) {
 #pragma unroll
         for (int q = 0; q < B_F4; ++q) {
-            const int idx = tid + q * 512;
+            const int idx = tid + q * TH;
             rb[q] = *(const f32x4*)(Ub + (size_t)(idx / KQ) * K + kt * CK + (idx % KQ) * 4);
         }
     };
     auto storeB = [&](float* Bb) {
 #pragma unroll
         for (int q = 0; q < B_F4; ++q) {
-            const int idx = tid + q * 512;
+            const int idx = tid + q * TH;
             *(f32x4*)(Bb + (idx / KQ) * PS + (idx % KQ) * 4) = rb[q];
         }
     };
