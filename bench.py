@@ -181,6 +181,18 @@ def main():
         if pj.get("batch") == bpl and pj.get("kernel", "").split("<")[0] == kname.split("<")[0]:
             traffic = pj.get("hbm_bytes_per_launch")
 
+    # HBM side of the search (north_star: tree kernels as a fraction of the HBM roofline), from the
+    # rocprofv3 PMC + kernel-trace summary committed for this slot count (tools/tree_hbm.py)
+    tree_hbm = None
+    tp = os.path.join(HERE, "profiles", {256: "r01_pmc_tree_c2_256.json", 2048: "r01_pmc_tree_c3_2048.json"}.get(G, "-"))
+    if mcts and os.path.exists(tp):
+        tj = json.load(open(tp))
+        if tj.get("slots") == G and "per_sim" in tj:
+            tree_hbm = {"kernels": "k_mcts_select + k_mcts_backup", "bytes_per_sim": tj["per_sim"]["bytes_per_sim"],
+                        "achieved_GBps": tj["per_sim"]["GBps"], "peak_GBps": tj["peak_GBps"],
+                        "frac": tj["per_sim"]["frac"], "source": os.path.relpath(tp, HERE),
+                        "note": "latency-bound: one wave per game; 16 KB of the ~21 KB/sim is the leaf's 4096 logits"}
+
     if rank == 0:
         if mcts:
             metric, unit, value = "MCTS simulations/sec + self-play games/hour", "sims/s", sims_done / dt
@@ -216,6 +228,8 @@ def main():
                          "direct_conv_equiv_tflops": (FLOP_RES_CONV_PER_BOARD * bpl / (conv_ms * 1e-3) / 1e12
                                                       if conv_ms > 0 else None)},
         }
+        if tree_hbm is not None:
+            out["tree_hbm"] = tree_hbm
         if direct is not None:
             d_ach = (FLOP_RES_CONV_PER_BOARD * G / (direct["conv_ms"] * 1e-3) / 1e12) if direct["conv_ms"] > 0 else None
             out["fp32_direct"] = {
