@@ -72,28 +72,28 @@ __global__ __launch_bounds__(64) void k_dev_make(int8_t* states, const int* inde
     status[i] = 0;
 }
 
-__global__ __launch_bounds__(64) void k_dev_dirichlet(const unsigned long long* seeds, double alpha, int k,
-                                                      int draws, double* out, long long* attempts, double* tail,
-                                                      uint32_t* state) {
-    __shared__ uint32_t a[MT_N], b[MT_N];
-    const int i = blockIdx.x, lane = threadIdx.x;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_dev_dirichlet(const unsigned long long* seeds, double alpha, int k,
+                                                       int draws, double* out, long long* attempts, double* tail,
+                                                       uint32_t* state) {
+    __shared__ uint32_t mt3[3 * MT_N];
+    __shared__ int scratch[8];
+    const int i = blockIdx.x, tid = threadIdx.x;
     uint32_t* g = state + (size_t)i * MT_WORDS;
-    if (lane == 0) mt_seed_genrand(g, (uint32_t)seeds[i]);
+    if (tid == 0) mt_seed_genrand(g, (uint32_t)seeds[i]);
     __syncthreads();
-    WaveMT w;
-    wmt_load(w, g, a, b, lane);
+    BlockMT w;
+    bmt_load(w, g, mt3, tid);
     for (int d = 0; d < draws; ++d) {
         double* o = out + ((size_t)i * draws + d) * k;
         long long att;
-        const double acc = wave_dirichlet_gamma(w, alpha, k, o, &att, lane);
-        __syncthreads();
+        const double acc = block_dirichlet_gamma(w, alpha, k, o, &att, scratch, tid);
         const double inv = 1 / acc;
-        for (int j = lane; j < k; j += 64) o[j] = o[j] * inv;
-        if (lane == 0) attempts[(size_t)i * draws + d] = att;
+        for (int j = tid; j < k; j += RNG_THREADS) o[j] = o[j] * inv;
+        if (tid == 0) attempts[(size_t)i * draws + d] = att;
         __syncthreads();
     }
-    const double t = wave_random(w, lane);
-    if (lane == 0) tail[i] = t;
+    const double t = block_random(w, tid);
+    if (tid == 0) tail[i] = t;
 }
 
 __global__ void k_dev_py_random(const unsigned long long* seeds, int n, int count, double* out, uint32_t* state) {
@@ -180,7 +180,7 @@ int kv_dev_dirichlet(int device, const uint64_t* seeds, int n, double alpha, int
     KV_HIP(at.alloc((size_t)n * draws));
     KV_HIP(st.alloc((size_t)n * kv::MT_WORDS));
     KV_HIP(hipMemcpy(sd.p, seeds, (size_t)n * 8, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(kv::k_dev_dirichlet, dim3(n), dim3(64), 0, 0, sd.p, alpha, k, draws, o.p, at.p, t.p, st.p);
+    hipLaunchKernelGGL(kv::k_dev_dirichlet, dim3(n), dim3(256), 0, 0, sd.p, alpha, k, draws, o.p, at.p, t.p, st.p);
     KV_HIP(hipGetLastError());
     KV_HIP(hipDeviceSynchronize());
     KV_HIP(hipMemcpy(out, o.p, (size_t)n * draws * k * sizeof(double), hipMemcpyDeviceToHost));

@@ -171,23 +171,23 @@ __device__ inline void wave_softmax_4096_stats(const float* lg, int lane, float&
 
 // mixed legal weights of the reference (self_play.py:147-160) for a slot's
 // move list: (1-eps)*softmax [fp32] + eps*dirichlet [fp64], in list order.
-// Consumes the slot's numpy stream exactly as np.random.dirichlet does.
+// Consumes the slot's numpy stream exactly as np.random.dirichlet does. All
+// 256 threads of the slot's workgroup; gam is 4096 doubles of LDS.
 __device__ inline void mixed_legal_weights(const DevCfg& cfg, const float* lp, const uint16_t* ml, int n,
-                                           double* gam_slot, uint32_t* np_state, uint32_t* mt_a, uint32_t* mt_b,
-                                           double* vals, int lane) {
-    WaveMT w;
-    wmt_load(w, np_state, mt_a, mt_b, lane);
+                                           double* gam, uint32_t* np_state, uint32_t* mt_lds3, int* scratch,
+                                           double* vals, int tid) {
+    BlockMT w;
+    bmt_load(w, np_state, mt_lds3, tid);
     long long att;
-    const double acc = wave_dirichlet_gamma(w, cfg.alpha, 4096, gam_slot, &att, lane);
-    wmt_store(w, np_state, lane);
+    const double acc = block_dirichlet_gamma(w, cfg.alpha, 4096, gam, &att, scratch, tid);
+    bmt_store(w, np_state, tid);
     const double invacc = 1 / acc;
-    __syncthreads();
     const float keep = (float)(1.0 - cfg.eps);
-    for (int j = lane; j < n; j += 64) {
+    for (int j = tid; j < n; j += RNG_THREADS) {
         const int mv = ml[j];
         const int idx = (mv & 63) * 64 + ((mv >> 6) & 63);
         const float p32 = keep * lp[idx];
-        const double noise = gam_slot[idx] * invacc;
+        const double noise = gam[idx] * invacc;
         vals[j] = (double)p32 + cfg.eps * noise;
     }
     __syncthreads();
@@ -220,13 +220,16 @@ __device__ inline int choose_weighted(const double* vals, double* cum, int n, ui
 // was chosen with), max_moves (:196). All lanes of the slot's wave.
 __device__ inline void commit_move(const DevCfg& cfg, Slot& s, int i, int mv, int8_t* boards, kv_record* rec,
                                    int8_t* last_board, Ctr* ctr, int lane) {
+    // lane = thread index of the slot's workgroup; lanes 0..63 (wave 0) carry
+    // the 64 squares, every thread reaches the barriers
     int8_t* board = boards + (size_t)i * 64;
+    const bool sqlane = lane < 64;
     const unsigned long long r = lane == 0 ? atomicAdd(&ctr->rec_count, 1ull) : 0ull;
     const unsigned long long ridx = __shfl(r, 0);
-    const int8_t sq = board[lane];
-    last_board[(size_t)i * 64 + lane] = sq;
+    const int8_t sq = sqlane ? board[lane] : 0;
+    if (sqlane) last_board[(size_t)i * 64 + lane] = sq;
     if ((long long)ridx < cfg.record_cap) {
-        rec[ridx].board[lane] = sq;
+        if (sqlane) rec[ridx].board[lane] = sq;
         if (lane == 0) {
             rec[ridx].game_id = s.game_id;
             rec[ridx].ply = s.ply;
@@ -243,7 +246,7 @@ __device__ inline void commit_move(const DevCfg& cfg, Slot& s, int i, int mv, in
         atomicAdd(&ctr->plies, 1ull);
     }
     __syncthreads();
-    const int8_t b2 = board[lane];
+    const int8_t b2 = sqlane ? board[lane] : 0;
     const bool non_king = b2 != 0 && b2 != 1 && b2 != 7;
     const bool draw = __ballot(non_king) == 0ull;
     if (lane == 0) {
@@ -263,7 +266,7 @@ __device__ inline void commit_move(const DevCfg& cfg, Slot& s, int i, int mv, in
 
 // MCTS launches (kv_mcts.hip), all on `st`
 int mcts_root(const DevCfg& cfg, const Tree& t, Slot* slots, const uint16_t* moves, const float* logits,
-              const float* values, float* probs_scratch, double* gam, uint32_t* np_mt, hipStream_t st);
+              const float* values, float* probs_scratch, uint32_t* np_mt, hipStream_t st);
 int mcts_select(const DevCfg& cfg, const Tree& t, const Slot* slots, const int8_t* boards, int8_t* nn_boards,
                 Ctr* ctr, hipStream_t st);
 int mcts_backup(const DevCfg& cfg, const Tree& t, const Slot* slots, const float* logits, const float* values,

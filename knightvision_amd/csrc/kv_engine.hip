@@ -114,26 +114,29 @@ __global__ __launch_bounds__(64) void k_movegen(DevCfg cfg, Slot* slots, int8_t*
 }
 
 // ------------------------------------------------------------- sample ----
-__global__ __launch_bounds__(64) void k_sample(DevCfg cfg, Slot* slots, int8_t* boards, const uint16_t* moves,
-                                               const float* logits, const float* values, float* last_probs,
-                                               double* gam, uint32_t* np_mt, uint32_t* py_mt, kv_record* rec,
-                                               int8_t* last_board, Ctr* ctr) {
-    __shared__ uint32_t mt_a[MT_N], mt_b[MT_N];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sample(DevCfg cfg, Slot* slots, int8_t* boards, const uint16_t* moves,
+                                                const float* logits, const float* values, float* last_probs,
+                                                uint32_t* np_mt, uint32_t* py_mt, kv_record* rec, int8_t* last_board,
+                                                Ctr* ctr) {
+    __shared__ uint32_t mt3[3 * MT_N];
+    __shared__ double gam[4096];
     __shared__ double vals[MAXM];
     __shared__ double cum[MAXM];
+    __shared__ int scratch[8];
     __shared__ int s_pick;
     const int i = blockIdx.x, lane = threadIdx.x;
     Slot s = slots[i];
     if (s.status != ST_ACTIVE) return;
     float* lp = last_probs + (size_t)i * 4096;
     if (s.need_flush) {  // previous game's final flush row (sequential mode)
-        wave_softmax_4096(logits + (size_t)(cfg.slots + i) * 4096, lp, lane);
+        if (lane < 64) wave_softmax_4096(logits + (size_t)(cfg.slots + i) * 4096, lp, lane);
         s.last_value = values[cfg.slots + i];
         s.has_last = 1;
         s.need_flush = 0;
     }
     if (s.consumed) {  // policy/value = _last_outputs[...][-1] (:147-150)
-        wave_softmax_4096(logits + (size_t)i * 4096, lp, lane);
+        __syncthreads();
+        if (lane < 64) wave_softmax_4096(logits + (size_t)i * 4096, lp, lane);
         s.last_value = values[i];
         s.has_last = 1;
         s.buf = 0;
@@ -142,8 +145,7 @@ __global__ __launch_bounds__(64) void k_sample(DevCfg cfg, Slot* slots, int8_t* 
     __syncthreads();
     const int n = s.nmoves;
     const uint16_t* ml = moves + (size_t)i * MAXM;
-    mixed_legal_weights(cfg, lp, ml, n, gam + (size_t)i * 4096, np_mt + (size_t)i * MT_WORDS, mt_a, mt_b, vals,
-                        lane);
+    mixed_legal_weights(cfg, lp, ml, n, gam, np_mt + (size_t)i * MT_WORDS, mt3, scratch, vals, lane);
     if (lane == 0) s_pick = choose_weighted(vals, cum, n, py_mt + (size_t)i * MT_WORDS);
     __syncthreads();
     commit_move(cfg, s, i, ml[s_pick], boards, rec, last_board, ctr, lane);
@@ -237,7 +239,6 @@ struct kv_engine {
     float* logits = nullptr;
     float* values = nullptr;
     float* last_probs = nullptr;
-    double* gam = nullptr;
     uint32_t* np_mt = nullptr;
     uint32_t* py_mt = nullptr;
     kv_record* rec = nullptr;
@@ -341,7 +342,6 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
     ALLOC(e->logits, R * 4096 * sizeof(float));
     ALLOC(e->values, R * sizeof(float));
     ALLOC(e->last_probs, S * 4096 * sizeof(float));
-    ALLOC(e->gam, S * 4096 * sizeof(double));
     ALLOC(e->np_mt, S * kv::MT_WORDS * sizeof(uint32_t));
     ALLOC(e->py_mt, S * kv::MT_WORDS * sizeof(uint32_t));
     ALLOC(e->rec, (size_t)e->cfg.record_cap * sizeof(kv_record));
@@ -464,14 +464,13 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
                                e->boards);
         if ((rc = eng_eval(e, e->boards, e->dc.rows))) return rc;
         if (!mcts) {
-            hipLaunchKernelGGL(kv::k_sample, dim3(S), dim3(64), 0, e->st, e->dc, e->slots, e->boards, e->moves,
-                               e->logits, e->values, e->last_probs, e->gam, e->np_mt, e->py_mt, e->rec,
-                               e->last_board, e->ctr);
+            hipLaunchKernelGGL(kv::k_sample, dim3(S), dim3(256), 0, e->st, e->dc, e->slots, e->boards, e->moves,
+                               e->logits, e->values, e->last_probs, e->np_mt, e->py_mt, e->rec, e->last_board,
+                               e->ctr);
             KV_HIP(hipGetLastError());
         } else {
             const kv::Tree& t = e->tree;
-            if ((rc = kv::mcts_root(e->dc, t, e->slots, e->moves, e->logits, e->values, e->probs, e->gam, e->np_mt,
-                                    e->st)))
+            if ((rc = kv::mcts_root(e->dc, t, e->slots, e->moves, e->logits, e->values, e->probs, e->np_mt, e->st)))
                 return rc;
             for (int k = 0; k < e->dc.sims; ++k) {
                 if ((rc = kv::mcts_select(e->dc, t, e->slots, e->boards, e->nn_boards, e->ctr, e->st))) return rc;
@@ -564,7 +563,7 @@ void kv_destroy(kv_engine* e) {
     (void)hipSetDevice(e->cfg.device);
     if (e->st) (void)hipStreamSynchronize(e->st);
     kv::Tree& t = e->tree;
-    void* bufs[] = {e->slots, e->boards, e->moves, e->logits, e->values, e->last_probs, e->gam,
+    void* bufs[] = {e->slots, e->boards, e->moves, e->logits, e->values, e->last_probs,
                     e->np_mt, e->py_mt, e->rec, e->games, e->last_board, e->ctr,
                     t.e_move, t.e_P, t.e_N, t.e_W, t.e_child, t.n_first, t.n_cnt, t.n_N, t.path,
                     t.leaf_moves, e->ms, e->nn_boards, e->probs, e->sqrt_tab};

@@ -49,21 +49,22 @@ __device__ inline float puct(float c_puct, float P, float sq, int N, float W) {
     return q + u;
 }
 
-__global__ __launch_bounds__(64) void k_mcts_root(DevCfg cfg, Tree t, Slot* slots, const uint16_t* moves,
-                                                  const float* logits, const float* values, float* probs,
-                                                  double* gam, uint32_t* np_mt) {
-    __shared__ uint32_t mt_a[MT_N], mt_b[MT_N];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_mcts_root(DevCfg cfg, Tree t, Slot* slots, const uint16_t* moves,
+                                                   const float* logits, const float* values, float* probs,
+                                                   uint32_t* np_mt) {
+    __shared__ uint32_t mt3[3 * MT_N];
+    __shared__ double gam[4096];
     __shared__ double vals[MAXM];
+    __shared__ int scratch[8];
     const int i = blockIdx.x, lane = threadIdx.x;
     Slot s = slots[i];
     if (s.status != ST_ACTIVE) return;
     float* lp = probs + (size_t)i * 4096;
-    wave_softmax_4096(logits + (size_t)i * 4096, lp, lane);
+    if (lane < 64) wave_softmax_4096(logits + (size_t)i * 4096, lp, lane);
     __syncthreads();
     const int n = s.nmoves;
     const uint16_t* ml = moves + (size_t)i * MAXM;
-    mixed_legal_weights(cfg, lp, ml, n, gam + (size_t)i * 4096, np_mt + (size_t)i * MT_WORDS, mt_a, mt_b, vals,
-                        lane);
+    mixed_legal_weights(cfg, lp, ml, n, gam, np_mt + (size_t)i * MT_WORDS, mt3, scratch, vals, lane);
     __shared__ double s_total;
     if (lane == 0) {
         double total = 0.0;
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(64) void k_mcts_root(DevCfg cfg, Tree t, Slot* slot
     __syncthreads();
     const double total = s_total;
     const size_t eb = (size_t)i * t.ecap, nb = (size_t)i * t.ncap;
-    for (int j = lane; j < n; j += 64) {
+    for (int j = lane; j < n; j += 256) {
         t.e_move[eb + j] = ml[j];
         t.e_P[eb + j] = total == 0.0 ? 1.0f / (float)n : (float)(vals[j] / total);
         t.e_N[eb + j] = 0;
@@ -284,9 +285,9 @@ __global__ void k_hash_eval(const int8_t* boards, int rows, float* logits, float
 }
 
 int mcts_root(const DevCfg& cfg, const Tree& t, Slot* slots, const uint16_t* moves, const float* logits,
-              const float* values, float* probs, double* gam, uint32_t* np_mt, hipStream_t st) {
-    hipLaunchKernelGGL(k_mcts_root, dim3(cfg.slots), dim3(64), 0, st, cfg, t, slots, moves, logits, values, probs,
-                       gam, np_mt);
+              const float* values, float* probs, uint32_t* np_mt, hipStream_t st) {
+    hipLaunchKernelGGL(k_mcts_root, dim3(cfg.slots), dim3(256), 0, st, cfg, t, slots, moves, logits, values, probs,
+                       np_mt);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }

@@ -7,13 +7,13 @@
 //     _randbelow_with_getrandbits).
 // A stream lives in HBM as 624 state words + the output index (625 u32).
 //
-// The Dirichlet draw is wave-parallel: each gamma attempt consumes exactly four
-// u32 (U = res53, V = -log(1 - res53)), so attempt a reads words 4a..4a+3 and
-// the 64 lanes of a wave run 64 consecutive attempts at once; accepted attempts
-// are compacted in order with a ballot + prefix popcount, and the draw stops at
-// the exact attempt that yields element k-1 so the stream position matches the
-// sequential generator word for word. The twist is done by the wave in three
-// dependency-free phases ([0,227), [227,454), [454,623) + the last word).
+// The Dirichlet draw is workgroup-parallel: each gamma attempt consumes exactly
+// four u32 (U = res53, V = -log(1 - res53)), so attempt a reads words
+// 4a..4a+3 and 256 threads run 256 consecutive attempts at once; accepted
+// attempts are ranked in order (ballots + prefix popcounts) and the draw stops
+// at the exact attempt that yields element k-1 so the stream position matches
+// the sequential generator word for word. The twist runs on the workgroup in
+// three dependency-free phases ([0,227), [227,454), [454,623) + the last word).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -108,109 +108,104 @@ __host__ __device__ inline int mt_randbelow_serial(uint32_t* mt, int n) {
     return (int)r;
 }
 
-// ------------------------------------------------------- wave forms ----
-// All of these are called by every lane of ONE 64-lane wave (blockDim 64).
+// ------------------------------------------------------ block forms ----
+// Called by every thread of ONE 256-thread workgroup (4 waves).
+constexpr int RNG_THREADS = 256;
 
-// in-place twist of an LDS state
-__device__ inline void mt_twist_wave(uint32_t* mt, int lane) {
-    for (int base = 0; base < MT_N - MT_M; base += 64) {  // [0,227): reads old words only
-        const int kk = base + lane;
+// in-place twist of an LDS state: three dependency-free phases
+// ([0,227) reads old words only; [227,454) and [454,623) read words the
+// previous phase produced), then the last word
+__device__ inline void mt_twist_block(uint32_t* mt, int tid) {
+    constexpr int P = MT_N - MT_M;  // 227
+#pragma unroll
+    for (int ph = 0; ph < 3; ++ph) {
+        const int lo = ph * P, hi = ph < 2 ? lo + P : MT_N - 1;
+        const int kk = lo + tid;
         uint32_t v = 0;
-        if (kk < MT_N - MT_M) v = mt_mix(mt[kk], mt[kk + 1], mt[kk + MT_M]);
+        if (kk < hi) v = mt_mix(mt[kk], mt[kk + 1], ph == 0 ? mt[kk + MT_M] : mt[kk + (MT_M - MT_N)]);
         __syncthreads();
-        if (kk < MT_N - MT_M) mt[kk] = v;
+        if (kk < hi) mt[kk] = v;
         __syncthreads();
     }
-    for (int lo = MT_N - MT_M; lo < MT_N - 1; lo += MT_N - MT_M) {  // [227,454), [454,623)
-        const int hi = lo + (MT_N - MT_M) < MT_N - 1 ? lo + (MT_N - MT_M) : MT_N - 1;
-        for (int base = lo; base < hi; base += 64) {
-            const int kk = base + lane;
-            uint32_t v = 0;
-            if (kk < hi) v = mt_mix(mt[kk], mt[kk + 1], mt[kk + (MT_M - MT_N)]);
-            __syncthreads();
-            if (kk < hi) mt[kk] = v;
-            __syncthreads();
-        }
-    }
-    if (lane == 0) mt[MT_N - 1] = mt_mix(mt[MT_N - 1], mt[0], mt[MT_M - 1]);
+    if (tid == 0) mt[MT_N - 1] = mt_mix(mt[MT_N - 1], mt[0], mt[MT_M - 1]);
     __syncthreads();
 }
 
-// A wave-local view of a stream: `cur` holds the raw state whose tempered
-// words are being consumed at index `pos`; `nxt` the state after one more
-// twist (valid when have_nxt).
-struct WaveMT {
-    uint32_t* cur;
-    uint32_t* nxt;
+// A block-local view of a stream: b0 is the raw state whose tempered words are
+// consumed from `pos`; b1, b2 the states after one / two more twists (valid
+// below nready).
+struct BlockMT {
+    uint32_t *b0, *b1, *b2;  // named, not an array: a runtime-indexed array would live in scratch
     int pos;
-    int have_nxt;
+    int nready;
 };
 
-__device__ inline void wmt_load(WaveMT& w, const uint32_t* g, uint32_t* lds_a, uint32_t* lds_b, int lane) {
-    for (int i = lane; i < MT_N; i += 64) lds_a[i] = g[i];
-    w.cur = lds_a;
-    w.nxt = lds_b;
+__device__ inline void bmt_load(BlockMT& w, const uint32_t* g, uint32_t* lds3, int tid) {
+    for (int i = tid; i < MT_N; i += RNG_THREADS) lds3[i] = g[i];
+    w.b0 = lds3;
+    w.b1 = lds3 + MT_N;
+    w.b2 = lds3 + 2 * MT_N;
     w.pos = (int)g[MT_N];
-    w.have_nxt = 0;
+    w.nready = 1;
     __syncthreads();
     if (w.pos >= MT_N) {
-        mt_twist_wave(w.cur, lane);
+        mt_twist_block(w.b0, tid);
         w.pos = 0;
     }
 }
 
-__device__ inline void wmt_store(const WaveMT& w, uint32_t* g, int lane) {
-    for (int i = lane; i < MT_N; i += 64) g[i] = w.cur[i];
-    if (lane == 0) g[MT_N] = (uint32_t)w.pos;
+__device__ inline void bmt_store(const BlockMT& w, uint32_t* g, int tid) {
+    for (int i = tid; i < MT_N; i += RNG_THREADS) g[i] = w.b0[i];
+    if (tid == 0) g[MT_N] = (uint32_t)w.pos;
 }
 
-// make words [pos, pos + need) addressable (need <= 624)
-__device__ inline void wmt_ensure(WaveMT& w, int need, int lane) {
-    if (w.pos + need > MT_N && !w.have_nxt) {
-        for (int i = lane; i < MT_N; i += 64) w.nxt[i] = w.cur[i];
+// make words [pos, pos + need) addressable (pos + need <= 3 * 624)
+__device__ inline void bmt_ensure(BlockMT& w, int need, int tid) {
+    while (w.pos + need > MT_N * w.nready) {
+        uint32_t* src = w.nready == 1 ? w.b0 : w.b1;
+        uint32_t* dst = w.nready == 1 ? w.b1 : w.b2;
+        for (int i = tid; i < MT_N; i += RNG_THREADS) dst[i] = src[i];
         __syncthreads();
-        mt_twist_wave(w.nxt, lane);
-        w.have_nxt = 1;
+        mt_twist_block(dst, tid);
+        ++w.nready;
     }
 }
 
-__device__ inline uint32_t wmt_word(const WaveMT& w, int j) {  // j relative to pos
+__device__ inline uint32_t bmt_word(const BlockMT& w, int j) {  // j relative to pos
     const int i = w.pos + j;
-    return mt_temper(i < MT_N ? w.cur[i] : w.nxt[i - MT_N]);
+    return mt_temper(i < MT_N ? w.b0[i] : (i < 2 * MT_N ? w.b1[i - MT_N] : w.b2[i - 2 * MT_N]));
 }
 
-__device__ inline void wmt_advance(WaveMT& w, int n) {
+__device__ inline void bmt_advance(BlockMT& w, int n) {
     w.pos += n;
-    if (w.pos >= MT_N && w.have_nxt) {  // pos == MT_N without nxt: cur exhausted, twist on demand
-        uint32_t* t = w.cur;
-        w.cur = w.nxt;
-        w.nxt = t;
+    while (w.pos >= MT_N && w.nready > 1) {  // pos == MT_N with nothing ready: twist on demand
+        uint32_t* t = w.b0;
+        w.b0 = w.b1;
+        w.b1 = w.b2;
+        w.b2 = t;
         w.pos -= MT_N;
-        w.have_nxt = 0;
+        --w.nready;
     }
 }
 
-__device__ inline double wave_bcast_d(double v, int src) {
-    const unsigned long long u = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffu), src);
-    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), src);
-    return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
-}
-
-// numpy RandomState.dirichlet([alpha]*k) (legacy). gamma values go to `gam`
-// (k doubles, global or LDS), the serial sum is returned to every lane;
-// *attempts receives the attempt count. Caller multiplies by 1/acc when it
-// needs normalised values (the reference computes val * invacc).
-__device__ inline double wave_dirichlet_gamma(WaveMT& w, double alpha, int k, double* gam, long long* attempts,
-                                              int lane) {
+// numpy RandomState.dirichlet([alpha]*k) (legacy) without the final scaling:
+// gamma values go to gam[0..k) (LDS or global), the serial left-to-right fp64
+// sum is returned to every thread, *attempts gets the attempt count. Each
+// attempt consumes exactly four u32 (U = res53, V = -log(1 - res53)), so the
+// 256 threads run 256 consecutive attempts at once; accepted attempts are
+// ranked in attempt order (wave ballots + a 4-wave prefix) and the draw stops
+// at the exact attempt that yields element k-1, leaving the stream where the
+// sequential generator leaves it. `scratch` is 8 ints of LDS.
+__device__ inline double block_dirichlet_gamma(BlockMT& w, double alpha, int k, double* gam, long long* attempts,
+                                               int* scratch, int tid) {
+    const int lane = tid & 63, wave = tid >> 6;
     const double one_m = 1.0 - alpha, inv_a = 1. / alpha;
-    double acc = 0.0;
     int base = 0;
     long long att = 0;
     while (base < k) {
-        wmt_ensure(w, 256, lane);
-        const uint32_t w0 = wmt_word(w, 4 * lane), w1 = wmt_word(w, 4 * lane + 1);
-        const uint32_t w2 = wmt_word(w, 4 * lane + 2), w3 = wmt_word(w, 4 * lane + 3);
+        bmt_ensure(w, 4 * RNG_THREADS, tid);
+        const uint32_t w0 = bmt_word(w, 4 * tid), w1 = bmt_word(w, 4 * tid + 1);
+        const uint32_t w2 = bmt_word(w, 4 * tid + 2), w3 = bmt_word(w, 4 * tid + 3);
         const double U = res53(w0, w1);
         const double V = -log(1.0 - res53(w2, w3));
         double X;
@@ -224,46 +219,43 @@ __device__ inline double wave_dirichlet_gamma(WaveMT& w, double alpha, int k, do
             ok = X <= (V + Y);
         }
         const unsigned long long mask = __ballot(ok);
-        const int cnt = __popcll(mask);
-        const int rem = k - base;
-        int used = 64;
-        unsigned long long take = mask;
-        if (cnt >= rem) {  // stop at the attempt that yields element k-1
-            unsigned long long m = mask;
-            for (int i = 0; i < rem - 1; ++i) m &= m - 1;
-            const int last = __ffsll(m) - 1;
-            used = last + 1;
-            take = (last == 63) ? mask : (mask & ((2ull << last) - 1));
+        if (lane == 0) scratch[wave] = __popcll(mask);
+        if (tid == 0) scratch[4] = RNG_THREADS;  // attempts used unless the draw completes here
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            before += q < wave ? scratch[q] : 0;
+            total += scratch[q];
         }
-        const unsigned long long below = lane == 0 ? 0ull : (take & ((1ull << lane) - 1));
-        if ((take >> lane) & 1) gam[base + __popcll(below)] = X;
-        // serial left-to-right accumulation in element order
-        for (unsigned long long m = take; m; m &= m - 1) acc = acc + wave_bcast_d(X, __ffsll(m) - 1);
-        base += __popcll(take);
+        const int rank = before + __popcll(mask & ((1ull << lane) - 1));
+        const int rem = k - base;
+        if (ok && rank == rem - 1) scratch[4] = tid + 1;  // the attempt that yields element k-1
+        if (ok && rank < rem) gam[base + rank] = X;
+        __syncthreads();
+        const int used = scratch[4];
+        base += total < rem ? total : rem;
         att += used;
-        wmt_advance(w, 4 * used);
+        bmt_advance(w, 4 * used);
+        __syncthreads();  // scratch reused by the next round
     }
+    __shared__ double s_acc;
+    if (tid == 0) {
+        double acc = 0.0;
+        for (int i = 0; i < k; ++i) acc = acc + gam[i];
+        s_acc = acc;
+    }
+    __syncthreads();
     *attempts = att;
-    return acc;
+    return s_acc;
 }
 
-// two consecutive u32 as res53 (CPython random() / numpy random_sample())
-__device__ inline double wave_random(WaveMT& w, int lane) {
-    wmt_ensure(w, 2, lane);
-    const double r = res53(wmt_word(w, 0), wmt_word(w, 1));
-    wmt_advance(w, 2);
+// two consecutive u32 as res53 (numpy random_sample()); all threads get it
+__device__ inline double block_random(BlockMT& w, int tid) {
+    bmt_ensure(w, 2, tid);
+    const double r = res53(bmt_word(w, 0), bmt_word(w, 1));
+    bmt_advance(w, 2);
     return r;
-}
-
-__device__ inline int wave_randbelow(WaveMT& w, int n, int lane) {
-    int k = 0;
-    while ((n >> k) != 0) ++k;
-    for (;;) {
-        wmt_ensure(w, 1, lane);
-        const uint32_t r = wmt_word(w, 0) >> (32 - k);
-        wmt_advance(w, 1);
-        if ((int)r < n) return (int)r;
-    }
 }
 
 }  // namespace kv
