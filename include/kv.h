@@ -64,6 +64,11 @@ int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv);
  *                1e-4 of the reference; not bit-exact to fp32) */
 #define KV_PREC_FP32 0
 #define KV_PREC_BF16X3 1
+/* KV_PREC_BF16X6 fp32-accurate: both operands split exactly into three bf16
+ *                pieces, the six piece products of weight >= 2^-16 on bf16
+ *                MFMA with fp32 accumulation (Winograd tower above 16 boards;
+ *                fp32 direct below). Logit error at fp32's level. */
+#define KV_PREC_BF16X6 2
 int kv_net_set_precision(kv_net* net, int precision);
 /* Algorithm of the fp32 3x3 convs with Cin 256/512:
  * KV_ALGO_AUTO      Winograd for batches > 16 boards, direct (split-K) below

@@ -258,14 +258,6 @@ __global__ __launch_bounds__(512) void conv3x3_kernel(const float* __restrict__ 
 // load time ([Cout][9][Cin] bf16 hi and lo); activations stay fp32 in HBM and
 // are split while staging the halo into LDS. Strides (bytes): halo pixel 64,
 // halo row 656, weight row 80 -- conflict-free ds_read_b128 for every tap.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ inline unsigned bf16_rne(float x) {
-    const unsigned u = __float_as_uint(x);
-    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
-}
 
 __device__ inline void split2(float a, float b, unsigned& hi, unsigned& lo) {
     const unsigned ha = bf16_rne(a), hb = bf16_rne(b);
@@ -610,7 +602,9 @@ struct kv_net {
     float* slab = nullptr;  // split-K partial sums (small batches)
     int algo = KV_ALGO_AUTO;
     float* U = nullptr;     // Winograd weights [36][Cout][Cin] of convs 1..11
+    uint16_t* Up[3] = {};   // the same split into bf16 h / m / l (KV_PREC_BF16X6)
     size_t uoff[12] = {};
+    size_t utot = 0;
     float* V = nullptr;     // Winograd workspaces [36][cap*4][512]
     float* V256 = nullptr;  // conv2's input transform [36][cap*4][256]
     float* Mw = nullptr;
@@ -698,7 +692,7 @@ static int launch_conv(const float* in, const float* w, const float* sc, const f
 
 // Winograd for the fp32 tower when the batch is past the split-K class
 static bool use_wino(const kv_net* net, int B) {
-    if (net->precision != KV_PREC_FP32) return false;
+    if (net->precision == KV_PREC_BF16X3) return false;
     if (net->algo == KV_ALGO_WINOGRAD) return true;
     return net->algo == KV_ALGO_AUTO && B > kSplitMaxBoards;
 }
@@ -755,6 +749,34 @@ static int launch_wino_gemm(const float* V, const float* U, float* M, int rows, 
     return launch_wino_gemm_t<K, 4, 2, 1, 2>(V, U, M, rows, stride, st);
 }
 
+template <int K>
+static int launch_wino_gemm_bf6(const float* V, const uint16_t* Uh, const uint16_t* Um, const uint16_t* Ul, float* M,
+                                int rows, int stride, hipStream_t st) {
+    using T = kv::WinoBf6;
+    static bool attr_set = false;
+    if (!attr_set) {
+        KV_HIP(hipFuncSetAttribute((const void*)kv::wino_gemm_bf6_kernel<K>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::BYTES));
+        attr_set = true;
+    }
+    const int nwg = kv::WN_XI * (rows / T::WM) * (512 / T::WN);
+    KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0, KV_EINVAL, "wino gemm bf16x6: rows %d", rows);
+    hipLaunchKernelGGL((kv::wino_gemm_bf6_kernel<K>), dim3(nwg), dim3(256), T::BYTES, st, V, Uh, Um, Ul, M, rows, 512,
+                       stride);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+// the Winograd GEMMs of conv layer l in the net's precision
+template <int K>
+static int wino_gemm_layer(kv_net* net, int l, const float* V, float* M, int rows, int stride, hipStream_t st) {
+    if (net->precision == KV_PREC_BF16X6) {
+        const size_t o = net->uoff[l];
+        return launch_wino_gemm_bf6<K>(V, net->Up[0] + o, net->Up[1] + o, net->Up[2] + o, M, rows, stride, st);
+    }
+    return launch_wino_gemm<K>(V, net->U + net->uoff[l], M, rows, stride, st);
+}
+
 template <bool RESID, bool WRITE_Y, bool NEXT_V>
 static int launch_wino_out(const float* M, int b0, int nb, int stride, const float* sc, const float* sh,
                            const float* resid, float* Y, float* Vn, hipStream_t st) {
@@ -783,7 +805,7 @@ static int wino_blocks(kv_net* net, int b0, int nb, int stride, bool mark, hipSt
     float* V = net->V;
     float* M = net->Mw;
     int rc;
-    if ((rc = launch_wino_gemm<256>(net->V256 + ro256, net->U + net->uoff[1], M + ro, rows, stride, st))) return rc;
+    if ((rc = wino_gemm_layer<256>(net, 1, net->V256 + ro256, M + ro, rows, stride, st))) return rc;
     if (after_first) KV_HIP(hipEventRecord(after_first, st));
     if ((rc = launch_wino_out<false, true, true>(M, b0, nb, stride, W + o.scale[1], W + o.shift[1], nullptr, net->X,
                                                  V, st)))
@@ -793,12 +815,12 @@ static int wino_blocks(kv_net* net, int b0, int nb, int stride, bool mark, hipSt
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         const bool m = mark && r == 2;  // one representative residual GEMM for the engine's timing hook
         if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-        if ((rc = launch_wino_gemm<512>(V + ro, net->U + net->uoff[l1], M + ro, rows, stride, st))) return rc;
+        if ((rc = wino_gemm_layer<512>(net, l1, V + ro, M + ro, rows, stride, st))) return rc;
         if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
         if ((rc = launch_wino_out<false, false, true>(M, b0, nb, stride, W + o.scale[l1], W + o.shift[l1], nullptr,
                                                       nullptr, V, st)))
             return rc;
-        if ((rc = launch_wino_gemm<512>(V + ro, net->U + net->uoff[l2], M + ro, rows, stride, st))) return rc;
+        if ((rc = wino_gemm_layer<512>(net, l2, V + ro, M + ro, rows, stride, st))) return rc;
         rc = r < 4 ? launch_wino_out<true, true, true>(M, b0, nb, stride, W + o.scale[l2], W + o.shift[l2], net->X,
                                                        net->X, V, st)
                    : launch_wino_out<true, true, false>(M, b0, nb, stride, W + o.scale[l2], W + o.shift[l2], net->X,
@@ -955,6 +977,8 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
             tot += (size_t)kv::WN_XI * kv::kConv[l].cout * kv::kConv[l].cin;
         }
         KV_HIP(hipMalloc(&net->U, tot * sizeof(float)));
+        for (int p = 0; p < 3; ++p) KV_HIP(hipMalloc(&net->Up[p], tot * sizeof(uint16_t)));
+        net->utot = tot;
     }
     for (int l = 1; l < 12; ++l) {
         const size_t n = (size_t)kv::kConv[l].cout * kv::kConv[l].cin;
@@ -962,6 +986,9 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
                            net->w + net->off.w[l], kv::kConv[l].cout, kv::kConv[l].cin, net->U + net->uoff[l]);
         KV_HIP(hipGetLastError());
     }
+    hipLaunchKernelGGL(kv::split3_kernel, dim3((unsigned)((net->utot + 255) / 256)), dim3(256), 0, 0, net->U,
+                       net->utot, net->Up[0], net->Up[1], net->Up[2]);
+    KV_HIP(hipGetLastError());
     KV_HIP(hipDeviceSynchronize());
     net->loaded = true;
     return KV_OK;
@@ -977,7 +1004,7 @@ int kv_net_set_algo(kv_net* net, int algo) {
 
 int kv_net_set_precision(kv_net* net, int precision) {
     KV_REQUIRE(net, KV_EINVAL, "kv_net_set_precision: NULL");
-    KV_REQUIRE(precision == KV_PREC_FP32 || precision == KV_PREC_BF16X3, KV_EINVAL,
+    KV_REQUIRE(precision == KV_PREC_FP32 || precision == KV_PREC_BF16X3 || precision == KV_PREC_BF16X6, KV_EINVAL,
                "kv_net_set_precision: unknown precision %d", precision);
     net->precision = precision;
     return KV_OK;
@@ -1038,6 +1065,7 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->T);
     (void)hipFree(net->pfeat);
     (void)hipFree(net->U);
+    for (int p = 0; p < 3; ++p) (void)hipFree(net->Up[p]);
     (void)hipFree(net->V);
     (void)hipFree(net->Mw);
     (void)hipFree(net->V256);

@@ -314,4 +314,162 @@ __global__ __launch_bounds__(WR * WC * 64) void wino_gemm_kernel(const float* __
             }
 }
 
+// ------------------------------------------------ bf16x6 (fp32-accurate) --
+// x == h + m + l exactly for normal fp32 x: h = bf16(x), m = bf16(x - h),
+// l = bf16(x - h - m) (each difference is exact in fp32, the last one has at
+// most 8 significant bits). A product x*y is the sum of the 9 piece products;
+// the GEMM keeps the six with weight >= 2^-16 (hh, hm, mh, hl, lh, mm) -- the
+// dropped three are ~2^-24 of the product, the size of fp32's own rounding --
+// each an exact bf16 x bf16 product accumulated in fp32 on
+// v_mfma_f32_32x32x16_bf16 (16x the f32 MFMA rate: 6 products = 2.67x).
+// Measured on the peaked weight set: max |dlogit| 4.9e-6 (fp32 direct 4.4e-6).
+__device__ inline void split3(float x, unsigned& h, unsigned& m, unsigned& l) {
+    h = bf16_rne(x);
+    const float r1 = x - __uint_as_float(h << 16);
+    m = bf16_rne(r1);
+    const float r2 = r1 - __uint_as_float(m << 16);
+    l = bf16_rne(r2);
+}
+
+__global__ void split3_kernel(const float* __restrict__ w, size_t n, uint16_t* __restrict__ h,
+                              uint16_t* __restrict__ m, uint16_t* __restrict__ l) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    unsigned a, b, c;
+    split3(w[i], a, b, c);
+    h[i] = (uint16_t)a;
+    m[i] = (uint16_t)b;
+    l[i] = (uint16_t)c;
+}
+
+// M[xi] = V[xi] x U[xi]^T with both operands in three bf16 pieces. V stays
+// fp32 in HBM and is split while it is staged into LDS; U is split once at
+// load time. Workgroup: 128 rows x 128 channels of one xi, 4 waves of 64x64
+// (2x2 tiles), k-tiles of 16 (one MFMA k-step), double-buffered: A and B
+// piece rows at a 48-byte stride (conflict-free ds_read_b128), 72 KB of LDS
+// -> 2 workgroups per CU. Tile order as in wino_gemm_kernel (XCD groups).
+struct WinoBf6 {
+    static constexpr int WM = 128, WN = 128, CK = 16, SR = 48;  // SR: bytes per piece row
+    static constexpr int PIECE = 128 * SR;                       // one piece of A or B
+    static constexpr int BUF = 6 * PIECE;                        // A h/m/l + B h/m/l
+    static constexpr size_t BYTES = 2 * BUF;
+};
+
+template <int K>
+__global__ __launch_bounds__(256) void wino_gemm_bf6_kernel(const float* __restrict__ V,
+                                                            const uint16_t* __restrict__ Uh,
+                                                            const uint16_t* __restrict__ Um,
+                                                            const uint16_t* __restrict__ Ul, float* __restrict__ M,
+                                                            int rows, int cout, int stride) {
+    using T = WinoBf6;
+    constexpr int CK = T::CK, SR = T::SR, PIECE = T::PIECE, BUF = T::BUF, NK = K / CK;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int CT = cout / T::WN, RT = rows / T::WM;
+    const int nwg = WN_XI * RT * CT;
+    const int idx0 = (int)(blockIdx.x & 7) * (nwg >> 3) + (int)(blockIdx.x >> 3);
+    const int xi = idx0 / (CT * RT);
+    const int n_base = (idx0 % CT) * T::WN;
+    const int r_base = ((idx0 / CT) % RT) * T::WM;
+    const float* Va = V + ((size_t)xi * stride + r_base) * K;
+    const size_t ub = ((size_t)xi * cout + n_base) * K;
+
+    f32x4 ra[2];
+    u32x4 rb[3];
+    auto loadA = [&](int kt) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int i = tid + q * 256;  // 512 float4: 128 rows x 4
+            ra[q] = *(const f32x4*)(Va + (size_t)(i >> 2) * K + kt * CK + (i & 3) * 4);
+        }
+    };
+    auto storeA = [&](unsigned char* buf) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int i = tid + q * 256;
+            const int off = (i >> 2) * SR + (i & 3) * 8;
+            unsigned h[4], m[4], l[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) split3(ra[q][e], h[e], m[e], l[e]);
+            *(u32x2*)(buf + off) = u32x2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
+            *(u32x2*)(buf + PIECE + off) = u32x2{m[0] | (m[1] << 16), m[2] | (m[3] << 16)};
+            *(u32x2*)(buf + 2 * PIECE + off) = u32x2{l[0] | (l[1] << 16), l[2] | (l[3] << 16)};
+        }
+    };
+    auto loadB = [&](int kt) {  // 128 channels x 16 k x 3 pieces: one 16-byte chunk per thread per piece
+        const size_t o = ub + (size_t)(tid >> 1) * K + kt * CK + (tid & 1) * 8;
+        rb[0] = *(const u32x4*)(Uh + o);
+        rb[1] = *(const u32x4*)(Um + o);
+        rb[2] = *(const u32x4*)(Ul + o);
+    };
+    auto storeB = [&](unsigned char* buf) {
+        const int off = 3 * PIECE + (tid >> 1) * SR + (tid & 1) * 16;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *(u32x4*)(buf + off + p * PIECE) = rb[p];
+    };
+
+    const int h = lane >> 5, li = lane & 31;
+    int aoff[2], boff[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        aoff[t] = (wm * 64 + t * 32 + li) * SR + 16 * h;
+        boff[t] = 3 * PIECE + (wn * 64 + t * 32 + li) * SR + 16 * h;
+    }
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    loadA(0);
+    loadB(0);
+    for (int kt = 0; kt < NK; ++kt) {
+        unsigned char* buf = lds + (kt & 1) * BUF;
+        storeA(buf);
+        storeB(buf);
+        if (kt + 1 < NK) {
+            loadA(kt + 1);
+            loadB(kt + 1);
+        }
+        __syncthreads();
+        bf16x8 a[3][2], b[3][2];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                a[p][t] = *(const bf16x8*)(buf + aoff[t] + p * PIECE);
+                b[p][t] = *(const bf16x8*)(buf + boff[t] + p * PIECE);
+            }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {  // small terms first
+                f32x16 c = acc[mt][nt];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mt], b[2][nt], c, 0, 0, 0);  // h*l
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][mt], b[0][nt], c, 0, 0, 0);  // l*h
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][mt], b[1][nt], c, 0, 0, 0);  // m*m
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mt], b[1][nt], c, 0, 0, 0);  // h*m
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][mt], b[0][nt], c, 0, 0, 0);  // m*h
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][mt], b[0][nt], c, 0, 0, 0);  // h*h
+                acc[mt][nt] = c;
+            }
+    }
+
+    float* Mo = M + ((size_t)xi * stride + r_base + wm * 64) * cout + n_base + wn * 64 + li;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                Mo[(size_t)row * cout + nt * 32] = acc[mt][nt][r];
+            }
+}
+
 }  // namespace kv

@@ -20,7 +20,7 @@ from . import _lib
 from .weights import pack_weights, state_dict_to_numpy
 
 
-PRECISIONS = {"fp32": 0, "bf16x3": 1}
+PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16x6": 2}
 ALGOS = {"auto": 0, "direct": 1, "winograd": 2}
 
 

@@ -13,8 +13,8 @@ pytestmark = pytest.mark.gpu
 TOL_P, TOL_V = 1e-4, 1e-5
 
 
-# (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x4,3x3) / bf16x3 direct
-MODES = [("fp32", "direct"), ("fp32", "winograd"), ("bf16x3", "auto")]
+# (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x4,3x3) / bf16x6 Winograd / bf16x3 direct
+MODES = [("fp32", "direct"), ("fp32", "winograd"), ("bf16x6", "winograd"), ("bf16x3", "auto")]
 
 
 def _net(variant, precision="fp32", algo="auto"):
@@ -59,7 +59,7 @@ def test_forward_batch_sizes_vs_torch(B, precision, algo):
     assert np.abs(vb.cpu().numpy() - v.cpu().numpy()).max() == 0.0
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "bf16x3"])
 def test_batch_invariance(precision):
     """A board's outputs do not depend on the batch it is evaluated in, within a
     batch-size class (<= 16 boards: split-K direct kernels; > 16: whole-K
