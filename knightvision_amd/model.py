@@ -2,11 +2,13 @@
 state_dict keys, ai/model.py:31-49), whose forward runs on the hand-written
 HIP kernels of libkv.so (knightvision_amd/csrc/kv_nn.hip).
 
-forward(x[N,12,8,8]) -> (policy logits [N,4096], value [N,1]), eval-mode
-BatchNorm semantics (the self-play path always calls model.eval(),
-self_play.py:77, :108). The module keeps torch Parameters so checkpoints load
-and save exactly like the reference's; the kernels read a BN-folded packed copy
-that is rebuilt whenever a parameter changes.
+forward(x[N,12,8,8]) -> (policy logits [N,4096], value [N,1]). In eval mode
+(the self-play path always calls model.eval(), self_play.py:77, :108) the
+forward is the HIP tower with BN folded; in train mode it is PyTorch-ROCm
+autograd over the same parameters (the update step of train.py, see
+knightvision_amd/train.py). The module keeps torch Parameters so checkpoints
+load and save exactly like the reference's; the kernels read a BN-folded packed
+copy that is rebuilt whenever a parameter or BN statistic changes.
 """
 from __future__ import annotations
 
@@ -15,6 +17,7 @@ import ctypes as C
 import numpy as np
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from . import _lib
 from .weights import pack_weights, state_dict_to_numpy
@@ -25,7 +28,8 @@ ALGOS = {"auto": 0, "direct": 1, "winograd": 2}
 
 
 class ResidualBlock(nn.Module):
-    """Parameter container for one residual block (ai/model.py:8-25)."""
+    """One residual block (ai/model.py:8-25). Its own forward is the training
+    path only; evaluation runs the whole tower in libkv.so."""
 
     def __init__(self, channels: int):
         super().__init__()
@@ -33,6 +37,10 @@ class ResidualBlock(nn.Module):
         self.bn1 = nn.BatchNorm2d(channels)
         self.conv2 = nn.Conv2d(channels, channels, kernel_size=3, padding=1)
         self.bn2 = nn.BatchNorm2d(channels)
+
+    def forward(self, x):
+        y = self.bn2(self.conv2(F.relu(self.bn1(self.conv1(x)))))
+        return F.relu(y + x)
 
 
 class KVNet:
@@ -128,10 +136,25 @@ class ChessNet(nn.Module):
             self._kv_key = key
         return self._kv
 
+    def _train_forward(self, x):
+        """Training mode (ai/model.py:51-77 with batch-statistics BatchNorm):
+        PyTorch-ROCm autograd over the same parameters, for train.py's update
+        step (knightvision_amd.train). Evaluation never comes here."""
+        p = next(self.parameters())
+        x = x.to(device=p.device, dtype=p.dtype)
+        h = F.relu(self.bn2(self.conv2(F.relu(self.bn1(self.conv1(x))))))
+        for blk in self.res_blocks:
+            h = blk(h)
+        pol = self.policy_fc(torch.flatten(F.relu(self.policy_bn(self.policy_conv(h))), 1))
+        v = torch.flatten(F.relu(self.value_bn(self.value_conv(h))), 1)
+        val = torch.tanh(self.value_fc2(F.relu(self.value_fc1(v))))
+        return pol, val
+
     def forward(self, x):
         if self.training:
-            raise RuntimeError("knightvision_amd.ChessNet runs the eval-mode HIP forward; call .eval() "
-                               "(the reference self-play path does, self_play.py:77)")
+            if not isinstance(x, torch.Tensor):
+                x = torch.as_tensor(np.asarray(x))
+            return self._train_forward(x)
         if not isinstance(x, torch.Tensor):
             x = torch.as_tensor(np.asarray(x))
         dev = x.device if x.is_cuda else torch.device("cuda", torch.cuda.current_device())

@@ -1,0 +1,159 @@
+"""Policy/value update step of the learn loop on MI355X:
+the per-batch math of scripts/train.py _train_one_epoch (:126-196) and
+evaluate (:109-124), data-parallel over RCCL with DistributedDataParallel (one
+process per GPU; the reference wraps nn.DataParallel, ai/model_utils.py:26-28).
+
+Per batch, as the reference:
+  * forward under torch.cuda.amp.autocast (:161-162), losses in fp32:
+    loss_policy = cross_entropy(policy, move) (:169), loss_value =
+    mse(value.squeeze(), outcome) (:171), entropy of softmax(policy) (:173-175),
+    loss = loss_policy + loss_value - ENTROPY_COEF * entropy (:176);
+  * NaN / Inf loss -> batch skipped (:178-180);
+  * loss / accumulate_steps, GradScaler backward (:183-184); every
+    accumulate_steps batches or at the last one: unscale, clip_grad_norm 1.0,
+    scaler.step, scaler.update, zero_grad (:187-192).
+Defaults follow the reference's environment variables: BATCH_SIZE 4096,
+ACCUM_STEPS 2, LR 5e-4 (train.py:17-20), ENTROPY_COEF 0.01 (:461).
+
+Data bridge: the engine's records (int8 board codes,
+encode_move index, per-game reward) are expanded to the (12,8,8) planes of
+encode_board (ai/ai.py:17-30) on the device; self-play keeps the reference's
+plane order (K,Q,R,B,N,p) and move indexing (row 0 = rank 8), which differ from
+the PGN dataset's (train.py:542-545, :553-558) exactly as in the reference.
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+BATCH_SIZE = int(os.getenv("BATCH_SIZE", "4096"))
+ACCUM_STEPS = int(os.getenv("ACCUM_STEPS", "2"))
+LR = float(os.getenv("LR", "5e-4"))
+ENTROPY_COEF = float(os.getenv("ENTROPY_COEF", "0.01"))
+CLIP_NORM = 1.0
+
+
+def codes_to_planes_t(codes: torch.Tensor) -> torch.Tensor:
+    """int8 board codes [N,64] (0 empty, 1..12 = wK..bp) -> fp32 planes [N,12,8,8]
+    in encode_board's channel order (ai/ai.py:7-10, :17-30), on codes' device."""
+    c = codes.long()
+    planes = F.one_hot(c, 13)[..., 1:]  # [N,64,12]
+    return planes.permute(0, 2, 1).reshape(-1, 12, 8, 8).to(torch.float32).contiguous()
+
+
+@dataclass
+class Batch:
+    boards: torch.Tensor    # [B,12,8,8] fp32
+    moves: torch.Tensor     # [B] int64
+    outcomes: torch.Tensor  # [B] fp32
+
+
+def records_to_tensors(records: np.ndarray, games: np.ndarray, device) -> tuple:
+    """Engine records + finished-game table -> (codes int8 [N,64], moves int64 [N],
+    rewards fp32 [N]) on `device`; every record of a game carries that game's
+    reward (self_play.py:245-253)."""
+    reward_of = {int(g["game_id"]): float(g["reward"]) for g in games}
+    keep = np.array([int(r) in reward_of for r in records["game_id"]], dtype=bool)
+    rec = records[keep]
+    codes = torch.from_numpy(np.ascontiguousarray(rec["board"]).astype(np.int8)).to(device)
+    moves = torch.from_numpy(rec["move"].astype(np.int64)).to(device)
+    rew = torch.tensor([reward_of[int(g)] for g in rec["game_id"]], dtype=torch.float32, device=device)
+    return codes, moves, rew
+
+
+def batches(codes, moves, rewards, batch_size: int, shuffle: bool, generator: torch.Generator | None = None,
+            total: int | None = None):
+    """DataLoader(batch_size, shuffle) over the tensors (train.py:238-249). With
+    `total` > len (data-parallel ranks holding unequal shards) the epoch order
+    wraps around to `total` samples, so every rank runs the same number of
+    equal batches (DistributedSampler's padding)."""
+    n = codes.shape[0]
+    order = torch.randperm(n, generator=generator) if shuffle else torch.arange(n)
+    if total is not None and total > n:
+        order = order.repeat((total + n - 1) // n)[:total]
+    order = order.to(codes.device)
+    for i in range(0, order.numel(), batch_size):
+        ix = order[i:i + batch_size]
+        yield Batch(codes_to_planes_t(codes[ix]), moves[ix], rewards[ix])
+
+
+def batch_loss(model, b: Batch, entropy_coef: float = ENTROPY_COEF, amp: bool = True):
+    """The reference's per-batch loss (train.py:161-176): returns
+    (loss, loss_policy, loss_value, entropy, policy_logits)."""
+    dev_type = b.boards.device.type
+    with torch.autocast(device_type=dev_type, enabled=amp and dev_type == "cuda"):
+        pol, val = model(b.boards)
+    loss_policy = F.cross_entropy(pol.float(), b.moves)
+    loss_value = F.mse_loss(val.squeeze().float(), b.outcomes)
+    logp = F.log_softmax(pol.float(), dim=1)
+    entropy = -(F.softmax(pol.float(), dim=1) * logp).sum(dim=1).mean()
+    loss = loss_policy + loss_value - entropy_coef * entropy
+    return loss, loss_policy, loss_value, entropy, pol
+
+
+def make_scaler(device) -> torch.amp.GradScaler:
+    return torch.amp.GradScaler("cuda", enabled=torch.device(device).type == "cuda")
+
+
+def train_one_epoch(model, data, optimizer, scaler, accumulate_steps: int = ACCUM_STEPS,
+                    entropy_coef: float = ENTROPY_COEF, amp: bool = True) -> dict:
+    """_train_one_epoch (train.py:126-196) over an iterable of Batch. `model` may be
+    a DistributedDataParallel wrapper: gradients are averaged over the ranks by
+    RCCL all-reduce during backward (bucketed, overlapped with the backward)."""
+    data = list(data)
+    n = len(data)
+    model.train()
+    optimizer.zero_grad()
+    total, skipped, correct, seen, steps = 0.0, 0, 0, 0, 0
+    for i, b in enumerate(data):
+        loss, lp, lv, ent, pol = batch_loss(model, b, entropy_coef, amp)
+        if not torch.isfinite(loss):
+            skipped += 1
+            continue
+        scaler.scale(loss / accumulate_steps).backward()
+        if (i + 1) % accumulate_steps == 0 or i == n - 1:
+            scaler.unscale_(optimizer)
+            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=CLIP_NORM)
+            scaler.step(optimizer)
+            scaler.update()
+            optimizer.zero_grad()
+            steps += 1
+        total += float(loss.detach())
+        correct += int((pol.detach().argmax(1) == b.moves).sum())
+        seen += b.moves.numel()
+    return {"loss": total, "batches": n, "skipped": skipped, "optimizer_steps": steps,
+            "accuracy": correct / max(seen, 1), "samples": seen}
+
+
+@torch.no_grad()
+def evaluate(model, data) -> float:
+    """evaluate (train.py:109-124): mean of (CE + MSE) over samples, eval-mode
+    forward (the HIP tower for knightvision_amd.ChessNet)."""
+    model = model.module if hasattr(model, "module") else model  # DDP wrapper: evaluate the local replica
+    was = model.training
+    model.eval()
+    tot, cnt = 0.0, 0
+    for b in data:
+        pol, val = model(b.boards)
+        lp = F.cross_entropy(pol.float(), b.moves)
+        lv = F.mse_loss(val.squeeze().float(), b.outcomes)
+        tot += float(lp + lv) * b.boards.shape[0]
+        cnt += b.boards.shape[0]
+    model.train(was)
+    return tot / cnt if cnt else math.inf
+
+
+def wrap_ddp(model, device):
+    """DistributedDataParallel over the default process group (RCCL on GPUs, gloo on
+    CPU) when one is initialised with more than one rank; else the model itself."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dev = torch.device(device)
+        ids = [dev.index if dev.index is not None else 0] if dev.type == "cuda" else None
+        return torch.nn.parallel.DistributedDataParallel(model, device_ids=ids, bucket_cap_mb=64)
+    return model

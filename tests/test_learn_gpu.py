@@ -1,0 +1,38 @@
+"""The learn loop on one GPU (knightvision_amd.learn): self-play on the HIP
+engine -> records -> update step (PyTorch-ROCm autograd) -> self-play with the
+updated weights; after training, the eval-mode HIP forward of the trained
+module (BN folded from the updated running statistics) must match the torch
+fp32 restatement of ai/model.py within the logit tolerance."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_learn_loop_two_iterations():
+    from knightvision_amd.learn import reinforcement_loop
+    from knightvision_amd.model import ChessNet
+    from knightvision_amd.weights import synthetic_state_dict, state_dict_to_numpy
+    from oracle import torch_ref
+    torch.manual_seed(0)
+    m = ChessNet()
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(42, "bn").items()})
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    stats = reinforcement_loop(m, iterations=2, games_per_iter=8, device="cuda:0", epochs=1, batch_size=64,
+                               max_moves=24, slots=8, log=None)
+    assert stats[0]["records"] > 0 and stats[0]["games"] == 8
+    assert stats[1]["optimizer_steps"] > 0 and np.isfinite(stats[1]["train_loss"])
+    after = m.state_dict()
+    assert any(not torch.equal(before[k].cpu(), after[k].cpu()) for k in before if "weight" in k)
+    # trained weights + updated BN statistics through the HIP eval forward
+    m.eval()
+    g = np.random.default_rng(1)
+    codes = (g.integers(0, 13, size=(24, 64)) * (g.random((24, 64)) < 0.4))
+    from knightvision_amd.ai import codes_to_planes
+    planes = codes_to_planes(codes)
+    p, v = m(torch.from_numpy(planes).cuda())
+    sd = state_dict_to_numpy(m.state_dict())
+    rp, rv = torch_ref.forward({k: torch.from_numpy(x) for k, x in sd.items()}, planes)
+    assert np.abs(p.cpu().numpy() - rp.numpy()).max() <= 1e-4
+    assert np.abs(v.cpu().numpy() - rv.numpy()).max() <= 1e-5

@@ -1,0 +1,194 @@
+"""CPU tests of the learn-loop update step (knightvision_amd.train / learn):
+the data bridge against encode_board, the per-batch loss and the epoch loop
+against a plain restatement of scripts/train.py _train_one_epoch (:126-196),
+ChessNet's training-mode forward against a functional restatement of
+ai/model.py:51-77, and the world-size-2 gloo paths (DDP gradient averaging,
+the end-of-iteration all-gather + re-shard)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+import torch.nn as nn
+import torch.nn.functional as F
+
+from knightvision_amd import train as T
+
+
+class TinyNet(nn.Module):
+    """Same output contract as ChessNet (policy [B,4096], value [B,1]); small
+    enough for fast CPU tests of the update-step logic."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv = nn.Conv2d(12, 4, 3, padding=1)
+        self.bn = nn.BatchNorm2d(4)
+        self.pol = nn.Linear(256, 4096)
+        self.val = nn.Linear(256, 1)
+
+    def forward(self, x):
+        h = torch.flatten(F.relu(self.bn(self.conv(x))), 1)
+        return self.pol(h), torch.tanh(self.val(h))
+
+
+def _data(n, seed):
+    g = np.random.default_rng(seed)
+    codes = torch.from_numpy((g.integers(0, 13, size=(n, 64)) * (g.random((n, 64)) < 0.4)).astype(np.int8))
+    moves = torch.from_numpy(g.integers(0, 4096, size=n).astype(np.int64))
+    rew = torch.from_numpy(g.choice([-1.0, 0.2, 1.0], size=n).astype(np.float32))
+    return codes, moves, rew
+
+
+def test_codes_to_planes_matches_encode_board():
+    from knightvision_amd.ai import codes_to_planes
+    codes, _, _ = _data(50, 0)
+    got = T.codes_to_planes_t(codes).numpy()
+    assert np.array_equal(got, codes_to_planes(codes.numpy().astype(np.int64)))
+
+
+def _ref_loss(pol, val, moves, outcomes, coef):
+    # scripts/train.py:169-176, restated
+    lp = F.cross_entropy(pol.float(), moves)
+    lv = F.mse_loss(val.squeeze().float(), outcomes)
+    probs = F.softmax(pol.float(), dim=1)
+    ent = -(probs * F.log_softmax(pol.float(), dim=1)).sum(dim=1).mean()
+    return lp + lv - coef * ent
+
+
+def test_batch_loss_matches_reference_formula():
+    torch.manual_seed(0)
+    m = TinyNet()
+    codes, moves, rew = _data(32, 1)
+    b = T.Batch(T.codes_to_planes_t(codes), moves, rew)
+    loss = T.batch_loss(m, b, 0.01)[0]
+    pol, val = m(b.boards)
+    assert torch.allclose(loss, _ref_loss(pol, val, moves, rew, 0.01), rtol=1e-6, atol=1e-6)
+
+
+def _ref_epoch(model, data, opt, accum, coef):
+    # scripts/train.py:138-192 without the logging (GradScaler disabled on CPU)
+    opt.zero_grad()
+    n = len(data)
+    for i, b in enumerate(data):
+        pol, val = model(b.boards)
+        loss = _ref_loss(pol, val, b.moves, b.outcomes, coef)
+        if torch.isnan(loss) or torch.isinf(loss):
+            continue
+        (loss / accum).backward()
+        if ((i + 1) % accum == 0) or (i == n - 1):
+            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+            opt.step()
+            opt.zero_grad()
+
+
+@pytest.mark.parametrize("accum", [1, 2, 3])
+def test_train_one_epoch_matches_reference_loop(accum):
+    torch.manual_seed(1)
+    a = TinyNet()
+    b = TinyNet()
+    b.load_state_dict(a.state_dict())
+    codes, moves, rew = _data(70, 2)
+    data = list(T.batches(codes, moves, rew, 16, shuffle=False))
+    oa = torch.optim.Adam(a.parameters(), lr=1e-3)
+    ob = torch.optim.Adam(b.parameters(), lr=1e-3)
+    st = T.train_one_epoch(a, data, oa, T.make_scaler("cpu"), accumulate_steps=accum, entropy_coef=0.01)
+    _ref_epoch(b, data, ob, accum, 0.01)
+    assert st["batches"] == 5 and st["optimizer_steps"] == -(-5 // accum)
+    for (k, x), y in zip(a.state_dict().items(), b.state_dict().values()):
+        assert torch.equal(x, y), k
+
+
+def test_chessnet_train_forward_matches_functional_restatement():
+    from knightvision_amd.model import ChessNet
+    torch.manual_seed(3)
+    m = ChessNet().train()
+    codes, _, _ = _data(6, 4)
+    x = T.codes_to_planes_t(codes)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    pol, val = m(x)
+
+    def cbr(h, c, bn, relu=True):  # conv + batch-statistics BN (+ ReLU), ai/model.py:58-73
+        h = F.conv2d(h, sd[c + ".weight"], sd[c + ".bias"], padding=sd[c + ".weight"].shape[-1] // 2)
+        h = F.batch_norm(h, sd[bn + ".running_mean"].clone(), sd[bn + ".running_var"].clone(),
+                         sd[bn + ".weight"], sd[bn + ".bias"], training=True, momentum=0.1, eps=1e-5)
+        return F.relu(h) if relu else h
+    h = cbr(cbr(x, "conv1", "bn1"), "conv2", "bn2")
+    for i in range(5):
+        p = f"res_blocks.{i}"
+        h = F.relu(cbr(cbr(h, p + ".conv1", p + ".bn1"), p + ".conv2", p + ".bn2", relu=False) + h)
+    rp = F.linear(torch.flatten(cbr(h, "policy_conv", "policy_bn"), 1), sd["policy_fc.weight"], sd["policy_fc.bias"])
+    v = torch.flatten(cbr(h, "value_conv", "value_bn"), 1)
+    rv = torch.tanh(F.linear(F.relu(F.linear(v, sd["value_fc1.weight"], sd["value_fc1.bias"])),
+                             sd["value_fc2.weight"], sd["value_fc2.bias"]))
+    assert torch.allclose(pol, rp, atol=1e-5) and torch.allclose(val, rv, atol=1e-6)
+    # the running statistics moved (training mode), so the eval-mode pack must be rebuilt
+    assert not torch.equal(m.state_dict()["bn1.running_mean"], sd["bn1.running_mean"])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ddp_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from knightvision_amd import learn as L
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(5)
+    m = TinyNet()
+    ddp = T.wrap_ddp(m, "cpu")
+    codes, moves, rew = _data(64, 6)
+    mine = [T.Batch(T.codes_to_planes_t(codes[i:i + 8][rank::2]), moves[i:i + 8][rank::2],
+                    rew[i:i + 8][rank::2]) for i in range(0, 64, 8)]
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)  # SGD: Adam would amplify the pure-noise conv-bias gradient
+    T.train_one_epoch(ddp, mine, opt, T.make_scaler("cpu"), accumulate_steps=2, entropy_coef=0.01)
+    # end-of-iteration exchange: all-gather + global decisive filter + round-robin re-shard
+    c2, m2, r2 = _data(5 + 3 * rank, 10 + rank)
+    union = [L._all_gather_rows(x) for x in (c2, m2, r2)]
+    q.put((rank, {k: v.numpy().copy() for k, v in m.state_dict().items()}, [u.numpy().copy() for u in union]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_world2_matches_gradient_average():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single process: each global batch of 8 split into the two ranks' halves; DDP averages the
+    # two halves' gradients (BatchNorm statistics stay per half, as in each DDP replica)
+    torch.manual_seed(5)
+    m = TinyNet()
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+    codes, moves, rew = _data(64, 6)
+    opt.zero_grad()
+    for j, i in enumerate(range(0, 64, 8)):
+        for r in range(2):
+            b = T.Batch(T.codes_to_planes_t(codes[i:i + 8][r::2]), moves[i:i + 8][r::2], rew[i:i + 8][r::2])
+            (T.batch_loss(m, b, 0.01)[0] / 2 / 2).backward()
+        if (j + 1) % 2 == 0 or j == 7:
+            torch.nn.utils.clip_grad_norm_(m.parameters(), max_norm=1.0)
+            opt.step()
+            opt.zero_grad()
+    for rank, sd, _ in res:
+        for k, v in m.state_dict().items():
+            if "running" in k or "num_batches" in k:
+                continue  # buffers follow rank 0's replica (DDP broadcast_buffers)
+            assert torch.allclose(torch.from_numpy(sd[k]), v, atol=2e-6), (rank, k)
+    # the gathered union is the same on both ranks, in rank order
+    want = [torch.cat([_data(5, 10)[t], _data(8, 11)[t]]) for t in range(3)]
+    for _, _, union in res:
+        for u, w in zip(union, want):
+            assert torch.equal(torch.from_numpy(u), w)

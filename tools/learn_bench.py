@@ -1,0 +1,66 @@
+"""Learn-loop throughput (BASELINE configs[4]): self-play
+on the HIP engine, then the update step with DDP over RCCL, per iteration.
+
+    python tools/learn_bench.py [--iterations 3] [--games 256] [--max-moves 80] [--sims 0]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/learn_bench.py ...
+
+Prints one JSON line from rank 0: self-play plies/s and training samples/s over
+all ranks for the last iteration, with the per-phase times (max over ranks).
+Synthetic random-init weights (seed 42), per-game seeds 42 + global id.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iterations", type=int, default=3)
+    ap.add_argument("--games", type=int, default=256, help="games per iteration over all ranks")
+    ap.add_argument("--max-moves", type=int, default=80)
+    ap.add_argument("--sims", type=int, default=0)
+    ap.add_argument("--batch-size", type=int, default=4096)
+    ap.add_argument("--epochs", type=int, default=1)
+    a = ap.parse_args()
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from knightvision_amd.learn import reinforcement_loop
+    from knightvision_amd.model import ChessNet
+    from knightvision_amd.weights import synthetic_state_dict
+    m = ChessNet()
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(42, "init").items()})
+    t0 = time.perf_counter()
+    stats = reinforcement_loop(m, a.iterations, a.games, f"cuda:{local}", epochs=a.epochs, batch_size=a.batch_size,
+                               max_moves=a.max_moves, sims=a.sims, log=None)
+    wall = time.perf_counter() - t0
+    last = stats[-1]
+    vals = torch.tensor([last.get("selfplay_s", 0.0), last.get("train_s", 0.0)], dtype=torch.float64, device="cuda")
+    cnt = torch.tensor([float(last.get("train_samples", 0))], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+        dist.all_reduce(cnt)
+    sp_s, tr_s = vals.tolist()
+    if rank == 0:
+        print(json.dumps({"metric": "learn loop: self-play + DDP update per iteration", "n_gpus": world,
+                          "iterations": a.iterations, "games_per_iteration": a.games, "max_moves": a.max_moves,
+                          "sims": a.sims, "selfplay_s": sp_s, "train_s": tr_s,
+                          "train_samples_per_s": cnt.item() / tr_s if tr_s else None,
+                          "records_per_rank": last["records"], "wall_s": wall, "data": "synthetic"}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
