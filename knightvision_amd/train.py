@@ -27,6 +27,12 @@ import math
 import os
 from dataclasses import dataclass
 
+# MIOpen's default find mode benchmarks every new convolution shape for tens of
+# seconds (measured 15-47 s per shape on MI355X); the update step sees a new
+# last-batch shape every iteration, so use the fast heuristic selection unless
+# the caller chose otherwise. Must be set before the first convolution runs.
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+
 import numpy as np
 import torch
 import torch.nn.functional as F
