@@ -177,6 +177,10 @@ void kv_destroy(kv_engine* e);
  * [n][80] (the reference may mutate the board); in_check [n]. */
 int kv_dev_valid_moves(int device, const int8_t* states, int n, uint16_t* moves_out, int cap, int* n_moves,
                        int8_t* states_after, uint8_t* in_check);
+/* squareUnderAttack (chessEngine.py:400-415) for all 64 squares: bit r*8+c of
+ * attacked[i] is set when an opponent pseudo-move of state i ends on (r, c);
+ * inCheck (:388-394) is the bit of the mover's stored king location. */
+int kv_dev_attacks(int device, const int8_t* states, int n, uint64_t* attacked);
 /* makeMove (chessEngine.py:127-197) of move index[i] of each state's list. */
 int kv_dev_make_move(int device, int8_t* states, const int* index, int n);
 /* numpy RandomState(seed[i]).dirichlet([alpha]*k) `draws` times per stream:

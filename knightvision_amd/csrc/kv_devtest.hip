@@ -72,6 +72,20 @@ __global__ __launch_bounds__(64) void k_dev_make(int8_t* states, const int* inde
     status[i] = 0;
 }
 
+// squareUnderAttack's set for the side to move (chessEngine.py:400-415): end
+// squares of every opponent pseudo-move, one bit per square
+__global__ void k_dev_attacks(const int8_t* states, int n, unsigned long long* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int8_t* v = states + (size_t)i * 80;
+    Pos p;
+    pos_from_board(p, v, v[64], v[65], v[66], v[67], v[68],
+                   (v[69] ? F_WKM : 0) | (v[70] ? F_BKM : 0) | (v[71] ? F_WRK : 0) | (v[72] ? F_WRQ : 0) |
+                       (v[73] ? F_BRK : 0) | (v[74] ? F_BRQ : 0),
+                   v[75] < 0 ? -1 : v[75] * 8 + v[76]);
+    out[i] = targets(p, p.wtm ? 1 : 0);
+}
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_dev_dirichlet(const unsigned long long* seeds, double alpha, int k,
                                                        int draws, double* out, long long* attempts, double* tail,
                                                        uint32_t* state) {
@@ -139,6 +153,21 @@ int kv_dev_valid_moves(int device, const int8_t* states, int n, uint16_t* moves_
     KV_HIP(hipMemcpy(n_moves, nm.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
     KV_HIP(hipMemcpy(states_after, a.p, (size_t)n * 80, hipMemcpyDeviceToHost));
     KV_HIP(hipMemcpy(in_check, c.p, (size_t)n, hipMemcpyDeviceToHost));
+    return KV_OK;
+}
+
+int kv_dev_attacks(int device, const int8_t* states, int n, uint64_t* attacked) {
+    KV_REQUIRE(n > 0 && states && attacked, KV_EINVAL, "kv_dev_attacks: bad arguments");
+    KV_HIP(hipSetDevice(device));
+    kv::DevBuf<int8_t> s;
+    kv::DevBuf<unsigned long long> o;
+    KV_HIP(s.alloc((size_t)n * 80));
+    KV_HIP(o.alloc(n));
+    KV_HIP(hipMemcpy(s.p, states, (size_t)n * 80, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(kv::k_dev_attacks, dim3((n + 63) / 64), dim3(64), 0, 0, s.p, n, o.p);
+    KV_HIP(hipGetLastError());
+    KV_HIP(hipDeviceSynchronize());
+    KV_HIP(hipMemcpy(attacked, o.p, (size_t)n * 8, hipMemcpyDeviceToHost));
     return KV_OK;
 }
 
