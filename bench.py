@@ -174,7 +174,9 @@ def main():
     bpl = min(G, int(round(m["dom_flop"] / per_board))) if m["dom_flop"] else G
     flop_alg = per_board * bpl
     achieved = flop_alg / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
-    kname = "wino_gemm_kernel<512,4,1,2>" if wino else "conv3x3_kernel<512,32>"
+    # the library picks the GEMM tile by batch (knightvision_amd/csrc/kv_nn.hip launch_wino_gemm)
+    kname = (("wino_gemm_kernel<512,2,2,1,2,16>" if bpl * 4 <= 1024 else "wino_gemm_kernel<512,4,2,1,2,32>")
+             if wino else "conv3x3_kernel<512,32>")
     traffic = None
     pmc = os.path.join(HERE, "profiles", "r01_pmc_wino_gemm.json" if wino else "r01_pmc_resconv.json")
     if os.path.exists(pmc):

@@ -723,30 +723,37 @@ static int net_reserve(kv_net* net, int nb_pad) {
 static int net_heads(kv_net* net, int nb, float* policy, float* value, hipStream_t st);
 
 // LDS_PAD: dynamic LDS requested beyond the tiles' need, to cap workgroups per CU
-template <int K, int WR, int WC, int MT, int NT, int LDS_PAD = 0>
+template <int K, int WR, int WC, int MT, int NT, int CK = 32, int LDS_PAD = 0>
 static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
-    using T = kv::WinoTile<WR, WC, MT, NT>;
+    using T = kv::WinoTile<WR, WC, MT, NT, CK>;
     constexpr size_t bytes = T::BYTES + LDS_PAD;
     static bool attr_set = false;
     if (!attr_set) {
-        KV_HIP(hipFuncSetAttribute((const void*)kv::wino_gemm_kernel<K, WR, WC, MT, NT>,
+        KV_HIP(hipFuncSetAttribute((const void*)kv::wino_gemm_kernel<K, WR, WC, MT, NT, CK>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
         attr_set = true;
     }
     const int nwg = kv::WN_XI * (rows / T::WM) * (512 / T::WN);
     KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0, KV_EINVAL, "wino gemm: rows %d vs tile %d", rows, T::WM);
-    hipLaunchKernelGGL((kv::wino_gemm_kernel<K, WR, WC, MT, NT>), dim3(nwg), dim3(T::THREADS), bytes, st, V, U, M,
-                       rows, 512, stride);
+    hipLaunchKernelGGL((kv::wino_gemm_kernel<K, WR, WC, MT, NT, CK>), dim3(nwg), dim3(T::THREADS), bytes, st, V, U,
+                       M, rows, 512, stride);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
 
-// 128 tiles x 128 channels per workgroup, 8 waves of 32x64, 74 KB LDS -> 2
-// workgroups per CU. Measured against 64x64, 64x128, 128x64 (1 or 2 per CU)
-// and 128x256 tiles at 256 and 2048 boards: fastest or within noise at both.
+// Tile per batch size. 36 GEMMs x (rows/WM) x (512/WN) tiles over the CUs'
+// resident slots: at 1,024 rows (256 boards) 128x128 tiles give 1,152 tiles
+// for 512 slots (2 per CU: 2.25 rounds), 64x128 tiles with 3 workgroups per CU
+// give 2,304 for 768 slots -- exactly 3 rounds -- and run 3 % faster; above
+// that the 128x128 tile's operand reuse wins (measured: forward 2.10 vs 2.17
+// ms at 256 boards, 15.7 vs 15.1 ms at 2048). Both tiles accumulate each
+// output over k in the same MFMA order, so the choice does not change a bit
+// of the result (batch invariance holds across it).
 template <int K>
 static int launch_wino_gemm(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
-    return launch_wino_gemm_t<K, 4, 2, 1, 2>(V, U, M, rows, stride, st);
+    if (rows <= 1024)  // 64 x 128, 4 waves of 32x64, k-tiles of 16, LDS padded to 48 KB -> 3 per CU
+        return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720>(V, U, M, rows, stride, st);
+    return launch_wino_gemm_t<K, 4, 2, 1, 2>(V, U, M, rows, stride, st);  // 128 x 128, 8 waves, 2 per CU
 }
 
 template <int K>

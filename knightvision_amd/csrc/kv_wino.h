@@ -173,21 +173,22 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
 // (double-buffered A [WM][32] and B [WN][32], row stride 36 floats:
 // conflict-free ds_read_b128), one barrier per k-tile, the next k-tile's
 // global loads issued before the current tile's MFMAs.
-template <int WR, int WC, int MT, int NT>
+template <int WR, int WC, int MT, int NT, int CK = 32>
 struct WinoTile {
     static constexpr int THREADS = WR * WC * 64;
     static constexpr int WM = WR * MT * 32, WN = WC * NT * 32;
-    static constexpr size_t BYTES = (size_t)(2 * WM * 36 + 2 * WN * 36) * 4;
+    static constexpr int PS = CK + 4;  // LDS row stride (floats): 36 / 20, conflict-free ds_read_b128
+    static constexpr size_t BYTES = (size_t)(2 * WM * PS + 2 * WN * PS) * 4;
 };
 
-template <int K, int WR, int WC, int MT, int NT>
+template <int K, int WR, int WC, int MT, int NT, int CK = 32>
 __global__ __launch_bounds__(WR * WC * 64) void wino_gemm_kernel(const float* __restrict__ V,
                                                                    const float* __restrict__ U,
                                                                    float* __restrict__ M, int rows, int cout,
                                                                    int stride) {
-    using T = WinoTile<WR, WC, MT, NT>;
+    using T = WinoTile<WR, WC, MT, NT, CK>;
     constexpr int WM = T::WM, WN = T::WN, TH = T::THREADS;
-    constexpr int CK = 32, PS = 36;
+    constexpr int PS = T::PS;
     constexpr int NK = K / CK;
     constexpr int KQ = CK / 4;
     constexpr int A_F4 = (WM * KQ) / TH;

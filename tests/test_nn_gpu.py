@@ -73,6 +73,11 @@ def test_batch_invariance(precision):
     p_all, v_all = m(planes)  # 40 boards: whole-K class
     p_20, v_20 = m(planes[20:])
     assert torch.equal(p_20, p_all[20:]) and torch.equal(v_20, v_all[20:])
+    if precision == "fp32":  # 300 boards run the 128x128 GEMM tile, 40 the 64x128 tile: same bits
+        codes_l = rng.integers(0, 13, size=(300, 64)) * (rng.random((300, 64)) < 0.4)
+        codes_l[:40] = codes
+        p_l, v_l = m(torch.from_numpy(codes_to_planes(codes_l)).cuda())
+        assert torch.equal(p_l[:40], p_all) and torch.equal(v_l[:40], v_all)
     p_16, v_16 = m(planes[:16])  # split-K class
     for i in (0, 5, 15):
         p1, v1 = m(planes[i:i + 1])

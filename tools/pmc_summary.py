@@ -11,7 +11,7 @@ import sys
 
 KERNELS = {
     "resconv": ("conv3x3_kernel<512,32", "conv3x3_kernel<512,32,*>"),
-    "wino_gemm": ("wino_gemm_kernel<512,", "wino_gemm_kernel<512,4,1,2>"),
+    "wino_gemm": ("wino_gemm_kernel<512,", "wino_gemm_kernel<512,2,2,1,2,16>"),
 }
 
 
