@@ -267,10 +267,11 @@ __device__ inline void commit_move(const DevCfg& cfg, Slot& s, int i, int mv, in
 // MCTS launches (kv_mcts.hip), all on `st`
 int mcts_root(const DevCfg& cfg, const Tree& t, Slot* slots, const uint16_t* moves, const float* logits,
               const float* values, float* probs_scratch, uint32_t* np_mt, hipStream_t st);
+// select / backup for slots [slot0, slot0 + count)
 int mcts_select(const DevCfg& cfg, const Tree& t, const Slot* slots, const int8_t* boards, int8_t* nn_boards,
-                Ctr* ctr, hipStream_t st);
+                Ctr* ctr, hipStream_t st, int slot0, int count);
 int mcts_backup(const DevCfg& cfg, const Tree& t, const Slot* slots, const float* logits, const float* values,
-                float* probs, Ctr* ctr, hipStream_t st);
+                float* probs, Ctr* ctr, hipStream_t st, int slot0, int count);
 int mcts_choose(const DevCfg& cfg, const Tree& t, Slot* slots, int8_t* boards, uint32_t* py_mt, kv_record* rec,
                 int8_t* last_board, Ctr* ctr, hipStream_t st);
 int hash_eval(const int8_t* boards, int rows, float* logits, float* values, hipStream_t st);

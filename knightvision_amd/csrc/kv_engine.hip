@@ -428,7 +428,11 @@ int kv_set_max_moves(kv_engine* e, int max_moves) {
 // one network pass over `rows` boards (or the hash test evaluator), with the
 // residual-tower section bracketed by HIP events for the roofline
 static int eng_eval(kv_engine* e, const int8_t* boards, int rows) {
-    if (e->dc.eval_mode == KV_EVAL_HASH) return kv::hash_eval(boards, rows, e->logits, e->values, e->st);
+    kv_net* net = e->net;
+    hipStream_t st = e->st;
+    float* logits = e->logits;
+    float* values = e->values;
+    if (e->dc.eval_mode == KV_EVAL_HASH) return kv::hash_eval(boards, rows, logits, values, st);
     if ((size_t)e->n_ev_used + 2 > e->ev.size()) {
         for (int k = 0; k < 2; ++k) {
             hipEvent_t x;
@@ -436,11 +440,11 @@ static int eng_eval(kv_engine* e, const int8_t* boards, int rows) {
             e->ev.push_back(x);
         }
     }
-    kv::net_set_res_events(e->net, e->ev[e->n_ev_used], e->ev[e->n_ev_used + 1]);
+    kv::net_set_res_events(net, e->ev[e->n_ev_used], e->ev[e->n_ev_used + 1]);
     e->n_ev_used += 2;
-    const int rc = kv::net_forward_boards_internal(e->net, boards, rows, e->logits, e->values, e->st);
-    kv::net_set_res_events(e->net, nullptr, nullptr);
-    kv::net_dom_info(e->net, &e->dom_algo, &e->dom_launches, &e->dom_flop);
+    const int rc = kv::net_forward_boards_internal(net, boards, rows, logits, values, st);
+    kv::net_set_res_events(net, nullptr, nullptr);
+    kv::net_dom_info(net, &e->dom_algo, &e->dom_launches, &e->dom_flop);
     return rc;
 }
 
@@ -473,9 +477,10 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
             if ((rc = kv::mcts_root(e->dc, t, e->slots, e->moves, e->logits, e->values, e->probs, e->np_mt, e->st)))
                 return rc;
             for (int k = 0; k < e->dc.sims; ++k) {
-                if ((rc = kv::mcts_select(e->dc, t, e->slots, e->boards, e->nn_boards, e->ctr, e->st))) return rc;
+                if ((rc = kv::mcts_select(e->dc, t, e->slots, e->boards, e->nn_boards, e->ctr, e->st, 0, S)))
+                    return rc;
                 if ((rc = eng_eval(e, e->nn_boards, S))) return rc;
-                if ((rc = kv::mcts_backup(e->dc, t, e->slots, e->logits, e->values, e->probs, e->ctr, e->st)))
+                if ((rc = kv::mcts_backup(e->dc, t, e->slots, e->logits, e->values, e->probs, e->ctr, e->st, 0, S)))
                     return rc;
             }
             if ((rc = kv::mcts_choose(e->dc, t, e->slots, e->boards, e->py_mt, e->rec, e->last_board, e->ctr,

@@ -99,10 +99,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 }
 
 __global__ __launch_bounds__(64) void k_mcts_select(DevCfg cfg, Tree t, const Slot* slots, const int8_t* boards,
-                                                    int8_t* nn_boards, Ctr* ctr) {
+                                                    int8_t* nn_boards, Ctr* ctr, int slot0) {
     __shared__ int8_t bd[64];
     __shared__ int s_meta[8];  // wtm wkr wkc bkr bkc flags ep
-    const int i = blockIdx.x, lane = threadIdx.x;
+    const int i = slot0 + blockIdx.x, lane = threadIdx.x;
     const Slot s = slots[i];
     if (s.status != ST_ACTIVE) return;
     bd[lane] = boards[(size_t)i * 64 + lane];
@@ -173,9 +173,9 @@ __global__ __launch_bounds__(64) void k_mcts_select(DevCfg cfg, Tree t, const Sl
 }
 
 __global__ __launch_bounds__(64) void k_mcts_backup(DevCfg cfg, Tree t, const Slot* slots, const float* logits,
-                                                    const float* values, float* probs, Ctr* ctr) {
+                                                    const float* values, float* probs, Ctr* ctr, int slot0) {
     __shared__ float pri[MAXM];
-    const int i = blockIdx.x, lane = threadIdx.x;
+    const int i = slot0 + blockIdx.x, lane = threadIdx.x;
     const Slot s = slots[i];
     if (s.status != ST_ACTIVE) return;
     MctsSlot m = t.ms[i];
@@ -293,15 +293,16 @@ int mcts_root(const DevCfg& cfg, const Tree& t, Slot* slots, const uint16_t* mov
 }
 
 int mcts_select(const DevCfg& cfg, const Tree& t, const Slot* slots, const int8_t* boards, int8_t* nn_boards,
-                Ctr* ctr, hipStream_t st) {
-    hipLaunchKernelGGL(k_mcts_select, dim3(cfg.slots), dim3(64), 0, st, cfg, t, slots, boards, nn_boards, ctr);
+                Ctr* ctr, hipStream_t st, int slot0, int count) {
+    hipLaunchKernelGGL(k_mcts_select, dim3(count), dim3(64), 0, st, cfg, t, slots, boards, nn_boards, ctr, slot0);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
 
 int mcts_backup(const DevCfg& cfg, const Tree& t, const Slot* slots, const float* logits, const float* values,
-                float* probs, Ctr* ctr, hipStream_t st) {
-    hipLaunchKernelGGL(k_mcts_backup, dim3(cfg.slots), dim3(64), 0, st, cfg, t, slots, logits, values, probs, ctr);
+                float* probs, Ctr* ctr, hipStream_t st, int slot0, int count) {
+    hipLaunchKernelGGL(k_mcts_backup, dim3(count), dim3(64), 0, st, cfg, t, slots, logits, values, probs, ctr,
+                       slot0);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
