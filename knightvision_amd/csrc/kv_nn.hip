@@ -609,8 +609,6 @@ struct kv_net {
     float* V256 = nullptr;  // conv2's input transform [36][cap*4][256]
     float* Mw = nullptr;
     // the dominant kernel bracketed by res_a/res_b in the last forward
-    hipStream_t s2 = nullptr;  // second stream of the split Winograd tower
-    hipEvent_t sev[3] = {};
     int dom_algo = KV_ALGO_DIRECT;
     int dom_launches = 10;
     double dom_flop = 0;
@@ -794,17 +792,8 @@ static int launch_wino_out(const float* M, int b0, int nb, int stride, const flo
     return KV_OK;
 }
 
-static int wino_streams() {
-    static int c = -1;
-    if (c < 0) {
-        const char* e = getenv("KV_WINO_STREAMS");
-        c = e ? atoi(e) : 1;
-    }
-    return c;
-}
-
 // conv2 + the 5 residual blocks for boards [b0, b0 + nb) on stream st
-static int wino_blocks(kv_net* net, int b0, int nb, int stride, bool mark, hipStream_t st, hipEvent_t after_first) {
+static int wino_blocks(kv_net* net, int b0, int nb, int stride, bool mark, hipStream_t st) {
     const float* W = net->w;
     const kv::PackOffsets& o = net->off;
     const size_t ro = (size_t)b0 * 4 * 512, ro256 = (size_t)b0 * 4 * 256;
@@ -813,7 +802,6 @@ static int wino_blocks(kv_net* net, int b0, int nb, int stride, bool mark, hipSt
     float* M = net->Mw;
     int rc;
     if ((rc = wino_gemm_layer<256>(net, 1, net->V256 + ro256, M + ro, rows, stride, st))) return rc;
-    if (after_first) KV_HIP(hipEventRecord(after_first, st));
     if ((rc = launch_wino_out<false, true, true>(M, b0, nb, stride, W + o.scale[1], W + o.shift[1], nullptr, net->X,
                                                  V, st)))
         return rc;
@@ -838,33 +826,14 @@ static int wino_blocks(kv_net* net, int b0, int nb, int stride, bool mark, hipSt
     return KV_OK;
 }
 
-// Winograd tower: conv2 and the 5 residual blocks (conv1 output in net->T).
-// With KV_WINO_STREAMS=2/3 and >= 64 boards the batch is split in two halves
-// that run on two streams (3: the second half starts one GEMM later), so one
-// half's memory-bound transforms overlap the other half's GEMMs.
+// Winograd tower: conv2 and the 5 residual blocks (conv1 output in net->T)
 static int net_tower_wino(kv_net* net, int nb_pad, hipStream_t st) {
     const int rows = nb_pad * 4;
     int rc;
     hipLaunchKernelGGL(kv::wino_in_kernel<256>, dim3(256 / 64, nb_pad), dim3(256), 0, st, net->T, rows, net->V256);
     KV_HIP(hipGetLastError());
-    const int ns = wino_streams();
-    if (ns >= 2 && nb_pad % 64 == 0) {
-        if (!net->s2) {
-            KV_HIP(hipStreamCreateWithFlags(&net->s2, hipStreamNonBlocking));
-            for (int i = 0; i < 3; ++i) KV_HIP(hipEventCreateWithFlags(&net->sev[i], hipEventDisableTiming));
-        }
-        const int half = nb_pad / 2;
-        KV_HIP(hipEventRecord(net->sev[0], st));
-        if ((rc = wino_blocks(net, 0, half, rows, true, st, ns >= 3 ? net->sev[1] : nullptr))) return rc;
-        KV_HIP(hipStreamWaitEvent(net->s2, ns >= 3 ? net->sev[1] : net->sev[0], 0));
-        if ((rc = wino_blocks(net, half, half, rows, false, net->s2, nullptr))) return rc;
-        KV_HIP(hipEventRecord(net->sev[2], net->s2));
-        KV_HIP(hipStreamWaitEvent(st, net->sev[2], 0));
-        net->dom_flop = 2.0 * kv::WN_XI * (half * 4) * 512.0 * 512.0;
-    } else {
-        if ((rc = wino_blocks(net, 0, nb_pad, rows, true, st, nullptr))) return rc;
-        net->dom_flop = 2.0 * kv::WN_XI * rows * 512.0 * 512.0;
-    }
+    if ((rc = wino_blocks(net, 0, nb_pad, rows, true, st))) return rc;
+    net->dom_flop = 2.0 * kv::WN_XI * rows * 512.0 * 512.0;
     net->dom_algo = KV_ALGO_WINOGRAD;
     net->dom_launches = 1;
     return KV_OK;
@@ -1077,10 +1046,6 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->Mw);
     (void)hipFree(net->V256);
     for (int i = 0; i < 3; ++i) (void)hipEventDestroy(net->ev[i]);
-    if (net->s2) {
-        for (int i = 0; i < 3; ++i) (void)hipEventDestroy(net->sev[i]);
-        (void)hipStreamDestroy(net->s2);
-    }
     delete net;
 }
 
