@@ -91,7 +91,9 @@ void kv_net_destroy(kv_net* net);
 #define KV_SEED_SEQUENTIAL 1 /* one numpy + one CPython stream seeded SEED, games in order */
 
 #define KV_EVAL_FAITHFUL 0 /* every board evaluated once, as the reference does */
-#define KV_EVAL_LAZY 1     /* only the rows the schedule consumes are evaluated */
+#define KV_EVAL_LAZY 1     /* the network runs only on the steps whose row the schedule consumes
+                              (reference move selection, <= 16 slots: the sequential drop-in path);
+                              identical outputs, 1/SELFPLAY_BATCH_SIZE of the network work */
 #define KV_EVAL_HASH 2     /* TEST ONLY: uniform logits + hash value instead of the network */
 
 typedef struct {

@@ -49,6 +49,8 @@ struct Ctr {
     unsigned long long sims;
     int active;
     int error;
+    int need_eval;  // KV_EVAL_LAZY: some slot consumes a network row this step
+    int pad;
 };
 
 struct DevCfg {

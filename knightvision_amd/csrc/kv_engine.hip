@@ -110,6 +110,7 @@ __global__ __launch_bounds__(64) void k_movegen(DevCfg cfg, Slot* slots, int8_t*
         s.consumed = (s.buf >= cfg.batch) || !has;
         atomicAdd(&ctr->nn_rows, 1ull);
     }
+    if (s.consumed || s.need_flush) ctr->need_eval = 1;  // read by the host in KV_EVAL_LAZY
     slots[i] = s;
 }
 
@@ -301,8 +302,10 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
     KV_REQUIRE(cfg->sims >= 0 && cfg->sims <= 100000, KV_EINVAL, "kv_create: sims out of range");
     KV_REQUIRE(cfg->sims == 0 || cfg->seed_mode == KV_SEED_PER_GAME, KV_EINVAL,
                "kv_create: MCTS mode uses per-game seeding");
-    KV_REQUIRE(cfg->eval_mode == KV_EVAL_FAITHFUL || cfg->eval_mode == KV_EVAL_HASH, KV_EINVAL,
-               "kv_create: eval_mode %d not available", cfg->eval_mode);
+    KV_REQUIRE(cfg->eval_mode == KV_EVAL_FAITHFUL || cfg->eval_mode == KV_EVAL_HASH ||
+                   (cfg->eval_mode == KV_EVAL_LAZY && cfg->sims == 0 && cfg->slots <= 16),
+               KV_EINVAL, "kv_create: eval_mode %d not available (lazy: reference move selection, <= 16 slots)",
+               cfg->eval_mode);
     KV_HIP(hipSetDevice(cfg->device));
     kv_engine* e = new kv_engine();
     e->cfg = *cfg;
@@ -460,13 +463,22 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
     long long done = 0;
     while ((max_steps < 0 || done < max_steps) && e->ctr_host->active > 0 &&
            (stop_after_games < 0 || (int64_t)e->ctr_host->games_count < stop_after_games)) {
+        const bool lazy = e->dc.eval_mode == KV_EVAL_LAZY;
+        if (lazy) KV_HIP(hipMemsetAsync(&e->ctr->need_eval, 0, sizeof(int), e->st));
         hipLaunchKernelGGL(kv::k_movegen, dim3(S), dim3(64), 0, e->st, e->dc, e->slots, e->boards,
                            e->moves, e->ctr);
         KV_HIP(hipGetLastError());
         if (e->dc.rows > S)
             hipLaunchKernelGGL(kv::k_flush_rows, dim3(S), dim3(64), 0, e->st, e->dc, e->slots, e->last_board,
                                e->boards);
-        if ((rc = eng_eval(e, e->boards, e->dc.rows))) return rc;
+        bool eval_now = true;
+        if (lazy) {  // evaluate only on the steps whose row the schedule consumes (identical outputs)
+            KV_HIP(hipMemcpyAsync(&e->ctr_host->need_eval, &e->ctr->need_eval, sizeof(int), hipMemcpyDeviceToHost,
+                                  e->st));
+            KV_HIP(hipStreamSynchronize(e->st));
+            eval_now = e->ctr_host->need_eval != 0;
+        }
+        if (eval_now && (rc = eng_eval(e, e->boards, e->dc.rows))) return rc;
         if (!mcts) {
             hipLaunchKernelGGL(kv::k_sample, dim3(S), dim3(256), 0, e->st, e->dc, e->slots, e->boards, e->moves,
                                e->logits, e->values, e->last_probs, e->np_mt, e->py_mt, e->rec, e->last_board,

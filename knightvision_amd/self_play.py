@@ -27,7 +27,7 @@ import numpy as np
 import torch
 
 from .ai import codes_to_planes
-from .engine import SEED_PER_GAME, SEED_SEQUENTIAL, REASONS, SelfPlayEngine, packed_from, records_by_game
+from .engine import EVAL_LAZY, SEED_PER_GAME, SEED_SEQUENTIAL, REASONS, SelfPlayEngine, packed_from, records_by_game
 
 EPSILON = float(os.getenv("DIR_NOISE_EPS", "0.25"))
 ALPHA = float(os.getenv("DIR_NOISE_ALPHA", "0.3"))
@@ -67,7 +67,7 @@ class _Stream:
         if self.engine is None:
             self.engine = SelfPlayEngine(packed_from(model), slots=1, n_games=1 << 40, seed=self.seed,
                                          seed_mode=SEED_SEQUENTIAL, batch=BATCH_SIZE, eps=EPSILON, alpha=ALPHA,
-                                         record_cap=1 << 20, recycle=True, device=dev_index)
+                                         eval_mode=EVAL_LAZY, record_cap=1 << 20, recycle=True, device=dev_index)
         elif key != self.weights_key:
             # new weights, same streams (the reference keeps its RNG state too)
             from . import _lib

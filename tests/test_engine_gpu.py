@@ -175,3 +175,19 @@ def test_sequential_self_play_api_matches_reference(golden_dir):
             break  # streams desynchronise after a tie; later games cannot be compared
         assert recs[0][2] == pytest.approx(g["reward"])
         assert recs[0][0].shape == (12, 8, 8) and recs[0][0].dtype == np.float32
+
+
+def test_lazy_eval_matches_faithful():
+    """KV_EVAL_LAZY (network only on the steps whose row the schedule consumes)
+    plays the same sequential games, record for record, as the faithful mode."""
+    from knightvision_amd.engine import EVAL_FAITHFUL, EVAL_LAZY, SEED_SEQUENTIAL, SelfPlayEngine
+    out = {}
+    for mode in (EVAL_FAITHFUL, EVAL_LAZY):
+        with SelfPlayEngine(synthetic_state_dict(42, "peaked"), slots=1, n_games=3, seed=42,
+                            seed_mode=SEED_SEQUENTIAL, max_moves=120, batch=16, eval_mode=mode) as eng:
+            eng.run()
+            out[mode] = (eng.records(), eng.games())
+    (ra, ga), (rb, gb) = out[EVAL_FAITHFUL], out[EVAL_LAZY]
+    assert len(ra) == len(rb) > 0 and np.array_equal(ra["move"], rb["move"])
+    assert np.array_equal(ra["board"], rb["board"])
+    assert np.array_equal(ga["reward"], gb["reward"]) and np.array_equal(ga["n_evals"], gb["n_evals"])
