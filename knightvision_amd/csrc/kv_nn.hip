@@ -561,6 +561,73 @@ __global__ void encode_boards_kernel(const int8_t* __restrict__ boards, int nb, 
     }
 }
 
+// Stem (conv1 12->256 + BN + ReLU, ai/model.py:58) straight from the int8
+// board codes: the input is one-hot, so an output is the sum of the weights of
+// the occupied 3x3 neighbours -- added in tap order, which is the order (and
+// rounding) in which conv3x3_kernel<16,16>'s MFMA chain adds them, so the
+// result is bit-identical to the encode + implicit-GEMM path.
+// Block = one board x 64 channels (grid 4 x nb_pad), 256 threads: the 64-channel
+// slice of conv1 ([tap][code][64], 30 KB, a zero row for empty) is staged in
+// LDS; wave w computes pixels 16w..16w+15. WINO: the activated 8x8 plane goes through
+// LDS to the four tile waves, which write conv2's Winograd input transform
+// (V [36][rows][256]); else NHWC T [board][64][256].
+template <bool WINO>
+__global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ boards, int nb,
+                                                   const float* __restrict__ wT, const float* __restrict__ scale,
+                                                   const float* __restrict__ shift, float* __restrict__ out,
+                                                   int rows) {
+    __shared__ float wl[9 * 13][64];  // [tap][code 0..12][channel], code 0 = empty = 0
+    __shared__ float plane[64][64];   // [pixel][channel]
+    __shared__ int codes[100];        // the board with a one-square empty border (10x10)
+    const int cl = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl, b = blockIdx.y;
+    if (threadIdx.x < 100) {
+        const int r = threadIdx.x / 10 - 1, f = threadIdx.x % 10 - 1;
+        codes[threadIdx.x] = (b < nb && r >= 0 && r < 8 && f >= 0 && f < 8) ? boards[(size_t)b * 64 + r * 8 + f] : 0;
+    }
+    for (int i = w; i < 9 * 13; i += 4) {
+        const int t = i / 13, code = i % 13;
+        wl[i][cl] = code ? wT[(size_t)(t * 12 + code - 1) * 256 + c] : 0.f;
+    }
+    __syncthreads();
+    const float sc = scale[c], sh = shift[c];
+    // branch-free: an empty or off-board neighbour adds +0 (exact, acc starts at +0),
+    // so every pixel issues its 9 independent LDS reads back to back
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+        const int p = w * 16 + k, py = p >> 3, px = p & 7;
+        float acc = 0.f;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc += wl[t * 13 + codes[(py + t / 3) * 10 + px + t % 3]][cl];
+        const float v = acc * sc + sh;
+        const float y = v > 0.f ? v : 0.f;
+        if (WINO)
+            plane[p][cl] = y;
+        else
+            out[((size_t)b * 64 + p) * 256 + c] = y;
+    }
+    if (!WINO) return;
+    __syncthreads();
+    const int y0 = (w >> 1) * 4 - 1, x0 = (w & 1) * 4 - 1;
+    float d[36];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const int yy = y0 + i, xx = x0 + j;
+            d[i * 6 + j] = (yy >= 0 && yy < 8 && xx >= 0 && xx < 8) ? plane[yy * 8 + xx][cl] : 0.f;
+        }
+    wino_input_tile(d, out, ((size_t)b * 4 + w) * 256 + c, (size_t)rows * 256);
+}
+
+// conv1 weights [256][9][16] -> [9][12][256] for stem_kernel
+__global__ void stem_weights_kernel(const float* __restrict__ w, float* __restrict__ wT) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (t*12 + ch)*256 + c
+    if (i >= 9 * 12 * 256) return;
+    const int c = i % 256, ch = (i / 256) % 12, t = i / (256 * 12);
+    wT[i] = w[((size_t)c * 9 + t) * 16 + ch];
+}
+
 // [B][12][8][8] NCHW planes -> NHWC16 (any values, not only one-hot)
 __global__ void planes_to_nhwc16_kernel(const float* __restrict__ planes, int nb, int nb_pad,
                                         float* __restrict__ x16) {
@@ -603,6 +670,7 @@ struct kv_net {
     int algo = KV_ALGO_AUTO;
     float* U = nullptr;     // Winograd weights [36][Cout][Cin] of convs 1..11
     uint16_t* Up[3] = {};   // the same split into bf16 h / m / l (KV_PREC_BF16X6)
+    float* stemT = nullptr; // conv1 as [tap][piece][cout] (stem_kernel)
     size_t uoff[12] = {};
     size_t utot = 0;
     float* V = nullptr;     // Winograd workspaces [36][cap*4][512]
@@ -826,12 +894,16 @@ static int wino_blocks(kv_net* net, int b0, int nb, int stride, bool mark, hipSt
     return KV_OK;
 }
 
-// Winograd tower: conv2 and the 5 residual blocks (conv1 output in net->T)
-static int net_tower_wino(kv_net* net, int nb_pad, hipStream_t st) {
+// Winograd tower: conv2 and the 5 residual blocks (conv1 output in net->T,
+// or conv2's input transform already in net->V256 when v256_ready)
+static int net_tower_wino(kv_net* net, int nb_pad, bool v256_ready, hipStream_t st) {
     const int rows = nb_pad * 4;
     int rc;
-    hipLaunchKernelGGL(kv::wino_in_kernel<256>, dim3(256 / 64, nb_pad), dim3(256), 0, st, net->T, rows, net->V256);
-    KV_HIP(hipGetLastError());
+    if (!v256_ready) {
+        hipLaunchKernelGGL(kv::wino_in_kernel<256>, dim3(256 / 64, nb_pad), dim3(256), 0, st, net->T, rows,
+                           net->V256);
+        KV_HIP(hipGetLastError());
+    }
     if ((rc = wino_blocks(net, 0, nb_pad, rows, true, st))) return rc;
     net->dom_flop = 2.0 * kv::WN_XI * rows * 512.0 * 512.0;
     net->dom_algo = KV_ALGO_WINOGRAD;
@@ -839,24 +911,32 @@ static int net_tower_wino(kv_net* net, int nb_pad, hipStream_t st) {
     return KV_OK;
 }
 
-// the tower + heads from net->x16 (already encoded, nb_pad rows)
-static int net_tower(kv_net* net, int nb, int nb_pad, float* policy, float* value, hipStream_t st) {
+// the tower + heads; the stem reads net->x16 (encoded planes) or, when
+// `boards` is given, the int8 board codes directly (stem_kernel)
+static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, float* policy, float* value,
+                     hipStream_t st) {
     const float* W = net->w;
     const kv::PackOffsets& o = net->off;
     int rc;
     const bool tm = net->timing;
-    if (use_wino(net, nb)) {
-        if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
-        if ((rc = launch_conv<16, 16, false>(net->x16, W + o.w[0], W + o.scale[0], W + o.shift[0], nullptr, net->T,
-                                             256, nb_pad, nullptr, st)))
-            return rc;
-        if ((rc = net_tower_wino(net, nb_pad, st))) return rc;
+    const bool wino = use_wino(net, nb);
+    if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
+    if (boards) {
+        if (wino)
+            hipLaunchKernelGGL(kv::stem_kernel<true>, dim3(4, nb_pad), dim3(256), 0, st, boards, nb, net->stemT,
+                               W + o.scale[0], W + o.shift[0], net->V256, nb_pad * 4);
+        else
+            hipLaunchKernelGGL(kv::stem_kernel<false>, dim3(4, nb_pad), dim3(256), 0, st, boards, nb, net->stemT,
+                               W + o.scale[0], W + o.shift[0], net->T, nb_pad * 4);
+        KV_HIP(hipGetLastError());
+    } else if ((rc = launch_conv<16, 16, false>(net->x16, W + o.w[0], W + o.scale[0], W + o.shift[0], nullptr,
+                                                net->T, 256, nb_pad, nullptr, st))) {
+        return rc;
+    }
+    if (wino) {
+        if ((rc = net_tower_wino(net, nb_pad, boards != nullptr, st))) return rc;
         return net_heads(net, nb, policy, value, st);
     }
-    if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
-    if ((rc = launch_conv<16, 16, false>(net->x16, W + o.w[0], W + o.scale[0], W + o.shift[0], nullptr, net->T, 256,
-                                         nb_pad, nullptr, st)))
-        return rc;
     const bool bf3 = net->precision == KV_PREC_BF16X3;
     if (bf3) {
         if ((rc = launch_conv_bf3<256, false>(net->T, net->whi + o.w[1], net->wlo + o.w[1], W + o.scale[1],
@@ -965,6 +1045,9 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
     hipLaunchKernelGGL(kv::split3_kernel, dim3((unsigned)((net->utot + 255) / 256)), dim3(256), 0, 0, net->U,
                        net->utot, net->Up[0], net->Up[1], net->Up[2]);
     KV_HIP(hipGetLastError());
+    if (!net->stemT) KV_HIP(hipMalloc(&net->stemT, 9 * 12 * 256 * sizeof(float)));
+    hipLaunchKernelGGL(kv::stem_weights_kernel, dim3(9 * 12), dim3(256), 0, 0, net->w + net->off.w[0], net->stemT);
+    KV_HIP(hipGetLastError());
     KV_HIP(hipDeviceSynchronize());
     net->loaded = true;
     return KV_OK;
@@ -996,7 +1079,7 @@ int kv_net_forward(kv_net* net, const float* planes_dev, int B, float* policy_de
     hipLaunchKernelGGL(kv::planes_to_nhwc16_kernel, dim3((nb_pad * 64 + 255) / 256), dim3(256), 0, st, planes_dev, B,
                        nb_pad, net->x16);
     KV_HIP(hipGetLastError());
-    return net_tower(net, B, nb_pad, policy_dev, value_dev, st);
+    return net_tower(net, B, nb_pad, nullptr, policy_dev, value_dev, st);
 }
 
 int kv_net_forward_boards(kv_net* net, const int8_t* boards_dev, int B, float* policy_dev, float* value_dev,
@@ -1007,10 +1090,7 @@ int kv_net_forward_boards(kv_net* net, const int8_t* boards_dev, int B, float* p
     const int nb_pad = net_pad(net, B);
     int rc = net_reserve(net, nb_pad);
     if (rc) return rc;
-    hipLaunchKernelGGL(kv::encode_boards_kernel, dim3((nb_pad * 64 + 255) / 256), dim3(256), 0, st, boards_dev, B,
-                       nb_pad, net->x16);
-    KV_HIP(hipGetLastError());
-    return net_tower(net, B, nb_pad, policy_dev, value_dev, st);
+    return net_tower(net, B, nb_pad, boards_dev, policy_dev, value_dev, st);  // stem_kernel encodes on the fly
 }
 
 int kv_net_set_timing(kv_net* net, int enable) {
@@ -1041,6 +1121,7 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->T);
     (void)hipFree(net->pfeat);
     (void)hipFree(net->U);
+    (void)hipFree(net->stemT);
     for (int p = 0; p < 3; ++p) (void)hipFree(net->Up[p]);
     (void)hipFree(net->V);
     (void)hipFree(net->Mw);

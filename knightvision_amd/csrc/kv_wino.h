@@ -25,14 +25,17 @@ namespace kv {
 
 constexpr int WN_XI = 36;
 
-// B^T (6x6) applied to one 6-vector
+// B^T (6x6) applied to one 6-vector. The only inexact product is the -5
+// term: it is an explicit fma so that its rounding does not depend on how the
+// compiler contracts a given call site (stem_kernel's inlined zero padding vs
+// wino_in_kernel's loads) -- every caller gives the same bits.
 __device__ inline void wino_bt(const float* d, float* o) {
-    o[0] = 4.f * d[0] - 5.f * d[2] + d[4];
+    o[0] = __builtin_fmaf(-5.f, d[2], 4.f * d[0]) + d[4];
     o[1] = -4.f * d[1] - 4.f * d[2] + d[3] + d[4];
     o[2] = 4.f * d[1] - 4.f * d[2] - d[3] + d[4];
     o[3] = -2.f * d[1] - d[2] + 2.f * d[3] + d[4];
     o[4] = 2.f * d[1] - d[2] - 2.f * d[3] + d[4];
-    o[5] = 4.f * d[1] - 5.f * d[3] + d[5];
+    o[5] = __builtin_fmaf(-5.f, d[3], 4.f * d[1]) + d[5];
 }
 
 // A^T (4x6) applied to one 6-vector
