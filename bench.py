@@ -44,12 +44,12 @@ def parse():
     ap.add_argument("--mode", choices=["mcts", "ref"], default=os.environ.get("KV_BENCH_MODE", "mcts"))
     ap.add_argument("--slots", type=int, default=256)
     ap.add_argument("--sims", type=int, default=400)
-    ap.add_argument("--precision", choices=["fp32", "bf16x6", "bf16x3"], default="fp32")
+    ap.add_argument("--precision", choices=["fp32", "f16x3", "bf16x6", "bf16x3"], default="fp32")
     ap.add_argument("--algo", choices=["auto", "direct", "winograd"], default="auto",
                     help="conv algorithm of the fp32 tower (auto: Winograd F(4x4,3x3) above 16 boards)")
     ap.add_argument("--compare-direct", type=int, default=1,
                     help="also measure the fp32 direct implicit-GEMM convs (reported under 'fp32_direct')")
-    ap.add_argument("--alt-precision", default="bf16x6",
+    ap.add_argument("--alt-precision", default="f16x3",
                     help="also measure this network precision (reported under 'alt_precision'; '' to skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -244,8 +244,12 @@ def main():
         if alt is not None:
             # dominant launch of the alternate run (Winograd GEMM or direct residual conv), fp32-equivalent FLOPs
             a_ach = (alt["dom_flop"] / (alt["conv_ms"] * 1e-3) / 1e12) if alt["conv_ms"] > 0 else None
-            a_prod = {"bf16x6": 6, "bf16x3": 3}.get(args.alt_precision)
+            a_prod = {"bf16x6": 6, "bf16x3": 3, "f16x3": 3}.get(args.alt_precision)
             notes = {
+                "f16x3": "fp32-accurate split: every fp32 operand scaled by an exact power of two (per layer for "
+                         "the weights, per board for the activations) and split into 2 fp16 pieces (22 significant "
+                         "bits), the 3 piece products of weight >= 2^-22 on f16 MFMA, fp32 accumulation, Winograd "
+                         "tower; batch-invariant; logits within the fp32 tolerance (tests/test_nn_gpu.py)",
                 "bf16x6": "fp32-accurate split: every fp32 operand = 3 exact bf16 pieces, the 6 piece products of "
                           "weight >= 2^-16 on bf16 MFMA, fp32 accumulation, Winograd tower; max |dlogit| 6.0e-6 on the "
                           "peaked weights (fp32 Winograd 7.2e-6, fp32 direct 5.2e-6; tolerance 1e-4)",
@@ -257,7 +261,9 @@ def main():
                 "value": (alt["sims"] if mcts else alt["plies"]) / alt["dt"], "unit": unit,
                 "ms_per_step": alt["dt"] * 1e3 / steps, "plies_per_s": alt["plies"] / alt["dt"],
                 "nn_tflops_fp32_equiv": alt["nn_rows"] * FLOP_PER_EVAL / alt["dt"] / 1e12,
-                "dominant_kernel": "wino_gemm_bf6_kernel<512>" if alt["dom_algo"] == 2 else "conv3x3 (direct)",
+                "dominant_kernel": ({"f16x3": "wino_gemm_h3_kernel<512,2>", "bf16x6": "wino_gemm_bf6_kernel<512>"}
+                                    .get(args.alt_precision, "wino_gemm_kernel<512>") if alt["dom_algo"] == 2
+                                    else "conv3x3 (direct)"),
                 "dominant_avg_launch_ms": alt["conv_ms"], "dominant_tflops_fp32_equiv": a_ach,
                 "dominant_bf16_mfma_frac": (a_ach * a_prod / BF16_MFMA_PEAK_TFLOPS) if (a_ach and a_prod) else None}
         if not args.no_cpu_baseline:

@@ -69,6 +69,13 @@ int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv);
  *                MFMA with fp32 accumulation (Winograd tower above 16 boards;
  *                fp32 direct below). Logit error at fp32's level. */
 #define KV_PREC_BF16X6 2
+/* KV_PREC_F16X3  fp32-accurate: both operands split into two fp16 pieces
+ *                (22 significant bits) after exact power-of-two scaling (per
+ *                layer for the weights, per board for the activations), the
+ *                three products of weight >= 2^-22 on f16 MFMA with fp32
+ *                accumulation (Winograd tower above 16 boards; fp32 direct
+ *                below). Batch-invariant; logit error at fp32's level. */
+#define KV_PREC_F16X3 3
 int kv_net_set_precision(kv_net* net, int precision);
 /* Algorithm of the fp32 3x3 convs with Cin 256/512:
  * KV_ALGO_AUTO      Winograd for batches > 16 boards, direct (split-K) below

@@ -575,8 +575,9 @@ template <bool WINO>
 __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ boards, int nb,
                                                    const float* __restrict__ wT, const float* __restrict__ scale,
                                                    const float* __restrict__ shift, float* __restrict__ out,
-                                                   int rows) {
-    __shared__ float wl[9 * 13][64];  // [tap][code 0..12][channel], code 0 = empty = 0
+                                                   int rows, unsigned* vmax) {
+    __shared__ float wl[9 * 13][64];
+    __shared__ float red[4];  // [tap][code 0..12][channel], code 0 = empty = 0
     __shared__ float plane[64][64];   // [pixel][channel]
     __shared__ int codes[100];        // the board with a one-square empty border (10x10)
     const int cl = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -617,7 +618,8 @@ __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ bo
             const int yy = y0 + i, xx = x0 + j;
             d[i * 6 + j] = (yy >= 0 && yy < 8 && xx >= 0 && xx < 8) ? plane[yy * 8 + xx][cl] : 0.f;
         }
-    wino_input_tile(d, out, ((size_t)b * 4 + w) * 256 + c, (size_t)rows * 256);
+    const float mx = wino_input_tile(d, out, ((size_t)b * 4 + w) * 256 + c, (size_t)rows * 256);
+    if (vmax) block_max_to(mx, vmax + b, red);  // KV_PREC_F16X3 operand scale of conv2
 }
 
 // conv1 weights [256][9][16] -> [9][12][256] for stem_kernel
@@ -670,6 +672,9 @@ struct kv_net {
     int algo = KV_ALGO_AUTO;
     float* U = nullptr;     // Winograd weights [36][Cout][Cin] of convs 1..11
     uint16_t* Up[3] = {};   // the same split into bf16 h / m / l (KV_PREC_BF16X6)
+    uint16_t* Uf[2] = {};   // fp16 pieces of U * 2^ut[l] (KV_PREC_F16X3)
+    int ut[12] = {};
+    unsigned* vmax = nullptr;  // f16x3: per-board max |V| of each conv's input, [12][cap]
     float* stemT = nullptr; // conv1 as [tap][piece][cout] (stem_kernel)
     size_t uoff[12] = {};
     size_t utot = 0;
@@ -770,8 +775,9 @@ static int net_reserve(kv_net* net, int nb_pad) {
     if (nb_pad <= net->cap) return KV_OK;
     int cap = nb_pad < 64 ? 64 : nb_pad;
     (void)hipFree(net->x16); (void)hipFree(net->X); (void)hipFree(net->T); (void)hipFree(net->pfeat);
-    (void)hipFree(net->V); (void)hipFree(net->Mw); (void)hipFree(net->V256);
+    (void)hipFree(net->V); (void)hipFree(net->Mw); (void)hipFree(net->V256); (void)hipFree(net->vmax);
     net->x16 = net->X = net->T = net->pfeat = net->V = net->Mw = net->V256 = nullptr;
+    net->vmax = nullptr;
     net->cap = 0;
     KV_HIP(hipMalloc(&net->x16, (size_t)cap * 64 * 16 * 4));
     KV_HIP(hipMalloc(&net->X, (size_t)cap * 64 * 512 * 4));
@@ -780,6 +786,7 @@ static int net_reserve(kv_net* net, int nb_pad) {
     KV_HIP(hipMalloc(&net->V, (size_t)kv::WN_XI * cap * 4 * 512 * 4));
     KV_HIP(hipMalloc(&net->Mw, (size_t)kv::WN_XI * cap * 4 * 512 * 4));
     KV_HIP(hipMalloc(&net->V256, (size_t)kv::WN_XI * cap * 4 * 256 * 4));
+    KV_HIP(hipMalloc(&net->vmax, (size_t)12 * cap * sizeof(unsigned)));
     if (!net->slab)  // 48 splits x 16 boards x 64 px x 512 channels
         KV_HIP(hipMalloc(&net->slab, (size_t)(144 / kSplitKt) * kSplitMaxBoards * 64 * 512 * 4));
     net->cap = cap;
@@ -822,6 +829,34 @@ static int launch_wino_gemm(const float* V, const float* U, float* M, int rows, 
     return launch_wino_gemm_t<K, 4, 2, 1, 2>(V, U, M, rows, stride, st);  // 128 x 128, 8 waves, 2 per CU
 }
 
+template <int K, int TM>
+static int launch_wino_gemm_h3_t(const float* V, const uint16_t* Uh, const uint16_t* Ul, const unsigned* vmax,
+                                 float* M, int rows, int stride, hipStream_t st) {
+    using T = kv::WinoH3<TM>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        KV_HIP(hipFuncSetAttribute((const void*)kv::wino_gemm_h3_kernel<K, TM>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::BYTES));
+        attr_set = true;
+    }
+    const int nwg = kv::WN_XI * (rows / T::WM) * (512 / T::WN);
+    KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0, KV_EINVAL, "wino gemm f16x3: rows %d", rows);
+    hipLaunchKernelGGL((kv::wino_gemm_h3_kernel<K, TM>), dim3(nwg), dim3(256), T::BYTES, st, V, Uh, Ul, vmax, M, rows,
+                       512, stride);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+// 128-row tiles (2 workgroups per CU) when the rows allow: at 1,024 rows 4 %
+// faster per forward than the 64-row tile's exact 3 rounds (operand traffic
+// into the CUs, not MFMA, bounds this kernel); same k order, same bits.
+template <int K>
+static int launch_wino_gemm_h3(const float* V, const uint16_t* Uh, const uint16_t* Ul, const unsigned* vmax, float* M,
+                               int rows, int stride, hipStream_t st) {
+    if (rows % 128) return launch_wino_gemm_h3_t<K, 1>(V, Uh, Ul, vmax, M, rows, stride, st);
+    return launch_wino_gemm_h3_t<K, 2>(V, Uh, Ul, vmax, M, rows, stride, st);
+}
+
 template <int K>
 static int launch_wino_gemm_bf6(const float* V, const uint16_t* Uh, const uint16_t* Um, const uint16_t* Ul, float* M,
                                 int rows, int stride, hipStream_t st) {
@@ -840,6 +875,11 @@ static int launch_wino_gemm_bf6(const float* V, const uint16_t* Uh, const uint16
     return KV_OK;
 }
 
+// f16x3: the per-board max |V| slot of conv layer l's input (nullptr otherwise)
+static unsigned* net_vmax(kv_net* net, int l) {
+    return net->precision == KV_PREC_F16X3 ? net->vmax + (size_t)l * net->cap : nullptr;
+}
+
 // the Winograd GEMMs of conv layer l in the net's precision
 template <int K>
 static int wino_gemm_layer(kv_net* net, int l, const float* V, float* M, int rows, int stride, hipStream_t st) {
@@ -847,47 +887,44 @@ static int wino_gemm_layer(kv_net* net, int l, const float* V, float* M, int row
         const size_t o = net->uoff[l];
         return launch_wino_gemm_bf6<K>(V, net->Up[0] + o, net->Up[1] + o, net->Up[2] + o, M, rows, stride, st);
     }
+    if (net->precision == KV_PREC_F16X3) {
+        const size_t o = net->uoff[l];
+        return launch_wino_gemm_h3<K>(V, net->Uf[0] + o, net->Uf[1] + o, net_vmax(net, l), M, rows, stride, st);
+    }
     return launch_wino_gemm<K>(V, net->U + net->uoff[l], M, rows, stride, st);
 }
 
+// output transform of conv layer l (its M) -> Y and / or the next conv's V
 template <bool RESID, bool WRITE_Y, bool NEXT_V>
-static int launch_wino_out(const float* M, int b0, int nb, int stride, const float* sc, const float* sh,
-                           const float* resid, float* Y, float* Vn, hipStream_t st) {
-    const size_t ro = (size_t)b0 * 4 * 512, po = (size_t)b0 * 64 * 512;
-    hipLaunchKernelGGL((kv::wino_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 64, nb), dim3(256), 0, st, M + ro,
-                       stride, sc, sh, resid ? resid + po : nullptr, Y ? Y + po : nullptr, Vn ? Vn + ro : nullptr);
+static int launch_wino_out(kv_net* net, int l, const float* M, int nb, int stride, const float* resid, float* Y,
+                           float* Vn, hipStream_t st) {
+    const float* W = net->w;
+    hipLaunchKernelGGL((kv::wino_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 64, nb), dim3(256), 0, st, M, stride,
+                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn, net_vmax(net, l), net->ut[l],
+                       NEXT_V ? net_vmax(net, l + 1) : nullptr);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
 
-// conv2 + the 5 residual blocks for boards [b0, b0 + nb) on stream st
-static int wino_blocks(kv_net* net, int b0, int nb, int stride, bool mark, hipStream_t st) {
-    const float* W = net->w;
-    const kv::PackOffsets& o = net->off;
-    const size_t ro = (size_t)b0 * 4 * 512, ro256 = (size_t)b0 * 4 * 256;
-    const int rows = nb * 4;
+// conv2 + the 5 residual blocks for boards [0, nb) on stream st
+static int wino_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
+    const int rows = nb * 4, stride = rows;
     float* V = net->V;
     float* M = net->Mw;
     int rc;
-    if ((rc = wino_gemm_layer<256>(net, 1, net->V256 + ro256, M + ro, rows, stride, st))) return rc;
-    if ((rc = launch_wino_out<false, true, true>(M, b0, nb, stride, W + o.scale[1], W + o.shift[1], nullptr, net->X,
-                                                 V, st)))
-        return rc;
+    if ((rc = wino_gemm_layer<256>(net, 1, net->V256, M, rows, stride, st))) return rc;
+    if ((rc = launch_wino_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st))) return rc;
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
     for (int r = 0; r < 5; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         const bool m = mark && r == 2;  // one representative residual GEMM for the engine's timing hook
         if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-        if ((rc = wino_gemm_layer<512>(net, l1, V + ro, M + ro, rows, stride, st))) return rc;
+        if ((rc = wino_gemm_layer<512>(net, l1, V, M, rows, stride, st))) return rc;
         if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
-        if ((rc = launch_wino_out<false, false, true>(M, b0, nb, stride, W + o.scale[l1], W + o.shift[l1], nullptr,
-                                                      nullptr, V, st)))
-            return rc;
-        if ((rc = wino_gemm_layer<512>(net, l2, V + ro, M + ro, rows, stride, st))) return rc;
-        rc = r < 4 ? launch_wino_out<true, true, true>(M, b0, nb, stride, W + o.scale[l2], W + o.shift[l2], net->X,
-                                                       net->X, V, st)
-                   : launch_wino_out<true, true, false>(M, b0, nb, stride, W + o.scale[l2], W + o.shift[l2], net->X,
-                                                        net->X, nullptr, st);
+        if ((rc = launch_wino_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st))) return rc;
+        if ((rc = wino_gemm_layer<512>(net, l2, V, M, rows, stride, st))) return rc;
+        rc = r < 4 ? launch_wino_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
+                   : launch_wino_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
         if (rc) return rc;
     }
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
@@ -901,10 +938,10 @@ static int net_tower_wino(kv_net* net, int nb_pad, bool v256_ready, hipStream_t 
     int rc;
     if (!v256_ready) {
         hipLaunchKernelGGL(kv::wino_in_kernel<256>, dim3(256 / 64, nb_pad), dim3(256), 0, st, net->T, rows,
-                           net->V256);
+                           net->V256, net_vmax(net, 1));
         KV_HIP(hipGetLastError());
     }
-    if ((rc = wino_blocks(net, 0, nb_pad, rows, true, st))) return rc;
+    if ((rc = wino_blocks(net, nb_pad, true, st))) return rc;
     net->dom_flop = 2.0 * kv::WN_XI * rows * 512.0 * 512.0;
     net->dom_algo = KV_ALGO_WINOGRAD;
     net->dom_launches = 1;
@@ -921,13 +958,15 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     const bool tm = net->timing;
     const bool wino = use_wino(net, nb);
     if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
+    if (wino && net->precision == KV_PREC_F16X3)
+        KV_HIP(hipMemsetAsync(net->vmax, 0, (size_t)12 * net->cap * sizeof(unsigned), st));
     if (boards) {
         if (wino)
             hipLaunchKernelGGL(kv::stem_kernel<true>, dim3(4, nb_pad), dim3(256), 0, st, boards, nb, net->stemT,
-                               W + o.scale[0], W + o.shift[0], net->V256, nb_pad * 4);
+                               W + o.scale[0], W + o.shift[0], net->V256, nb_pad * 4, net_vmax(net, 1));
         else
             hipLaunchKernelGGL(kv::stem_kernel<false>, dim3(4, nb_pad), dim3(256), 0, st, boards, nb, net->stemT,
-                               W + o.scale[0], W + o.shift[0], net->T, nb_pad * 4);
+                               W + o.scale[0], W + o.shift[0], net->T, nb_pad * 4, nullptr);
         KV_HIP(hipGetLastError());
     } else if ((rc = launch_conv<16, 16, false>(net->x16, W + o.w[0], W + o.scale[0], W + o.shift[0], nullptr,
                                                 net->T, 256, nb_pad, nullptr, st))) {
@@ -1034,6 +1073,7 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
         }
         KV_HIP(hipMalloc(&net->U, tot * sizeof(float)));
         for (int p = 0; p < 3; ++p) KV_HIP(hipMalloc(&net->Up[p], tot * sizeof(uint16_t)));
+        for (int p = 0; p < 2; ++p) KV_HIP(hipMalloc(&net->Uf[p], tot * sizeof(uint16_t)));
         net->utot = tot;
     }
     for (int l = 1; l < 12; ++l) {
@@ -1045,6 +1085,32 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
     hipLaunchKernelGGL(kv::split3_kernel, dim3((unsigned)((net->utot + 255) / 256)), dim3(256), 0, 0, net->U,
                        net->utot, net->Up[0], net->Up[1], net->Up[2]);
     KV_HIP(hipGetLastError());
+    {  // f16x3: per-layer scale 2^ut putting max |U| in [2^14, 2^15), then the fp16 pieces
+        unsigned* umax = nullptr;
+        KV_HIP(hipMalloc(&umax, 12 * sizeof(unsigned)));
+        KV_HIP(hipMemset(umax, 0, 12 * sizeof(unsigned)));
+        for (int l = 1; l < 12; ++l) {
+            const size_t n = (size_t)kv::WN_XI * kv::kConv[l].cout * kv::kConv[l].cin;
+            hipLaunchKernelGGL(kv::absmax_kernel, dim3(1024), dim3(256), 0, 0, net->U + net->uoff[l], n, umax + l);
+            KV_HIP(hipGetLastError());
+        }
+        unsigned hmax[12];
+        const hipError_t e = hipMemcpy(hmax, umax, sizeof(hmax), hipMemcpyDeviceToHost);
+        (void)hipFree(umax);
+        KV_HIP(e);
+        for (int l = 1; l < 12; ++l) {
+            const size_t n = (size_t)kv::WN_XI * kv::kConv[l].cout * kv::kConv[l].cin;
+            int ex = 0;
+            float mf;
+            memcpy(&mf, &hmax[l], sizeof mf);
+            (void)frexp(hmax[l] ? (double)mf : 1.0, &ex);  // max in [2^(ex-1), 2^ex)
+            net->ut[l] = 15 - ex;
+            hipLaunchKernelGGL(kv::split_f16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0,
+                               net->U + net->uoff[l], kv::kConv[l].cout, kv::kConv[l].cin, net->ut[l],
+                               net->Uf[0] + net->uoff[l], net->Uf[1] + net->uoff[l]);
+            KV_HIP(hipGetLastError());
+        }
+    }
     if (!net->stemT) KV_HIP(hipMalloc(&net->stemT, 9 * 12 * 256 * sizeof(float)));
     hipLaunchKernelGGL(kv::stem_weights_kernel, dim3(9 * 12), dim3(256), 0, 0, net->w + net->off.w[0], net->stemT);
     KV_HIP(hipGetLastError());
@@ -1063,7 +1129,9 @@ int kv_net_set_algo(kv_net* net, int algo) {
 
 int kv_net_set_precision(kv_net* net, int precision) {
     KV_REQUIRE(net, KV_EINVAL, "kv_net_set_precision: NULL");
-    KV_REQUIRE(precision == KV_PREC_FP32 || precision == KV_PREC_BF16X3 || precision == KV_PREC_BF16X6, KV_EINVAL,
+    KV_REQUIRE(precision == KV_PREC_FP32 || precision == KV_PREC_BF16X3 || precision == KV_PREC_BF16X6 ||
+                   precision == KV_PREC_F16X3,
+               KV_EINVAL,
                "kv_net_set_precision: unknown precision %d", precision);
     net->precision = precision;
     return KV_OK;
@@ -1123,6 +1191,8 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->U);
     (void)hipFree(net->stemT);
     for (int p = 0; p < 3; ++p) (void)hipFree(net->Up[p]);
+    for (int p = 0; p < 2; ++p) (void)hipFree(net->Uf[p]);
+    (void)hipFree(net->vmax);
     (void)hipFree(net->V);
     (void)hipFree(net->Mw);
     (void)hipFree(net->V256);

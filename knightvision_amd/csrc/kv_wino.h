@@ -48,8 +48,9 @@ __device__ inline void wino_at(const float* m, float* o) {
 
 // V of one tile (t = ty*2 + tx) of one channel from its 6x6 input patch d
 // (row-major, zero padded) -> V[xi][row][c] at stride xi_stride
-__device__ inline void wino_input_tile(const float (&d)[36], float* V, size_t off, size_t xi_stride) {
+__device__ inline float wino_input_tile(const float (&d)[36], float* V, size_t off, size_t xi_stride) {
     float tmp[6][6];  // B^T d (columns)
+    float mx = 0.f;   // max |V| written (the f16x3 operand scale; dead code for the other callers)
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
         float col[6], o[6];
@@ -64,8 +65,35 @@ __device__ inline void wino_input_tile(const float (&d)[36], float* V, size_t of
         float o[6];
         wino_bt(tmp[i], o);
 #pragma unroll
-        for (int j = 0; j < 6; ++j) V[(size_t)(i * 6 + j) * xi_stride + off] = o[j];
+        for (int j = 0; j < 6; ++j) {
+            V[(size_t)(i * 6 + j) * xi_stride + off] = o[j];
+            mx = fmaxf(mx, fabsf(o[j]));
+        }
     }
+    return mx;
+}
+
+// KV_PREC_F16X3 operand scaling. The GEMM splits every V element of board b
+// into fp16 pieces after scaling by 2^s_b, s_b = 14 - exponent(max_b |V|), so
+// the board's largest element lands in [2^14, 2^15): no fp16 overflow and the
+// low piece stays normal for everything within 2^-17 of the maximum. The scale
+// depends on the board alone (batch invariance) and is a power of two (exact).
+// vmax holds max_b |V| as float bits (non-negative floats order as unsigned).
+__device__ inline int h3_exp(unsigned mx) {
+    if (mx == 0u) return 0;
+    const int e = (int)((mx >> 23) & 0xFFu) - 127;
+    const int s = 14 - e;
+    return s < -100 ? -100 : (s > 100 ? 100 : s);
+}
+
+// block-wide max of v (every thread calls), then one atomicMax into *dst;
+// red: 4 floats of LDS (256-thread blocks)
+__device__ inline void block_max_to(float v, unsigned* dst, float* red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(dst, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
 // U = G g G^T for every (cout, cin) of one conv, in fp64, rounded once to fp32.
@@ -100,7 +128,9 @@ __global__ void wino_weights_kernel(const float* __restrict__ w, int cout, int c
 // input transform of an NHWC activation [boards][64][C] (the stem output).
 // Block: 4 waves = the 4 tiles of one board, lane = channel (64 per block).
 template <int C>
-__global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ X, int rows, float* __restrict__ V) {
+__global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ X, int rows, float* __restrict__ V,
+                                                      unsigned* vmax) {
+    __shared__ float red[4];
     const int t = threadIdx.x >> 6, c = blockIdx.x * 64 + (threadIdx.x & 63), b = blockIdx.y;
     const int y0 = (t >> 1) * 4 - 1, x0 = (t & 1) * 4 - 1;
     float d[36];
@@ -111,7 +141,8 @@ __global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ 
             const int yy = y0 + i, xx = x0 + j;
             d[i * 6 + j] = (yy >= 0 && yy < 8 && xx >= 0 && xx < 8) ? X[((size_t)b * 64 + yy * 8 + xx) * C + c] : 0.f;
         }
-    wino_input_tile(d, V, ((size_t)b * 4 + t) * C + c, (size_t)rows * C);
+    const float mx = wino_input_tile(d, V, ((size_t)b * 4 + t) * C + c, (size_t)rows * C);
+    if (vmax) block_max_to(mx, vmax + b, red);
 }
 
 // output transform of layer l + folded BN (+ residual) + ReLU -> Y (NHWC,
@@ -122,20 +153,24 @@ __global__ __launch_bounds__(256) void wino_in_kernel(const float* __restrict__ 
 template <bool RESID, bool WRITE_Y, bool NEXT_V>
 __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__ M, int rows,
                                                        const float* __restrict__ scale, const float* __restrict__ shift,
-                                                       const float* resid, float* Y, float* __restrict__ Vn) {
+                                                       const float* resid, float* Y, float* __restrict__ Vn,
+                                                       const unsigned* vmax_in, int ut, unsigned* vmax_out) {
     constexpr int C = 512;
     __shared__ float plane[64][64];  // [pixel][channel]
+    __shared__ float red[4];
     const int t = threadIdx.x >> 6, cl = threadIdx.x & 63;
     const int c = blockIdx.x * 64 + cl, b = blockIdx.y;
     const size_t xs = (size_t)rows * C;
     const size_t base = ((size_t)b * 4 + t) * C + c;
     const float sc = scale[c], sh = shift[c];
+    // f16x3: M was computed on operands scaled by 2^(s_b + ut); undo it (exact). 1 otherwise.
+    const float inv = vmax_in ? ldexpf(1.f, -(h3_exp(vmax_in[b]) + ut)) : 1.f;
     float tmp[4][6];  // A^T m (columns)
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
         float col[6], o[4];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) col[i] = M[(size_t)(i * 6 + j) * xs + base];
+        for (int i = 0; i < 6; ++i) col[i] = M[(size_t)(i * 6 + j) * xs + base] * inv;
         wino_at(col, o);
 #pragma unroll
         for (int i = 0; i < 4; ++i) tmp[i][j] = o[i];
@@ -166,7 +201,8 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
             const int yy = y0 - 1 + i, xx = x0 - 1 + j;
             d[i * 6 + j] = (yy >= 0 && yy < 8 && xx >= 0 && xx < 8) ? plane[yy * 8 + xx][cl] : 0.f;
         }
-    wino_input_tile(d, Vn, base, xs);
+    const float mx = wino_input_tile(d, Vn, base, xs);
+    if (vmax_out) block_max_to(mx, vmax_out + b, red);
 }
 
 // The 36 GEMMs M[xi] = V[xi] x U[xi]^T on v_mfma_f32_32x32x2_f32, over `rows`
@@ -474,6 +510,219 @@ __global__ __launch_bounds__(256) void wino_gemm_bf6_kernel(const float* __restr
                 const int row = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 Mo[(size_t)row * cout + nt * 32] = acc[mt][nt][r];
             }
+}
+
+// ------------------------------------------------------------ f16x3 --
+// KV_PREC_F16X3: M[xi] = V[xi] x U[xi]^T with both operands split into two
+// fp16 pieces, x*2^s = h + l (h = fp16(x*2^s), l = fp16(x*2^s - h): 22
+// significant bits), and the three products of weight >= 2^-22 -- h*l, l*h,
+// h*h -- on v_mfma_f32_32x32x16_f16 with fp32 accumulation. Host emulation of
+// the whole tower: 2x the error of rounding the operands to fp32, well under
+// the direct fp32 conv's accumulation error. U is split once at load time
+// with a per-layer scale 2^ut; V is split while it is staged into LDS with the
+// per-board scale of h3_exp; the consumer (wino_out_kernel) multiplies M by
+// 2^-(s_b + ut). 3 MFMAs of 32 cycles per 32x32x16 block instead of the fp32
+// kernel's 8 of 64: the f16 rate is 5.3x the fp32 MFMA rate per product.
+//
+// Workgroup: 64 rows x 128 channels of one xi (the fp32 kernel's 64x128 tile:
+// exactly 3 rounds at 1,024 rows with LDS padded for 3 workgroups per CU),
+// 4 waves of 32x64 (1x2 MFMA tiles), k-tiles of 16, double-buffered; piece
+// rows at a 48-byte stride (conflict-free ds_read_b128).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Workgroup tile: WM = 64 * TM rows x 128 channels of one xi, 4 waves in a
+// 2 x 2 grid of (32 TM) x 64 (TM x 2 MFMA tiles each). LDS stage (two
+// stages): A h / l [WM rows][64 B], B h / l [128 rows][64 B] = 32 k. The four
+// 16-byte chunks of a row are XOR-swizzled by (row / 4) % 4, which spreads
+// every ds_read_b128 lane group (16 lanes = 16 rows) over all 64 banks with no
+// padding -- so the B image can be filled by lane-linear global_load_lds
+// straight from a Uf laid out as that image.
+template <int TM>
+struct WinoH3 {
+    static constexpr int WM = 64 * TM, WN = 128, CK = 32, SR = 64;
+    static constexpr int PA = WM * SR, PB = WN * SR;  // one piece of A / B
+    static constexpr int STAGE = 2 * PA + 2 * PB;     // 24 / 32 KB
+    static constexpr size_t BYTES = 2 * STAGE;
+};
+__host__ __device__ inline int h3_off(int row, int c) { return row * 64 + ((c ^ ((row >> 2) & 3)) << 4); }
+
+// Uf (KV_PREC_F16X3): per (xi, 128-channel block, 32-k tile, piece) one 8 KB
+// block holding the B image of that tile.
+__host__ __device__ inline size_t h3_uidx(int xi, int co, int ci, int cout, int K) {
+    const size_t blk = ((size_t)xi * (cout >> 7) + (co >> 7)) * (K >> 5) + (ci >> 5);
+    return blk * 4096 + (h3_off(co & 127, (ci & 31) >> 3) >> 1) + (ci & 7);
+}
+
+// One barrier per k-tile. Iteration kt: B(kt+1) global_load_lds into the
+// other stage; MFMAs on stage kt; A(kt+1) (in registers since iteration kt-2)
+// split and written to the other stage; A(kt+3) loads issued; barrier. A
+// (V, streamed from HBM / the Infinity Cache) has two k-tiles of latency
+// cover, B (U, L2-resident) one compute phase.
+template <int K, int TM>
+__global__ __launch_bounds__(256) void wino_gemm_h3_kernel(const float* __restrict__ V, const uint16_t* __restrict__ Uh,
+                                                           const uint16_t* __restrict__ Ul,
+                                                           const unsigned* __restrict__ vmax, float* __restrict__ M,
+                                                           int rows, int cout, int stride) {
+    using T = WinoH3<TM>;
+    constexpr int CK = T::CK, PA = T::PA, PB = T::PB, STAGE = T::STAGE, NK = K / CK;
+    static_assert(NK % 2 == 0 && NK >= 4, "k-tiles");
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int CT = cout / T::WN, RT = rows / T::WM;
+    const int nwg = WN_XI * RT * CT;
+    const int idx0 = (int)(blockIdx.x & 7) * (nwg >> 3) + (int)(blockIdx.x >> 3);
+    const int xi = idx0 / (CT * RT);
+    const int nb_ = idx0 % CT;
+    const int r_base = ((idx0 / CT) % RT) * T::WM;
+    const float* Va = V + ((size_t)xi * stride + r_base) * K;
+    const size_t ub = ((size_t)xi * CT + nb_) * NK * 4096;  // this workgroup's Uf blocks (halves)
+
+    // A: thread = rows tid/4 + 64 i, 8 consecutive k each; the rows' board scales are fixed for the K loop
+    const int ar = tid >> 2, ac = tid & 3;
+    float asc[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) asc[i] = ldexpf(1.f, h3_exp(vmax[(r_base + ar + 64 * i) >> 2]));
+    const float* asrc = Va + (size_t)ar * K + ac * 8;
+    f32x4 ra[2][TM][2];
+    auto loadA = [&](int kt, f32x4 (&a)[TM][2]) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            a[i][0] = *(const f32x4*)(asrc + (size_t)64 * i * K + kt * CK);
+            a[i][1] = *(const f32x4*)(asrc + (size_t)64 * i * K + kt * CK + 4);
+        }
+    };
+    auto writeA = [&](unsigned char* st, const f32x4 (&a)[TM][2]) {
+        // split in pairs: v_pk_mul_f32, v_cvt_pk_f16_f32 (RNE), two v_cvt_f32_f16, v_pk_fma, v_cvt_pk_f16_f32
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            h16x2 hp[4], lp[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const f32x2 x = f32x2{a[i][e >> 1][(e & 1) * 2], a[i][e >> 1][(e & 1) * 2 + 1]} * asc[i];
+                hp[e] = __builtin_convertvector(x, h16x2);
+                lp[e] = __builtin_convertvector(x - __builtin_convertvector(hp[e], f32x2), h16x2);
+            }
+            const int w = h3_off(ar + 64 * i, ac);
+            *(u32x4*)(st + w) = __builtin_bit_cast(u32x4, hp);
+            *(u32x4*)(st + PA + w) = __builtin_bit_cast(u32x4, lp);
+        }
+    };
+    // B: 2 x 8 KB per stage, lane-linear: chunk q*256 + tid of each piece image
+    auto loadB = [&](int kt, unsigned char* st) {
+        const size_t o = ub + (size_t)kt * 4096;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int ch = q * 256 + wave * 64;  // this wave's first 16-byte chunk
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(Uh + o + (q * 256 + tid) * 8),
+                                             (__attribute__((address_space(3))) void*)(st + 2 * PA + ch * 16), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(Ul + o + (q * 256 + tid) * 8),
+                                             (__attribute__((address_space(3))) void*)(st + 2 * PA + PB + ch * 16), 16, 0,
+                                             0);
+        }
+    };
+
+    const int h = lane >> 5, li = lane & 31;
+    f32x16 acc[TM][2];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    auto compute = [&](const unsigned char* st) {
+#pragma unroll
+        for (int kk = 0; kk < CK / 16; ++kk) {
+            f16x8 ah[TM], al[TM], bh[2], bl[2];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int ao = h3_off(wm * 32 * TM + i * 32 + li, kk * 2 + h);
+                ah[i] = *(const f16x8*)(st + ao);
+                al[i] = *(const f16x8*)(st + PA + ao);
+            }
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                const int bo = 2 * PA + h3_off(wn * 64 + nt * 32 + li, kk * 2 + h);
+                bh[nt] = *(const f16x8*)(st + bo);
+                bl[nt] = *(const f16x8*)(st + bo + PB);
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) {  // small terms first
+                    f32x16 c = acc[i][nt];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[nt], c, 0, 0, 0);  // h*l
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[nt], c, 0, 0, 0);  // l*h
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[nt], c, 0, 0, 0);  // h*h
+                    acc[i][nt] = c;
+                }
+        }
+    };
+
+    // prologue: stage 0 = A(0) + B(0); A(1), A(2) in flight
+    loadA(0, ra[0]);
+    loadB(0, lds);
+    writeA(lds, ra[0]);
+    loadA(1, ra[1]);
+    loadA(2, ra[0]);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int kt0 = 0; kt0 < NK; kt0 += 2) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {  // j = kt & 1: this stage; A(kt + 1) is in register slot 1 - j
+            const int kt = kt0 + j;
+            unsigned char* cur = lds + j * STAGE;
+            unsigned char* nxt = lds + (1 - j) * STAGE;
+            if (kt + 1 < NK) loadB(kt + 1, nxt);
+            compute(cur);
+            if (kt + 1 < NK) {
+                writeA(nxt, ra[1 - j]);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // B(kt+1) landed (and A(kt+2))
+                if (kt + 3 < NK) loadA(kt + 3, ra[1 - j]);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+    }
+
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        float* Mo = M + ((size_t)xi * stride + r_base + wm * 32 * TM + i * 32) * cout + nb_ * 128 + wn * 64 + li;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+                Mo[(size_t)row * cout + nt * 32] = acc[i][nt][r];
+            }
+    }
+}
+
+// max |x| over n floats into *out (as float bits); grid-stride, one atomic per wave
+__global__ void absmax_kernel(const float* __restrict__ x, size_t n, unsigned* out) {
+    float m = 0.f;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        m = fmaxf(m, fabsf(x[i]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+// U [36][cout][cin] (one layer) -> fp16 pieces of U * 2^ut in the Uf layout (h3_uidx)
+__global__ void split_f16_kernel(const float* __restrict__ u, int cout, int cin, int ut, uint16_t* __restrict__ h,
+                                 uint16_t* __restrict__ l) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)WN_XI * cout * cin) return;
+    const int ci = (int)(i % cin), co = (int)((i / cin) % cout), xi = (int)(i / ((size_t)cin * cout));
+    const float a = ldexpf(u[i], ut);
+    const _Float16 hh = (_Float16)a;
+    const size_t o = h3_uidx(xi, co, ci, cout, cin);
+    h[o] = __builtin_bit_cast(uint16_t, hh);
+    l[o] = __builtin_bit_cast(uint16_t, (_Float16)(a - (float)hh));
 }
 
 }  // namespace kv

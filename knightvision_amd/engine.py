@@ -46,7 +46,7 @@ class SelfPlayEngine:
                           game_id_stride=game_id_stride, seed=seed, seed_mode=seed_mode,
                           max_moves=max_moves if max_moves else 0, batch=batch, eps=eps, alpha=alpha, sims=sims,
                           c_puct=c_puct, eval_mode=eval_mode, record_cap=record_cap, recycle=1 if recycle else 0,
-                          precision={"fp32": 0, "bf16x3": 1, "bf16x6": 2}[precision], algo=ALGOS[algo])
+                          precision={"fp32": 0, "bf16x3": 1, "bf16x6": 2, "f16x3": 3}[precision], algo=ALGOS[algo])
         h = C.c_void_p()
         _lib.check(L.kv_create(C.byref(cfg), C.byref(h)), "kv_create")
         self.h = h

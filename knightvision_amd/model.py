@@ -23,7 +23,7 @@ from . import _lib
 from .weights import pack_weights, state_dict_to_numpy
 
 
-PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16x6": 2}
+PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "f16x3": 3}
 ALGOS = {"auto": 0, "direct": 1, "winograd": 2}
 
 

@@ -131,7 +131,7 @@ GROUPS = {"pg_init_mm80": ("init", 80, 16), "pg_peaked_mm80": ("peaked", 80, 16)
           "pg_init_b1_mm60": ("init", 60, 1), "pg_init_full": ("init", None, 16)}
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "bf16x3"])
+@pytest.mark.parametrize("precision", ["fp32", "f16x3", "bf16x6", "bf16x3"])
 @pytest.mark.parametrize("group", list(GROUPS))
 def test_engine_games_match_reference(golden_dir, group, precision):
     from knightvision_amd.engine import SelfPlayEngine, records_by_game

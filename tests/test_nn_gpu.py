@@ -14,7 +14,7 @@ TOL_P, TOL_V = 1e-4, 1e-5
 
 
 # (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x4,3x3) / bf16x6 Winograd / bf16x3 direct
-MODES = [("fp32", "direct"), ("fp32", "winograd"), ("bf16x6", "winograd"), ("bf16x3", "auto")]
+MODES = [("fp32", "direct"), ("fp32", "winograd"), ("f16x3", "winograd"), ("bf16x6", "winograd"), ("bf16x3", "auto")]
 
 
 def _net(variant, precision="fp32", algo="auto"):
@@ -59,7 +59,7 @@ def test_forward_batch_sizes_vs_torch(B, precision, algo):
     assert np.abs(vb.cpu().numpy() - v.cpu().numpy()).max() == 0.0
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x6", "bf16x3"])
+@pytest.mark.parametrize("precision", ["fp32", "f16x3", "bf16x6", "bf16x3"])
 def test_batch_invariance(precision):
     """A board's outputs do not depend on the batch it is evaluated in, within a
     batch-size class (<= 16 boards: split-K direct kernels; > 16: whole-K
@@ -73,7 +73,7 @@ def test_batch_invariance(precision):
     p_all, v_all = m(planes)  # 40 boards: whole-K class
     p_20, v_20 = m(planes[20:])
     assert torch.equal(p_20, p_all[20:]) and torch.equal(v_20, v_all[20:])
-    if precision == "fp32":  # 300 boards run the 128x128 GEMM tile, 40 the 64x128 tile: same bits
+    if precision in ("fp32", "f16x3"):  # fp32: 300 boards run the 128x128 GEMM tile, 40 the 64x128 tile: same bits
         codes_l = rng.integers(0, 13, size=(300, 64)) * (rng.random((300, 64)) < 0.4)
         codes_l[:40] = codes
         p_l, v_l = m(torch.from_numpy(codes_to_planes(codes_l)).cuda())
