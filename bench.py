@@ -51,6 +51,9 @@ def parse():
                     help="also measure the fp32 direct implicit-GEMM convs (reported under 'fp32_direct')")
     ap.add_argument("--alt-precision", default="f16x3",
                     help="also measure this network precision (reported under 'alt_precision'; '' to skip)")
+    ap.add_argument("--ref-block", type=int, default=1,
+                    help="mcts mode: also run the reference's own move selection (sims=0, C2-ref) long enough for "
+                         "games to complete, reported under 'ref_selection' with measured games/hour")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
@@ -111,7 +114,7 @@ def main():
     warmup = args.warmup if args.warmup is not None else (1 if mcts else 8)
     G = args.slots
 
-    def measure(precision, algo="auto"):
+    def measure(precision, algo="auto", sims=sims, steps=steps, warmup=warmup):
         eng = SelfPlayEngine(synthetic_state_dict(42, "init"), slots=G, n_games=1 << 40, seed=42, max_moves=None,
                              batch=16, sims=sims, game_id_base=rank, game_id_stride=world,
                              record_cap=max(1 << 16, G * (steps + warmup + 8)), device=local, precision=precision,
@@ -150,6 +153,12 @@ def main():
     alt = None
     if args.alt_precision and args.alt_precision != args.precision:
         alt = measure(args.alt_precision)
+    refsel = None
+    if mcts and args.ref_block:
+        # C2-ref: the reference's move selection (one network row per ply, sampled move) on the same slots;
+        # 1,200 warm-up ply-steps fill the slots with games at every stage, the 2,400 timed ones complete
+        # games at the steady-state rate
+        refsel = measure(args.precision, sims=0, steps=2400, warmup=1200)
     direct = None
     if args.compare_direct and args.precision == "fp32" and m["dom_algo"] == 2:
         direct = measure("fp32", "direct")
@@ -266,6 +275,18 @@ def main():
                                     else "conv3x3 (direct)"),
                 "dominant_avg_launch_ms": alt["conv_ms"], "dominant_tflops_fp32_equiv": a_ach,
                 "dominant_bf16_mfma_frac": (a_ach * a_prod / BF16_MFMA_PEAK_TFLOPS) if (a_ach and a_prod) else None}
+        if refsel is not None:
+            g = refsel["gms"]
+            rl = float(g["plies"].mean()) if len(g) else float("nan")
+            out["ref_selection"] = {
+                "note": "C2-ref: the reference's own move selection (sims=0: one network row per ply, softmax + "
+                        "Dirichlet + random.choices) on the same slots, uncapped games, slots recycled; "
+                        "games/hour counts games completed inside the timed region",
+                "plies_per_s": refsel["plies"] / refsel["dt"], "games_per_hour": refsel["games_done"] / refsel["dt"] * 3600.0,
+                "games_completed": refsel["games_done"], "timed_s": refsel["dt"], "steps": 2400, "warmup": 1200,
+                "mean_plies_per_game": rl if rl == rl else None,
+                "reference_cpu": {"plies_per_s": 250.0, "games_per_hour": 2424.0,
+                                  "source": "BASELINE.md: reference self_play.py (SELFPLAY_SEQ=1) on 8 Xeon cores"}}
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, sims)
         print(json.dumps(out), flush=True)
