@@ -80,7 +80,7 @@ def cpu_baseline(seconds: float, sims: int):
             games += 1
             seed += 1
         dt = time.perf_counter() - t0
-        return dict(value=done / dt, unit="sims/s", cores=torch.get_num_threads(), kind="port",
+        return dict(value=done / dt, unit="sims/s", cores=torch.get_num_threads(), cpu=cpu_model(), kind="port",
                     sample=f"{games} games x 2 moves x {s_cpu} sims (per-game seeds 42+), oracle PUCT restatement "
                            f"+ torch-CPU ChessNet fp32, one leaf per network call, {dt:.1f}s")
     while time.perf_counter() - t0 < seconds:
@@ -90,9 +90,19 @@ def cpu_baseline(seconds: float, sims: int):
         games += 1
         seed += 1
     dt = time.perf_counter() - t0
-    return dict(value=plies / dt, unit="plies/s", cores=torch.get_num_threads(), kind="port",
+    return dict(value=plies / dt, unit="plies/s", cores=torch.get_num_threads(), cpu=cpu_model(), kind="port",
                 sample=f"{games} games x <=64 plies (per-game seeds 42+), oracle rules/RNG + torch-CPU "
                        f"ChessNet fp32, batch-16 reference schedule, {dt:.1f}s")
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def main():
@@ -287,6 +297,18 @@ def main():
                 "mean_plies_per_game": rl if rl == rl else None,
                 "reference_cpu": {"plies_per_s": 250.0, "games_per_hour": 2424.0,
                                   "source": "BASELINE.md: reference self_play.py (SELFPLAY_SEQ=1) on 8 Xeon cores"}}
+            cal = os.path.join(HERE, "profiles", "r01_cpu_calibration.json")
+            if not args.no_cpu_baseline:
+                # the reference's selection restated on this box's host cores, and the reference-equivalent rate
+                # through the container calibration (reference / port on identical work, tools/calibrate_cpu.py)
+                port = cpu_baseline(min(args.cpu_seconds, 8.0), 0)
+                out["ref_selection"]["cpu_port_box"] = port
+                if os.path.exists(cal):
+                    r = json.load(open(cal))["ref_over_port"]
+                    eq = port["value"] * r
+                    out["ref_selection"]["reference_equiv_box"] = {
+                        "plies_per_s": eq, "ref_over_port": r, "source": os.path.relpath(cal, HERE),
+                        "gpu_over_reference_equiv": (refsel["plies"] / refsel["dt"]) / eq}
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, sims)
         print(json.dumps(out), flush=True)
