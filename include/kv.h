@@ -200,6 +200,42 @@ int kv_dev_dirichlet(int device, const uint64_t* seeds, int n, double alpha, int
 /* CPython random.Random(seed[i]): count random() values -> out [n][count]. */
 int kv_dev_py_random(int device, const uint64_t* seeds, int n, int count, double* out);
 
+/* ------------------------------------------------------- data pipeline ---
+ * Full-rules chess (python-chess 1.999 semantics, csrc/kv_chess.cpp) for the
+ * reference's PGN -> JSONL ingestion and its JSONL datasets. Host code: no
+ * GPU is touched. Squares here are python-chess's (a1 = 0, h8 = 63).
+ *
+ * kv_pgn_extract replaces data_utils/parser_pgn.py:81-118
+ * extract_data_from_pgn's loop (chess.pgn.read_game + board.fen() /
+ * board.san(move) / board.push(move) per mainline move): one record per
+ * mainline move of every game in `text`, in file order. Stops before a game
+ * whose records would not fit in `cap` and reports in *consumed the bytes of
+ * `text` processed (whole games), so callers loop over large inputs;
+ * KV_EOVERFLOW if a single game does not fit (*n_out = its move count). */
+#define KV_PGN_OUTCOME_NONE (-128) /* Result "*" or unknown: the reference's `outcome = None` */
+typedef struct kv_pgn_record {
+    char fen[100];   /* board.fen() before the move, NUL-terminated */
+    char san[12];    /* board.san(move) */
+    int32_t outcome; /* 1 ("1-0"), -1 ("0-1"), 0 ("1/2-1/2"), KV_PGN_OUTCOME_NONE */
+    int32_t game;    /* index of the game within this call */
+} kv_pgn_record;
+int kv_pgn_extract(const char* text, size_t len, kv_pgn_record* out, size_t cap, size_t* n_out, size_t* consumed,
+                   int64_t* n_games);
+/* fen_to_tensor's piece scan (data_utils/dataset.py:59-68, scripts/train.py:531-545):
+ * n FENs, `stride` bytes apart (NUL-terminated) -> codes[n][64] int8, 0 empty,
+ * 1..12 = P N B R Q K p n b r q k (the PGN plane order + 1), index row*8+col
+ * with row 0 = rank 8. */
+int kv_fen_codes(const char* fens, size_t stride, int n, int8_t* codes);
+/* ChessPGNDataset.default_move_encoder (scripts/train.py:553-558):
+ * board.parse_san(san) -> from_square*64 + to_square. */
+int kv_san_move_index(const char* fens, size_t fen_stride, const char* sans, size_t san_stride, int n,
+                      int32_t* out);
+/* test / tooling entry points: perft node count, SAN round trip (parse_san ->
+ * san, fen after push), Board(fen).fen() */
+int kv_chess_perft(const char* fen, int depth, uint64_t* nodes);
+int kv_chess_san(const char* fen, const char* san_in, char* san_out, size_t san_cap, char* fen_after, size_t fen_cap);
+int kv_chess_fen(const char* fen_in, char* fen_out, size_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,6 +23,7 @@ the PGN dataset's (train.py:542-545, :553-558) exactly as in the reference.
 """
 from __future__ import annotations
 
+import json
 import math
 import os
 from dataclasses import dataclass
@@ -163,3 +164,80 @@ def wrap_ddp(model, device):
         ids = [dev.index if dev.index is not None else 0] if dev.type == "cuda" else None
         return torch.nn.parallel.DistributedDataParallel(model, device_ids=ids, bucket_cap_mb=64)
     return model
+
+
+class ChessPGNDataset(torch.utils.data.Dataset):
+    """The trainer's JSONL dataset (scripts/train.py:497-561), chess work native
+    (kv_fen_codes / kv_san_move_index, csrc/kv_chess.cpp). As the reference:
+      * indexes the byte offsets of the first max_samples lines; a sample is read
+        and decoded on access; extend() appends ready samples after them;
+      * board = fen_to_tensor(fen): numpy fp32 [12,8,8], planes P N B R Q K
+        p n b r q k, row 0 = rank 8 (:531-545);
+      * move = move_encoder(san, fen), default board.parse_san -> from*64+to in
+        python-chess squares (:553-558) -- not the self-play encode_move indexing;
+      * outcome from record.get("result", "1/2-1/2") (:525-532): the parser writes
+        "outcome", not "result", so file samples read 0.0 -- kept as is.
+    `materialize(device)` decodes every file sample at once (codes, move
+    indices and outcomes as device tensors) for batched training."""
+
+    def __init__(self, path, move_encoder=None, max_samples=10000):
+        self.file_path = path
+        self.move_encoder = move_encoder or self.default_move_encoder
+        self.max_samples = max_samples
+        self.additional_data = []
+        self.line_offsets = []
+        with open(self.file_path, "rb") as f:
+            offset = 0
+            for i, line in enumerate(f):
+                if i >= self.max_samples:
+                    break
+                self.line_offsets.append(offset)
+                offset += len(line)
+
+    def __len__(self):
+        return len(self.line_offsets) + len(self.additional_data)
+
+    @staticmethod
+    def _outcome(record):
+        result = record.get("result", "1/2-1/2")
+        return 1.0 if result == "1-0" else (-1.0 if result == "0-1" else 0.0)
+
+    def __getitem__(self, idx):
+        if idx >= len(self.line_offsets):
+            return self.additional_data[idx - len(self.line_offsets)]
+        with open(self.file_path, "rb") as f:
+            f.seek(self.line_offsets[idx])
+            record = json.loads(f.readline().decode().strip())
+        fen = record["fen"]
+        return self.fen_to_tensor(fen), self.move_encoder(record["move"], fen), self._outcome(record)
+
+    def fen_to_tensor(self, fen):
+        from .data_utils import _chess
+        from .data_utils.dataset import codes_to_tensor
+        return codes_to_tensor(_chess.fen_codes([fen])[0]).numpy()
+
+    def default_move_encoder(self, move_san, fen):
+        from .data_utils import _chess
+        return int(_chess.san_move_index([fen], [move_san])[0])
+
+    def extend(self, new_records):
+        self.additional_data.extend(new_records)
+
+    def materialize(self, device):
+        """(codes int8 [N,64], moves int64 [N], outcomes fp32 [N]) of the file samples
+        on `device` (default move encoder only)."""
+        from .data_utils import _chess
+        if getattr(self.move_encoder, "__func__", None) is not ChessPGNDataset.default_move_encoder:
+            raise ValueError("materialize() decodes moves with the default encoder only")
+        fens, sans, outs = [], [], []
+        with open(self.file_path, "rb") as f:
+            for i, line in enumerate(f):
+                if i >= len(self.line_offsets):
+                    break
+                rec = json.loads(line.decode().strip())
+                fens.append(rec["fen"])
+                sans.append(rec["move"])
+                outs.append(self._outcome(rec))
+        codes = torch.from_numpy(_chess.fen_codes(fens)).to(device)
+        moves = torch.from_numpy(_chess.san_move_index(fens, sans).astype(np.int64)).to(device)
+        return codes, moves, torch.tensor(outs, dtype=torch.float32, device=device)
