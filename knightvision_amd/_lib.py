@@ -6,7 +6,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libkv.so")
+LIB_PATH = os.environ.get("KV_LIB_PATH") or os.path.join(HERE, "libkv.so")  # override: A/B of two builds
 
 _lib = None
 

@@ -38,11 +38,8 @@ __constant__ const int8_t kStart[64] = {9, 11, 10, 8, 7, 10, 11, 9, 12, 12, 12, 
                                         0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
                                         6, 6, 6, 6, 6, 6, 6, 6, 3, 5, 4, 2, 1, 4, 5, 3};
 
-// GameState() :34-84 + per-game seeding (_init_worker :81-85 with SEED+g)
-__device__ void start_game(const DevCfg& cfg, Slot& s, int8_t* board, uint32_t* np_mt, uint32_t* py_mt,
-                           long long k) {
-    const long long gid = cfg.id_base + k * cfg.id_stride;
-    for (int i = 0; i < 64; ++i) board[i] = kStart[i];
+// GameState() :34-84: the slot fields of a new game (board and streams set by the caller)
+__device__ void start_game_fields(const DevCfg& cfg, Slot& s, long long gid) {
     s.game_id = gid;
     s.status = ST_ACTIVE;
     s.ply = 0;
@@ -55,11 +52,21 @@ __device__ void start_game(const DevCfg& cfg, Slot& s, int8_t* board, uint32_t* 
     s.outcome = 0;
     s.reason = -1;
     if (cfg.seed_mode == KV_SEED_PER_GAME) {
+        s.has_last = 0;
+        s.need_flush = 0;
+    }
+}
+
+// GameState() + per-game seeding (_init_worker :81-85 with SEED+g), one thread
+__device__ void start_game(const DevCfg& cfg, Slot& s, int8_t* board, uint32_t* np_mt, uint32_t* py_mt,
+                           long long k) {
+    const long long gid = cfg.id_base + k * cfg.id_stride;
+    for (int i = 0; i < 64; ++i) board[i] = kStart[i];
+    start_game_fields(cfg, s, gid);
+    if (cfg.seed_mode == KV_SEED_PER_GAME) {
         const unsigned long long sd = cfg.seed + (unsigned long long)gid;
         mt_seed_genrand(np_mt, (uint32_t)sd);
         mt_seed_python(py_mt, sd);
-        s.has_last = 0;
-        s.need_flush = 0;
     }
 }
 
@@ -154,18 +161,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 }
 
 // ------------------------------------------------------------- finish ----
-__global__ __launch_bounds__(64) void k_finish(DevCfg cfg, Slot* slots, int8_t* boards, uint16_t* moves,
-                                               uint32_t* np_mt, uint32_t* py_mt, kv_game* games, Ctr* ctr) {
-    const int i = blockIdx.x, lane = threadIdx.x;
+// two waves per slot: wave 0 scores the game, sets up the next one and seeds
+// its numpy stream while wave 1 seeds the CPython stream (the longer chain)
+__global__ __launch_bounds__(128) void k_finish(DevCfg cfg, Slot* slots, int8_t* boards, uint16_t* moves,
+                                                uint32_t* np_mt, uint32_t* py_mt, kv_game* games, Ctr* ctr) {
+    const int i = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Slot s = slots[i];
     if (s.status == ST_ACTIVE) {
-        if (lane == 0) atomicAdd(&ctr->active, 1);
+        if (tid == 0) atomicAdd(&ctr->active, 1);
         return;
     }
     if (s.status != ST_FINISHED) return;
     int8_t* board = boards + (size_t)i * 64;
     // outcome (:210-238)
-    if (s.end_kind == END_MAXED) {
+    if (wave == 1) {
+    } else if (s.end_kind == END_MAXED) {
         s.outcome = 0;
         s.reason = 0;
     } else if (s.end_kind != END_RESIGN) {
@@ -191,32 +201,49 @@ __global__ __launch_bounds__(64) void k_finish(DevCfg cfg, Slot* slots, int8_t* 
         s.flags = p.flags;
         s.ep = p.ep;
     }
+    __shared__ long long s_next;
     __syncthreads();
-    if (lane != 0) return;
-    // flush of a non-empty buffer (:202-208): one more forward call
-    if (cfg.sims == 0 && s.buf > 0) {
-        s.n_evals += 1;
-        if (cfg.seed_mode == KV_SEED_SEQUENTIAL) s.need_flush = 1;
-    }
-    const unsigned long long gi = atomicAdd(&ctr->games_count, 1ull);
-    kv_game gm;
-    gm.game_id = s.game_id;
-    gm.plies = s.ply;
-    gm.outcome = s.outcome;
-    gm.reward = s.outcome == 1 ? 1.0f : (s.outcome == 0 ? 0.2f : -1.0f);
-    gm.reason = s.reason;
-    gm.n_evals = s.n_evals;
-    gm.pad = 0;
-    games[gi % (unsigned long long)cfg.games_cap] = gm;
-    s.status = ST_IDLE;
-    if (cfg.recycle) {
-        const unsigned long long k = atomicAdd(&ctr->next_game, 1ull);
-        if ((long long)k < cfg.n_games) {
-            start_game(cfg, s, board, np_mt + (size_t)i * MT_WORDS, py_mt + (size_t)i * MT_WORDS, (long long)k);
-            atomicAdd(&ctr->active, 1);
+    if (tid == 0) {
+        // flush of a non-empty buffer (:202-208): one more forward call
+        if (cfg.sims == 0 && s.buf > 0) {
+            s.n_evals += 1;
+            if (cfg.seed_mode == KV_SEED_SEQUENTIAL) s.need_flush = 1;
         }
+        const unsigned long long gi = atomicAdd(&ctr->games_count, 1ull);
+        kv_game gm;
+        gm.game_id = s.game_id;
+        gm.plies = s.ply;
+        gm.outcome = s.outcome;
+        gm.reward = s.outcome == 1 ? 1.0f : (s.outcome == 0 ? 0.2f : -1.0f);
+        gm.reason = s.reason;
+        gm.n_evals = s.n_evals;
+        gm.pad = 0;
+        games[gi % (unsigned long long)cfg.games_cap] = gm;
+        s.status = ST_IDLE;
+        long long next = -1;
+        if (cfg.recycle) {
+            const unsigned long long k = atomicAdd(&ctr->next_game, 1ull);
+            if ((long long)k < cfg.n_games) {
+                next = (long long)k;
+                atomicAdd(&ctr->active, 1);
+            }
+        }
+        s_next = next;
     }
-    slots[i] = s;
+    __syncthreads();
+    const long long k = s_next;
+    if (k >= 0) {  // the slot starts game k: fields by thread 0, board + numpy stream by wave 0, CPython by wave 1
+        const long long gid = cfg.id_base + k * cfg.id_stride;
+        const unsigned long long sd = cfg.seed + (unsigned long long)gid;
+        if (wave == 0) {
+            board[lane] = kStart[lane];
+            if (cfg.seed_mode == KV_SEED_PER_GAME) wave_seed_genrand(np_mt + (size_t)i * MT_WORDS, (uint32_t)sd, lane);
+        } else if (cfg.seed_mode == KV_SEED_PER_GAME) {
+            wave_seed_python(py_mt + (size_t)i * MT_WORDS, sd, lane);
+        }
+        if (tid == 0) start_game_fields(cfg, s, gid);
+    }
+    if (tid == 0) slots[i] = s;
 }
 
 // the flush rows of sequential mode: boards [slots, 2*slots) = last appended board
@@ -500,7 +527,7 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
                 return rc;
         }
         KV_HIP(hipMemsetAsync(&e->ctr->active, 0, sizeof(int), e->st));
-        hipLaunchKernelGGL(kv::k_finish, dim3(S), dim3(64), 0, e->st, e->dc, e->slots, e->boards,
+        hipLaunchKernelGGL(kv::k_finish, dim3(S), dim3(128), 0, e->st, e->dc, e->slots, e->boards,
                            e->moves, e->np_mt, e->py_mt, e->games, e->ctr);
         KV_HIP(hipGetLastError());
         ++done;

@@ -74,6 +74,94 @@ __host__ __device__ inline void mt_seed_python(uint32_t* mt, uint64_t seed) {
     mt_seed_by_array(mt, key, n);
 }
 
+// Wave-level seeding (one 64-lane wave, every lane calls): the same words as
+// mt_seed_genrand / mt_seed_python. The recurrences are serial, so the chain
+// runs on wave-uniform values (scalar ALU) and each word is parked with
+// v_writelane in lane (i & 63) of register i >> 6; the state is then written
+// to global memory with coalesced stores. No memory round trip sits on the
+// chain: k_finish (which seeds every recycled slot) went from 115 to 55 us
+// per step at 256 slots (rocprofv3, reference move selection).
+constexpr int MT_REGS = (MT_N + 63) / 64;  // 10
+
+// v_writelane: word x into lane l of r (x wave-uniform)
+__device__ inline uint32_t put_lane(uint32_t r, uint32_t x, int l) { return (int)__lane_id() == l ? x : r; }
+
+__device__ inline void wave_mt_store(const uint32_t (&r)[MT_REGS], uint32_t* g, int lane) {
+#pragma unroll
+    for (int m = 0; m < MT_REGS; ++m)
+        if (m * 64 + lane < MT_N) g[m * 64 + lane] = r[m];
+    if (lane == 0) g[MT_N] = MT_N;
+}
+
+__device__ inline void wave_seed_genrand(uint32_t* g, uint32_t s, int lane) {
+    uint32_t r[MT_REGS] = {};
+    uint32_t x = __builtin_amdgcn_readfirstlane(s);
+    (void)lane;
+#pragma unroll
+    for (int m = 0; m < MT_REGS; ++m) {
+        const int lend = m == MT_REGS - 1 ? MT_N - 64 * m : 64;
+        for (int l = 0; l < lend; ++l) {
+            const int i = m * 64 + l;
+            if (i > 0) x = 1812433253U * (x ^ (x >> 30)) + (uint32_t)i;
+            r[m] = put_lane(r[m], x, l);
+        }
+    }
+    wave_mt_store(r, g, lane);
+}
+
+// init_genrand(19650218): the words init_by_array starts from, the same for every seed
+struct MtInit19650218 {
+    uint32_t v[MT_N];
+    constexpr MtInit19650218() : v() {
+        v[0] = 19650218U;
+        for (int i = 1; i < MT_N; ++i) v[i] = 1812433253U * (v[i - 1] ^ (v[i - 1] >> 30)) + (uint32_t)i;
+    }
+};
+__constant__ constexpr MtInit19650218 kMtInitPy{};
+
+__device__ inline void wave_seed_python(uint32_t* g, uint64_t seed, int lane) {
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane((uint32_t)seed);
+    const uint32_t k1 = __builtin_amdgcn_readfirstlane((uint32_t)(seed >> 32));
+    const int len = k1 ? 2 : 1;
+    uint32_t r[MT_REGS] = {};
+    // init_by_array pass 1 (mt_seed_by_array's first loop, i = 1..623), fused with
+    // the init_genrand(19650218) words it reads
+    uint32_t prev = 19650218U;
+    int j = 0;
+#pragma unroll
+    for (int m = 0; m < MT_REGS; ++m) {
+        const int lend = m == MT_REGS - 1 ? MT_N - 64 * m : 64;
+        for (int l = (m == 0 ? 1 : 0); l < lend; ++l) {
+            const int i = m * 64 + l;
+            const uint32_t gi = kMtInitPy.v[i];
+            const uint32_t cur = (gi ^ ((prev ^ (prev >> 30)) * 1664525U)) + (j ? k1 : k0) + (uint32_t)j;
+            r[m] = put_lane(r[m], cur, l);
+            prev = cur;
+            if (++j >= len) j = 0;
+        }
+    }
+    // the 624th iteration after the wrap: mt[0] = mt[623], i = 1
+    uint32_t cur = (__builtin_amdgcn_readlane(r[0], 1) ^ ((prev ^ (prev >> 30)) * 1664525U)) + (j ? k1 : k0) +
+                   (uint32_t)j;
+    r[0] = put_lane(r[0], cur, 1);
+    prev = cur;
+    // pass 2: i = 2..623, then the wrap and i = 1
+#pragma unroll
+    for (int m = 0; m < MT_REGS; ++m) {
+        const int lend = m == MT_REGS - 1 ? MT_N - 64 * m : 64;
+        for (int l = (m == 0 ? 2 : 0); l < lend; ++l) {
+            const int i = m * 64 + l;
+            cur = (__builtin_amdgcn_readlane(r[m], l) ^ ((prev ^ (prev >> 30)) * 1566083941U)) - (uint32_t)i;
+            r[m] = put_lane(r[m], cur, l);
+            prev = cur;
+        }
+    }
+    cur = (__builtin_amdgcn_readlane(r[0], 1) ^ ((prev ^ (prev >> 30)) * 1566083941U)) - 1U;
+    r[0] = put_lane(r[0], cur, 1);
+    r[0] = put_lane(r[0], 0x80000000U, 0);
+    wave_mt_store(r, g, lane);
+}
+
 __host__ __device__ inline void mt_twist_serial(uint32_t* mt) {
     int kk;
     for (kk = 0; kk < MT_N - MT_M; ++kk) mt[kk] = mt_mix(mt[kk], mt[kk + 1], mt[kk + MT_M]);
