@@ -32,6 +32,7 @@ sys.path.insert(0, HERE)
 FLOP_PER_EVAL = 3175744512            # SURVEY.md 8d, ChessNet forward per position
 FLOP_RES_CONV_PER_BOARD = 301989888   # one 3x3 512->512 conv on 8x8 (2*64*512*4608)
 FLOP_WINO_GEMM_PER_BOARD = 75497472   # its Winograd F(4x4,3x3) GEMMs: 2 * 4 tiles * 36 * 512 * 512
+FLOP_WINO48_GEMM_PER_BOARD = 62914560  # its Winograd F(4x8,3x3) GEMMs: 2 * 2 tiles * 60 * 512 * 512
 FP32_MFMA_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md, f32-input MFMA (dense)
 BF16_MFMA_PEAK_TFLOPS = 2500.0        # dense bf16 MFMA
 
@@ -45,8 +46,8 @@ def parse():
     ap.add_argument("--slots", type=int, default=256)
     ap.add_argument("--sims", type=int, default=400)
     ap.add_argument("--precision", choices=["fp32", "f16x3", "bf16x6", "bf16x3"], default="fp32")
-    ap.add_argument("--algo", choices=["auto", "direct", "winograd"], default="auto",
-                    help="conv algorithm of the fp32 tower (auto: Winograd F(4x4,3x3) above 16 boards)")
+    ap.add_argument("--algo", choices=["auto", "direct", "winograd", "winograd48"], default="auto",
+                    help="conv algorithm of the fp32 tower (auto: Winograd F(4x8,3x3) above 16 boards)")
     ap.add_argument("--compare-direct", type=int, default=1,
                     help="also measure the fp32 direct implicit-GEMM convs (reported under 'fp32_direct')")
     ap.add_argument("--alt-precision", default="f16x3",
@@ -169,8 +170,11 @@ def main():
         # 1,200 warm-up ply-steps fill the slots with games at every stage, the 2,400 timed ones complete
         # games at the steady-state rate
         refsel = measure(args.precision, sims=0, steps=2400, warmup=1200)
+    wino44 = None
+    if args.compare_direct and args.precision == "fp32" and m["dom_algo"] == 3:
+        wino44 = measure("fp32", "winograd")
     direct = None
-    if args.compare_direct and args.precision == "fp32" and m["dom_algo"] == 2:
+    if args.compare_direct and args.precision == "fp32" and m["dom_algo"] in (2, 3):
         direct = measure("fp32", "direct")
 
     # experience gather (RCCL all-gather of packed records), outside `value`
@@ -186,21 +190,30 @@ def main():
 
     # roofline of the dominant kernel, timed with HIP events on the engine stream: the residual-tower
     # Winograd GEMM launch (36 x [4*boards x 512 x 512]) or, for the direct algorithm, the residual conv
-    wino = m["dom_algo"] == 2
-    # boards one measured launch covers (the Winograd tower may run the batch as two halves on two streams);
-    # padding rows are not algorithmic work
-    per_board = FLOP_WINO_GEMM_PER_BOARD if wino else FLOP_RES_CONV_PER_BOARD
+    algo = m["dom_algo"]  # 1 direct, 2 Winograd F(4x4), 3 Winograd F(4x8)
+    wino = algo in (2, 3)
+    # boards one measured launch covers; padding rows are not algorithmic work
+    per_board = {2: FLOP_WINO_GEMM_PER_BOARD, 3: FLOP_WINO48_GEMM_PER_BOARD}.get(algo, FLOP_RES_CONV_PER_BOARD)
     bpl = min(G, int(round(m["dom_flop"] / per_board))) if m["dom_flop"] else G
     flop_alg = per_board * bpl
     achieved = flop_alg / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
-    # the library picks the GEMM tile by batch (knightvision_amd/csrc/kv_nn.hip launch_wino_gemm)
-    kname = (("wino_gemm_kernel<512,2,2,1,2,16>" if bpl * 4 <= 1024 else "wino_gemm_kernel<512,4,2,1,2,32>")
-             if wino else "conv3x3_kernel<512,32>")
+    # the library picks the GEMM tile by rows (knightvision_amd/csrc/kv_nn.hip launch_wino_gemm / launch_wino48_gemm)
+    pad = (bpl + 31) // 32 * 32
+    if algo == 3:
+        kname = ("wino_gemm_kernel<512,4,2,1,2,32,60>" if (pad * 2) % 128 == 0
+                 else "wino_gemm_kernel<512,2,2,1,2,16,60>")
+        kdesc = " (residual-tower Winograd F(4x8,3x3) GEMMs, 60 points)"
+    elif algo == 2:
+        kname = "wino_gemm_kernel<512,2,2,1,2,16,36>" if pad * 4 <= 1024 else "wino_gemm_kernel<512,4,2,1,2,32,36>"
+        kdesc = " (residual-tower Winograd F(4x4,3x3) GEMMs)"
+    else:
+        kname, kdesc = "conv3x3_kernel<512,32>", " (residual-tower 3x3 conv, implicit GEMM)"
     traffic = None
-    pmc = os.path.join(HERE, "profiles", "r01_pmc_wino_gemm.json" if wino else "r01_pmc_resconv.json")
+    pmc = os.path.join(HERE, "profiles", {2: "r01_pmc_wino_gemm.json", 3: "r01_pmc_wino48_gemm.json"}
+                       .get(algo, "r01_pmc_resconv.json"))
     if os.path.exists(pmc):
         pj = json.load(open(pmc))
-        if pj.get("batch") == bpl and pj.get("kernel", "").split("<")[0] == kname.split("<")[0]:
+        if pj.get("batch") == bpl and pj.get("kernel", "").replace(" ", "") == kname:
             traffic = pj.get("hbm_bytes_per_launch")
 
     # HBM side of the search (north_star: tree kernels as a fraction of the HBM roofline), from the
@@ -241,8 +254,7 @@ def main():
             "nn_tflops": nn_rows * FLOP_PER_EVAL / dt / 1e12, "gather_ms": gather_ms,
             "records_gathered": int(len(recs_all)),
             "roofline": {"bound": "mfma",
-                         "kernel": kname + (" (residual-tower Winograd F(4x4,3x3) GEMMs)" if wino
-                                            else " (residual-tower 3x3 conv, implicit GEMM)"),
+                         "kernel": kname + kdesc,
                          "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic, "avg_launch_ms": conv_ms, "boards_per_launch": bpl,
@@ -260,6 +272,13 @@ def main():
                 "ms_per_step": direct["dt"] * 1e3 / steps,
                 "res_conv_avg_launch_ms": direct["conv_ms"], "res_conv_tflops": d_ach,
                 "res_conv_frac": (d_ach / FP32_MFMA_PEAK_TFLOPS) if d_ach else None}
+        if wino44 is not None:
+            w_ach = (FLOP_WINO_GEMM_PER_BOARD * G / (wino44["conv_ms"] * 1e-3) / 1e12) if wino44["conv_ms"] > 0 else None
+            out["fp32_winograd44"] = {
+                "note": "same fp32 network with the Winograd F(4x4,3x3) tower (36 points, 4 tiles per board)",
+                "value": (wino44["sims"] if mcts else wino44["plies"]) / wino44["dt"], "unit": unit,
+                "ms_per_step": wino44["dt"] * 1e3 / steps, "res_gemm_avg_launch_ms": wino44["conv_ms"],
+                "res_gemm_tflops": w_ach, "res_gemm_frac": (w_ach / FP32_MFMA_PEAK_TFLOPS) if w_ach else None}
         if alt is not None:
             # dominant launch of the alternate run (Winograd GEMM or direct residual conv), fp32-equivalent FLOPs
             a_ach = (alt["dom_flop"] / (alt["conv_ms"] * 1e-3) / 1e12) if alt["conv_ms"] > 0 else None

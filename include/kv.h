@@ -78,14 +78,19 @@ int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv);
 #define KV_PREC_F16X3 3
 int kv_net_set_precision(kv_net* net, int precision);
 /* Algorithm of the fp32 3x3 convs with Cin 256/512:
- * KV_ALGO_AUTO      Winograd for batches > 16 boards, direct (split-K) below
+ * KV_ALGO_AUTO      Winograd for batches > 16 boards (F(4x8) in fp32, F(4x4)
+ *                   for the split precisions), direct (split-K) below
  * KV_ALGO_DIRECT    implicit GEMM over the 9 taps (exact fp32 products)
  * KV_ALGO_WINOGRAD  F(4x4,3x3): 36 GEMMs of 4 tiles x Cin x Cout per board, 4x
  *                   fewer FLOPs, fp32 transforms (logits within 1e-4)
+ * KV_ALGO_WINOGRAD48 F(4x8,3x3): 60 GEMMs of 2 tiles x Cin x Cout per board,
+ *                   4.8x fewer FLOPs than direct (fp32 only; the split
+ *                   precisions run F(4x4) under this setting)
  * Results are batch-invariant inside a class (<= 16 boards, > 16 boards). */
 #define KV_ALGO_AUTO 0
 #define KV_ALGO_DIRECT 1
 #define KV_ALGO_WINOGRAD 2
+#define KV_ALGO_WINOGRAD48 3
 int kv_net_set_algo(kv_net* net, int algo);
 int kv_net_set_timing(kv_net* net, int enable);
 void kv_net_destroy(kv_net* net);
@@ -155,7 +160,7 @@ typedef struct {
     int64_t res_conv_launches;
     double step_ms;       /* wall time inside kv_run */
     double dom_flop;      /* MFMA FLOPs of one measured launch (padded rows included) */
-    int64_t dom_algo;     /* KV_ALGO_DIRECT or KV_ALGO_WINOGRAD for those launches */
+    int64_t dom_algo;     /* KV_ALGO_DIRECT, KV_ALGO_WINOGRAD or KV_ALGO_WINOGRAD48 for those launches */
 } kv_stats;
 
 typedef struct kv_engine kv_engine;

@@ -20,6 +20,7 @@
 
 #include "kv_common.h"
 #include "kv_wino.h"
+#include "kv_wino48.h"
 
 namespace kv {
 
@@ -571,7 +572,7 @@ __global__ void encode_boards_kernel(const int8_t* __restrict__ boards, int nb, 
 // LDS; wave w computes pixels 16w..16w+15. WINO: the activated 8x8 plane goes through
 // LDS to the four tile waves, which write conv2's Winograd input transform
 // (V [36][rows][256]); else NHWC T [board][64][256].
-template <bool WINO>
+template <int WINO>  // 0: NHWC out, 1: F(4x4) V of conv2, 2: F(4x8) V of conv2
 __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ boards, int nb,
                                                    const float* __restrict__ wT, const float* __restrict__ scale,
                                                    const float* __restrict__ shift, float* __restrict__ out,
@@ -609,6 +610,19 @@ __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ bo
     }
     if (!WINO) return;
     __syncthreads();
+    if (WINO == 2) {  // waves 0, 1 = the two 4x8 tiles
+        if (w >= 2) return;
+        float d48[60];
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = 0; j < 10; ++j) {
+                const int yy = w * 4 - 1 + i, xx = j - 1;
+                d48[i * 10 + j] = (yy >= 0 && yy < 8 && xx >= 0 && xx < 8) ? plane[yy * 8 + xx][cl] : 0.f;
+            }
+        wino48_input_tile(d48, out, ((size_t)b * 2 + w) * 256 + c, (size_t)rows * 256);
+        return;
+    }
     const int y0 = (w >> 1) * 4 - 1, x0 = (w & 1) * 4 - 1;
     float d[36];
 #pragma unroll
@@ -671,6 +685,8 @@ struct kv_net {
     float* slab = nullptr;  // split-K partial sums (small batches)
     int algo = KV_ALGO_AUTO;
     float* U = nullptr;     // Winograd weights [36][Cout][Cin] of convs 1..11
+    float* U48 = nullptr;   // F(4x8) weights [60][Cout][Cin] of convs 1..11
+    size_t uoff48[12] = {};
     uint16_t* Up[3] = {};   // the same split into bf16 h / m / l (KV_PREC_BF16X6)
     uint16_t* Uf[2] = {};   // fp16 pieces of U * 2^ut[l] (KV_PREC_F16X3)
     int ut[12] = {};
@@ -764,8 +780,13 @@ static int launch_conv(const float* in, const float* w, const float* sc, const f
 // Winograd for the fp32 tower when the batch is past the split-K class
 static bool use_wino(const kv_net* net, int B) {
     if (net->precision == KV_PREC_BF16X3) return false;
-    if (net->algo == KV_ALGO_WINOGRAD) return true;
+    if (net->algo == KV_ALGO_WINOGRAD || net->algo == KV_ALGO_WINOGRAD48) return true;
     return net->algo == KV_ALGO_AUTO && B > kSplitMaxBoards;
+}
+
+// the F(4x8) variant: fp32 only (AUTO and WINOGRAD48); the split precisions keep F(4x4)
+static bool use_wino48(const kv_net* net, int B) {
+    return use_wino(net, B) && net->precision == KV_PREC_FP32 && net->algo != KV_ALGO_WINOGRAD;
 }
 
 // padded batch: a multiple of 4 boards (direct tiles) or 32 (128-row GEMM tiles)
@@ -796,20 +817,20 @@ static int net_reserve(kv_net* net, int nb_pad) {
 static int net_heads(kv_net* net, int nb, float* policy, float* value, hipStream_t st);
 
 // LDS_PAD: dynamic LDS requested beyond the tiles' need, to cap workgroups per CU
-template <int K, int WR, int WC, int MT, int NT, int CK = 32, int LDS_PAD = 0>
+template <int K, int WR, int WC, int MT, int NT, int CK = 32, int LDS_PAD = 0, int XI = kv::WN_XI>
 static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
     using T = kv::WinoTile<WR, WC, MT, NT, CK>;
     constexpr size_t bytes = T::BYTES + LDS_PAD;
     static bool attr_set = false;
     if (!attr_set) {
-        KV_HIP(hipFuncSetAttribute((const void*)kv::wino_gemm_kernel<K, WR, WC, MT, NT, CK>,
+        KV_HIP(hipFuncSetAttribute((const void*)kv::wino_gemm_kernel<K, WR, WC, MT, NT, CK, XI>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
         attr_set = true;
     }
-    const int nwg = kv::WN_XI * (rows / T::WM) * (512 / T::WN);
+    const int nwg = XI * (rows / T::WM) * (512 / T::WN);
     KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0, KV_EINVAL, "wino gemm: rows %d vs tile %d", rows, T::WM);
-    hipLaunchKernelGGL((kv::wino_gemm_kernel<K, WR, WC, MT, NT, CK>), dim3(nwg), dim3(T::THREADS), bytes, st, V, U,
-                       M, rows, 512, stride);
+    hipLaunchKernelGGL((kv::wino_gemm_kernel<K, WR, WC, MT, NT, CK, XI>), dim3(nwg), dim3(T::THREADS), bytes, st, V,
+                       U, M, rows, 512, stride);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -827,6 +848,14 @@ static int launch_wino_gemm(const float* V, const float* U, float* M, int rows, 
     if (rows <= 1024)  // 64 x 128, 4 waves of 32x64, k-tiles of 16, LDS padded to 48 KB -> 3 per CU
         return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720>(V, U, M, rows, stride, st);
     return launch_wino_gemm_t<K, 4, 2, 1, 2>(V, U, M, rows, stride, st);  // 128 x 128, 8 waves, 2 per CU
+}
+
+// F(4x8) GEMMs (60 points, rows = 2 per board): 128x128 tiles (8 waves, 2 per CU) when
+// the rows allow, else 64x128 (3 per CU); same k order, same bits
+template <int K>
+static int launch_wino48_gemm(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
+    if (rows % 128 == 0) return launch_wino_gemm_t<K, 4, 2, 1, 2, 32, 0, kv::W48_XI>(V, U, M, rows, stride, st);
+    return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720, kv::W48_XI>(V, U, M, rows, stride, st);
 }
 
 template <int K, int TM>
@@ -931,11 +960,59 @@ static int wino_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     return KV_OK;
 }
 
+template <bool RESID, bool WRITE_Y, bool NEXT_V>
+static int launch_wino48_out(kv_net* net, int l, const float* M, int nb, int stride, const float* resid, float* Y,
+                             float* Vn, hipStream_t st) {
+    const float* W = net->w;
+    hipLaunchKernelGGL((kv::wino48_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 64, nb), dim3(128), 0, st, M,
+                       stride, W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+// conv2 + the 5 residual blocks for boards [0, nb), F(4x8)
+static int wino48_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
+    const int rows = nb * 2, stride = rows;
+    float* V = net->V;
+    float* M = net->Mw;
+    int rc;
+    if ((rc = launch_wino48_gemm<256>(net->V256, net->U48 + net->uoff48[1], M, rows, stride, st))) return rc;
+    if ((rc = launch_wino48_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st))) return rc;
+    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
+    for (int r = 0; r < 5; ++r) {
+        const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
+        const bool m = mark && r == 2;  // one representative residual GEMM for the engine's timing hook
+        if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
+        if ((rc = launch_wino48_gemm<512>(V, net->U48 + net->uoff48[l1], M, rows, stride, st))) return rc;
+        if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
+        if ((rc = launch_wino48_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st))) return rc;
+        if ((rc = launch_wino48_gemm<512>(V, net->U48 + net->uoff48[l2], M, rows, stride, st))) return rc;
+        rc = r < 4 ? launch_wino48_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
+                   : launch_wino48_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
+        if (rc) return rc;
+    }
+    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
+    return KV_OK;
+}
+
 // Winograd tower: conv2 and the 5 residual blocks (conv1 output in net->T,
 // or conv2's input transform already in net->V256 when v256_ready)
 static int net_tower_wino(kv_net* net, int nb_pad, bool v256_ready, hipStream_t st) {
-    const int rows = nb_pad * 4;
     int rc;
+    if (use_wino48(net, nb_pad)) {
+        const int rows48 = nb_pad * 2;
+        if (!v256_ready) {
+            hipLaunchKernelGGL(kv::wino48_in_kernel<256>, dim3(256 / 64, nb_pad), dim3(128), 0, st, net->T, rows48,
+                               net->V256);
+            KV_HIP(hipGetLastError());
+        }
+        if ((rc = wino48_blocks(net, nb_pad, true, st))) return rc;
+        net->dom_flop = 2.0 * kv::W48_XI * rows48 * 512.0 * 512.0;
+        net->dom_algo = KV_ALGO_WINOGRAD48;
+        net->dom_launches = 1;
+        return KV_OK;
+    }
+    const int rows = nb_pad * 4;
     if (!v256_ready) {
         hipLaunchKernelGGL(kv::wino_in_kernel<256>, dim3(256 / 64, nb_pad), dim3(256), 0, st, net->T, rows,
                            net->V256, net_vmax(net, 1));
@@ -961,11 +1038,14 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     if (wino && net->precision == KV_PREC_F16X3)
         KV_HIP(hipMemsetAsync(net->vmax, 0, (size_t)12 * net->cap * sizeof(unsigned), st));
     if (boards) {
-        if (wino)
-            hipLaunchKernelGGL(kv::stem_kernel<true>, dim3(4, nb_pad), dim3(256), 0, st, boards, nb, net->stemT,
+        if (wino && use_wino48(net, nb))
+            hipLaunchKernelGGL(kv::stem_kernel<2>, dim3(4, nb_pad), dim3(256), 0, st, boards, nb, net->stemT,
+                               W + o.scale[0], W + o.shift[0], net->V256, nb_pad * 2, nullptr);
+        else if (wino)
+            hipLaunchKernelGGL(kv::stem_kernel<1>, dim3(4, nb_pad), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], net->V256, nb_pad * 4, net_vmax(net, 1));
         else
-            hipLaunchKernelGGL(kv::stem_kernel<false>, dim3(4, nb_pad), dim3(256), 0, st, boards, nb, net->stemT,
+            hipLaunchKernelGGL(kv::stem_kernel<0>, dim3(4, nb_pad), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], net->T, nb_pad * 4, nullptr);
         KV_HIP(hipGetLastError());
     } else if ((rc = launch_conv<16, 16, false>(net->x16, W + o.w[0], W + o.scale[0], W + o.shift[0], nullptr,
@@ -1082,6 +1162,20 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
                            net->w + net->off.w[l], kv::kConv[l].cout, kv::kConv[l].cin, net->U + net->uoff[l]);
         KV_HIP(hipGetLastError());
     }
+    if (!net->U48) {
+        size_t tot = 0;
+        for (int l = 1; l < 12; ++l) {
+            net->uoff48[l] = tot;
+            tot += (size_t)kv::W48_XI * kv::kConv[l].cout * kv::kConv[l].cin;
+        }
+        KV_HIP(hipMalloc(&net->U48, tot * sizeof(float)));
+    }
+    for (int l = 1; l < 12; ++l) {
+        const size_t n = (size_t)kv::kConv[l].cout * kv::kConv[l].cin;
+        hipLaunchKernelGGL(kv::wino48_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0,
+                           net->w + net->off.w[l], kv::kConv[l].cout, kv::kConv[l].cin, net->U48 + net->uoff48[l]);
+        KV_HIP(hipGetLastError());
+    }
     hipLaunchKernelGGL(kv::split3_kernel, dim3((unsigned)((net->utot + 255) / 256)), dim3(256), 0, 0, net->U,
                        net->utot, net->Up[0], net->Up[1], net->Up[2]);
     KV_HIP(hipGetLastError());
@@ -1121,7 +1215,9 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
 
 int kv_net_set_algo(kv_net* net, int algo) {
     KV_REQUIRE(net, KV_EINVAL, "kv_net_set_algo: NULL");
-    KV_REQUIRE(algo == KV_ALGO_AUTO || algo == KV_ALGO_DIRECT || algo == KV_ALGO_WINOGRAD, KV_EINVAL,
+    KV_REQUIRE(algo == KV_ALGO_AUTO || algo == KV_ALGO_DIRECT || algo == KV_ALGO_WINOGRAD ||
+                   algo == KV_ALGO_WINOGRAD48,
+               KV_EINVAL,
                "kv_net_set_algo: unknown algo %d", algo);
     net->algo = algo;
     return KV_OK;
@@ -1189,6 +1285,7 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->T);
     (void)hipFree(net->pfeat);
     (void)hipFree(net->U);
+    (void)hipFree(net->U48);
     (void)hipFree(net->stemT);
     for (int p = 0; p < 3; ++p) (void)hipFree(net->Up[p]);
     for (int p = 0; p < 2; ++p) (void)hipFree(net->Uf[p]);

@@ -220,7 +220,7 @@ struct WinoTile {
     static constexpr size_t BYTES = (size_t)(2 * WM * PS + 2 * WN * PS) * 4;
 };
 
-template <int K, int WR, int WC, int MT, int NT, int CK = 32>
+template <int K, int WR, int WC, int MT, int NT, int CK = 32, int XI = WN_XI>
 __global__ __launch_bounds__(WR * WC * 64) void wino_gemm_kernel(const float* __restrict__ V,
                                                                    const float* __restrict__ U,
                                                                    float* __restrict__ M, int rows, int cout,
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(WR * WC * 64) void wino_gemm_kernel(const float* __
     // order -- the 4 column tiles of a row panel and the row panels of one xi
     // run on one XCD and re-read V / U from its L2 instead of HBM.
     const int CT = cout / WN, RT = rows / WM;
-    const int nwg = WN_XI * RT * CT;  // a multiple of 8 (36 * 4 * RT)
+    const int nwg = XI * RT * CT;  // a multiple of 8 (36 or 60 points x 4 column tiles x RT)
     const int idx = (int)(blockIdx.x & 7) * (nwg >> 3) + (int)(blockIdx.x >> 3);
     const int xi = idx / (CT * RT);
     const int n_base = (idx % CT) * WN;

@@ -3,7 +3,8 @@
 
   * slot-count invariance: with per-game seeds a game's trajectory depends only
     on its seed and on the network rows of its own boards, and the Winograd
-    tower is batch-invariant bit for bit (tests/test_nn_gpu.py), so the first
+    towers (F(4x8), the fp32 default, and F(4x4)) are batch-invariant bit for
+    bit (tests/test_nn_gpu.py), so the first
     16 games of a 256- or 2,048-slot run must equal a 16-slot run move for move;
   * every recorded game replays legally on the oracle rules from the start
     position, record boards equal the replayed boards, and the recorded end
@@ -22,9 +23,9 @@ pytestmark = pytest.mark.gpu
 SD = synthetic_state_dict(42, "init")
 
 
-def _run(slots, n_games, sims, max_moves, steps=-1):
+def _run(slots, n_games, sims, max_moves, steps=-1, algo="winograd48"):
     with SelfPlayEngine(SD, slots=slots, n_games=n_games, seed=42, max_moves=max_moves, batch=16, sims=sims,
-                        algo="winograd") as eng:
+                        algo=algo) as eng:
         eng.run(steps)
         return eng.records(), eng.games(), eng.stats()
 
@@ -75,10 +76,11 @@ def test_c3_2048x800_one_move():
         _replay(by[g][0], by[g][1], None)
 
 
-def test_c2_256x400_three_moves():
-    big = _run(256, 256, 400, 3)
+@pytest.mark.parametrize("algo", ["winograd48", "winograd"])
+def test_c2_256x400_three_moves(algo):
+    big = _run(256, 256, 400, 3, algo=algo)
     assert big[2]["sims"] == 256 * 3 * 400 and len(big[1]) == 256
-    small = _run(16, 16, 400, 3)
+    small = _run(16, 16, 400, 3, algo=algo)
     _same_first_games(big, small, 16)
     by = records_by_game(big[0], big[1])
     for g in range(256):

@@ -13,8 +13,10 @@ pytestmark = pytest.mark.gpu
 TOL_P, TOL_V = 1e-4, 1e-5
 
 
-# (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x4,3x3) / bf16x6 Winograd / bf16x3 direct
-MODES = [("fp32", "direct"), ("fp32", "winograd"), ("f16x3", "winograd"), ("bf16x6", "winograd"), ("bf16x3", "auto")]
+# (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x4,3x3) / fp32 Winograd F(4x8,3x3) (the fp32
+# default above 16 boards) / f16x3 and bf16x6 Winograd F(4x4) / bf16x3 direct
+MODES = [("fp32", "direct"), ("fp32", "winograd"), ("fp32", "winograd48"), ("f16x3", "winograd"),
+         ("bf16x6", "winograd"), ("bf16x3", "auto")]
 
 
 def _net(variant, precision="fp32", algo="auto"):

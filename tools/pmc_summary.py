@@ -2,7 +2,7 @@
 (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts half of a wide
 coalesced read, MI355X_MICROARCH.md HBM section).
 
-    python tools/pmc_summary.py FETCH_GLOB WRITE_GLOB BATCH [resconv|wino_gemm]
+    python tools/pmc_summary.py FETCH_GLOB WRITE_GLOB BATCH [resconv|wino_gemm|wino48_gemm]
 """
 import csv
 import glob
@@ -11,7 +11,8 @@ import sys
 
 KERNELS = {
     "resconv": ("conv3x3_kernel<512,32", "conv3x3_kernel<512,32,*>"),
-    "wino_gemm": ("wino_gemm_kernel<512,", "wino_gemm_kernel<512,2,2,1,2,16>"),
+    "wino_gemm": ("wino_gemm_kernel<512,2,2,1,2,16,36>", "wino_gemm_kernel<512,2,2,1,2,16,36>"),
+    "wino48_gemm": ("wino_gemm_kernel<512,4,2,1,2,32,60>", "wino_gemm_kernel<512,4,2,1,2,32,60>"),
 }
 
 
@@ -27,8 +28,8 @@ def load(pattern, counter, sub):
 def algorithmic_bytes(kind, B):
     if kind == "resconv":  # activations in + out, weights once
         return B * 64 * 512 * 4 * 2 + 512 * 9 * 512 * 4
-    rows = 4 * B  # V read + M write over the 36 GEMMs, U once
-    return 36 * rows * 512 * 4 * 2 + 36 * 512 * 512 * 4
+    xi, rows = (60, 2 * B) if kind == "wino48_gemm" else (36, 4 * B)  # V read + M write over the GEMMs, U once
+    return xi * rows * 512 * 4 * 2 + xi * 512 * 512 * 4
 
 
 def main():
