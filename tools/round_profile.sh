@@ -17,4 +17,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/trace -o bench -- pytho
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "wino_gemm|conv3x3" -f csv -d $O/pmc_fetch -o f -- python3 $R/tools/nn_speed.py 256 > $O/pmc_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "wino_gemm|conv3x3" -f csv -d $O/pmc_write -o w -- python3 $R/tools/nn_speed.py 256 > $O/pmc_write.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "wino_gemm|conv3x3" -f csv -d $O/pmc_sq -o s -- python3 $R/tools/nn_speed.py 256 > $O/pmc_sq.log 2>&1
+
+cd $R
+timeout -k 10 300 python -u -m pytest tests/test_nn_gpu.py -q -s -k "golden" --timeout 200 --timeout-method thread > $O/nn_errors.log 2>&1
 echo done
