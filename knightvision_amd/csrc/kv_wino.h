@@ -176,6 +176,12 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
         for (int i = 0; i < 4; ++i) tmp[i][j] = o[i];
     }
     const int y0 = (t >> 1) * 4, x0 = (t & 1) * 4;
+    // the residual is read in full before Y is written: they alias (in place), so
+    // loads interleaved with the stores could not be issued ahead of them
+    float res[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+        res[q] = RESID ? resid[((size_t)b * 64 + (y0 + q / 4) * 8 + x0 + q % 4) * C + c] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         float o[4];
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(256) void wino_out_kernel(const float* __restrict__
             const int p = (y0 + i) * 8 + x0 + j;
             const size_t idx = ((size_t)b * 64 + p) * C + c;
             float v = o[j] * sc + sh;
-            if (RESID) v += resid[idx];
+            if (RESID) v += res[i * 4 + j];
             v = v > 0.f ? v : 0.f;
             if (WRITE_Y) Y[idx] = v;
             if (NEXT_V) plane[p][cl] = v;
