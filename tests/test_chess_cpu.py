@@ -182,8 +182,9 @@ def _planes_by_hand(fen):
     return t
 
 
-def test_datasets(tmp_path):
+def test_datasets(tmp_path, monkeypatch):
     from knightvision_amd.data_utils import parser_pgn
+    monkeypatch.setattr(parser_pgn, "ZST_LOG", str(tmp_path / "zst.log"))
     from knightvision_amd.data_utils.dataset import ChessDataset
     from knightvision_amd.train import ChessPGNDataset
     (tmp_path / "a.pgn").write_text(PGN)
