@@ -27,6 +27,31 @@ PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "f16x3": 3}
 ALGOS = {"auto": 0, "direct": 1, "winograd": 2, "winograd48": 3}
 
 
+def batch_norm_rows(bn: nn.BatchNorm2d, x, n_real=None):
+    """Training-mode BatchNorm2d whose batch statistics (and running-statistics
+    update) cover only the first n_real rows -- the rows after them are padding
+    that gives the update step a bucketed batch shape (knightvision_amd.train);
+    those rows are normalised with the real rows' statistics and carry no loss.
+    n_real None / = batch: the module itself."""
+    if n_real is None or n_real >= x.shape[0] or not bn.training:
+        return bn(x)
+    acc = torch.float32 if x.dtype in (torch.float16, torch.bfloat16) else x.dtype  # statistics at >= fp32
+    xr = x[:n_real].to(acc)
+    mean = xr.mean(dim=(0, 2, 3))
+    var = xr.var(dim=(0, 2, 3), unbiased=False)
+    if bn.track_running_stats:
+        with torch.no_grad():
+            cnt = xr.numel() // xr.shape[1]
+            bn.num_batches_tracked.add_(1)
+            mom = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
+            bn.running_mean.mul_(1 - mom).add_(mom * mean)
+            bn.running_var.mul_(1 - mom).add_(mom * var * (cnt / max(cnt - 1, 1)))
+    inv = torch.rsqrt(var + bn.eps)
+    y = (x.to(acc) - mean[None, :, None, None]) * (inv * bn.weight.to(acc))[None, :, None, None] \
+        + bn.bias.to(acc)[None, :, None, None]
+    return y.to(x.dtype)
+
+
 class ResidualBlock(nn.Module):
     """One residual block (ai/model.py:8-25). Its own forward is the training
     path only; evaluation runs the whole tower in libkv.so."""
@@ -38,8 +63,9 @@ class ResidualBlock(nn.Module):
         self.conv2 = nn.Conv2d(channels, channels, kernel_size=3, padding=1)
         self.bn2 = nn.BatchNorm2d(channels)
 
-    def forward(self, x):
-        y = self.bn2(self.conv2(F.relu(self.bn1(self.conv1(x)))))
+    def forward(self, x, n_real=None):
+        y = batch_norm_rows(self.bn1, self.conv1(x), n_real)
+        y = batch_norm_rows(self.bn2, self.conv2(F.relu(y)), n_real)
         return F.relu(y + x)
 
 
@@ -136,25 +162,30 @@ class ChessNet(nn.Module):
             self._kv_key = key
         return self._kv
 
-    def _train_forward(self, x):
+    supports_row_padding = True  # training forward takes n_real (knightvision_amd.train bucketing)
+
+    def _train_forward(self, x, n_real=None):
         """Training mode (ai/model.py:51-77 with batch-statistics BatchNorm):
         PyTorch-ROCm autograd over the same parameters, for train.py's update
-        step (knightvision_amd.train). Evaluation never comes here."""
+        step (knightvision_amd.train). Evaluation never comes here. n_real:
+        rows after the first n_real are padding (batch_norm_rows)."""
         p = next(self.parameters())
         x = x.to(device=p.device, dtype=p.dtype)
-        h = F.relu(self.bn2(self.conv2(F.relu(self.bn1(self.conv1(x))))))
+        bn = batch_norm_rows
+        h = F.relu(bn(self.bn1, self.conv1(x), n_real))
+        h = F.relu(bn(self.bn2, self.conv2(h), n_real))
         for blk in self.res_blocks:
-            h = blk(h)
-        pol = self.policy_fc(torch.flatten(F.relu(self.policy_bn(self.policy_conv(h))), 1))
-        v = torch.flatten(F.relu(self.value_bn(self.value_conv(h))), 1)
+            h = blk(h, n_real)
+        pol = self.policy_fc(torch.flatten(F.relu(bn(self.policy_bn, self.policy_conv(h), n_real)), 1))
+        v = torch.flatten(F.relu(bn(self.value_bn, self.value_conv(h), n_real)), 1)
         val = torch.tanh(self.value_fc2(F.relu(self.value_fc1(v))))
         return pol, val
 
-    def forward(self, x):
+    def forward(self, x, n_real=None):
         if self.training:
             if not isinstance(x, torch.Tensor):
                 x = torch.as_tensor(np.asarray(x))
-            return self._train_forward(x)
+            return self._train_forward(x, n_real)
         if not isinstance(x, torch.Tensor):
             x = torch.as_tensor(np.asarray(x))
         dev = x.device if x.is_cuda else torch.device("cuda", torch.cuda.current_device())

@@ -89,12 +89,35 @@ def batches(codes, moves, rewards, batch_size: int, shuffle: bool, generator: to
         yield Batch(codes_to_planes_t(codes[ix]), moves[ix], rewards[ix])
 
 
-def batch_loss(model, b: Batch, entropy_coef: float = ENTROPY_COEF, amp: bool = True):
+# MIOpen selects convolution solutions per input shape (≈0.85 s for each new
+# batch size on MI355X, measured: tools/_shape_probe.py), and the learn loop's
+# last batch has a new size every iteration. On the GPU the batch is padded to a
+# multiple of ROW_BUCKET rows; the padding rows are excluded from every
+# BatchNorm statistic (model.batch_norm_rows) and from the loss, so the update
+# is the unpadded batch's. 0 disables.
+ROW_BUCKET = int(os.getenv("KV_TRAIN_ROW_BUCKET", "256"))
+
+
+def _pad_rows(model, x, bucket):
+    m = model.module if hasattr(model, "module") else model
+    n = x.shape[0]
+    if bucket <= 0 or not getattr(m, "supports_row_padding", False) or n % bucket == 0:
+        return x, None
+    pad = (n + bucket - 1) // bucket * bucket - n
+    return torch.cat([x, x.new_zeros((pad,) + tuple(x.shape[1:]))]), n
+
+
+def batch_loss(model, b: Batch, entropy_coef: float = ENTROPY_COEF, amp: bool = True, bucket: int | None = None):
     """The reference's per-batch loss (train.py:161-176): returns
     (loss, loss_policy, loss_value, entropy, policy_logits)."""
     dev_type = b.boards.device.type
+    if bucket is None:
+        bucket = ROW_BUCKET if dev_type == "cuda" else 0
+    x, n_real = _pad_rows(model, b.boards, bucket)
     with torch.autocast(device_type=dev_type, enabled=amp and dev_type == "cuda"):
-        pol, val = model(b.boards)
+        pol, val = model(x, n_real) if n_real is not None else model(x)
+    if n_real is not None:
+        pol, val = pol[:n_real], val[:n_real]
     loss_policy = F.cross_entropy(pol.float(), b.moves)
     loss_value = F.mse_loss(val.squeeze().float(), b.outcomes)
     logp = F.log_softmax(pol.float(), dim=1)

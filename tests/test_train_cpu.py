@@ -192,3 +192,35 @@ def test_ddp_world2_matches_gradient_average():
     for _, _, union in res:
         for u, w in zip(union, want):
             assert torch.equal(torch.from_numpy(u), w)
+
+
+def test_row_bucketing_is_the_unpadded_update():
+    """batch_loss with the batch padded to a row bucket (the GPU path, which keeps
+    MIOpen's convolution shapes fixed): the padding rows are excluded from every
+    BatchNorm statistic and from the loss, so loss, gradients and BN running
+    statistics equal the unpadded batch's."""
+    from knightvision_amd.model import ChessNet
+    from knightvision_amd.weights import synthetic_state_dict
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(42, "bn").items()}
+    codes, moves, rew = _data(5, 3)
+    # float64: the update is the same function of the real rows; in fp32 the
+    # BatchNorm backward's cancellations turn kernel-order noise into ~1e-3
+    b = T.Batch(T.codes_to_planes_t(codes).double(), moves, rew)
+    outs = []
+    for bucket in (0, 8):
+        torch.manual_seed(0)
+        m = ChessNet()
+        m.load_state_dict(sd)
+        m = m.double()
+        m.train()
+        loss = T.batch_loss(m, b, amp=False, bucket=bucket)[0]
+        loss.backward()
+        grads = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+        stats = {k: v.detach().clone() for k, v in m.state_dict().items() if "running" in k or "num_batches" in k}
+        outs.append((float(loss), grads, stats))
+    (l0, g0, s0), (l1, g1, s1) = outs
+    assert abs(l0 - l1) < 1e-9 * max(1.0, abs(l0))
+    for k in g0:
+        assert torch.allclose(g0[k], g1[k], rtol=1e-9, atol=1e-12), k
+    for k in s0:
+        assert torch.allclose(s0[k].double(), s1[k].double(), rtol=1e-9, atol=1e-12), k
