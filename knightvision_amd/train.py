@@ -90,7 +90,7 @@ def batches(codes, moves, rewards, batch_size: int, shuffle: bool, generator: to
 
 
 # MIOpen selects convolution solutions per input shape (≈0.85 s for each new
-# batch size on MI355X, measured: tools/_shape_probe.py), and the learn loop's
+# batch size on MI355X, measured: tools/shape_probe.py), and the learn loop's
 # last batch has a new size every iteration. On the GPU the batch is padded to a
 # multiple of ROW_BUCKET rows; the padding rows are excluded from every
 # BatchNorm statistic (model.batch_norm_rows) and from the loss, so the update

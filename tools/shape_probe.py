@@ -1,3 +1,5 @@
+"""MIOpen cost of a new training batch size: one update step per listed size (the
+first call of a size pays the convolution solution selection)."""
 import os, sys, time
 import numpy as np, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
