@@ -12,6 +12,8 @@ copy that is rebuilt whenever a parameter or BN statistic changes.
 """
 from __future__ import annotations
 
+import os
+
 import ctypes as C
 
 import numpy as np
@@ -52,6 +54,19 @@ def batch_norm_rows(bn: nn.BatchNorm2d, x, n_real=None):
     return y.to(x.dtype)
 
 
+# MIOpen runs these 8x8 convolutions well up to ~1024 images per call and
+# several times slower above (measured per update step: 21 ms at 1024, 272 ms at
+# 4096): convolution is per image, so training-mode calls are split into chunks
+# of CONV_CHUNK images (BatchNorm still sees the whole batch).
+CONV_CHUNK = int(os.getenv("KV_TRAIN_CONV_CHUNK", "1024"))
+
+
+def conv_chunked(conv: nn.Conv2d, x):
+    if CONV_CHUNK <= 0 or x.shape[0] <= CONV_CHUNK or not x.is_cuda:
+        return conv(x)
+    return torch.cat([conv(c) for c in x.split(CONV_CHUNK)])
+
+
 class ResidualBlock(nn.Module):
     """One residual block (ai/model.py:8-25). Its own forward is the training
     path only; evaluation runs the whole tower in libkv.so."""
@@ -64,8 +79,8 @@ class ResidualBlock(nn.Module):
         self.bn2 = nn.BatchNorm2d(channels)
 
     def forward(self, x, n_real=None):
-        y = batch_norm_rows(self.bn1, self.conv1(x), n_real)
-        y = batch_norm_rows(self.bn2, self.conv2(F.relu(y)), n_real)
+        y = batch_norm_rows(self.bn1, conv_chunked(self.conv1, x), n_real)
+        y = batch_norm_rows(self.bn2, conv_chunked(self.conv2, F.relu(y)), n_real)
         return F.relu(y + x)
 
 
@@ -172,12 +187,13 @@ class ChessNet(nn.Module):
         p = next(self.parameters())
         x = x.to(device=p.device, dtype=p.dtype)
         bn = batch_norm_rows
-        h = F.relu(bn(self.bn1, self.conv1(x), n_real))
-        h = F.relu(bn(self.bn2, self.conv2(h), n_real))
+        cv = conv_chunked
+        h = F.relu(bn(self.bn1, cv(self.conv1, x), n_real))
+        h = F.relu(bn(self.bn2, cv(self.conv2, h), n_real))
         for blk in self.res_blocks:
             h = blk(h, n_real)
-        pol = self.policy_fc(torch.flatten(F.relu(bn(self.policy_bn, self.policy_conv(h), n_real)), 1))
-        v = torch.flatten(F.relu(bn(self.value_bn, self.value_conv(h), n_real)), 1)
+        pol = self.policy_fc(torch.flatten(F.relu(bn(self.policy_bn, cv(self.policy_conv, h), n_real)), 1))
+        v = torch.flatten(F.relu(bn(self.value_bn, cv(self.value_conv, h), n_real)), 1)
         val = torch.tanh(self.value_fc2(F.relu(self.value_fc1(v))))
         return pol, val
 

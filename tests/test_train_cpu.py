@@ -224,3 +224,4 @@ def test_row_bucketing_is_the_unpadded_update():
         assert torch.allclose(g0[k], g1[k], rtol=1e-9, atol=1e-12), k
     for k in s0:
         assert torch.allclose(s0[k].double(), s1[k].double(), rtol=1e-9, atol=1e-12), k
+
