@@ -287,7 +287,7 @@ def main():
                 "f16x3": "fp32-accurate split: every fp32 operand scaled by an exact power of two (per layer for "
                          "the weights, per board for the activations) and split into 2 fp16 pieces (22 significant "
                          "bits), the 3 piece products of weight >= 2^-22 on f16 MFMA, fp32 accumulation, Winograd "
-                         "tower; batch-invariant; logits within the fp32 tolerance (tests/test_nn_gpu.py)",
+                         "F(4x8) tower; batch-invariant; logits within the fp32 tolerance (tests/test_nn_gpu.py)",
                 "bf16x6": "fp32-accurate split: every fp32 operand = 3 exact bf16 pieces, the 6 piece products of "
                           "weight >= 2^-16 on bf16 MFMA, fp32 accumulation, Winograd tower; max |dlogit| 6.0e-6 on the "
                           "peaked weights (fp32 Winograd 7.2e-6, fp32 direct 5.2e-6; tolerance 1e-4)",
@@ -299,8 +299,10 @@ def main():
                 "value": (alt["sims"] if mcts else alt["plies"]) / alt["dt"], "unit": unit,
                 "ms_per_step": alt["dt"] * 1e3 / steps, "plies_per_s": alt["plies"] / alt["dt"],
                 "nn_tflops_fp32_equiv": alt["nn_rows"] * FLOP_PER_EVAL / alt["dt"] / 1e12,
-                "dominant_kernel": ({"f16x3": "wino_gemm_h3_kernel<512,2>", "bf16x6": "wino_gemm_bf6_kernel<512>"}
-                                    .get(args.alt_precision, "wino_gemm_kernel<512>") if alt["dom_algo"] == 2
+                "dominant_kernel": ({"f16x3": "wino_gemm_h3_kernel<512,2,60,1>" if alt["dom_algo"] == 3
+                                     else "wino_gemm_h3_kernel<512,2,36,2>",
+                                     "bf16x6": "wino_gemm_bf6_kernel<512>"}
+                                    .get(args.alt_precision, "wino_gemm_kernel<512>") if alt["dom_algo"] in (2, 3)
                                     else "conv3x3 (direct)"),
                 "dominant_avg_launch_ms": alt["conv_ms"], "dominant_tflops_fp32_equiv": a_ach,
                 "dominant_bf16_mfma_frac": (a_ach * a_prod / BF16_MFMA_PEAK_TFLOPS) if (a_ach and a_prod) else None}

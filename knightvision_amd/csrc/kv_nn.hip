@@ -610,17 +610,20 @@ __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ bo
     }
     if (!WINO) return;
     __syncthreads();
-    if (WINO == 2) {  // waves 0, 1 = the two 4x8 tiles
-        if (w >= 2) return;
-        float d48[60];
+    if (WINO == 2) {  // waves 0, 1 = the two 4x8 tiles (2, 3 only join the f16x3 max)
+        float mx = 0.f;
+        if (w < 2) {
+            float d48[60];
 #pragma unroll
-        for (int i = 0; i < 6; ++i)
+            for (int i = 0; i < 6; ++i)
 #pragma unroll
-            for (int j = 0; j < 10; ++j) {
-                const int yy = w * 4 - 1 + i, xx = j - 1;
-                d48[i * 10 + j] = (yy >= 0 && yy < 8 && xx >= 0 && xx < 8) ? plane[yy * 8 + xx][cl] : 0.f;
-            }
-        wino48_input_tile(d48, out, ((size_t)b * 2 + w) * 256 + c, (size_t)rows * 256);
+                for (int j = 0; j < 10; ++j) {
+                    const int yy = w * 4 - 1 + i, xx = j - 1;
+                    d48[i * 10 + j] = (yy >= 0 && yy < 8 && xx >= 0 && xx < 8) ? plane[yy * 8 + xx][cl] : 0.f;
+                }
+            mx = wino48_input_tile(d48, out, ((size_t)b * 2 + w) * 256 + c, (size_t)rows * 256);
+        }
+        if (vmax) block_max_to(mx, vmax + b, red);
         return;
     }
     const int y0 = (w >> 1) * 4 - 1, x0 = (w & 1) * 4 - 1;
@@ -687,6 +690,8 @@ struct kv_net {
     float* U = nullptr;     // Winograd weights [36][Cout][Cin] of convs 1..11
     float* U48 = nullptr;   // F(4x8) weights [60][Cout][Cin] of convs 1..11
     size_t uoff48[12] = {};
+    uint16_t* Uf48[2] = {};  // fp16 pieces of U48 * 2^ut48[l] (KV_PREC_F16X3 on F(4x8))
+    int ut48[12] = {};
     uint16_t* Up[3] = {};   // the same split into bf16 h / m / l (KV_PREC_BF16X6)
     uint16_t* Uf[2] = {};   // fp16 pieces of U * 2^ut[l] (KV_PREC_F16X3)
     int ut[12] = {};
@@ -784,9 +789,10 @@ static bool use_wino(const kv_net* net, int B) {
     return net->algo == KV_ALGO_AUTO && B > kSplitMaxBoards;
 }
 
-// the F(4x8) variant: fp32 only (AUTO and WINOGRAD48); the split precisions keep F(4x4)
+// the F(4x8) variant: fp32 and f16x3 (AUTO and WINOGRAD48); bf16x6 keeps F(4x4)
 static bool use_wino48(const kv_net* net, int B) {
-    return use_wino(net, B) && net->precision == KV_PREC_FP32 && net->algo != KV_ALGO_WINOGRAD;
+    return use_wino(net, B) && (net->precision == KV_PREC_FP32 || net->precision == KV_PREC_F16X3) &&
+           net->algo != KV_ALGO_WINOGRAD;
 }
 
 // padded batch: a multiple of 4 boards (direct tiles) or 32 (128-row GEMM tiles)
@@ -862,20 +868,20 @@ static int launch_wino48_gemm(const float* V, const float* U, float* M, int rows
     return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720, kv::W48_XI>(V, U, M, rows, stride, st);
 }
 
-template <int K, int TM>
+template <int K, int TM, int XI = kv::WN_XI, int RSH = 2>
 static int launch_wino_gemm_h3_t(const float* V, const uint16_t* Uh, const uint16_t* Ul, const unsigned* vmax,
                                  float* M, int rows, int stride, hipStream_t st) {
     using T = kv::WinoH3<TM>;
     static bool attr_set = false;
     if (!attr_set) {
-        KV_HIP(hipFuncSetAttribute((const void*)kv::wino_gemm_h3_kernel<K, TM>,
+        KV_HIP(hipFuncSetAttribute((const void*)kv::wino_gemm_h3_kernel<K, TM, XI, RSH>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::BYTES));
         attr_set = true;
     }
-    const int nwg = kv::WN_XI * (rows / T::WM) * (512 / T::WN);
+    const int nwg = XI * (rows / T::WM) * (512 / T::WN);
     KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0, KV_EINVAL, "wino gemm f16x3: rows %d", rows);
-    hipLaunchKernelGGL((kv::wino_gemm_h3_kernel<K, TM>), dim3(nwg), dim3(256), T::BYTES, st, V, Uh, Ul, vmax, M, rows,
-                       512, stride);
+    hipLaunchKernelGGL((kv::wino_gemm_h3_kernel<K, TM, XI, RSH>), dim3(nwg), dim3(256), T::BYTES, st, V, Uh, Ul, vmax,
+                       M, rows, 512, stride);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -883,11 +889,11 @@ static int launch_wino_gemm_h3_t(const float* V, const uint16_t* Uh, const uint1
 // 128-row tiles (2 workgroups per CU) when the rows allow: at 1,024 rows 4 %
 // faster per forward than the 64-row tile's exact 3 rounds (operand traffic
 // into the CUs, not MFMA, bounds this kernel); same k order, same bits.
-template <int K>
+template <int K, int XI = kv::WN_XI, int RSH = 2>
 static int launch_wino_gemm_h3(const float* V, const uint16_t* Uh, const uint16_t* Ul, const unsigned* vmax, float* M,
                                int rows, int stride, hipStream_t st) {
-    if (rows % 128) return launch_wino_gemm_h3_t<K, 1>(V, Uh, Ul, vmax, M, rows, stride, st);
-    return launch_wino_gemm_h3_t<K, 2>(V, Uh, Ul, vmax, M, rows, stride, st);
+    if (rows % 128) return launch_wino_gemm_h3_t<K, 1, XI, RSH>(V, Uh, Ul, vmax, M, rows, stride, st);
+    return launch_wino_gemm_h3_t<K, 2, XI, RSH>(V, Uh, Ul, vmax, M, rows, stride, st);
 }
 
 template <int K>
@@ -969,9 +975,20 @@ static int launch_wino48_out(kv_net* net, int l, const float* M, int nb, int str
                              float* Vn, hipStream_t st) {
     const float* W = net->w;
     hipLaunchKernelGGL((kv::wino48_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 64, nb), dim3(128), 0, st, M,
-                       stride, W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn);
+                       stride, W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn, net_vmax(net, l),
+                       net->ut48[l], NEXT_V ? net_vmax(net, l + 1) : nullptr);
     KV_HIP(hipGetLastError());
     return KV_OK;
+}
+
+// the F(4x8) GEMMs of conv layer l in the net's precision (fp32 or f16x3)
+template <int K>
+static int wino48_gemm_layer(kv_net* net, int l, const float* V, float* M, int rows, int stride, hipStream_t st) {
+    const size_t o = net->uoff48[l];
+    if (net->precision == KV_PREC_F16X3)
+        return launch_wino_gemm_h3<K, kv::W48_XI, 1>(V, net->Uf48[0] + o, net->Uf48[1] + o, net_vmax(net, l), M, rows,
+                                                      stride, st);
+    return launch_wino48_gemm<K>(V, net->U48 + o, M, rows, stride, st);
 }
 
 // conv2 + the 5 residual blocks for boards [0, nb), F(4x8)
@@ -980,17 +997,17 @@ static int wino48_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     float* V = net->V;
     float* M = net->Mw;
     int rc;
-    if ((rc = launch_wino48_gemm<256>(net->V256, net->U48 + net->uoff48[1], M, rows, stride, st))) return rc;
+    if ((rc = wino48_gemm_layer<256>(net, 1, net->V256, M, rows, stride, st))) return rc;
     if ((rc = launch_wino48_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st))) return rc;
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
     for (int r = 0; r < 5; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         const bool m = mark && r == 2;  // one representative residual GEMM for the engine's timing hook
         if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-        if ((rc = launch_wino48_gemm<512>(V, net->U48 + net->uoff48[l1], M, rows, stride, st))) return rc;
+        if ((rc = wino48_gemm_layer<512>(net, l1, V, M, rows, stride, st))) return rc;
         if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
         if ((rc = launch_wino48_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st))) return rc;
-        if ((rc = launch_wino48_gemm<512>(V, net->U48 + net->uoff48[l2], M, rows, stride, st))) return rc;
+        if ((rc = wino48_gemm_layer<512>(net, l2, V, M, rows, stride, st))) return rc;
         rc = r < 4 ? launch_wino48_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
                    : launch_wino48_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
         if (rc) return rc;
@@ -1007,7 +1024,7 @@ static int net_tower_wino(kv_net* net, int nb_pad, bool v256_ready, hipStream_t 
         const int rows48 = nb_pad * 2;
         if (!v256_ready) {
             hipLaunchKernelGGL(kv::wino48_in_kernel<256>, dim3(256 / 64, nb_pad), dim3(128), 0, st, net->T, rows48,
-                               net->V256);
+                               net->V256, net_vmax(net, 1));
             KV_HIP(hipGetLastError());
         }
         if ((rc = wino48_blocks(net, nb_pad, true, st))) return rc;
@@ -1044,7 +1061,7 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     if (boards) {
         if (wino && use_wino48(net, nb))
             hipLaunchKernelGGL(kv::stem_kernel<2>, dim3(4, nb_pad), dim3(256), 0, st, boards, nb, net->stemT,
-                               W + o.scale[0], W + o.shift[0], net->V256, nb_pad * 2, nullptr);
+                               W + o.scale[0], W + o.shift[0], net->V256, nb_pad * 2, net_vmax(net, 1));
         else if (wino)
             hipLaunchKernelGGL(kv::stem_kernel<1>, dim3(4, nb_pad), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], net->V256, nb_pad * 4, net_vmax(net, 1));
@@ -1106,6 +1123,35 @@ static int net_heads(kv_net* net, int nb, float* policy, float* value, hipStream
     hipLaunchKernelGGL(kv::policy_fc_kernel, dim3(4096 / 128, (nb + 31) / 32), dim3(256), 0, st, net->pfeat,
                        W + o.pfc_w, W + o.pfc_b, policy, nb);
     KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+// f16x3 weights of one Winograd set: per-layer scale 2^ut putting max |U| in
+// [2^14, 2^15), then the two fp16 pieces in the GEMM's B-image layout
+static int split_f16_set(const float* U, const size_t* uoff, int nxi, uint16_t* const* Uf, int* ut) {
+    unsigned* umax = nullptr;
+    KV_HIP(hipMalloc(&umax, 12 * sizeof(unsigned)));
+    KV_HIP(hipMemset(umax, 0, 12 * sizeof(unsigned)));
+    for (int l = 1; l < 12; ++l) {
+        const size_t n = (size_t)nxi * kv::kConv[l].cout * kv::kConv[l].cin;
+        hipLaunchKernelGGL(kv::absmax_kernel, dim3(1024), dim3(256), 0, 0, U + uoff[l], n, umax + l);
+        KV_HIP(hipGetLastError());
+    }
+    unsigned hmax[12];
+    const hipError_t e = hipMemcpy(hmax, umax, sizeof(hmax), hipMemcpyDeviceToHost);
+    (void)hipFree(umax);
+    KV_HIP(e);
+    for (int l = 1; l < 12; ++l) {
+        const size_t n = (size_t)nxi * kv::kConv[l].cout * kv::kConv[l].cin;
+        int ex = 0;
+        float mf;
+        memcpy(&mf, &hmax[l], sizeof mf);
+        (void)frexp(hmax[l] ? (double)mf : 1.0, &ex);  // max in [2^(ex-1), 2^ex)
+        ut[l] = 15 - ex;
+        hipLaunchKernelGGL(kv::split_f16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, U + uoff[l],
+                           kv::kConv[l].cout, kv::kConv[l].cin, ut[l], Uf[0] + uoff[l], Uf[1] + uoff[l], nxi);
+        KV_HIP(hipGetLastError());
+    }
     return KV_OK;
 }
 
@@ -1173,6 +1219,7 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
             tot += (size_t)kv::W48_XI * kv::kConv[l].cout * kv::kConv[l].cin;
         }
         KV_HIP(hipMalloc(&net->U48, tot * sizeof(float)));
+        for (int p = 0; p < 2; ++p) KV_HIP(hipMalloc(&net->Uf48[p], tot * sizeof(uint16_t)));
     }
     for (int l = 1; l < 12; ++l) {
         const size_t n = (size_t)kv::kConv[l].cout * kv::kConv[l].cin;
@@ -1183,32 +1230,9 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
     hipLaunchKernelGGL(kv::split3_kernel, dim3((unsigned)((net->utot + 255) / 256)), dim3(256), 0, 0, net->U,
                        net->utot, net->Up[0], net->Up[1], net->Up[2]);
     KV_HIP(hipGetLastError());
-    {  // f16x3: per-layer scale 2^ut putting max |U| in [2^14, 2^15), then the fp16 pieces
-        unsigned* umax = nullptr;
-        KV_HIP(hipMalloc(&umax, 12 * sizeof(unsigned)));
-        KV_HIP(hipMemset(umax, 0, 12 * sizeof(unsigned)));
-        for (int l = 1; l < 12; ++l) {
-            const size_t n = (size_t)kv::WN_XI * kv::kConv[l].cout * kv::kConv[l].cin;
-            hipLaunchKernelGGL(kv::absmax_kernel, dim3(1024), dim3(256), 0, 0, net->U + net->uoff[l], n, umax + l);
-            KV_HIP(hipGetLastError());
-        }
-        unsigned hmax[12];
-        const hipError_t e = hipMemcpy(hmax, umax, sizeof(hmax), hipMemcpyDeviceToHost);
-        (void)hipFree(umax);
-        KV_HIP(e);
-        for (int l = 1; l < 12; ++l) {
-            const size_t n = (size_t)kv::WN_XI * kv::kConv[l].cout * kv::kConv[l].cin;
-            int ex = 0;
-            float mf;
-            memcpy(&mf, &hmax[l], sizeof mf);
-            (void)frexp(hmax[l] ? (double)mf : 1.0, &ex);  // max in [2^(ex-1), 2^ex)
-            net->ut[l] = 15 - ex;
-            hipLaunchKernelGGL(kv::split_f16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0,
-                               net->U + net->uoff[l], kv::kConv[l].cout, kv::kConv[l].cin, net->ut[l],
-                               net->Uf[0] + net->uoff[l], net->Uf[1] + net->uoff[l]);
-            KV_HIP(hipGetLastError());
-        }
-    }
+    int rc;
+    if ((rc = split_f16_set(net->U, net->uoff, kv::WN_XI, net->Uf, net->ut))) return rc;
+    if ((rc = split_f16_set(net->U48, net->uoff48, kv::W48_XI, net->Uf48, net->ut48))) return rc;
     if (!net->stemT) KV_HIP(hipMalloc(&net->stemT, 9 * 12 * 256 * sizeof(float)));
     hipLaunchKernelGGL(kv::stem_weights_kernel, dim3(9 * 12), dim3(256), 0, 0, net->w + net->off.w[0], net->stemT);
     KV_HIP(hipGetLastError());
@@ -1293,6 +1317,7 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->stemT);
     for (int p = 0; p < 3; ++p) (void)hipFree(net->Up[p]);
     for (int p = 0; p < 2; ++p) (void)hipFree(net->Uf[p]);
+    for (int p = 0; p < 2; ++p) (void)hipFree(net->Uf48[p]);
     (void)hipFree(net->vmax);
     (void)hipFree(net->V);
     (void)hipFree(net->Mw);

@@ -566,7 +566,8 @@ __host__ __device__ inline size_t h3_uidx(int xi, int co, int ci, int cout, int 
 // split and written to the other stage; A(kt+3) loads issued; barrier. A
 // (V, streamed from HBM / the Infinity Cache) has two k-tiles of latency
 // cover, B (U, L2-resident) one compute phase.
-template <int K, int TM>
+// XI transform points; RSH: log2 of the V rows per board (2 for F(4x4), 1 for F(4x8))
+template <int K, int TM, int XI = WN_XI, int RSH = 2>
 __global__ __launch_bounds__(256) void wino_gemm_h3_kernel(const float* __restrict__ V, const uint16_t* __restrict__ Uh,
                                                            const uint16_t* __restrict__ Ul,
                                                            const unsigned* __restrict__ vmax, float* __restrict__ M,
@@ -579,7 +580,7 @@ __global__ __launch_bounds__(256) void wino_gemm_h3_kernel(const float* __restri
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
     const int CT = cout / T::WN, RT = rows / T::WM;
-    const int nwg = WN_XI * RT * CT;
+    const int nwg = XI * RT * CT;
     const int idx0 = (int)(blockIdx.x & 7) * (nwg >> 3) + (int)(blockIdx.x >> 3);
     const int xi = idx0 / (CT * RT);
     const int nb_ = idx0 % CT;
@@ -591,7 +592,7 @@ __global__ __launch_bounds__(256) void wino_gemm_h3_kernel(const float* __restri
     const int ar = tid >> 2, ac = tid & 3;
     float asc[TM];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) asc[i] = ldexpf(1.f, h3_exp(vmax[(r_base + ar + 64 * i) >> 2]));
+    for (int i = 0; i < TM; ++i) asc[i] = ldexpf(1.f, h3_exp(vmax[(r_base + ar + 64 * i) >> RSH]));
     const float* asrc = Va + (size_t)ar * K + ac * 8;
     f32x4 ra[2][TM][2];
     auto loadA = [&](int kt, f32x4 (&a)[TM][2]) {
@@ -720,9 +721,9 @@ __global__ void absmax_kernel(const float* __restrict__ x, size_t n, unsigned* o
 
 // U [36][cout][cin] (one layer) -> fp16 pieces of U * 2^ut in the Uf layout (h3_uidx)
 __global__ void split_f16_kernel(const float* __restrict__ u, int cout, int cin, int ut, uint16_t* __restrict__ h,
-                                 uint16_t* __restrict__ l) {
+                                 uint16_t* __restrict__ l, int nxi) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (size_t)WN_XI * cout * cin) return;
+    if (i >= (size_t)nxi * cout * cin) return;
     const int ci = (int)(i % cin), co = (int)((i / cin) % cout), xi = (int)(i / ((size_t)cin * cout));
     const float a = ldexpf(u[i], ut);
     const _Float16 hh = (_Float16)a;

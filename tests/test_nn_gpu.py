@@ -14,9 +14,9 @@ TOL_P, TOL_V = 1e-4, 1e-5
 
 
 # (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x4,3x3) / fp32 Winograd F(4x8,3x3) (the fp32
-# default above 16 boards) / f16x3 and bf16x6 Winograd F(4x4) / bf16x3 direct
+# default above 16 boards) / f16x3 Winograd F(4x4) and F(4x8) (its default) / bf16x6 Winograd F(4x4) / bf16x3 direct
 MODES = [("fp32", "direct"), ("fp32", "winograd"), ("fp32", "winograd48"), ("f16x3", "winograd"),
-         ("bf16x6", "winograd"), ("bf16x3", "auto")]
+         ("f16x3", "winograd48"), ("bf16x6", "winograd"), ("bf16x3", "auto")]
 
 
 def _net(variant, precision="fp32", algo="auto"):
