@@ -862,6 +862,8 @@ static int launch_wino_gemm(const float* V, const float* U, float* M, int rows, 
 // 12.88; 64x128 uncapped (5 per CU) 1.88 / 13.12; 64x128 capped at 3 per CU 1.95 / 13.26;
 // 64x64 (3,840 tiles: an equal share per CU) 1.87 / 13.49; 64x128 as 8 waves of 32x32 1.89 / 13.18;
 // 128x128 as 4 waves of 64x64 1.82 / 13.06 (k-tile 16: 1.85 / 13.20), as 8 waves of 64x32 1.79 / 12.60
+// (re-measured A/B on the final out kernels: 8 waves of 32x64 1.78 / 12.55, of 64x32 1.80 / 12.77,
+// 4 waves of 64x64 1.84 / 13.07)
 template <int K>
 static int launch_wino48_gemm(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
     if (rows % 128 == 0) return launch_wino_gemm_t<K, 4, 2, 1, 2, 32, 0, kv::W48_XI>(V, U, M, rows, stride, st);
