@@ -457,22 +457,24 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slab, int splits,
 // ------------------------------------------------------------- heads --
 // policy_conv/value_conv (1x1, 512->2 / 512->1) + BN + ReLU, NCHW flatten
 // (c*64+sq, ai/model.py:65), value_fc1 + ReLU, value_fc2 + tanh (:70-73).
-__global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ X, const float* __restrict__ hw,
-                                                    const float* __restrict__ hs, const float* __restrict__ hb,
-                                                    const float* __restrict__ v1w, const float* __restrict__ v1b,
-                                                    const float* __restrict__ v2w, const float* __restrict__ v2b,
-                                                    float* __restrict__ pfeat, float* __restrict__ value) {
+// One board per 1,024-thread block: 16 lanes per pixel split its 512 channels
+// (32 each), so the board's 128 KB are read with 16 waves' loads in flight.
+__global__ __launch_bounds__(1024) void heads_kernel(const float* __restrict__ X, const float* __restrict__ hw,
+                                                     const float* __restrict__ hs, const float* __restrict__ hb,
+                                                     const float* __restrict__ v1wT, const float* __restrict__ v1b,
+                                                     const float* __restrict__ v2w, const float* __restrict__ v2b,
+                                                     float* __restrict__ pfeat, float* __restrict__ value) {
     __shared__ float s_pf[128];
     __shared__ float s_v[64];
     __shared__ float s_h[512];
-    __shared__ float s_red[4];
+    __shared__ float s_red[8];
     const int b = blockIdx.x, t = threadIdx.x;
-    const int p = t >> 2, q = t & 3;
+    const int p = t >> 4, q = t & 15;
     const float* xp = X + ((size_t)b * 64 + p) * 512;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-#pragma unroll 8
-    for (int j = 0; j < 32; ++j) {
-        const int c = q * 4 + 16 * j;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int c = q * 4 + 64 * j;
         const f32x4 x = *(const f32x4*)(xp + c);
         const f32x4 w0 = *(const f32x4*)(hw + c);
         const f32x4 w1 = *(const f32x4*)(hw + 512 + c);
@@ -485,7 +487,7 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ X,
         }
     }
 #pragma unroll
-    for (int m = 1; m < 4; m <<= 1) {
+    for (int m = 1; m < 16; m <<= 1) {
         a0 += __shfl_xor(a0, m);
         a1 += __shfl_xor(a1, m);
         a2 += __shfl_xor(a2, m);
@@ -498,18 +500,19 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ X,
     }
     __syncthreads();
     if (t < 128) pfeat[(size_t)b * 128 + t] = s_pf[t];
-    for (int o = t; o < 512; o += 256) {
-        float hsum = v1b[o];
-        const float* wr = v1w + (size_t)o * 64;
+    if (t < 512) {  // value_fc1 from its [k][o] copy: lanes read adjacent outputs
+        float hsum = v1b[t];
 #pragma unroll 16
-        for (int k = 0; k < 64; ++k) hsum += wr[k] * s_v[k];
-        s_h[o] = hsum > 0.f ? hsum : 0.f;
+        for (int k = 0; k < 64; ++k) hsum += v1wT[k * 512 + t] * s_v[k];
+        s_h[t] = hsum > 0.f ? hsum : 0.f;
     }
     __syncthreads();
-    float part = v2w[t] * s_h[t] + v2w[t + 256] * s_h[t + 256];
+    if (t < 256) {
+        float part = v2w[t] * s_h[t] + v2w[t + 256] * s_h[t + 256];
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m);
-    if ((t & 63) == 0) s_red[t >> 6] = part;
+        for (int m = 32; m >= 1; m >>= 1) part += __shfl_xor(part, m);
+        if ((t & 63) == 0) s_red[t >> 6] = part;
+    }
     __syncthreads();
     if (t == 0) value[b] = tanhf(s_red[0] + s_red[1] + s_red[2] + s_red[3] + v2b[0]);
 }
@@ -567,76 +570,91 @@ __global__ void encode_boards_kernel(const int8_t* __restrict__ boards, int nb, 
 // the occupied 3x3 neighbours -- added in tap order, which is the order (and
 // rounding) in which conv3x3_kernel<16,16>'s MFMA chain adds them, so the
 // result is bit-identical to the encode + implicit-GEMM path.
-// Block = one board x 64 channels (grid 4 x nb_pad), 256 threads: the 64-channel
-// slice of conv1 ([tap][code][64], 30 KB, a zero row for empty) is staged in
-// LDS; wave w computes pixels 16w..16w+15. WINO: the activated 8x8 plane goes through
-// LDS to the four tile waves, which write conv2's Winograd input transform
-// (V [36][rows][256]); else NHWC T [board][64][256].
+// Block = two boards x 64 channels (grid 4 x nb_pad/2), 256 threads: the
+// 64-channel slice of conv1 ([tap][code][64], 30 KB, a zero row for empty) is
+// staged in LDS once for both boards; waves 2b, 2b+1 compute board b's pixels
+// 0..31 / 32..63. WINO: the activated 8x8 planes go through LDS to the tile
+// transforms -- wave w writes board w/2's tile w%2 (F(4x8)) or tiles 2(w%2),
+// 2(w%2)+1 (F(4x4)) of conv2's Winograd input V [points][rows][256]; else
+// NHWC T [board][64][256].
 template <int WINO>  // 0: NHWC out, 1: F(4x4) V of conv2, 2: F(4x8) V of conv2
 __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ boards, int nb,
                                                    const float* __restrict__ wT, const float* __restrict__ scale,
                                                    const float* __restrict__ shift, float* __restrict__ out,
                                                    int rows, unsigned* vmax) {
-    __shared__ float wl[9 * 13][64];
-    __shared__ float red[4];  // [tap][code 0..12][channel], code 0 = empty = 0
-    __shared__ float plane[64][64];   // [pixel][channel]
-    __shared__ int codes[100];        // the board with a one-square empty border (10x10)
+    __shared__ float wl[9 * 13][64];    // [tap][code 0..12][channel], code 0 = empty = 0
+    __shared__ float plane[2][64][64];  // [board][pixel][channel]
+    __shared__ int codes[2][100];       // the boards with a one-square empty border (10x10)
     const int cl = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = blockIdx.x * 64 + cl, b = blockIdx.y;
-    if (threadIdx.x < 100) {
-        const int r = threadIdx.x / 10 - 1, f = threadIdx.x % 10 - 1;
-        codes[threadIdx.x] = (b < nb && r >= 0 && r < 8 && f >= 0 && f < 8) ? boards[(size_t)b * 64 + r * 8 + f] : 0;
+    const int c = blockIdx.x * 64 + cl, b0 = blockIdx.y * 2;
+    if (threadIdx.x < 200) {
+        const int bb = threadIdx.x / 100, i = threadIdx.x % 100;
+        const int r = i / 10 - 1, f = i % 10 - 1, b = b0 + bb;
+        codes[bb][i] = (b < nb && r >= 0 && r < 8 && f >= 0 && f < 8) ? boards[(size_t)b * 64 + r * 8 + f] : 0;
     }
-    for (int i = w; i < 9 * 13; i += 4) {
-        const int t = i / 13, code = i % 13;
-        wl[i][cl] = code ? wT[(size_t)(t * 12 + code - 1) * 256 + c] : 0.f;
+    // all 30 of this thread's weight loads in flight at once (a rolled loop waits
+    // one L2 round trip per row)
+    float wv[30];
+#pragma unroll
+    for (int it = 0; it < 30; ++it) {
+        const int i = w + 4 * it, t = i / 13, code = i % 13;
+        wv[it] = (i < 9 * 13 && code) ? wT[(size_t)(t * 12 + code - 1) * 256 + c] : 0.f;
     }
+#pragma unroll
+    for (int it = 0; it < 30; ++it)
+        if (w + 4 * it < 9 * 13) wl[w + 4 * it][cl] = wv[it];
     __syncthreads();
     const float sc = scale[c], sh = shift[c];
+    const int bb = w >> 1, b = b0 + bb;
     // branch-free: an empty or off-board neighbour adds +0 (exact, acc starts at +0),
     // so every pixel issues its 9 independent LDS reads back to back
 #pragma unroll 4
-    for (int k = 0; k < 16; ++k) {
-        const int p = w * 16 + k, py = p >> 3, px = p & 7;
+    for (int k = 0; k < 32; ++k) {
+        const int p = (w & 1) * 32 + k, py = p >> 3, px = p & 7;
         float acc = 0.f;
 #pragma unroll
-        for (int t = 0; t < 9; ++t) acc += wl[t * 13 + codes[(py + t / 3) * 10 + px + t % 3]][cl];
+        for (int t = 0; t < 9; ++t) acc += wl[t * 13 + codes[bb][(py + t / 3) * 10 + px + t % 3]][cl];
         const float v = acc * sc + sh;
         const float y = v > 0.f ? v : 0.f;
         if (WINO)
-            plane[p][cl] = y;
+            plane[bb][p][cl] = y;
         else
             out[((size_t)b * 64 + p) * 256 + c] = y;
     }
     if (!WINO) return;
     __syncthreads();
-    if (WINO == 2) {  // waves 0, 1 = the two 4x8 tiles (2, 3 only join the f16x3 max)
-        float mx = 0.f;
-        if (w < 2) {
-            float d48[60];
+    float mx = 0.f;
+    if (WINO == 2) {
+        const int tile = w & 1;
+        float d48[60];
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = 0; j < 10; ++j) {
+                const int yy = tile * 4 - 1 + i, xx = j - 1;
+                d48[i * 10 + j] = (yy >= 0 && yy < 8 && xx >= 0 && xx < 8) ? plane[bb][yy * 8 + xx][cl] : 0.f;
+            }
+        mx = wino48_input_tile(d48, out, ((size_t)b * 2 + tile) * 256 + c, (size_t)rows * 256);
+    } else {
+        for (int tt = 0; tt < 2; ++tt) {
+            const int tile = (w & 1) * 2 + tt;
+            const int y0 = (tile >> 1) * 4 - 1, x0 = (tile & 1) * 4 - 1;
+            float d[36];
 #pragma unroll
             for (int i = 0; i < 6; ++i)
 #pragma unroll
-                for (int j = 0; j < 10; ++j) {
-                    const int yy = w * 4 - 1 + i, xx = j - 1;
-                    d48[i * 10 + j] = (yy >= 0 && yy < 8 && xx >= 0 && xx < 8) ? plane[yy * 8 + xx][cl] : 0.f;
+                for (int j = 0; j < 6; ++j) {
+                    const int yy = y0 + i, xx = x0 + j;
+                    d[i * 6 + j] = (yy >= 0 && yy < 8 && xx >= 0 && xx < 8) ? plane[bb][yy * 8 + xx][cl] : 0.f;
                 }
-            mx = wino48_input_tile(d48, out, ((size_t)b * 2 + w) * 256 + c, (size_t)rows * 256);
+            mx = fmaxf(mx, wino_input_tile(d, out, ((size_t)b * 4 + tile) * 256 + c, (size_t)rows * 256));
         }
-        if (vmax) block_max_to(mx, vmax + b, red);
-        return;
     }
-    const int y0 = (w >> 1) * 4 - 1, x0 = (w & 1) * 4 - 1;
-    float d[36];
+    if (vmax) {  // KV_PREC_F16X3 operand scale of conv2: per-board max |V| (vmax zeroed per forward)
 #pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            const int yy = y0 + i, xx = x0 + j;
-            d[i * 6 + j] = (yy >= 0 && yy < 8 && xx >= 0 && xx < 8) ? plane[yy * 8 + xx][cl] : 0.f;
-        }
-    const float mx = wino_input_tile(d, out, ((size_t)b * 4 + w) * 256 + c, (size_t)rows * 256);
-    if (vmax) block_max_to(mx, vmax + b, red);  // KV_PREC_F16X3 operand scale of conv2
+        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        if (cl == 0) atomicMax(vmax + b, __float_as_uint(mx));
+    }
 }
 
 // conv1 weights [256][9][16] -> [9][12][256] for stem_kernel
@@ -645,6 +663,12 @@ __global__ void stem_weights_kernel(const float* __restrict__ w, float* __restri
     if (i >= 9 * 12 * 256) return;
     const int c = i % 256, ch = (i / 256) % 12, t = i / (256 * 12);
     wT[i] = w[((size_t)c * 9 + t) * 16 + ch];
+}
+
+// value_fc1 weight [512][64] -> [64][512] for heads_kernel
+__global__ void transpose_v1_kernel(const float* __restrict__ w, float* __restrict__ wT) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;  // k*512 + o
+    if (i < 64 * 512) wT[i] = w[(i % 512) * 64 + i / 512];
 }
 
 // [B][12][8][8] NCHW planes -> NHWC16 (any values, not only one-hot)
@@ -697,6 +721,7 @@ struct kv_net {
     int ut[12] = {};
     unsigned* vmax = nullptr;  // f16x3: per-board max |V| of each conv's input, [12][cap]
     float* stemT = nullptr; // conv1 as [tap][piece][cout] (stem_kernel)
+    float* v1wT = nullptr;  // value_fc1 weight as [k][o] (heads_kernel)
     size_t uoff[12] = {};
     size_t utot = 0;
     float* V = nullptr;     // Winograd workspaces [36][cap*4][512]
@@ -1062,13 +1087,13 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
         KV_HIP(hipMemsetAsync(net->vmax, 0, (size_t)12 * net->cap * sizeof(unsigned), st));
     if (boards) {
         if (wino && use_wino48(net, nb))
-            hipLaunchKernelGGL(kv::stem_kernel<2>, dim3(4, nb_pad), dim3(256), 0, st, boards, nb, net->stemT,
+            hipLaunchKernelGGL(kv::stem_kernel<2>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], net->V256, nb_pad * 2, net_vmax(net, 1));
         else if (wino)
-            hipLaunchKernelGGL(kv::stem_kernel<1>, dim3(4, nb_pad), dim3(256), 0, st, boards, nb, net->stemT,
+            hipLaunchKernelGGL(kv::stem_kernel<1>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], net->V256, nb_pad * 4, net_vmax(net, 1));
         else
-            hipLaunchKernelGGL(kv::stem_kernel<0>, dim3(4, nb_pad), dim3(256), 0, st, boards, nb, net->stemT,
+            hipLaunchKernelGGL(kv::stem_kernel<0>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], net->T, nb_pad * 4, nullptr);
         KV_HIP(hipGetLastError());
     } else if ((rc = launch_conv<16, 16, false>(net->x16, W + o.w[0], W + o.scale[0], W + o.shift[0], nullptr,
@@ -1119,8 +1144,8 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
 static int net_heads(kv_net* net, int nb, float* policy, float* value, hipStream_t st) {
     const float* W = net->w;
     const kv::PackOffsets& o = net->off;
-    hipLaunchKernelGGL(kv::heads_kernel, dim3(nb), dim3(256), 0, st, net->X, W + o.head_w, W + o.head_scale,
-                       W + o.head_shift, W + o.vfc1_w, W + o.vfc1_b, W + o.vfc2_w, W + o.vfc2_b, net->pfeat, value);
+    hipLaunchKernelGGL(kv::heads_kernel, dim3(nb), dim3(1024), 0, st, net->X, W + o.head_w, W + o.head_scale,
+                       W + o.head_shift, net->v1wT, W + o.vfc1_b, W + o.vfc2_w, W + o.vfc2_b, net->pfeat, value);
     KV_HIP(hipGetLastError());
     hipLaunchKernelGGL(kv::policy_fc_kernel, dim3(4096 / 128, (nb + 31) / 32), dim3(256), 0, st, net->pfeat,
                        W + o.pfc_w, W + o.pfc_b, policy, nb);
@@ -1237,6 +1262,9 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
     if ((rc = split_f16_set(net->U48, net->uoff48, kv::W48_XI, net->Uf48, net->ut48))) return rc;
     if (!net->stemT) KV_HIP(hipMalloc(&net->stemT, 9 * 12 * 256 * sizeof(float)));
     hipLaunchKernelGGL(kv::stem_weights_kernel, dim3(9 * 12), dim3(256), 0, 0, net->w + net->off.w[0], net->stemT);
+    if (!net->v1wT) KV_HIP(hipMalloc(&net->v1wT, 64 * 512 * sizeof(float)));
+    hipLaunchKernelGGL(kv::transpose_v1_kernel, dim3(64 * 512 / 256), dim3(256), 0, 0, net->w + net->off.vfc1_w,
+                       net->v1wT);
     KV_HIP(hipGetLastError());
     KV_HIP(hipDeviceSynchronize());
     net->loaded = true;
@@ -1317,6 +1345,7 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->U);
     (void)hipFree(net->U48);
     (void)hipFree(net->stemT);
+    (void)hipFree(net->v1wT);
     for (int p = 0; p < 3; ++p) (void)hipFree(net->Up[p]);
     for (int p = 0; p < 2; ++p) (void)hipFree(net->Uf[p]);
     for (int p = 0; p < 2; ++p) (void)hipFree(net->Uf48[p]);
