@@ -533,13 +533,16 @@ __global__ __launch_bounds__(256) void policy_fc_kernel(const float* __restrict_
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll 4
-    for (int s = 0; s < 16; ++s) {
-        const f32x4 a = *(const f32x4*)(ap + 8 * s);
-        const f32x4 v = *(const f32x4*)(bp + 8 * s);
+    f32x4 a[16], v[16];  // every operand load in flight at once (one memory latency per wave)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], v[j], acc, 0, 0, 0);
+    for (int s = 0; s < 16; ++s) {
+        a[s] = *(const f32x4*)(ap + 8 * s);
+        v[s] = *(const f32x4*)(bp + 8 * s);
     }
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s][j], v[s][j], acc, 0, 0, 0);
     const int n = n0 + li;
     const float bn = bias[n];
 #pragma unroll
