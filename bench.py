@@ -110,11 +110,17 @@ def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; more ranks than GPUs (a rehearsal of the sharded path on a 1-GPU box, with
+    # KV_BENCH_BACKEND=gloo since RCCL refuses two ranks on one device) share the devices round-robin
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     import torch.distributed as dist
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("KV_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     from knightvision_amd.engine import SelfPlayEngine
     from knightvision_amd.weights import synthetic_state_dict
     from knightvision_amd.distributed import gather_experience
@@ -319,7 +325,7 @@ def main():
                 "reference_cpu": {"plies_per_s": 250.0, "games_per_hour": 2424.0,
                                   "source": "BASELINE.md: reference self_play.py (SELFPLAY_SEQ=1) on 8 Xeon cores"}}
             cal = os.path.join(HERE, "profiles", "r01_cpu_calibration.json")
-            if not args.no_cpu_baseline:
+            if not args.no_cpu_baseline and world == 1:
                 # the reference's selection restated on this box's host cores, and the reference-equivalent rate
                 # through the container calibration (reference / port on identical work, tools/calibrate_cpu.py)
                 port = cpu_baseline(min(args.cpu_seconds, 8.0), 0)
@@ -330,7 +336,7 @@ def main():
                     out["ref_selection"]["reference_equiv_box"] = {
                         "plies_per_s": eq, "ref_over_port": r, "source": os.path.relpath(cal, HERE),
                         "gpu_over_reference_equiv": (refsel["plies"] / refsel["dt"]) / eq}
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU leg is timed at N=1 only
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, sims)
         print(json.dumps(out), flush=True)
     if world > 1:
