@@ -176,10 +176,10 @@ __device__ inline void wave_softmax_4096_stats(const float* lg, int lane, float&
 // Consumes the slot's numpy stream exactly as np.random.dirichlet does. All
 // 256 threads of the slot's workgroup; gam is 4096 doubles of LDS.
 __device__ inline void mixed_legal_weights(const DevCfg& cfg, const float* lp, const uint16_t* ml, int n,
-                                           double* gam, uint32_t* np_state, uint32_t* mt_lds3, int* scratch,
+                                           double* gam, uint32_t* np_state, uint32_t* mt_ring, int* scratch,
                                            double* vals, int tid) {
     BlockMT w;
-    bmt_load(w, np_state, mt_lds3, tid);
+    bmt_load(w, np_state, mt_ring, tid);
     long long att;
     const double acc = block_dirichlet_gamma(w, cfg.alpha, 4096, gam, &att, scratch, tid);
     bmt_store(w, np_state, tid);
@@ -197,17 +197,16 @@ __device__ inline void mixed_legal_weights(const DevCfg& cfg, const float* lp, c
 
 // random.choices(population, weights) / random.choice when the total is 0
 // (self_play.py:162-167, CPython random.py:506-541). Lane 0 only.
-__device__ inline int choose_weighted(const double* vals, double* cum, int n, uint32_t* py) {
-    double total = 0.0;
-    for (int j = 0; j < n; ++j) total = total + vals[j];
-    if (total == 0.0) return mt_randbelow_serial(py, n);
+// the pick of random.choices for a non-zero total with r = random() already
+// drawn (cum_weights by serial accumulation, bisect_right on r * total)
+__device__ inline int choose_from(const double* vals, double* cum, int n, double total, double r) {
     double c = 0.0;
     for (int j = 0; j < n; ++j) {
         c = c + vals[j] / total;
         cum[j] = c;
     }
     const double tot = cum[n - 1] + 0.0;
-    const double x = mt_random_serial(py) * tot;
+    const double x = r * tot;
     int lo = 0, hi = n - 1;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
@@ -215,6 +214,13 @@ __device__ inline int choose_weighted(const double* vals, double* cum, int n, ui
         else lo = mid + 1;
     }
     return lo;
+}
+
+__device__ inline int choose_weighted(const double* vals, double* cum, int n, uint32_t* py) {
+    double total = 0.0;
+    for (int j = 0; j < n; ++j) total = total + vals[j];
+    if (total == 0.0) return mt_randbelow_serial(py, n);
+    return choose_from(vals, cum, n, total, mt_random_serial(py));
 }
 
 // record the position + move, makeMove, then the reference's termination

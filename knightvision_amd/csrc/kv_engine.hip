@@ -126,11 +126,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                                                 const float* logits, const float* values, float* last_probs,
                                                 uint32_t* np_mt, uint32_t* py_mt, kv_record* rec, int8_t* last_board,
                                                 Ctr* ctr) {
-    __shared__ uint32_t mt3[3 * MT_N];
+    __shared__ uint32_t mt3[MT_RING * MT_N];
     __shared__ double gam[4096];
     __shared__ double vals[MAXM];
     __shared__ double cum[MAXM];
-    __shared__ int scratch[8];
+    __shared__ int scratch[RNG_SCRATCH];
     __shared__ int s_pick;
     const int i = blockIdx.x, lane = threadIdx.x;
     Slot s = slots[i];
@@ -154,7 +154,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     const int n = s.nmoves;
     const uint16_t* ml = moves + (size_t)i * MAXM;
     mixed_legal_weights(cfg, lp, ml, n, gam, np_mt + (size_t)i * MT_WORDS, mt3, scratch, vals, lane);
-    if (lane == 0) s_pick = choose_weighted(vals, cum, n, py_mt + (size_t)i * MT_WORDS);
+    // random.choices (:162-167): the total, then random() drawn by the whole
+    // workgroup (a twist of the CPython state, every 312 plies of a game, runs
+    // block-parallel in LDS -- one slot's serial twist would stretch the launch)
+    __shared__ double s_total;
+    if (lane == 0) {
+        double total = 0.0;
+        for (int j = 0; j < n; ++j) total = total + vals[j];
+        s_total = total;
+    }
+    __syncthreads();
+    uint32_t* py = py_mt + (size_t)i * MT_WORDS;
+    if (s_total == 0.0) {
+        if (lane == 0) s_pick = mt_randbelow_serial(py, n);  // random.choice
+    } else {
+        const double r = block_mt_random(py, mt3, lane);
+        if (lane == 0) s_pick = choose_from(vals, cum, n, s_total, r);
+    }
     __syncthreads();
     commit_move(cfg, s, i, ml[s_pick], boards, rec, last_board, ctr, lane);
     if (lane == 0) slots[i] = s;

@@ -9,7 +9,7 @@
 //
 // The Dirichlet draw is workgroup-parallel: each gamma attempt consumes exactly
 // four u32 (U = res53, V = -log(1 - res53)), so attempt a reads words
-// 4a..4a+3 and 256 threads run 256 consecutive attempts at once; accepted
+// 4a..4a+3 and 256 threads run 1,024 consecutive attempts at once; accepted
 // attempts are ranked in order (ballots + prefix popcounts) and the draw stops
 // at the exact attempt that yields element k-1 so the stream position matches
 // the sequential generator word for word. The twist runs on the workgroup in
@@ -219,39 +219,41 @@ __device__ inline void mt_twist_block(uint32_t* mt, int tid) {
     __syncthreads();
 }
 
-// A block-local view of a stream: b0 is the raw state whose tempered words are
-// consumed from `pos`; b1, b2 the states after one / two more twists (valid
-// below nready).
+// A block-local view of a stream: a ring of MT_RING states in LDS. Slot `head`
+// is the raw state whose tempered words are consumed from `pos`; the next
+// nready-1 slots hold the states after one, two, ... more twists.
+constexpr int MT_RING = 8;
 struct BlockMT {
-    uint32_t *b0, *b1, *b2;  // named, not an array: a runtime-indexed array would live in scratch
+    uint32_t* ring;  // MT_RING * MT_N words of LDS
+    int head;
     int pos;
     int nready;
 };
 
-__device__ inline void bmt_load(BlockMT& w, const uint32_t* g, uint32_t* lds3, int tid) {
-    for (int i = tid; i < MT_N; i += RNG_THREADS) lds3[i] = g[i];
-    w.b0 = lds3;
-    w.b1 = lds3 + MT_N;
-    w.b2 = lds3 + 2 * MT_N;
+__device__ inline void bmt_load(BlockMT& w, const uint32_t* g, uint32_t* lds_ring, int tid) {
+    for (int i = tid; i < MT_N; i += RNG_THREADS) lds_ring[i] = g[i];
+    w.ring = lds_ring;
+    w.head = 0;
     w.pos = (int)g[MT_N];
     w.nready = 1;
     __syncthreads();
     if (w.pos >= MT_N) {
-        mt_twist_block(w.b0, tid);
+        mt_twist_block(w.ring, tid);
         w.pos = 0;
     }
 }
 
 __device__ inline void bmt_store(const BlockMT& w, uint32_t* g, int tid) {
-    for (int i = tid; i < MT_N; i += RNG_THREADS) g[i] = w.b0[i];
+    const uint32_t* b0 = w.ring + w.head * MT_N;
+    for (int i = tid; i < MT_N; i += RNG_THREADS) g[i] = b0[i];
     if (tid == 0) g[MT_N] = (uint32_t)w.pos;
 }
 
-// make words [pos, pos + need) addressable (pos + need <= 3 * 624)
+// make words [pos, pos + need) addressable (pos + need <= MT_RING * 624)
 __device__ inline void bmt_ensure(BlockMT& w, int need, int tid) {
     while (w.pos + need > MT_N * w.nready) {
-        uint32_t* src = w.nready == 1 ? w.b0 : w.b1;
-        uint32_t* dst = w.nready == 1 ? w.b1 : w.b2;
+        const uint32_t* src = w.ring + ((w.head + w.nready - 1) % MT_RING) * MT_N;
+        uint32_t* dst = w.ring + ((w.head + w.nready) % MT_RING) * MT_N;
         for (int i = tid; i < MT_N; i += RNG_THREADS) dst[i] = src[i];
         __syncthreads();
         mt_twist_block(dst, tid);
@@ -260,68 +262,118 @@ __device__ inline void bmt_ensure(BlockMT& w, int need, int tid) {
 }
 
 __device__ inline uint32_t bmt_word(const BlockMT& w, int j) {  // j relative to pos
-    const int i = w.pos + j;
-    return mt_temper(i < MT_N ? w.b0[i] : (i < 2 * MT_N ? w.b1[i - MT_N] : w.b2[i - 2 * MT_N]));
+    const int i = w.pos + j, s = i / MT_N;
+    return mt_temper(w.ring[((w.head + s) % MT_RING) * MT_N + (i - s * MT_N)]);
 }
 
 __device__ inline void bmt_advance(BlockMT& w, int n) {
     w.pos += n;
     while (w.pos >= MT_N && w.nready > 1) {  // pos == MT_N with nothing ready: twist on demand
-        uint32_t* t = w.b0;
-        w.b0 = w.b1;
-        w.b1 = w.b2;
-        w.b2 = t;
+        w.head = (w.head + 1) % MT_RING;
         w.pos -= MT_N;
         --w.nready;
     }
 }
 
+// random() (two words as res53) from a stream in HBM, for every thread of the
+// workgroup. When the draw crosses the end of the state the stream goes
+// through LDS (`lds`, 624 words) and twists block-parallel instead of one
+// lane walking 624 global read-modify-writes; same words as mt_random_serial.
+__device__ inline double block_mt_random(uint32_t* g, uint32_t* lds, int tid) {
+    __shared__ double s_r;
+    const int idx = (int)g[MT_N];
+    __syncthreads();  // every thread has the index before it is rewritten
+    if (idx + 2 <= MT_N) {
+        if (tid == 0) {
+            s_r = res53(mt_temper(g[idx]), mt_temper(g[idx + 1]));
+            g[MT_N] = (uint32_t)(idx + 2);
+        }
+        __syncthreads();
+        return s_r;
+    }
+    for (int i = tid; i < MT_N; i += RNG_THREADS) lds[i] = g[i];
+    __syncthreads();
+    int p = idx;
+    uint32_t wd[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        if (p >= MT_N) {
+            mt_twist_block(lds, tid);
+            p = 0;
+        }
+        wd[j] = mt_temper(lds[p]);
+        ++p;
+    }
+    for (int i = tid; i < MT_N; i += RNG_THREADS) g[i] = lds[i];
+    if (tid == 0) g[MT_N] = (uint32_t)p;
+    __syncthreads();
+    return res53(wd[0], wd[1]);
+}
+
 // numpy RandomState.dirichlet([alpha]*k) (legacy) without the final scaling:
 // gamma values go to gam[0..k) (LDS or global), the serial left-to-right fp64
 // sum is returned to every thread, *attempts gets the attempt count. Each
-// attempt consumes exactly four u32 (U = res53, V = -log(1 - res53)), so the
-// 256 threads run 256 consecutive attempts at once; accepted attempts are
-// ranked in attempt order (wave ballots + a 4-wave prefix) and the draw stops
+// attempt consumes exactly four u32 (U = res53, V = -log(1 - res53)), so a
+// round runs DIR_AP x 256 consecutive attempts at once (attempt j*256 + tid of
+// the round on thread tid: DIR_AP independent log/pow chains per thread for the
+// scheduler to interleave); accepted attempts are ranked in attempt order
+// (wave ballots + a prefix over the DIR_AP x 4 wave counts) and the draw stops
 // at the exact attempt that yields element k-1, leaving the stream where the
-// sequential generator leaves it. `scratch` is 8 ints of LDS.
+// sequential generator leaves it. `scratch` is RNG_SCRATCH ints of LDS.
+constexpr int DIR_AP = 4;
+constexpr int RNG_SCRATCH = 4 * DIR_AP + 1;
 __device__ inline double block_dirichlet_gamma(BlockMT& w, double alpha, int k, double* gam, long long* attempts,
                                                int* scratch, int tid) {
+    constexpr int RA = DIR_AP * RNG_THREADS;  // attempts per round
+    static_assert(MT_N - 1 + 4 * RA <= MT_RING * MT_N, "MT ring too small for a round");
     const int lane = tid & 63, wave = tid >> 6;
     const double one_m = 1.0 - alpha, inv_a = 1. / alpha;
     int base = 0;
     long long att = 0;
     while (base < k) {
-        bmt_ensure(w, 4 * RNG_THREADS, tid);
-        const uint32_t w0 = bmt_word(w, 4 * tid), w1 = bmt_word(w, 4 * tid + 1);
-        const uint32_t w2 = bmt_word(w, 4 * tid + 2), w3 = bmt_word(w, 4 * tid + 3);
-        const double U = res53(w0, w1);
-        const double V = -log(1.0 - res53(w2, w3));
-        double X;
-        bool ok;
-        if (U <= one_m) {
-            X = pow(U, inv_a);
-            ok = X <= V;
-        } else {
-            const double Y = -log((1 - U) / alpha);
-            X = pow(one_m + alpha * Y, inv_a);
-            ok = X <= (V + Y);
-        }
-        const unsigned long long mask = __ballot(ok);
-        if (lane == 0) scratch[wave] = __popcll(mask);
-        if (tid == 0) scratch[4] = RNG_THREADS;  // attempts used unless the draw completes here
-        __syncthreads();
-        int before = 0, total = 0;
+        bmt_ensure(w, 4 * RA, tid);
+        double X[DIR_AP];
+        bool ok[DIR_AP];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            before += q < wave ? scratch[q] : 0;
-            total += scratch[q];
+        for (int j = 0; j < DIR_AP; ++j) {
+            const int a = j * RNG_THREADS + tid;
+            const uint32_t w0 = bmt_word(w, 4 * a), w1 = bmt_word(w, 4 * a + 1);
+            const uint32_t w2 = bmt_word(w, 4 * a + 2), w3 = bmt_word(w, 4 * a + 3);
+            const double U = res53(w0, w1);
+            const double V = -log(1.0 - res53(w2, w3));
+            if (U <= one_m) {
+                X[j] = pow(U, inv_a);
+                ok[j] = X[j] <= V;
+            } else {
+                const double Y = -log((1 - U) / alpha);
+                X[j] = pow(one_m + alpha * Y, inv_a);
+                ok[j] = X[j] <= (V + Y);
+            }
         }
-        const int rank = before + __popcll(mask & ((1ull << lane) - 1));
-        const int rem = k - base;
-        if (ok && rank == rem - 1) scratch[4] = tid + 1;  // the attempt that yields element k-1
-        if (ok && rank < rem) gam[base + rank] = X;
+        unsigned long long mask[DIR_AP];
+#pragma unroll
+        for (int j = 0; j < DIR_AP; ++j) {
+            mask[j] = __ballot(ok[j]);
+            if (lane == 0) scratch[j * 4 + wave] = __popcll(mask[j]);
+        }
+        if (tid == 0) scratch[4 * DIR_AP] = RA;  // attempts used unless the draw completes here
         __syncthreads();
-        const int used = scratch[4];
+        const int rem = k - base;
+        int before = 0, total = 0;  // accepted in (sub-round, wave) groups ahead of this thread's group
+#pragma unroll
+        for (int j = 0; j < DIR_AP; ++j) {
+            int bj = before;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bj += q < wave ? scratch[j * 4 + q] : 0;
+            const int rank = bj + __popcll(mask[j] & ((1ull << lane) - 1));
+            if (ok[j] && rank == rem - 1) scratch[4 * DIR_AP] = j * RNG_THREADS + tid + 1;  // yields element k-1
+            if (ok[j] && rank < rem) gam[base + rank] = X[j];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) before += scratch[j * 4 + q];
+        }
+        total = before;
+        __syncthreads();
+        const int used = scratch[4 * DIR_AP];
         base += total < rem ? total : rem;
         att += used;
         bmt_advance(w, 4 * used);
