@@ -89,7 +89,7 @@ __global__ void k_dev_attacks(const int8_t* states, int n, unsigned long long* o
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_dev_dirichlet(const unsigned long long* seeds, double alpha, int k,
                                                        int draws, double* out, long long* attempts, double* tail,
                                                        uint32_t* state) {
-    __shared__ uint32_t mt3[MT_RING * MT_N];
+    __shared__ uint32_t mt3[MT_RW];
     __shared__ int scratch[RNG_SCRATCH];
     const int i = blockIdx.x, tid = threadIdx.x;
     uint32_t* g = state + (size_t)i * MT_WORDS;

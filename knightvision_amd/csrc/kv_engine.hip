@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                                                 const float* logits, const float* values, float* last_probs,
                                                 uint32_t* np_mt, uint32_t* py_mt, kv_record* rec, int8_t* last_board,
                                                 Ctr* ctr) {
-    __shared__ uint32_t mt3[MT_RING * MT_N];
+    __shared__ uint32_t mt3[MT_RW];
     __shared__ double gam[4096];
     __shared__ double vals[MAXM];
     __shared__ double cum[MAXM];

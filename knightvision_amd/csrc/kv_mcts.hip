@@ -52,7 +52,7 @@ __device__ inline float puct(float c_puct, float P, float sq, int N, float W) {
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_mcts_root(DevCfg cfg, Tree t, Slot* slots, const uint16_t* moves,
                                                    const float* logits, const float* values, float* probs,
                                                    uint32_t* np_mt) {
-    __shared__ uint32_t mt3[MT_RING * MT_N];
+    __shared__ uint32_t mt3[MT_RW];
     __shared__ double gam[4096];
     __shared__ double vals[MAXM];
     __shared__ int scratch[RNG_SCRATCH];

@@ -12,8 +12,8 @@
 // 4a..4a+3 and 256 threads run 1,024 consecutive attempts at once; accepted
 // attempts are ranked in order (ballots + prefix popcounts) and the draw stops
 // at the exact attempt that yields element k-1 so the stream position matches
-// the sequential generator word for word. The twist runs on the workgroup in
-// three dependency-free phases ([0,227), [227,454), [454,623) + the last word).
+// the sequential generator word for word. The twist runs on the workgroup as
+// the word recurrence, 227 words per barrier-separated step (BlockMT).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -219,60 +219,60 @@ __device__ inline void mt_twist_block(uint32_t* mt, int tid) {
     __syncthreads();
 }
 
-// A block-local view of a stream: a ring of MT_RING states in LDS. Slot `head`
-// is the raw state whose tempered words are consumed from `pos`; the next
-// nready-1 slots hold the states after one, two, ... more twists.
-constexpr int MT_RING = 8;
+// A block-local view of a stream as the word sequence x_m of MT19937: the
+// twist is the recurrence x_{m+624} = mix(x_m, x_{m+1}, x_{m+397}), so any 227
+// consecutive new words depend only on older ones and one barrier-separated
+// step of the workgroup extends the sequence by 227 words. The words live in
+// an LDS ring of MT_RW (stream index m at ring[m & (MT_RW - 1)]); m counts from
+// word 0 of the state loaded from HBM. rd = next word to consume, wr = words
+// generated so far.
+constexpr int MT_RW = 8192;
+constexpr int MT_STEP = MT_N - MT_M;  // 227
 struct BlockMT {
-    uint32_t* ring;  // MT_RING * MT_N words of LDS
-    int head;
-    int pos;
-    int nready;
+    uint32_t* ring;  // MT_RW words of LDS
+    int rd;
+    int wr;
 };
 
 __device__ inline void bmt_load(BlockMT& w, const uint32_t* g, uint32_t* lds_ring, int tid) {
     for (int i = tid; i < MT_N; i += RNG_THREADS) lds_ring[i] = g[i];
     w.ring = lds_ring;
-    w.head = 0;
-    w.pos = (int)g[MT_N];
-    w.nready = 1;
+    w.rd = (int)g[MT_N];  // 624: the state is spent, the next word needs the twist
+    w.wr = MT_N;
     __syncthreads();
-    if (w.pos >= MT_N) {
-        mt_twist_block(w.ring, tid);
-        w.pos = 0;
-    }
 }
 
-__device__ inline void bmt_store(const BlockMT& w, uint32_t* g, int tid) {
-    const uint32_t* b0 = w.ring + w.head * MT_N;
-    for (int i = tid; i < MT_N; i += RNG_THREADS) g[i] = b0[i];
-    if (tid == 0) g[MT_N] = (uint32_t)w.pos;
+// extend the sequence by MT_STEP words (every thread of the workgroup)
+__device__ inline void bmt_step(BlockMT& w, int tid) {
+    constexpr int K = MT_RW - 1;
+    const int m = w.wr + tid;
+    if (tid < MT_STEP) w.ring[m & K] = mt_mix(w.ring[(m - MT_N) & K], w.ring[(m - MT_N + 1) & K], w.ring[(m - MT_STEP) & K]);
+    w.wr += MT_STEP;
+    __syncthreads();
 }
 
-// make words [pos, pos + need) addressable (pos + need <= MT_RING * 624)
+// make words [rd, rd + need) addressable (need + 624 + 227 <= MT_RW)
 __device__ inline void bmt_ensure(BlockMT& w, int need, int tid) {
-    while (w.pos + need > MT_N * w.nready) {
-        const uint32_t* src = w.ring + ((w.head + w.nready - 1) % MT_RING) * MT_N;
-        uint32_t* dst = w.ring + ((w.head + w.nready) % MT_RING) * MT_N;
-        for (int i = tid; i < MT_N; i += RNG_THREADS) dst[i] = src[i];
-        __syncthreads();
-        mt_twist_block(dst, tid);
-        ++w.nready;
-    }
+    while (w.rd + need > w.wr) bmt_step(w, tid);
 }
 
-__device__ inline uint32_t bmt_word(const BlockMT& w, int j) {  // j relative to pos
-    const int i = w.pos + j, s = i / MT_N;
-    return mt_temper(w.ring[((w.head + s) % MT_RING) * MT_N + (i - s * MT_N)]);
+__device__ inline uint32_t bmt_word(const BlockMT& w, int j) {  // j relative to rd
+    return mt_temper(w.ring[(w.rd + j) & (MT_RW - 1)]);
 }
 
-__device__ inline void bmt_advance(BlockMT& w, int n) {
-    w.pos += n;
-    while (w.pos >= MT_N && w.nready > 1) {  // pos == MT_N with nothing ready: twist on demand
-        w.head = (w.head + 1) % MT_RING;
-        w.pos -= MT_N;
-        --w.nready;
+__device__ inline void bmt_advance(BlockMT& w, int n) { w.rd += n; }
+
+// back to HBM as (state, index): the state holding word rd (a spent state with
+// index 624 when rd sits on a state boundary), completed first if needed
+__device__ inline void bmt_store(BlockMT& w, uint32_t* g, int tid) {
+    int S = w.rd / MT_N, pos = w.rd - S * MT_N;
+    if (pos == 0 && S > 0) {
+        --S;
+        pos = MT_N;
     }
+    while (w.wr < MT_N * (S + 1)) bmt_step(w, tid);
+    for (int i = tid; i < MT_N; i += RNG_THREADS) g[i] = w.ring[(MT_N * S + i) & (MT_RW - 1)];
+    if (tid == 0) g[MT_N] = (uint32_t)pos;
 }
 
 // random() (two words as res53) from a stream in HBM, for every thread of the
@@ -325,7 +325,7 @@ constexpr int RNG_SCRATCH = 4 * DIR_AP + 1;
 __device__ inline double block_dirichlet_gamma(BlockMT& w, double alpha, int k, double* gam, long long* attempts,
                                                int* scratch, int tid) {
     constexpr int RA = DIR_AP * RNG_THREADS;  // attempts per round
-    static_assert(MT_N - 1 + 4 * RA <= MT_RING * MT_N, "MT ring too small for a round");
+    static_assert(4 * RA + MT_N + MT_STEP <= MT_RW, "MT ring too small for a round");
     const int lane = tid & 63, wave = tid >> 6;
     const double one_m = 1.0 - alpha, inv_a = 1. / alpha;
     int base = 0;
