@@ -93,6 +93,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         m.path_len = 0;
         m.leaf_pending = 0;
         m.pad[0] = 1;  // network rows consumed this move
+        m.pad[1] = 0;  // leaf rows sent to the network this move (Ctr::nn_rows at the choice)
         t.ms[i] = m;
         slots[i].last_value = values[i];
     }
@@ -164,7 +165,7 @@ __global__ __launch_bounds__(64) void k_mcts_select(DevCfg cfg, Tree t, const Sl
             bd[lane] = (int8_t)pos_at(p, lane);  // the board the reference would encode (after getValidMoves)
             m.leaf_pending = 1;
             m.leaf_n = n < MAXM ? n : MAXM;
-            if (lane == 0) atomicAdd(&ctr->nn_rows, 1ull);
+            m.pad[1] += 1;
         }
     }
     if (lane == 0) t.ms[i] = m;
@@ -242,7 +243,6 @@ __global__ __launch_bounds__(64) void k_mcts_backup(DevCfg cfg, Tree t, const Sl
             if (node >= 0) t.n_N[nb + node] += 1;
         }
         t.ms[i] = m;
-        atomicAdd(&ctr->sims, 1ull);
     }
 }
 
@@ -261,6 +261,12 @@ __global__ __launch_bounds__(64) void k_mcts_choose(DevCfg cfg, Tree t, Slot* sl
     __syncthreads();
     if (lane == 0) s_pick = choose_weighted(vals, cum, n, py_mt + (size_t)i * MT_WORDS);
     __syncthreads();
+    // the move's counters in one update per slot (one device-scope atomic per
+    // slot and sim-step on a shared counter cost ~3.5 us per select / backup)
+    if (lane == 0) {
+        atomicAdd(&ctr->sims, (unsigned long long)cfg.sims);
+        atomicAdd(&ctr->nn_rows, (unsigned long long)m.pad[1]);
+    }
     s.last_value = m.root_value;  // resign test on the root's network value (:185)
     s.n_evals += m.pad[0];
     commit_move(cfg, s, i, t.e_move[eb + s_pick], boards, rec, last_board, ctr, lane);
