@@ -36,7 +36,9 @@ struct Slot {
     int end_kind;
     int outcome;
     int reason;
-    int pad[11];
+    int rows_total;   // network rows this slot has appended (all its games; k_count sums them)
+    int plies_total;  // moves this slot has committed (all its games)
+    int pad[9];
 };
 static_assert(sizeof(Slot) == 128, "slot is one cache line");
 
@@ -47,6 +49,7 @@ struct Ctr {
     unsigned long long plies;
     unsigned long long nn_rows;
     unsigned long long sims;
+    unsigned long long nn_rows_slots;  // k_count: sum of Slot::rows_total (nn_rows adds the MCTS leaf rows)
     int active;
     int error;
     int need_eval;  // KV_EVAL_LAZY: some slot consumes a network row this step
@@ -251,7 +254,7 @@ __device__ inline void commit_move(const DevCfg& cfg, Slot& s, int i, int mv, in
     if (lane == 0) {
         make_move_board(board, s.wtm, s.wkr, s.wkc, s.bkr, s.bkc, s.flags, s.ep, mv);
         s.ply += 1;
-        atomicAdd(&ctr->plies, 1ull);
+        s.plies_total += 1;
     }
     __syncthreads();
     const int8_t b2 = sqlane ? board[lane] : 0;

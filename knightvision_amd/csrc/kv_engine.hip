@@ -89,6 +89,39 @@ __global__ void k_init(DevCfg cfg, Slot* slots, int8_t* boards, uint32_t* np_mt,
     slots[i] = s;
 }
 
+// ------------------------------------------------------------- counts ----
+// the per-ply counters from the slots themselves, one workgroup: active slots,
+// and the running sums of the slots' committed plies and appended network rows
+// (per-slot fields instead of one device-scope atomic per slot and kernel on a
+// shared counter, which serialised across the XCDs at ~0.1 us each)
+__global__ __launch_bounds__(256) void k_count(DevCfg cfg, const Slot* slots, Ctr* ctr) {
+    __shared__ unsigned long long red[3][4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    unsigned long long a = 0, rows = 0, pl = 0;
+    for (int j = tid; j < cfg.slots; j += 256) {
+        a += slots[j].status == ST_ACTIVE;
+        rows += (unsigned long long)slots[j].rows_total;
+        pl += (unsigned long long)slots[j].plies_total;
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        a += __shfl_xor(a, m);
+        rows += __shfl_xor(rows, m);
+        pl += __shfl_xor(pl, m);
+    }
+    if (lane == 0) {
+        red[0][wave] = a;
+        red[1][wave] = rows;
+        red[2][wave] = pl;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        ctr->active = (int)(red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+        ctr->nn_rows_slots = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        ctr->plies = red[2][0] + red[2][1] + red[2][2] + red[2][3];
+    }
+}
+
 // ------------------------------------------------------------ movegen ----
 __global__ __launch_bounds__(64) void k_movegen(DevCfg cfg, Slot* slots, int8_t* boards, uint16_t* moves,
                                                 Ctr* ctr) {
@@ -115,7 +148,7 @@ __global__ __launch_bounds__(64) void k_movegen(DevCfg cfg, Slot* slots, int8_t*
         s.buf += 1;
         const bool has = s.has_last || s.need_flush;
         s.consumed = (s.buf >= cfg.batch) || !has;
-        atomicAdd(&ctr->nn_rows, 1ull);
+        s.rows_total += 1;
     }
     if (s.consumed || s.need_flush) ctr->need_eval = 1;  // read by the host in KV_EVAL_LAZY
     slots[i] = s;
@@ -183,10 +216,6 @@ __global__ __launch_bounds__(128) void k_finish(DevCfg cfg, Slot* slots, int8_t*
                                                 uint32_t* np_mt, uint32_t* py_mt, kv_game* games, Ctr* ctr) {
     const int i = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Slot s = slots[i];
-    if (s.status == ST_ACTIVE) {
-        if (tid == 0) atomicAdd(&ctr->active, 1);
-        return;
-    }
     if (s.status != ST_FINISHED) return;
     int8_t* board = boards + (size_t)i * 64;
     // outcome (:210-238)
@@ -239,10 +268,7 @@ __global__ __launch_bounds__(128) void k_finish(DevCfg cfg, Slot* slots, int8_t*
         long long next = -1;
         if (cfg.recycle) {
             const unsigned long long k = atomicAdd(&ctr->next_game, 1ull);
-            if ((long long)k < cfg.n_games) {
-                next = (long long)k;
-                atomicAdd(&ctr->active, 1);
-            }
+            if ((long long)k < cfg.n_games) next = (long long)k;
         }
         s_next = next;
     }
@@ -542,9 +568,10 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
                                       e->st)))
                 return rc;
         }
-        KV_HIP(hipMemsetAsync(&e->ctr->active, 0, sizeof(int), e->st));
         hipLaunchKernelGGL(kv::k_finish, dim3(S), dim3(128), 0, e->st, e->dc, e->slots, e->boards,
                            e->moves, e->np_mt, e->py_mt, e->games, e->ctr);
+        KV_HIP(hipGetLastError());
+        hipLaunchKernelGGL(kv::k_count, dim3(1), dim3(256), 0, e->st, e->dc, e->slots, e->ctr);
         KV_HIP(hipGetLastError());
         ++done;
         ++e->steps;
@@ -607,7 +634,7 @@ int kv_stats_get(kv_engine* e, kv_stats* out) {
     out->steps = e->steps;
     out->plies = (int64_t)e->ctr_host->plies;
     out->games_done = (int64_t)e->ctr_host->games_count;
-    out->nn_rows = (int64_t)e->ctr_host->nn_rows;
+    out->nn_rows = (int64_t)(e->ctr_host->nn_rows + e->ctr_host->nn_rows_slots);
     out->sims = (int64_t)e->ctr_host->sims;
     out->records = (int64_t)e->ctr_host->rec_count;
     out->res_conv_ms = e->nn_res_ms;
