@@ -38,7 +38,8 @@ struct Slot {
     int reason;
     int rows_total;   // network rows this slot has appended (all its games; k_count sums them)
     int plies_total;  // moves this slot has committed (all its games)
-    int pad[9];
+    int movegen_clean;  // k_movegen's getValidMoves left the position as it found it
+    int pad[8];
 };
 static_assert(sizeof(Slot) == 128, "slot is one cache line");
 

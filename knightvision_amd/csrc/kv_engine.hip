@@ -129,11 +129,16 @@ __global__ __launch_bounds__(64) void k_movegen(DevCfg cfg, Slot* slots, int8_t*
     Slot s = slots[i];
     if (s.status != ST_ACTIVE) return;
     int8_t* board = boards + (size_t)i * 64;
-    Pos p = wave_pos(board[lane], s.wtm, s.wkr, s.wkc, s.bkr, s.bkc, s.flags, s.ep);
+    const int8_t before = board[lane];
+    Pos p = wave_pos(before, s.wtm, s.wkr, s.wkc, s.bkr, s.bkc, s.flags, s.ep);
     const int n = wave_valid_moves(p, moves + (size_t)i * MAXM, MAXM, lane);
-    board[lane] = (int8_t)pos_at(p, lane);  // the reference may mutate the board (stale king, double check)
+    const int8_t after = (int8_t)pos_at(p, lane);
+    board[lane] = after;  // the reference may mutate the board (stale king, double check)
+    const bool board_same = __ballot(after != before) == 0ull;
     if (lane != 0) return;
     if (n > MAXM) atomicOr(&ctr->error, 1);
+    s.movegen_clean = board_same && p.wtm == s.wtm && p.wkr == s.wkr && p.wkc == s.wkc && p.bkr == s.bkr &&
+                      p.bkc == s.bkc && p.flags == s.flags && p.ep == s.ep;
     s.wtm = p.wtm;
     s.wkr = p.wkr; s.wkc = p.wkc; s.bkr = p.bkr; s.bkc = p.bkc;
     s.flags = p.flags;
@@ -210,19 +215,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 }
 
 // ------------------------------------------------------------- finish ----
-// two waves per slot: wave 0 scores the game, sets up the next one and seeds
-// its numpy stream while wave 1 seeds the CPython stream (the longer chain)
+// two waves per slot: wave 1 takes the slot's next game and seeds its CPython
+// stream (the longer chain) while wave 0 scores the finished game, then sets up
+// the next one and seeds its numpy stream
 __global__ __launch_bounds__(128) void k_finish(DevCfg cfg, Slot* slots, int8_t* boards, uint16_t* moves,
                                                 uint32_t* np_mt, uint32_t* py_mt, kv_game* games, Ctr* ctr) {
     const int i = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Slot s = slots[i];
     if (s.status != ST_FINISHED) return;
     int8_t* board = boards + (size_t)i * 64;
-    // outcome (:210-238)
+    // the slot's next game first, so that wave 1 seeds its CPython stream (the
+    // longer chain) while wave 0 scores the finished game
+    __shared__ long long s_next;
+    if (tid == 64) {
+        long long next = -1;
+        if (cfg.recycle) {
+            const unsigned long long k = atomicAdd(&ctr->next_game, 1ull);
+            if ((long long)k < cfg.n_games) next = (long long)k;
+        }
+        s_next = next;
+    }
+    __syncthreads();
+    const long long k = s_next;
+    const long long gid = cfg.id_base + k * cfg.id_stride;
+    const unsigned long long sd = cfg.seed + (unsigned long long)gid;
     if (wave == 1) {
-    } else if (s.end_kind == END_MAXED) {
+        if (k >= 0 && cfg.seed_mode == KV_SEED_PER_GAME) wave_seed_python(py_mt + (size_t)i * MT_WORDS, sd, lane);
+        return;
+    }
+    // outcome (:210-238)
+    if (s.end_kind == END_MAXED) {
         s.outcome = 0;
         s.reason = 0;
+    } else if (s.end_kind == END_NOMOVES && s.movegen_clean) {
+        // k_movegen's getValidMoves on this very position found no moves and
+        // rewrote nothing, so both getValidMoves calls of the chain below would
+        // return none on it: inCheck alone decides mate / stalemate
+        const Pos p = wave_pos(board[lane], s.wtm, s.wkr, s.wkc, s.bkr, s.bkc, s.flags, s.ep);
+        const bool chk = in_check(p);
+        s.outcome = chk ? (p.wtm ? -1 : 1) : 0;
+        s.reason = chk ? 2 : 3;
     } else if (s.end_kind != END_RESIGN) {
         Pos p = wave_pos(board[lane], s.wtm, s.wkr, s.wkc, s.bkr, s.bkc, s.flags, s.ep);
         uint16_t* ml = moves + (size_t)i * MAXM;
@@ -246,8 +278,6 @@ __global__ __launch_bounds__(128) void k_finish(DevCfg cfg, Slot* slots, int8_t*
         s.flags = p.flags;
         s.ep = p.ep;
     }
-    __shared__ long long s_next;
-    __syncthreads();
     if (tid == 0) {
         // flush of a non-empty buffer (:202-208): one more forward call
         if (cfg.sims == 0 && s.buf > 0) {
@@ -265,24 +295,10 @@ __global__ __launch_bounds__(128) void k_finish(DevCfg cfg, Slot* slots, int8_t*
         gm.pad = 0;
         games[gi % (unsigned long long)cfg.games_cap] = gm;
         s.status = ST_IDLE;
-        long long next = -1;
-        if (cfg.recycle) {
-            const unsigned long long k = atomicAdd(&ctr->next_game, 1ull);
-            if ((long long)k < cfg.n_games) next = (long long)k;
-        }
-        s_next = next;
     }
-    __syncthreads();
-    const long long k = s_next;
-    if (k >= 0) {  // the slot starts game k: fields by thread 0, board + numpy stream by wave 0, CPython by wave 1
-        const long long gid = cfg.id_base + k * cfg.id_stride;
-        const unsigned long long sd = cfg.seed + (unsigned long long)gid;
-        if (wave == 0) {
-            board[lane] = kStart[lane];
-            if (cfg.seed_mode == KV_SEED_PER_GAME) wave_seed_genrand(np_mt + (size_t)i * MT_WORDS, (uint32_t)sd, lane);
-        } else if (cfg.seed_mode == KV_SEED_PER_GAME) {
-            wave_seed_python(py_mt + (size_t)i * MT_WORDS, sd, lane);
-        }
+    if (k >= 0) {  // the slot starts game k: board + numpy stream by wave 0, fields by thread 0
+        board[lane] = kStart[lane];
+        if (cfg.seed_mode == KV_SEED_PER_GAME) wave_seed_genrand(np_mt + (size_t)i * MT_WORDS, (uint32_t)sd, lane);
         if (tid == 0) start_game_fields(cfg, s, gid);
     }
     if (tid == 0) slots[i] = s;
