@@ -284,6 +284,10 @@ int mcts_select(const DevCfg& cfg, const Tree& t, const Slot* slots, const int8_
                 Ctr* ctr, hipStream_t st, int slot0, int count);
 int mcts_backup(const DevCfg& cfg, const Tree& t, const Slot* slots, const float* logits, const float* values,
                 float* probs, Ctr* ctr, hipStream_t st, int slot0, int count);
+// backup of one sim-step fused with the next sim-step's select
+int mcts_backup_select(const DevCfg& cfg, const Tree& t, const Slot* slots, const int8_t* boards, const float* logits,
+                       const float* values, float* probs, int8_t* nn_boards, Ctr* ctr, hipStream_t st, int slot0,
+                       int count);
 int mcts_choose(const DevCfg& cfg, const Tree& t, Slot* slots, int8_t* boards, uint32_t* py_mt, kv_record* rec,
                 int8_t* last_board, Ctr* ctr, hipStream_t st);
 int hash_eval(const int8_t* boards, int rows, float* logits, float* values, hipStream_t st);

@@ -573,12 +573,14 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
             const kv::Tree& t = e->tree;
             if ((rc = kv::mcts_root(e->dc, t, e->slots, e->moves, e->logits, e->values, e->probs, e->np_mt, e->st)))
                 return rc;
+            if ((rc = kv::mcts_select(e->dc, t, e->slots, e->boards, e->nn_boards, e->ctr, e->st, 0, S))) return rc;
             for (int k = 0; k < e->dc.sims; ++k) {
-                if ((rc = kv::mcts_select(e->dc, t, e->slots, e->boards, e->nn_boards, e->ctr, e->st, 0, S)))
-                    return rc;
                 if ((rc = eng_eval(e, e->nn_boards, S))) return rc;
-                if ((rc = kv::mcts_backup(e->dc, t, e->slots, e->logits, e->values, e->probs, e->ctr, e->st, 0, S)))
-                    return rc;
+                rc = k + 1 < e->dc.sims
+                         ? kv::mcts_backup_select(e->dc, t, e->slots, e->boards, e->logits, e->values, e->probs,
+                                                  e->nn_boards, e->ctr, e->st, 0, S)
+                         : kv::mcts_backup(e->dc, t, e->slots, e->logits, e->values, e->probs, e->ctr, e->st, 0, S);
+                if (rc) return rc;
             }
             if ((rc = kv::mcts_choose(e->dc, t, e->slots, e->boards, e->py_mt, e->rec, e->last_board, e->ctr,
                                       e->st)))

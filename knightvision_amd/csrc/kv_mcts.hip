@@ -99,11 +99,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     }
 }
 
-__global__ __launch_bounds__(64) void k_mcts_select(DevCfg cfg, Tree t, const Slot* slots, const int8_t* boards,
-                                                    int8_t* nn_boards, Ctr* ctr, int slot0) {
+// one slot's select, by the 64 threads of its workgroup
+__device__ inline void mcts_select_slot(const DevCfg& cfg, const Tree& t, const Slot* slots, const int8_t* boards,
+                                        int8_t* nn_boards, Ctr* ctr, int i) {
     __shared__ int8_t bd[64];
     __shared__ int s_meta[8];  // wtm wkr wkc bkr bkc flags ep
-    const int i = slot0 + blockIdx.x, lane = threadIdx.x;
+    const int lane = threadIdx.x;
     const Slot s = slots[i];
     if (s.status != ST_ACTIVE) return;
     bd[lane] = boards[(size_t)i * 64 + lane];
@@ -173,10 +174,11 @@ __global__ __launch_bounds__(64) void k_mcts_select(DevCfg cfg, Tree t, const Sl
     nn_boards[(size_t)i * 64 + lane] = bd[lane];
 }
 
-__global__ __launch_bounds__(64) void k_mcts_backup(DevCfg cfg, Tree t, const Slot* slots, const float* logits,
-                                                    const float* values, float* probs, Ctr* ctr, int slot0) {
+// one slot's backup, by the 64 threads of its workgroup
+__device__ inline void mcts_backup_slot(const DevCfg& cfg, const Tree& t, const Slot* slots, const float* logits,
+                                        const float* values, float* probs, Ctr* ctr, int i) {
     __shared__ float pri[MAXM];
-    const int i = slot0 + blockIdx.x, lane = threadIdx.x;
+    const int lane = threadIdx.x;
     const Slot s = slots[i];
     if (s.status != ST_ACTIVE) return;
     MctsSlot m = t.ms[i];
@@ -246,6 +248,30 @@ __global__ __launch_bounds__(64) void k_mcts_backup(DevCfg cfg, Tree t, const Sl
     }
 }
 
+__global__ __launch_bounds__(64) void k_mcts_select(DevCfg cfg, Tree t, const Slot* slots, const int8_t* boards,
+                                                    int8_t* nn_boards, Ctr* ctr, int slot0) {
+    mcts_select_slot(cfg, t, slots, boards, nn_boards, ctr, slot0 + blockIdx.x);
+}
+
+__global__ __launch_bounds__(64) void k_mcts_backup(DevCfg cfg, Tree t, const Slot* slots, const float* logits,
+                                                    const float* values, float* probs, Ctr* ctr, int slot0) {
+    mcts_backup_slot(cfg, t, slots, logits, values, probs, ctr, slot0 + blockIdx.x);
+}
+
+// backup of sim-step k and select of sim-step k+1 for the same slot in one
+// launch (a slot's next descent depends only on its own tree): one kernel
+// boundary less per sim-step. The barrier orders thread 0's tree writes
+// before the descent reads them (workgroup scope).
+__global__ __launch_bounds__(64) void k_mcts_backup_select(DevCfg cfg, Tree t, const Slot* slots,
+                                                           const int8_t* boards, const float* logits,
+                                                           const float* values, float* probs, int8_t* nn_boards,
+                                                           Ctr* ctr, int slot0) {
+    const int i = slot0 + blockIdx.x;
+    mcts_backup_slot(cfg, t, slots, logits, values, probs, ctr, i);
+    __syncthreads();
+    mcts_select_slot(cfg, t, slots, boards, nn_boards, ctr, i);
+}
+
 __global__ __launch_bounds__(64) void k_mcts_choose(DevCfg cfg, Tree t, Slot* slots, int8_t* boards,
                                                     uint32_t* py_mt, kv_record* rec, int8_t* last_board, Ctr* ctr) {
     __shared__ double vals[MAXM];
@@ -309,6 +335,15 @@ int mcts_backup(const DevCfg& cfg, const Tree& t, const Slot* slots, const float
                 float* probs, Ctr* ctr, hipStream_t st, int slot0, int count) {
     hipLaunchKernelGGL(k_mcts_backup, dim3(count), dim3(64), 0, st, cfg, t, slots, logits, values, probs, ctr,
                        slot0);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+int mcts_backup_select(const DevCfg& cfg, const Tree& t, const Slot* slots, const int8_t* boards, const float* logits,
+                       const float* values, float* probs, int8_t* nn_boards, Ctr* ctr, hipStream_t st, int slot0,
+                       int count) {
+    hipLaunchKernelGGL(k_mcts_backup_select, dim3(count), dim3(64), 0, st, cfg, t, slots, boards, logits, values, probs,
+                       nn_boards, ctr, slot0);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
