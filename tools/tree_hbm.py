@@ -14,7 +14,7 @@ import sqlite3
 import sys
 from collections import defaultdict
 
-KERNELS = ("k_mcts_select", "k_mcts_backup", "k_mcts_root", "k_mcts_choose", "k_movegen")
+KERNELS = ("k_mcts_backup_select", "k_mcts_select", "k_mcts_backup", "k_mcts_root", "k_mcts_choose", "k_movegen")
 PEAK_GBPS = 8000.0
 
 
@@ -50,8 +50,12 @@ def main():
             ns = dur[k][0]
             res["kernels"][k] = {"bytes_per_launch": b, "bytes_per_slot": b / slots, "avg_ns": ns,
                                  "GBps": b / ns, "frac": b / ns / PEAK_GBPS}
+    fused = res["kernels"].get("k_mcts_backup_select")
     sel, bak = res["kernels"].get("k_mcts_select"), res["kernels"].get("k_mcts_backup")
-    if sel and bak:
+    if fused:  # backup of sim-step k + select of k+1, one launch per sim-step
+        res["per_sim"] = {"bytes_per_sim": fused["bytes_per_launch"] / slots, "GBps": fused["GBps"],
+                          "frac": fused["frac"], "note": "k_mcts_backup_select, one backup + one select per slot per launch"}
+    elif sel and bak:
         b = sel["bytes_per_launch"] + bak["bytes_per_launch"]
         ns = sel["avg_ns"] + bak["avg_ns"]
         res["per_sim"] = {"bytes_per_sim": b / slots, "GBps": b / ns, "frac": b / ns / PEAK_GBPS,
