@@ -229,7 +229,7 @@ def main():
     if mcts and os.path.exists(tp):
         tj = json.load(open(tp))
         if tj.get("slots") == G and "per_sim" in tj:
-            tree_hbm = {"kernels": "k_mcts_backup_select (backup of sim-step k + select of k+1)", "bytes_per_sim": tj["per_sim"]["bytes_per_sim"],
+            tree_hbm = {"kernels": tj["per_sim"].get("note", "k_mcts_select + k_mcts_backup"), "bytes_per_sim": tj["per_sim"]["bytes_per_sim"],
                         "achieved_GBps": tj["per_sim"]["GBps"], "peak_GBps": tj["peak_GBps"],
                         "frac": tj["per_sim"]["frac"], "source": os.path.relpath(tp, HERE),
                         "note": "latency-bound: one wave per game; 16 KB of the ~21 KB/sim is the leaf's 4096 logits"}
