@@ -350,6 +350,9 @@ struct kv_engine {
 };
 
 static int eng_counters(kv_engine* e) {
+    // active slots / plies / rows are summed from the slots only when the host reads them
+    hipLaunchKernelGGL(kv::k_count, dim3(1), dim3(256), 0, e->st, e->dc, e->slots, e->ctr);
+    KV_HIP(hipGetLastError());
     KV_HIP(hipMemcpyAsync(e->ctr_host, e->ctr, sizeof(kv::Ctr), hipMemcpyDeviceToHost, e->st));
     KV_HIP(hipStreamSynchronize(e->st));
     if (e->ctr_host->error) {
@@ -588,8 +591,6 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
         }
         hipLaunchKernelGGL(kv::k_finish, dim3(S), dim3(128), 0, e->st, e->dc, e->slots, e->boards,
                            e->moves, e->np_mt, e->py_mt, e->games, e->ctr);
-        KV_HIP(hipGetLastError());
-        hipLaunchKernelGGL(kv::k_count, dim3(1), dim3(256), 0, e->st, e->dc, e->slots, e->ctr);
         KV_HIP(hipGetLastError());
         ++done;
         ++e->steps;
