@@ -2,24 +2,36 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--mode mcts|ref] ...
 
-One step = one ply-step of every concurrent game slot on a GPU (sims > 0: the
-full PUCT search of every slot's current move -- `sims` network batches --
-then the move; ref: one network row per slot, then the reference's sampled
-move). Inputs are synthetic: build-defined random-init weights (seed 42,
-knightvision_amd.weights), games from the initial position, per-game seeds
-42 + global game id, slots recycled so every step is steady state.
+Workload (BASELINE.json configs[2], C3 -- the largest single-GPU config):
+2,048 concurrent games per GPU, 800 PUCT simulations per move, fp32 ChessNet
+(the reference's precision), batch-2048 network evaluation, random-init
+synthetic weights (seed 42, knightvision_amd.weights), games from the initial
+position with per-game seeds 42 + global game id, slots recycled.
 
-N > 1: launched by torch.distributed.run, one process per GPU; games are
-sharded by global id (weak scaling, no collective in the loop); the timed
-region is bracketed by barrier + synchronize and the max over ranks is used.
-After the timed region the ranks all-gather their experience records over
-RCCL (reported as gather_ms, not part of `value`).
+One step = one move of every slot: the full search (800 sim-steps, each one
+2,048-board network batch + the tree kernels) and the committed move. The
+timed region covers plies W+1 .. W+K of games started at the initial position;
+no MCTS game finishes inside it at the default K, so MCTS games/hour is
+reported only when games actually completed (else null), and the measured
+games/hour comes from the C3-ref block: the reference's own move selection
+(sims = 0, one network row per ply, softmax + Dirichlet + random.choices) on
+the same 2,048 slots, long enough for thousands of games to complete.
+
+N > 1: `bench.py --gpus N` starts N ranks itself (torch.distributed.run as a
+child process, before any GPU call), or runs under an external
+torch.distributed.run; one process per GPU, games sharded by global id (weak
+scaling, no collective in the loop); the timed region is bracketed by barrier
++ synchronize and the max over ranks is used. After the timed region the
+ranks gather their device-resident experience records to rank 0 over RCCL
+(gather_ms, not part of `value`).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -43,47 +55,80 @@ def parse():
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--mode", choices=["mcts", "ref"], default=os.environ.get("KV_BENCH_MODE", "mcts"))
-    ap.add_argument("--slots", type=int, default=256)
-    ap.add_argument("--sims", type=int, default=400)
+    ap.add_argument("--slots", type=int, default=2048)
+    ap.add_argument("--sims", type=int, default=800)
     ap.add_argument("--precision", choices=["fp32", "f16x3", "bf16x6", "bf16x3"], default="fp32")
     ap.add_argument("--algo", choices=["auto", "direct", "winograd", "winograd48"], default="auto",
                     help="conv algorithm of the fp32 tower (auto: Winograd F(4x8,3x3) above 16 boards)")
-    ap.add_argument("--compare-direct", type=int, default=1,
-                    help="also measure the fp32 direct implicit-GEMM convs (reported under 'fp32_direct')")
+    ap.add_argument("--compare-direct", type=int, default=0,
+                    help="also measure the fp32 direct implicit-GEMM and F(4x4) towers ('fp32_direct', "
+                         "'fp32_winograd44'; ~40 s per step at C3)")
     ap.add_argument("--alt-precision", default="f16x3",
                     help="also measure this network precision (reported under 'alt_precision'; '' to skip)")
+    ap.add_argument("--alt-steps", type=int, default=2)
+    ap.add_argument("--alt-warmup", type=int, default=1)
     ap.add_argument("--ref-block", type=int, default=1,
-                    help="mcts mode: also run the reference's own move selection (sims=0, C2-ref) long enough for "
-                         "games to complete, reported under 'ref_selection' with measured games/hour")
+                    help="mcts mode: also run the reference's own move selection (sims=0) on the same slots long "
+                         "enough for games to complete, reported under 'ref_selection' with measured games/hour")
+    ap.add_argument("--ref-steps", type=int, default=1200)
+    ap.add_argument("--ref-warmup", type=int, default=600)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without an external launcher: run N ranks under
+    torch.distributed.run as a child process (nothing here has touched the GPU;
+    rank 0 prints the JSON line) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
+def host_cpu() -> dict:
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count()
+    return {"cpu": cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": aff,
+            "torch_threads": torch.get_num_threads()}
+
+
 def cpu_baseline(seconds: float, sims: int):
-    """The oracle restatement (C rules + RNG + reference eval schedule) with the
-    reference's network run by torch on the host CPU, faithful one-eval-per-ply
-    (test infrastructure; never the measured product)."""
+    """The oracle restatement (C rules + RNG + the reference's eval schedule /
+    the build's PUCT restatement) with the reference's network run by torch on
+    the host CPU (test infrastructure; never the measured product). MCTS: the
+    same sims/move as the GPU, one leaf per network call."""
     from oracle import oracle as O
     from oracle import torch_ref
     from knightvision_amd.weights import synthetic_state_dict
     ev = torch_ref.make_eval_fn(synthetic_state_dict(42, "init"))
+    host = host_cpu()
     t0 = time.perf_counter()
     plies = games = 0
     seed = 42
     if sims > 0:
-        s_cpu = min(sims, 64)
         done = 0
         while time.perf_counter() - t0 < seconds:
-            r = O.mcts_play_game(s_cpu, O.MT(seed, "numpy"), O.MT(seed, "python"), ev, max_moves=2,
-                                 softmax_fn=torch_ref.torch_softmax)
-            done += r["plies"] * s_cpu
+            r = O.mcts_play_game(sims, O.MT(seed, "numpy"), O.MT(seed, "python"), ev, max_moves=1)
+            done += r["plies"] * sims
             games += 1
             seed += 1
         dt = time.perf_counter() - t0
-        return dict(value=done / dt, unit="sims/s", cores=torch.get_num_threads(), cpu=cpu_model(), kind="port",
-                    sample=f"{games} games x 2 moves x {s_cpu} sims (per-game seeds 42+), oracle PUCT restatement "
-                           f"+ torch-CPU ChessNet fp32, one leaf per network call, {dt:.1f}s")
+        return dict(value=done / dt, unit="sims/s", cores=host["torch_threads"], kind="port", **host,
+                    sample=f"{games} games x 1 move x {sims} sims (per-game seeds 42+), oracle PUCT restatement "
+                           f"+ torch-CPU ChessNet fp32 on {host['torch_threads']} threads, one leaf per network "
+                           f"call, {dt:.1f}s")
     while time.perf_counter() - t0 < seconds:
         r = O.play_game(ev, O.MT(seed, "numpy"), O.MT(seed, "python"), O.Last(), max_moves=64, batch=16,
                         softmax_fn=torch_ref.torch_softmax)
@@ -91,9 +136,9 @@ def cpu_baseline(seconds: float, sims: int):
         games += 1
         seed += 1
     dt = time.perf_counter() - t0
-    return dict(value=plies / dt, unit="plies/s", cores=torch.get_num_threads(), cpu=cpu_model(), kind="port",
+    return dict(value=plies / dt, unit="plies/s", cores=host["torch_threads"], kind="port", **host,
                 sample=f"{games} games x <=64 plies (per-game seeds 42+), oracle rules/RNG + torch-CPU "
-                       f"ChessNet fp32, batch-16 reference schedule, {dt:.1f}s")
+                       f"ChessNet fp32 on {host['torch_threads']} threads, batch-16 reference schedule, {dt:.1f}s")
 
 
 def cpu_model() -> str:
@@ -106,38 +151,73 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def _pmc_traffic(kname: str, bpl: int):
+    """HBM bytes per launch of the dominant kernel at this batch from the newest
+    committed PMC summary (tools/pmc_summary.py), or None."""
+    for f in sorted((x for x in os.listdir(os.path.join(HERE, "profiles")) if "pmc" in x and x.endswith(".json")),
+                    reverse=True):
+        try:
+            pj = json.load(open(os.path.join(HERE, "profiles", f)))
+        except (OSError, ValueError):
+            continue
+        if (isinstance(pj, dict) and pj.get("batch") == bpl and
+                pj.get("kernel", "").replace(" ", "") == kname and "hbm_bytes_per_launch" in pj):
+            return pj["hbm_bytes_per_launch"], f
+    return None, None
+
+
+def _tree_pmc(G: int):
+    """Tree-kernel HBM summary (tools/tree_hbm.py) for this slot count, newest round first."""
+    for f in sorted((x for x in os.listdir(os.path.join(HERE, "profiles")) if x.endswith(".json") and "pmc_tree" in x),
+                    reverse=True):
+        tj = json.load(open(os.path.join(HERE, "profiles", f)))
+        if tj.get("slots") == G and "per_sim" in tj:
+            return tj, f
+    return None, None
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
     # one rank per GPU; more ranks than GPUs (a rehearsal of the sharded path on a 1-GPU box, with
     # KV_BENCH_BACKEND=gloo since RCCL refuses two ranks on one device) share the devices round-robin
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     import torch.distributed as dist
+    backend = None
     if world > 1:
         backend = os.environ.get("KV_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
     from knightvision_amd.engine import SelfPlayEngine
     from knightvision_amd.weights import synthetic_state_dict
     from knightvision_amd.distributed import gather_experience
 
     mcts = args.mode == "mcts"
     sims = args.sims if mcts else 0
-    steps = args.steps if args.steps is not None else (2 if mcts else 40)
-    warmup = args.warmup if args.warmup is not None else (1 if mcts else 8)
+    steps = args.steps if args.steps is not None else (2 if mcts else 600)
+    warmup = args.warmup if args.warmup is not None else (1 if mcts else 300)
     G = args.slots
+    dev = torch.device("cuda", local)
 
-    def measure(precision, algo="auto", sims=sims, steps=steps, warmup=warmup):
+    def measure(precision, algo="auto", sims=sims, steps=steps, warmup=warmup, keep=False):
         eng = SelfPlayEngine(synthetic_state_dict(42, "init"), slots=G, n_games=1 << 40, seed=42, max_moves=None,
                              batch=16, sims=sims, game_id_base=rank, game_id_stride=world,
                              record_cap=max(1 << 16, G * (steps + warmup + 8)), device=local, precision=precision,
                              algo=algo)
         eng.run(warmup)
         s0 = eng.stats()
+        eng.reset_records()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -148,57 +228,54 @@ def main():
             dist.barrier()
         dt = time.perf_counter() - t0
         s1 = eng.stats()
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
         d = {k: s1[k] - s0[k] for k in ("plies", "games_done", "nn_rows", "sims", "res_conv_ms", "res_conv_launches")}
-        tot = torch.tensor([d["plies"], d["games_done"], d["nn_rows"], d["sims"]], dtype=torch.float64, device="cuda")
+        tot = torch.tensor([d["plies"], d["games_done"], d["nn_rows"], d["sims"]], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(tot)
         plies, games_done, nn_rows, sims_done = (float(x) for x in tot.tolist())
-        recs, gms = eng.records(), eng.games()
+        out = dict(dt=dt, plies=plies, games_done=games_done, nn_rows=nn_rows, sims=sims_done,
+                   conv_ms=d["res_conv_ms"] / max(d["res_conv_launches"], 1), dom_flop=s1["dom_flop"],
+                   dom_algo=s1["dom_algo"], tree_overflows=s1["tree_overflows"], steps=steps, warmup=warmup)
+        if keep:  # the timed region's experience, left in HBM for the gather
+            out["recs_dev"], out["gms"] = eng.records_device(), eng.games()
         eng.close()
-        launches = max(d["res_conv_launches"], 1)
-        conv_ms = d["res_conv_ms"] / launches
-        return dict(dt=dt, plies=plies, games_done=games_done, nn_rows=nn_rows, sims=sims_done, conv_ms=conv_ms,
-                    recs=recs, gms=gms, dom_flop=s1["dom_flop"], dom_algo=s1["dom_algo"])
+        return out
 
-    m = measure(args.precision, args.algo)
+    m = measure(args.precision, args.algo, keep=True)
     dt, plies, games_done, nn_rows, sims_done, conv_ms = (m[k] for k in ("dt", "plies", "games_done", "nn_rows",
                                                                           "sims", "conv_ms"))
+
+    # end-of-iteration experience gather to rank 0 (RCCL over xGMI from HBM), outside `value`
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    tg = time.perf_counter()
+    recs_all, gms_all = gather_experience(m.pop("recs_dev"), m["gms"], dst=0)
+    gather_ms = (time.perf_counter() - tg) * 1e3 if world > 1 else None
+    n_records = int(len(recs_all)) if recs_all is not None else 0
+
     alt = None
     if args.alt_precision and args.alt_precision != args.precision:
-        alt = measure(args.alt_precision)
+        alt = measure(args.alt_precision, steps=args.alt_steps, warmup=args.alt_warmup)
     refsel = None
     if mcts and args.ref_block:
-        # C2-ref: the reference's move selection (one network row per ply, sampled move) on the same slots;
-        # 1,200 warm-up ply-steps fill the slots with games at every stage, the 2,400 timed ones complete
-        # games at the steady-state rate
-        refsel = measure(args.precision, sims=0, steps=2400, warmup=1200)
-    wino44 = None
+        # C3-ref: the reference's move selection (one network row per ply, sampled move) on the same slots;
+        # the warm-up ply-steps fill the slots with games at every stage, the timed ones complete games at
+        # the steady-state rate
+        refsel = measure(args.precision, sims=0, steps=args.ref_steps, warmup=args.ref_warmup)
+    wino44 = direct = None
     if args.compare_direct and args.precision == "fp32" and m["dom_algo"] == 3:
-        wino44 = measure("fp32", "winograd")
-    direct = None
+        wino44 = measure("fp32", "winograd", steps=1, warmup=1)
     if args.compare_direct and args.precision == "fp32" and m["dom_algo"] in (2, 3):
-        direct = measure("fp32", "direct")
-
-    # experience gather (RCCL all-gather of packed records), outside `value`
-    recs, gms = m["recs"], m["gms"]
-    torch.cuda.synchronize()
-    tg = time.perf_counter()
-    if world > 1:
-        recs_all, gms_all = gather_experience(recs, gms)
-    else:
-        recs_all, gms_all = recs, gms
-    gather_ms = (time.perf_counter() - tg) * 1e3
-    mean_len = float(gms_all["plies"].mean()) if len(gms_all) else float("nan")
+        direct = measure("fp32", "direct", steps=1, warmup=1)
 
     # roofline of the dominant kernel, timed with HIP events on the engine stream: the residual-tower
-    # Winograd GEMM launch (36 x [4*boards x 512 x 512]) or, for the direct algorithm, the residual conv
+    # Winograd GEMM launch (60 x [2*boards x 512 x 512]) or, for the direct algorithm, the residual conv
     algo = m["dom_algo"]  # 1 direct, 2 Winograd F(4x4), 3 Winograd F(4x8)
-    wino = algo in (2, 3)
-    # boards one measured launch covers; padding rows are not algorithmic work
     per_board = {2: FLOP_WINO_GEMM_PER_BOARD, 3: FLOP_WINO48_GEMM_PER_BOARD}.get(algo, FLOP_RES_CONV_PER_BOARD)
     bpl = min(G, int(round(m["dom_flop"] / per_board))) if m["dom_flop"] else G
     flop_alg = per_board * bpl
@@ -214,25 +291,18 @@ def main():
         kdesc = " (residual-tower Winograd F(4x4,3x3) GEMMs)"
     else:
         kname, kdesc = "conv3x3_kernel<512,32>", " (residual-tower 3x3 conv, implicit GEMM)"
-    traffic = None
-    pmc = os.path.join(HERE, "profiles", {2: "r01_pmc_wino_gemm.json", 3: "r01_pmc_wino48_gemm.json"}
-                       .get(algo, "r01_pmc_resconv.json"))
-    if os.path.exists(pmc):
-        pj = json.load(open(pmc))
-        if pj.get("batch") == bpl and pj.get("kernel", "").replace(" ", "") == kname:
-            traffic = pj.get("hbm_bytes_per_launch")
+    traffic, traffic_src = _pmc_traffic(kname, bpl)
 
     # HBM side of the search (north_star: tree kernels as a fraction of the HBM roofline), from the
     # rocprofv3 PMC + kernel-trace summary committed for this slot count (tools/tree_hbm.py)
     tree_hbm = None
-    tp = os.path.join(HERE, "profiles", {256: "r01_pmc_tree_c2_256.json", 2048: "r01_pmc_tree_c3_2048.json"}.get(G, "-"))
-    if mcts and os.path.exists(tp):
-        tj = json.load(open(tp))
-        if tj.get("slots") == G and "per_sim" in tj:
-            tree_hbm = {"kernels": tj["per_sim"].get("note", "k_mcts_select + k_mcts_backup"), "bytes_per_sim": tj["per_sim"]["bytes_per_sim"],
-                        "achieved_GBps": tj["per_sim"]["GBps"], "peak_GBps": tj["peak_GBps"],
-                        "frac": tj["per_sim"]["frac"], "source": os.path.relpath(tp, HERE),
-                        "note": "latency-bound: one wave per game; 16 KB of the ~21 KB/sim is the leaf's 4096 logits"}
+    tj, tf = _tree_pmc(G)
+    if mcts and tj is not None:
+        tree_hbm = {"kernels": tj["per_sim"].get("note", "k_mcts_select + k_mcts_backup"),
+                    "bytes_per_sim": tj["per_sim"]["bytes_per_sim"], "achieved_GBps": tj["per_sim"]["GBps"],
+                    "peak_GBps": tj["peak_GBps"], "frac": tj["per_sim"]["frac"],
+                    "source": "profiles/" + tf,
+                    "note": "latency-bound: one wave per game (select descent + leaf getValidMoves, backup)"}
 
     if rank == 0:
         if mcts:
@@ -240,30 +310,36 @@ def main():
         else:
             metric, unit, value = "self-play plies/sec + games/hour (reference move selection, sims=0)", \
                 "plies/s", plies / dt
-        # games/hour: plies/s over the mean game length -- measured when >= 20 games completed in the
-        # run, else the reference's measured mean of 371 plies/game (random-init weights)
-        if len(gms_all) >= 20:
-            basis, glen = f"measured mean over {len(gms_all)} games", mean_len
-        else:
-            basis, glen = "reference mean game length 371 plies (SURVEY.md 6)", 371.0
-        games_per_hour = plies / dt * 3600.0 / glen
+        mean_len = float(gms_all["plies"].mean()) if gms_all is not None and len(gms_all) else None
+        gph = games_done / dt * 3600.0 if games_done > 0 else None
+        wl = (f"{G} concurrent games/GPU, {sims} sims/move, batch-{G} NN eval, fp32" if mcts else
+              f"{G} concurrent games/GPU, reference move selection (sims=0), batch-{G} NN eval, fp32")
         out = {
             "metric": metric, "value": value, "unit": unit, "n_gpus": world, "steps": steps, "warmup": warmup,
             "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": args.precision, "data": "synthetic (random-init weights seed 42, self-play from the start position)",
-            "config": {"workload": f"{G} concurrent games/GPU, {'%d sims/move' % sims if mcts else 'reference sampled move (sims=0)'}, "
-                                   f"batch-{G} NN eval, faithful one-eval-per-position",
-                       "slots_per_gpu": G, "sims_per_move": sims, "nn_batch": G, "parallelism": f"games sharded x{world}"},
-            "plies_per_s": plies / dt, "games_per_hour": games_per_hour, "games_per_hour_basis": basis,
-            "mean_plies_per_game": mean_len if mean_len == mean_len else None,
+            "dtype": args.precision,
+            "data": "synthetic (random-init weights seed 42, self-play from the start position, per-game seeds)",
+            "config": {"workload": wl + (" (BASELINE configs[2], C3)" if (mcts and G == 2048 and sims == 800) else ""),
+                       "slots_per_gpu": G, "sims_per_move": sims, "nn_batch": G, "parallelism": f"games sharded x{world}",
+                       "step": "one move of every slot (the whole search + the committed move)" if mcts else
+                               "one ply of every slot"},
+            "plies_per_s": plies / dt, "games_per_hour": gph,
+            "games_per_hour_note": ("games completed inside the timed region / its duration" if gph is not None else
+                                    f"no game completed inside the {steps} timed moves (plies {warmup + 1}-"
+                                    f"{warmup + steps} of games from the start position); measured games/hour: "
+                                    f"ref_selection"),
             "games_completed": games_done, "nn_evals_per_s": nn_rows / dt,
             "nn_tflops": nn_rows * FLOP_PER_EVAL / dt / 1e12, "gather_ms": gather_ms,
-            "records_gathered": int(len(recs_all)),
+            "gather": ("RCCL gather to rank 0 of the timed region's device-resident records" if world > 1 else
+                       "none at N=1 (no collective)"),
+            "records_gathered": n_records, "mean_plies_per_game": mean_len,
+            "tree_overflows": m["tree_overflows"],
             "roofline": {"bound": "mfma",
                          "kernel": kname + kdesc,
                          "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None,
-                         "traffic": traffic, "avg_launch_ms": conv_ms, "boards_per_launch": bpl,
+                         "traffic": traffic, "traffic_source": ("profiles/" + traffic_src) if traffic_src else None,
+                         "avg_launch_ms": conv_ms, "boards_per_launch": bpl,
                          "flop_per_launch": flop_alg, "mfma_flop_per_launch_incl_padding": m["dom_flop"],
                          "direct_conv_equiv_tflops": (FLOP_RES_CONV_PER_BOARD * bpl / (conv_ms * 1e-3) / 1e12
                                                       if conv_ms > 0 else None)},
@@ -275,7 +351,7 @@ def main():
             out["fp32_direct"] = {
                 "note": "same fp32 network with the direct implicit-GEMM convs (exact fp32 products, 9 taps)",
                 "value": (direct["sims"] if mcts else direct["plies"]) / direct["dt"], "unit": unit,
-                "ms_per_step": direct["dt"] * 1e3 / steps,
+                "ms_per_step": direct["dt"] * 1e3 / direct["steps"],
                 "res_conv_avg_launch_ms": direct["conv_ms"], "res_conv_tflops": d_ach,
                 "res_conv_frac": (d_ach / FP32_MFMA_PEAK_TFLOPS) if d_ach else None}
         if wino44 is not None:
@@ -283,7 +359,7 @@ def main():
             out["fp32_winograd44"] = {
                 "note": "same fp32 network with the Winograd F(4x4,3x3) tower (36 points, 4 tiles per board)",
                 "value": (wino44["sims"] if mcts else wino44["plies"]) / wino44["dt"], "unit": unit,
-                "ms_per_step": wino44["dt"] * 1e3 / steps, "res_gemm_avg_launch_ms": wino44["conv_ms"],
+                "ms_per_step": wino44["dt"] * 1e3 / wino44["steps"], "res_gemm_avg_launch_ms": wino44["conv_ms"],
                 "res_gemm_tflops": w_ach, "res_gemm_frac": (w_ach / FP32_MFMA_PEAK_TFLOPS) if w_ach else None}
         if alt is not None:
             # dominant launch of the alternate run (Winograd GEMM or direct residual conv), fp32-equivalent FLOPs
@@ -293,17 +369,17 @@ def main():
                 "f16x3": "fp32-accurate split: every fp32 operand scaled by an exact power of two (per layer for "
                          "the weights, per board for the activations) and split into 2 fp16 pieces (22 significant "
                          "bits), the 3 piece products of weight >= 2^-22 on f16 MFMA, fp32 accumulation, Winograd "
-                         "F(4x8) tower; batch-invariant; logits within the fp32 tolerance (tests/test_nn_gpu.py)",
+                         "F(4x8) tower; batch-invariant; logits within the fp32 tolerance (tests/test_nn_gpu.py); "
+                         "narrower operands than the reference's fp32, so never the headline",
                 "bf16x6": "fp32-accurate split: every fp32 operand = 3 exact bf16 pieces, the 6 piece products of "
-                          "weight >= 2^-16 on bf16 MFMA, fp32 accumulation, Winograd tower; max |dlogit| 6.0e-6 on the "
-                          "peaked weights (fp32 Winograd 7.2e-6, fp32 direct 5.2e-6; tolerance 1e-4)",
-                "bf16x3": "convs 2-12 as bf16 hi/lo split, 3 bf16 MFMAs per product, fp32 accumulation, direct conv; "
-                          "max |dlogit| 2.4e-5 (tolerance 1e-4)",
+                          "weight >= 2^-16 on bf16 MFMA, fp32 accumulation, Winograd tower",
+                "bf16x3": "convs 2-12 as bf16 hi/lo split, 3 bf16 MFMAs per product, fp32 accumulation, direct conv",
                 "fp32": "exact f32 MFMA"}
             out["alt_precision"] = {
                 "precision": args.alt_precision, "note": notes.get(args.alt_precision, ""),
                 "value": (alt["sims"] if mcts else alt["plies"]) / alt["dt"], "unit": unit,
-                "ms_per_step": alt["dt"] * 1e3 / steps, "plies_per_s": alt["plies"] / alt["dt"],
+                "steps": alt["steps"], "warmup": alt["warmup"],
+                "ms_per_step": alt["dt"] * 1e3 / alt["steps"], "plies_per_s": alt["plies"] / alt["dt"],
                 "nn_tflops_fp32_equiv": alt["nn_rows"] * FLOP_PER_EVAL / alt["dt"] / 1e12,
                 "dominant_kernel": ({"f16x3": "wino_gemm_h3_kernel<512,2,60,1>" if alt["dom_algo"] == 3
                                      else "wino_gemm_h3_kernel<512,2,36,2>",
@@ -313,15 +389,15 @@ def main():
                 "dominant_avg_launch_ms": alt["conv_ms"], "dominant_tflops_fp32_equiv": a_ach,
                 "dominant_bf16_mfma_frac": (a_ach * a_prod / BF16_MFMA_PEAK_TFLOPS) if (a_ach and a_prod) else None}
         if refsel is not None:
-            g = refsel["gms"]
-            rl = float(g["plies"].mean()) if len(g) else float("nan")
             out["ref_selection"] = {
-                "note": "C2-ref: the reference's own move selection (sims=0: one network row per ply, softmax + "
-                        "Dirichlet + random.choices) on the same slots, uncapped games, slots recycled; "
-                        "games/hour counts games completed inside the timed region",
-                "plies_per_s": refsel["plies"] / refsel["dt"], "games_per_hour": refsel["games_done"] / refsel["dt"] * 3600.0,
-                "games_completed": refsel["games_done"], "timed_s": refsel["dt"], "steps": 2400, "warmup": 1200,
-                "mean_plies_per_game": rl if rl == rl else None,
+                "note": f"C{'3' if G == 2048 else '2' if G == 256 else ''}-ref: the reference's own move selection "
+                        "(sims=0: one network row per ply, softmax + Dirichlet + random.choices) on the same "
+                        f"{G} slots, uncapped games, slots recycled; games/hour counts games completed inside the "
+                        "timed region",
+                "slots": G, "plies_per_s": refsel["plies"] / refsel["dt"],
+                "games_per_hour": refsel["games_done"] / refsel["dt"] * 3600.0,
+                "games_completed": refsel["games_done"], "timed_s": refsel["dt"], "steps": refsel["steps"],
+                "warmup": refsel["warmup"],
                 "reference_cpu": {"plies_per_s": 250.0, "games_per_hour": 2424.0,
                                   "source": "BASELINE.md: reference self_play.py (SELFPLAY_SEQ=1) on 8 Xeon cores"}}
             cal = os.path.join(HERE, "profiles", "r01_cpu_calibration.json")
@@ -342,7 +418,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -127,7 +127,12 @@ typedef struct {
     int recycle;          /* 1: a finished slot starts the next game id */
     int precision;        /* KV_PREC_* of the network convs */
     int algo;             /* KV_ALGO_* of the network convs */
+    int tree_edge_cap;    /* MCTS edges per slot; <= 0: KV_MAXM x (sims + 1), which cannot overflow. An
+                             expansion that does not fit raises KV_EOVERFLOW (kv_stats.tree_overflows) */
+    int keep_root_visits; /* 1: keep each MCTS move's root visit counts for kv_root_visits (tests) */
 } kv_config;
+
+#define KV_MAXM 320 /* move-list capacity per position */
 
 typedef struct {
     int64_t game_id;
@@ -161,6 +166,7 @@ typedef struct {
     double step_ms;       /* wall time inside kv_run */
     double dom_flop;      /* MFMA FLOPs of one measured launch (padded rows included) */
     int64_t dom_algo;     /* KV_ALGO_DIRECT, KV_ALGO_WINOGRAD or KV_ALGO_WINOGRAD48 for those launches */
+    int64_t tree_overflows; /* MCTS expansions dropped for a full edge pool (each also fails kv_run) */
 } kv_stats;
 
 typedef struct kv_engine kv_engine;
@@ -173,11 +179,21 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games);
 /* max_moves for games from now on (_run_single_game's max_moves argument) */
 int kv_set_max_moves(kv_engine* e, int max_moves);
 int kv_records(kv_engine* e, kv_record* out, size_t cap, size_t* n);
+/* The same records, unsorted (allocation order), copied device-to-device into
+ * out_dev (a device buffer of cap records on the engine's GPU) on `stream`:
+ * the experience stays in HBM for the RCCL gather. out_dev
+ * NULL: only *n. */
+int kv_records_device(kv_engine* e, kv_record* out_dev, size_t cap, size_t* n, void* stream);
 /* finished games (the last 2^20 at most), ordered by game id */
 int kv_games(kv_engine* e, kv_game* out, size_t cap, size_t* n);
 /* drop the records collected so far (between kv_run calls) */
 int kv_reset_records(kv_engine* e);
 int kv_stats_get(kv_engine* e, kv_stats* out);
+/* MCTS root visit counts of every committed move (keep_root_visits = 1):
+ * out [n][KV_MAXM] in root move-list order, -1 padded, rows in kv_records'
+ * order. No reference counterpart (the reference has no search); used by the
+ * parity tests against the oracle's PUCT restatement. */
+int kv_root_visits(kv_engine* e, int32_t* out, size_t cap, size_t* n);
 int kv_sync(kv_engine* e);
 void kv_destroy(kv_engine* e);
 

@@ -20,7 +20,8 @@ class Config(C.Structure):
                 ("game_id_stride", C.c_int64), ("seed", C.c_uint64), ("seed_mode", C.c_int),
                 ("max_moves", C.c_int), ("batch", C.c_int), ("eps", C.c_double), ("alpha", C.c_double),
                 ("sims", C.c_int), ("c_puct", C.c_float), ("eval_mode", C.c_int), ("record_cap", C.c_int64),
-                ("recycle", C.c_int), ("precision", C.c_int), ("algo", C.c_int)]
+                ("recycle", C.c_int), ("precision", C.c_int), ("algo", C.c_int), ("tree_edge_cap", C.c_int),
+                ("keep_root_visits", C.c_int)]
 
 
 class Record(C.Structure):
@@ -37,7 +38,7 @@ class Stats(C.Structure):
     _fields_ = [("steps", C.c_int64), ("plies", C.c_int64), ("games_done", C.c_int64), ("nn_rows", C.c_int64),
                 ("sims", C.c_int64), ("records", C.c_int64), ("res_conv_ms", C.c_double),
                 ("res_conv_launches", C.c_int64), ("step_ms", C.c_double), ("dom_flop", C.c_double),
-                ("dom_algo", C.c_int64)]
+                ("dom_algo", C.c_int64), ("tree_overflows", C.c_int64)]
 
 
 class PgnRecord(C.Structure):
@@ -45,6 +46,7 @@ class PgnRecord(C.Structure):
 
 
 PGN_OUTCOME_NONE = -128
+MAXM = 320  # KV_MAXM, move-list capacity per position
 
 assert C.sizeof(Record) == 80 and C.sizeof(Game) == 32 and C.sizeof(PgnRecord) == 120
 
@@ -72,6 +74,8 @@ def _declare(L):
         "kv_records": ([vp, P(Record), sz, P(sz)], i),
         "kv_games": ([vp, P(Game), sz, P(sz)], i),
         "kv_stats_get": ([vp, P(Stats)], i),
+        "kv_root_visits": ([vp, P(C.c_int32), sz, P(sz)], i),
+        "kv_records_device": ([vp, vp, sz, P(sz), vp], i),
         "kv_sync": ([vp], i),
         "kv_reset_records": ([vp], i),
         "kv_destroy": ([vp], None),
@@ -99,7 +103,7 @@ def _declare(L):
 EXPORTED = ["kv_last_error", "kv_version", "kv_net_packed_size", "kv_net_create", "kv_net_load", "kv_net_forward",
             "kv_net_forward_boards", "kv_net_set_timing", "kv_net_last_timing", "kv_net_destroy", "kv_net_set_precision", "kv_net_set_algo",
             "kv_create",
-            "kv_load_weights", "kv_run", "kv_set_max_moves", "kv_records", "kv_games", "kv_stats_get", "kv_sync", "kv_reset_records", "kv_destroy",
+            "kv_load_weights", "kv_run", "kv_set_max_moves", "kv_records", "kv_games", "kv_stats_get", "kv_root_visits", "kv_records_device", "kv_sync", "kv_reset_records", "kv_destroy",
             "kv_dev_valid_moves", "kv_dev_make_move", "kv_dev_attacks", "kv_dev_dirichlet", "kv_dev_py_random",
             "kv_pgn_extract", "kv_fen_codes", "kv_san_move_index", "kv_chess_perft", "kv_chess_san", "kv_chess_fen"]
 

@@ -51,6 +51,7 @@ struct Ctr {
     unsigned long long nn_rows;
     unsigned long long sims;
     unsigned long long nn_rows_slots;  // k_count: sum of Slot::rows_total (nn_rows adds the MCTS leaf rows)
+    unsigned long long tree_overflows;  // MCTS expansions that did not fit the slot's pools (error flag 4)
     int active;
     int error;
     int need_eval;  // KV_EVAL_LAZY: some slot consumes a network row this step
@@ -100,7 +101,7 @@ struct MctsSlot {  // per-slot search scratch (kv_mcts.hip)
     float leaf_value;  // terminal value (white perspective) when !leaf_pending
     float root_value;
     int root_wtm;
-    int overflow;
+    int overflow;      // expansions skipped because the slot's edge / node pool was full (an error)
     int pad[5];
 };
 
@@ -117,6 +118,7 @@ struct Tree {  // per-slot SoA node / edge pools, slot i at i*ecap / i*ncap
     uint16_t* leaf_moves;  // [slot][MAXM]
     MctsSlot* ms;
     const float* sqrt_tab;  // (float)sqrt((double)n), n < ncap + 2
+    int* root_visits;       // optional [record_cap][MAXM]: root visit counts of each committed move (-1 padded)
     int ecap, ncap;
     float c_puct;
     int sims;
@@ -156,9 +158,37 @@ __device__ void wave_softmax_4096(const float* lg, float* out, int lane) {
     for (int j = 0; j < 64; ++j) out[j * 64 + lane] = v[j] * inv;
 }
 
-// max and 1/sum of the same softmax, without writing it out: entry i of the
-// softmax is then expf(lg[i] - m) * inv, bit for bit (same sum order)
-__device__ inline void wave_softmax_4096_stats(const float* lg, int lane, float& m_out, float& inv_out) {
+// exp(x) for the MCTS priors (build-defined; no reference counterpart),
+// made of IEEE double basic operations only -- Cody-Waite reduction by ln 2,
+// degree-11 Taylor polynomial, exact power-of-two scaling, one rounding to
+// float -- so that oracle/kv_oracle.c det_expf reproduces it bit for bit
+// (ocml's expf and glibc's expf differ in the last bit). Results below
+// e^-87 (float subnormals) are 0.
+__device__ inline float det_expf(float x) {
+    if (!(x >= -87.0f)) return 0.0f;
+    const double xd = (double)x;
+    const double kd = rint(xd * 1.4426950408889634);
+    const double r = (xd - kd * 6.93147180369123816490e-01) - kd * 1.90821492927058770002e-10;
+    double p = 2.5052108385441720e-08;  // 1/11!
+    p = p * r + 2.7557319223985893e-07;
+    p = p * r + 2.7557319223985888e-06;
+    p = p * r + 2.4801587301587302e-05;
+    p = p * r + 1.9841269841269841e-04;
+    p = p * r + 1.3888888888888889e-03;
+    p = p * r + 8.3333333333333332e-03;
+    p = p * r + 4.1666666666666664e-02;
+    p = p * r + 1.6666666666666666e-01;
+    p = p * r + 0.5;
+    p = p * r + 1.0;
+    p = p * r + 1.0;
+    const double scale = __longlong_as_double((long long)((int)kd + 1023) << 52);
+    return (float)(p * scale);
+}
+
+// softmax over 4096 logits with det_expf (MCTS root): max, e = det_expf(x -
+// max), each lane sums its 64 entries j*64+lane in j order, xor-butterfly
+// over the wave (offsets 32..1), x * (1/sum)
+__device__ void wave_softmax_4096_det(const float* lg, float* out, int lane) {
     float v[64];
     float m = -INFINITY;
 #pragma unroll
@@ -169,10 +199,14 @@ __device__ inline void wave_softmax_4096_stats(const float* lg, int lane, float&
     m = wave_max(m);
     float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < 64; ++j) s += expf(v[j] - m);
+    for (int j = 0; j < 64; ++j) {
+        v[j] = det_expf(v[j] - m);
+        s += v[j];
+    }
     s = wave_sum(s);
-    m_out = m;
-    inv_out = 1.0f / s;
+    const float inv = 1.0f / s;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) out[j * 64 + lane] = v[j] * inv;
 }
 
 // mixed legal weights of the reference (self_play.py:147-160) for a slot's
@@ -230,8 +264,8 @@ __device__ inline int choose_weighted(const double* vals, double* cum, int n, ui
 // record the position + move, makeMove, then the reference's termination
 // checks in order: isDraw (:180), resign (:185, `value` is the row the move
 // was chosen with), max_moves (:196). All lanes of the slot's wave.
-__device__ inline void commit_move(const DevCfg& cfg, Slot& s, int i, int mv, int8_t* boards, kv_record* rec,
-                                   int8_t* last_board, Ctr* ctr, int lane) {
+__device__ inline unsigned long long commit_move(const DevCfg& cfg, Slot& s, int i, int mv, int8_t* boards,
+                                                 kv_record* rec, int8_t* last_board, Ctr* ctr, int lane) {
     // lane = thread index of the slot's workgroup; lanes 0..63 (wave 0) carry
     // the 64 squares, every thread reaches the barriers
     int8_t* board = boards + (size_t)i * 64;
@@ -274,6 +308,7 @@ __device__ inline void commit_move(const DevCfg& cfg, Slot& s, int i, int mv, in
         if (s.end_kind != END_NONE) s.status = ST_FINISHED;
         s.consumed = 0;
     }
+    return ridx;  // the record's index
 }
 
 // MCTS launches (kv_mcts.hip), all on `st`

@@ -349,15 +349,16 @@ struct kv_engine {
     float* sqrt_tab = nullptr;
 };
 
-static int eng_counters(kv_engine* e) {
+static int eng_counters(kv_engine* e, bool check_error = true) {
     // active slots / plies / rows are summed from the slots only when the host reads them
     hipLaunchKernelGGL(kv::k_count, dim3(1), dim3(256), 0, e->st, e->dc, e->slots, e->ctr);
     KV_HIP(hipGetLastError());
     KV_HIP(hipMemcpyAsync(e->ctr_host, e->ctr, sizeof(kv::Ctr), hipMemcpyDeviceToHost, e->st));
     KV_HIP(hipStreamSynchronize(e->st));
-    if (e->ctr_host->error) {
-        kv::set_error("engine device error flags 0x%x (1: move list overflow, 2: record buffer full)",
-                      e->ctr_host->error);
+    if (check_error && e->ctr_host->error) {
+        kv::set_error("engine device error flags 0x%x (1: move list overflow, 2: record buffer full, "
+                      "4: MCTS tree pool full, %llu expansions dropped -- raise kv_config.tree_edge_cap)",
+                      e->ctr_host->error, (unsigned long long)e->ctr_host->tree_overflows);
         return KV_EOVERFLOW;
     }
     return KV_OK;
@@ -388,6 +389,8 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
     KV_REQUIRE(cfg->seed_mode != KV_SEED_SEQUENTIAL || cfg->slots == 1, KV_EINVAL,
                "kv_create: sequential seeding plays games in order on one slot");
     KV_REQUIRE(cfg->sims >= 0 && cfg->sims <= 100000, KV_EINVAL, "kv_create: sims out of range");
+    KV_REQUIRE(cfg->tree_edge_cap <= 0 || cfg->tree_edge_cap >= kv::MAXM, KV_EINVAL,
+               "kv_create: tree_edge_cap %d must be 0 (auto) or >= KV_MAXM (the root's list)", cfg->tree_edge_cap);
     KV_REQUIRE(cfg->sims == 0 || cfg->seed_mode == KV_SEED_PER_GAME, KV_EINVAL,
                "kv_create: MCTS mode uses per-game seeding");
     KV_REQUIRE(cfg->eval_mode == KV_EVAL_FAITHFUL || cfg->eval_mode == KV_EVAL_HASH ||
@@ -442,7 +445,11 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
     if (cfg->sims > 0) {
         kv::Tree& t = e->tree;
         t.ncap = cfg->sims + 2;
-        t.ecap = 48 * (cfg->sims + 1) + kv::MAXM;
+        // every expansion adds <= MAXM edges: (sims + 1) x MAXM edges can never
+        // overflow (C3: 2,048 slots x 801 x 320 x 18 B = 9.4 GB of the 288 GB);
+        // a smaller cap is honoured and an overflow raises KV_EOVERFLOW
+        const long long full = (long long)kv::MAXM * (cfg->sims + 1);
+        t.ecap = (int)(cfg->tree_edge_cap > 0 ? std::min<long long>(cfg->tree_edge_cap, full) : full);
         t.c_puct = cfg->c_puct > 0.f ? cfg->c_puct : 1.5f;
         t.sims = cfg->sims;
         const size_t E = S * (size_t)t.ecap, N = S * (size_t)t.ncap;
@@ -460,6 +467,7 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
         ALLOC(e->nn_boards, S * 64);
         ALLOC(e->probs, S * 4096 * sizeof(float));
         ALLOC(e->sqrt_tab, (size_t)(t.ncap + 2) * sizeof(float));
+        if (cfg->keep_root_visits) ALLOC(t.root_visits, (size_t)e->cfg.record_cap * kv::MAXM * sizeof(int));
         t.ms = e->ms;
         std::vector<float> sq(t.ncap + 2);
         for (int k = 0; k < t.ncap + 2; ++k) sq[k] = (float)sqrt((double)k);
@@ -633,6 +641,20 @@ int kv_records(kv_engine* e, kv_record* out, size_t cap, size_t* n) {
     return KV_OK;
 }
 
+int kv_records_device(kv_engine* e, kv_record* out_dev, size_t cap, size_t* n, void* stream) {
+    KV_REQUIRE(e && n, KV_EINVAL, "kv_records_device: NULL argument");
+    int rc = eng_counters(e);
+    if (rc) return rc;
+    const size_t cnt =
+        (size_t)std::min<unsigned long long>(e->ctr_host->rec_count, (unsigned long long)e->cfg.record_cap);
+    *n = cnt;
+    if (!out_dev) return KV_OK;
+    KV_REQUIRE(cap >= cnt, KV_EINVAL, "kv_records_device: buffer holds %zu, need %zu", cap, cnt);
+    // the engine stream is idle after eng_counters; the copy runs on the caller's stream
+    KV_HIP(hipMemcpyAsync(out_dev, e->rec, cnt * sizeof(kv_record), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return KV_OK;
+}
+
 int kv_games(kv_engine* e, kv_game* out, size_t cap, size_t* n) {
     KV_REQUIRE(e && n, KV_EINVAL, "kv_games: NULL argument");
     int rc = eng_counters(e);
@@ -648,7 +670,7 @@ int kv_games(kv_engine* e, kv_game* out, size_t cap, size_t* n) {
 
 int kv_stats_get(kv_engine* e, kv_stats* out) {
     KV_REQUIRE(e && out, KV_EINVAL, "kv_stats_get: NULL argument");
-    int rc = eng_counters(e);
+    int rc = eng_counters(e, false);  // readable after an error too (tree_overflows)
     if (rc) return rc;
     out->steps = e->steps;
     out->plies = (int64_t)e->ctr_host->plies;
@@ -661,6 +683,30 @@ int kv_stats_get(kv_engine* e, kv_stats* out) {
     out->step_ms = e->wall_ms;
     out->dom_flop = e->dom_flop;
     out->dom_algo = e->dom_algo;
+    out->tree_overflows = (int64_t)e->ctr_host->tree_overflows;
+    return KV_OK;
+}
+
+int kv_root_visits(kv_engine* e, int32_t* out, size_t cap, size_t* n) {
+    KV_REQUIRE(e && n, KV_EINVAL, "kv_root_visits: NULL argument");
+    KV_REQUIRE(e->tree.root_visits, KV_EINVAL, "kv_root_visits: engine was created without keep_root_visits");
+    int rc = eng_counters(e);
+    if (rc) return rc;
+    const size_t cnt = (size_t)std::min<unsigned long long>(e->ctr_host->rec_count, (unsigned long long)e->cfg.record_cap);
+    *n = cnt;
+    if (!out) return KV_OK;
+    KV_REQUIRE(cap >= cnt, KV_EINVAL, "kv_root_visits: buffer holds %zu records, need %zu", cap, cnt);
+    std::vector<kv_record> rec(cnt);
+    std::vector<int32_t> vis(cnt * kv::MAXM);
+    KV_HIP(hipMemcpy(rec.data(), e->rec, cnt * sizeof(kv_record), hipMemcpyDeviceToHost));
+    KV_HIP(hipMemcpy(vis.data(), e->tree.root_visits, vis.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    std::vector<size_t> ord(cnt);
+    for (size_t k = 0; k < cnt; ++k) ord[k] = k;
+    std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {  // kv_records' order
+        return rec[a].game_id != rec[b].game_id ? rec[a].game_id < rec[b].game_id : rec[a].ply < rec[b].ply;
+    });
+    for (size_t k = 0; k < cnt; ++k)
+        memcpy(out + k * kv::MAXM, vis.data() + ord[k] * kv::MAXM, kv::MAXM * sizeof(int32_t));
     return KV_OK;
 }
 
@@ -672,7 +718,7 @@ void kv_destroy(kv_engine* e) {
     void* bufs[] = {e->slots, e->boards, e->moves, e->logits, e->values, e->last_probs,
                     e->np_mt, e->py_mt, e->rec, e->games, e->last_board, e->ctr,
                     t.e_move, t.e_P, t.e_N, t.e_W, t.e_child, t.n_first, t.n_cnt, t.n_N, t.path,
-                    t.leaf_moves, e->ms, e->nn_boards, e->probs, e->sqrt_tab};
+                    t.leaf_moves, e->ms, e->nn_boards, e->probs, e->sqrt_tab, t.root_visits};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (e->ctr_host) (void)hipHostFree(e->ctr_host);

@@ -14,9 +14,14 @@
 //            with no child: isDraw => value 0; no legal moves => mate (-1 for
 //            the side to move) or stalemate 0; else the leaf board joins this
 //            step's network batch (one row per slot) -> backup: priors =
-//            softmax restricted to the legal list and renormalised, node
-//            created, N += 1 and W += value from the mover's side along the
-//            path (the value head is white-perspective, self_play.py:253).
+//            softmax over the legal moves' logits only, node created, N += 1
+//            and W += value from the mover's side along the path (the value
+//            head is white-perspective, self_play.py:253).
+//            Softmaxes use det_expf (kv_engine.h) with a fixed summation
+//            order, so the CPU restatement reproduces every prior bit for bit.
+//            An expansion that does not fit the slot's edge pool (sized
+//            MAXM x (sims + 1) by default, so it cannot happen unless the
+//            caller shrinks it) raises KV_EOVERFLOW.
 //   choose : random.choices over the root visit counts on the CPython stream
 //            (tau = 1), then makeMove / record / termination as the reference.
 // Tree: structure-of-arrays node and edge pools per slot in HBM
@@ -60,7 +65,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     Slot s = slots[i];
     if (s.status != ST_ACTIVE) return;
     float* lp = probs + (size_t)i * 4096;
-    if (lane < 64) wave_softmax_4096(logits + (size_t)i * 4096, lp, lane);
+    if (lane < 64) wave_softmax_4096_det(logits + (size_t)i * 4096, lp, lane);
     __syncthreads();
     const int n = s.nmoves;
     const uint16_t* ml = moves + (size_t)i * MAXM;
@@ -186,31 +191,34 @@ __device__ inline void mcts_backup_slot(const DevCfg& cfg, const Tree& t, const 
     float v = m.leaf_value;
     if (m.leaf_pending) {
         v = values[i];
+        // priors = softmax over the legal moves' logits only (the 16 KB row is
+        // never swept): max, e_j = det_expf(l_j - max) kept in LDS, lane
+        // partial sums over j = lane, lane+64, ... in order, xor butterfly
         const float* lg = logits + (size_t)i * 4096;
-        float sm_max, sm_inv;  // softmax entries of the legal moves only (no 16 KB round trip)
-        wave_softmax_4096_stats(lg, lane, sm_max, sm_inv);
         const uint16_t* lm = t.leaf_moves + (size_t)i * MAXM;
         const int n = m.leaf_n;
+        float mx = -INFINITY;
         for (int j = lane; j < n; j += 64) {
             const int mv = lm[j];
-            pri[j] = expf(lg[(mv & 63) * 64 + ((mv >> 6) & 63)] - sm_max) * sm_inv;
+            const float l = lg[(mv & 63) * 64 + ((mv >> 6) & 63)];
+            pri[j] = l;
+            mx = fmaxf(mx, l);
         }
-        __syncthreads();
-        __shared__ float s_sum;
-        if (lane == 0) {
-            float sum = 0.f;
-            for (int j = 0; j < n; ++j) sum = sum + pri[j];
-            s_sum = sum;
+        mx = wave_max(mx);
+        float part = 0.f;
+        for (int j = lane; j < n; j += 64) {
+            const float e = det_expf(pri[j] - mx);
+            pri[j] = e;
+            part += e;
         }
-        __syncthreads();
-        const float sum = s_sum;
+        const float sum = wave_sum(part);
         const bool fits = m.edge_count + n <= t.ecap && m.node_count < t.ncap;
         if (fits) {
             const int first = m.edge_count;
             for (int j = lane; j < n; j += 64) {
                 const size_t e = eb + first + j;
                 t.e_move[e] = lm[j];
-                t.e_P[e] = sum > 0.f ? pri[j] / sum : 1.0f / (float)n;
+                t.e_P[e] = sum > 0.f ? pri[j] / sum : 1.0f / (float)n;  // sum >= 1 for finite logits
                 t.e_N[e] = 0;
                 t.e_W[e] = 0.f;
                 t.e_child[e] = -1;
@@ -226,7 +234,11 @@ __device__ inline void mcts_backup_slot(const DevCfg& cfg, const Tree& t, const 
                 m.node_count += 1;
                 m.edge_count += n;
             } else {
+                // the expansion does not fit the slot's pools: counted and
+                // raised as an error (kv_run -> KV_EOVERFLOW), never silent
                 m.overflow += 1;
+                atomicAdd(&ctr->tree_overflows, 1ull);
+                atomicOr(&ctr->error, 4);
             }
             m.pad[0] += 1;
         }
@@ -295,7 +307,11 @@ __global__ __launch_bounds__(64) void k_mcts_choose(DevCfg cfg, Tree t, Slot* sl
     }
     s.last_value = m.root_value;  // resign test on the root's network value (:185)
     s.n_evals += m.pad[0];
-    commit_move(cfg, s, i, t.e_move[eb + s_pick], boards, rec, last_board, ctr, lane);
+    const unsigned long long ridx = commit_move(cfg, s, i, t.e_move[eb + s_pick], boards, rec, last_board, ctr, lane);
+    if (t.root_visits && (long long)ridx < cfg.record_cap) {
+        int* rv = t.root_visits + (size_t)ridx * MAXM;
+        for (int j = lane; j < MAXM; j += 64) rv[j] = j < n ? t.e_N[eb + j] : -1;
+    }
     if (lane == 0) slots[i] = s;
 }
 

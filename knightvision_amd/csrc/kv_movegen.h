@@ -20,6 +20,7 @@
 namespace kv {
 
 constexpr int MAXM = 320;  // move-list capacity per position
+static_assert(MAXM == KV_MAXM, "include/kv.h KV_MAXM");
 constexpr uint64_t FILE_A = 0x0101010101010101ull;
 constexpr uint64_t FILE_H = 0x8080808080808080ull;
 constexpr uint64_t ROW_1 = 0x000000000000FF00ull;  // row 1 (black pawn start)

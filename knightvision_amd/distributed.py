@@ -1,12 +1,20 @@
 """Multi-GPU self-play: one process per GPU, games sharded by global id
 (rank r plays ids r, r+W, r+2W, ... -- per-game seeds make the shards
 independent, so there is no collective in the inner loop), and one gather of
-the packed experience records to rank 0 at the end of an iteration.
+the packed experience records at the end of an iteration.
 
 The gather moves packed 80-byte records (kv_record: game id, ply, move index,
 64 board codes) -- 38x smaller than the (12,8,8) float32 planes the trainer
-expands them into. With the "nccl" backend (RCCL over xGMI on ROCm) the
-buffers are GPU tensors; with "gloo" (CPU tests) they are host tensors.
+expands them into -- straight from HBM: the engine copies its record buffer
+device-to-device (kv_records_device) and RCCL (the "nccl" backend on ROCm,
+over xGMI) moves it; "gloo" (CPU tests) moves host tensors.
+
+One implementation, `gather_rows`, serves both consumers:
+  * dst=0: gather to the root (the data-generation path: one trainer process,
+    as the reference's generate_self_play_data returns the list to its caller,
+    scripts/learn.py:186-191) -- N-1 shards cross xGMI once;
+  * dst=None: all-gather (the data-parallel learn loop, knightvision_amd/
+    learn.py, where every rank trains on its slice of the filtered union).
 """
 from __future__ import annotations
 
@@ -23,36 +31,71 @@ def rank_world():
     return 0, 1
 
 
-def _gather_bytes(buf: np.ndarray, device) -> list:
-    """all-gather variable-length uint8 arrays (counts first, then padded)."""
+def comm_device(t: torch.Tensor | None = None) -> torch.device:
+    """Where collectives run: the current GPU under RCCL, the host under gloo."""
+    if dist.is_initialized() and dist.get_backend() == "nccl":
+        return t.device if (t is not None and t.is_cuda) else torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def gather_rows(t: torch.Tensor, dst: int | None = 0):
+    """Concatenation over ranks (rank order) of a tensor whose first dimension
+    differs per rank: per-rank row counts are all-gathered (int64), then the
+    rows padded to the largest count are gathered to `dst` (None: to every
+    rank). Returns the concatenation on `dst` / every rank, None elsewhere."""
     rank, world = rank_world()
     if world == 1:
-        return [buf]
-    n = torch.tensor([buf.size], dtype=torch.int64, device=device)
+        return t
+    dev = comm_device(t)
+    src = t.to(dev)
+    n = torch.tensor([src.shape[0]], dtype=torch.int64, device=dev)
     counts = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(counts, n)
     counts = [int(c.item()) for c in counts]
     mx = max(max(counts), 1)
-    t = torch.zeros(mx, dtype=torch.uint8, device=device)
-    if buf.size:
-        t[:buf.size] = torch.from_numpy(buf).to(device)
-    outs = [torch.zeros(mx, dtype=torch.uint8, device=device) for _ in range(world)]
-    dist.all_gather(outs, t)
-    return [o[:c].cpu().numpy() for o, c in zip(outs, counts)]
+    pad = torch.zeros((mx,) + tuple(src.shape[1:]), dtype=src.dtype, device=dev)
+    pad[:src.shape[0]] = src
+    if dst is None:
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad)
+    else:
+        parts = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+        dist.gather(pad, parts, dst=dst)
+        if rank != dst:
+            return None
+    return torch.cat([p[:k] for p, k in zip(parts, counts)])
 
 
-def gather_experience(records: np.ndarray, games: np.ndarray, device=None):
-    """-> (records, games) of every rank, ordered by (game_id, ply), on every
-    rank (all-gather: the data-parallel trainer of the next iteration reads it
-    on every rank)."""
-    if device is None:
-        backend = dist.get_backend() if dist.is_initialized() else "gloo"
-        device = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
-    r = _gather_bytes(np.ascontiguousarray(records).view(np.uint8).reshape(-1), device)
-    g = _gather_bytes(np.ascontiguousarray(games).view(np.uint8).reshape(-1), device)
-    recs = np.concatenate([x.view(RECORD_DTYPE) for x in r]) if r else np.zeros(0, RECORD_DTYPE)
-    gms = np.concatenate([x.view(GAME_DTYPE) for x in g]) if g else np.zeros(0, GAME_DTYPE)
-    recs = recs[np.lexsort((recs["ply"], recs["game_id"]))]
+def sort_records(rows: torch.Tensor) -> torch.Tensor:
+    """uint8 [n, 80] kv_record rows -> ordered by (game_id, ply) (two stable sorts, on the rows' device)."""
+    if rows.shape[0] == 0:
+        return rows
+    gid = rows[:, 0:8].contiguous().view(torch.int64).reshape(-1)
+    ply = rows[:, 8:12].contiguous().view(torch.int32).reshape(-1)
+    o1 = torch.sort(ply, stable=True).indices
+    o2 = torch.sort(gid[o1], stable=True).indices
+    return rows[o1[o2]]
+
+
+def _as_rows(x, dtype) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        return x.reshape(-1, dtype.itemsize)
+    return torch.from_numpy(np.ascontiguousarray(x).view(np.uint8).reshape(-1, dtype.itemsize))
+
+
+def gather_experience(records, games, dst: int | None = 0):
+    """End-of-iteration gather of every rank's (records, games), ordered by
+    (game_id, ply) / game_id. `records` is a numpy RECORD_DTYPE array or the
+    engine's device tensor (SelfPlayEngine.records_device(), uint8 [n, 80]);
+    `games` a GAME_DTYPE array. Returns numpy arrays on `dst` (every rank when
+    dst is None) and (None, None) elsewhere."""
+    r = gather_rows(_as_rows(records, RECORD_DTYPE), dst)
+    g = gather_rows(_as_rows(games, GAME_DTYPE), dst)
+    if r is None:
+        return None, None
+    r = sort_records(r).cpu().numpy()
+    gms = g.cpu().numpy().reshape(-1).view(GAME_DTYPE) if g.numel() else np.zeros(0, GAME_DTYPE)
+    recs = np.ascontiguousarray(r).reshape(-1).view(RECORD_DTYPE) if r.size else np.zeros(0, RECORD_DTYPE)
     gms = gms[np.argsort(gms["game_id"], kind="stable")]
     return recs, gms
 

@@ -38,7 +38,7 @@ class SelfPlayEngine:
     def __init__(self, weights, *, slots=256, n_games=256, seed=42, seed_mode=SEED_PER_GAME, max_moves=None,
                  batch=16, eps=0.25, alpha=0.3, sims=0, c_puct=1.5, eval_mode=EVAL_FAITHFUL, record_cap=None,
                  recycle=True, device=0, game_id_base=0, game_id_stride=1, precision="fp32",
-                 algo="auto"):
+                 algo="auto", tree_edge_cap=0, keep_root_visits=False):
         L = _lib.lib()
         if record_cap is None:
             record_cap = max(1 << 16, min(1 << 26, int(n_games) * 400))
@@ -46,7 +46,8 @@ class SelfPlayEngine:
                           game_id_stride=game_id_stride, seed=seed, seed_mode=seed_mode,
                           max_moves=max_moves if max_moves else 0, batch=batch, eps=eps, alpha=alpha, sims=sims,
                           c_puct=c_puct, eval_mode=eval_mode, record_cap=record_cap, recycle=1 if recycle else 0,
-                          precision={"fp32": 0, "bf16x3": 1, "bf16x6": 2, "f16x3": 3}[precision], algo=ALGOS[algo])
+                          precision={"fp32": 0, "bf16x3": 1, "bf16x6": 2, "f16x3": 3}[precision], algo=ALGOS[algo],
+                          tree_edge_cap=int(tree_edge_cap), keep_root_visits=1 if keep_root_visits else 0)
         h = C.c_void_p()
         _lib.check(L.kv_create(C.byref(cfg), C.byref(h)), "kv_create")
         self.h = h
@@ -76,6 +77,33 @@ class SelfPlayEngine:
         if n.value:
             _lib.check(L.kv_records(self.h, out.ctypes.data_as(C.POINTER(_lib.Record)), n.value, C.byref(n)),
                        "kv_records")
+        return out
+
+    def records_device(self):
+        """The records as a uint8 CUDA tensor [n, 80] on the engine's GPU, in allocation order
+        (kv_records_device: no host round trip; sort after gathering)."""
+        import torch
+        L = _lib.lib()
+        n = C.c_size_t()
+        _lib.check(L.kv_records_device(self.h, None, 0, C.byref(n), None), "kv_records_device")
+        dev = torch.device("cuda", self.cfg.device)
+        out = torch.empty((n.value, RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        if n.value:
+            st = torch.cuda.current_stream(dev).cuda_stream
+            _lib.check(L.kv_records_device(self.h, C.c_void_p(out.data_ptr()), n.value, C.byref(n), C.c_void_p(st)),
+                       "kv_records_device")
+        return out
+
+    def root_visits(self) -> np.ndarray:
+        """MCTS root visit counts [records, MAXM] (-1 padded), rows in records() order
+        (needs keep_root_visits=True)."""
+        L = _lib.lib()
+        n = C.c_size_t()
+        _lib.check(L.kv_root_visits(self.h, None, 0, C.byref(n)), "kv_root_visits")
+        out = np.zeros((n.value, _lib.MAXM), dtype=np.int32)
+        if n.value:
+            _lib.check(L.kv_root_visits(self.h, out.ctypes.data_as(C.POINTER(C.c_int32)), n.value, C.byref(n)),
+                       "kv_root_visits")
         return out
 
     def games(self) -> np.ndarray:

@@ -10,9 +10,14 @@ Every rank keeps a shard of the experience on its GPU (int8 board codes, move
 index, reward: 74 B per record instead of a 3 KB plane tensor, expanded per
 batch on the device) and trains on it; DistributedDataParallel averages the
 gradients with bucketed RCCL all-reduces overlapped with the backward pass.
-The one data exchange is the end-of-iteration all-gather of the new records,
-filtered as one dataset (the reference's global decisive filter) and
-re-sharded round-robin. Self-play game g of iteration i has the global id
+The one data exchange is the end-of-iteration all-gather of the new records
+(distributed.gather_rows, dst=None), filtered as one dataset (the reference's
+global decisive filter) and re-sharded round-robin.
+The global batch is the reference's: nn.DataParallel splits one batch of
+BATCH_SIZE over the GPUs (utils/model_utils.py:26-28), so each of the W ranks
+trains on batch_size // W rows per micro-batch with the same accumulation
+count -- W x (batch_size // W) rows per micro-batch, one optimizer step per
+accumulate_steps micro-batches, as on one process. Self-play game g of iteration i has the global id
 i * games_per_iter + g and the seeds SEED + id (per-game seeding).
 
 Not reproduced (out of the self-play path): the PGN dataset and
@@ -26,6 +31,7 @@ import time
 import torch
 
 from . import train as T
+from .distributed import gather_rows
 from .engine import SelfPlayEngine, packed_from
 from .self_play import ALPHA, BATCH_SIZE as SELFPLAY_BATCH, EPSILON, SEED
 
@@ -64,23 +70,10 @@ def _max_over_ranks(n: int, dev) -> int:
     return int(t.item())
 
 
-def _all_gather_rows(t: torch.Tensor) -> torch.Tensor:
-    """Concatenation over ranks (rank order) of a tensor whose first dimension
-    differs per rank (RCCL all-gather of the padded rows)."""
-    dist, _, world = _dist()
-    if dist is None or world == 1:
-        return t
-    comm_dev = t.device if dist.get_backend() == "nccl" else torch.device("cpu")
-    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=comm_dev)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    sizes = [int(x.item()) for x in sizes]
-    m = max(sizes)
-    pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=comm_dev)
-    pad[:t.shape[0]] = t.to(comm_dev)
-    parts = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad)
-    return torch.cat([p[:k] for p, k in zip(parts, sizes)]).to(t.device)
+def rank_batch_size(batch_size: int, world: int) -> int:
+    """Per-rank micro-batch that keeps the reference's global batch (DataParallel
+    scatters one batch of `batch_size` rows over the devices)."""
+    return max(1, batch_size // world)
 
 
 def decisive_filter(codes, moves, rewards):
@@ -103,7 +96,7 @@ def extend_dataset(data, recs, games, dev):
     else:
         local = (torch.zeros((0, 64), dtype=torch.int8, device=dev), torch.zeros(0, dtype=torch.int64, device=dev),
                  torch.zeros(0, dtype=torch.float32, device=dev))
-    union = decisive_filter(*(_all_gather_rows(x) for x in local))
+    union = decisive_filter(*(gather_rows(x, dst=None).to(dev) for x in local))
     mine = tuple(x[rank::world] for x in union)
     return mine if data is None else tuple(torch.cat([a, b]) for a, b in zip(data, mine))
 
@@ -129,8 +122,9 @@ def reinforcement_loop(model, iterations: int, games_per_iter: int, device, *, e
         n_min = -_max_over_ranks(-n_local, dev)
         if n_min > 0:  # every rank holds data (fewer records than ranks: no update this iteration)
             t0 = time.perf_counter()
+            per_rank = rank_batch_size(batch_size, world)
             for _ in range(epochs):
-                ep = T.train_one_epoch(ddp, T.batches(*data, batch_size, True, gen, total=n_max), optimizer, scaler,
+                ep = T.train_one_epoch(ddp, T.batches(*data, per_rank, True, gen, total=n_max), optimizer, scaler,
                                        accumulate_steps=accumulate_steps)
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)

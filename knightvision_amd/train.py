@@ -126,6 +126,19 @@ def batch_loss(model, b: Batch, entropy_coef: float = ENTROPY_COEF, amp: bool = 
     return loss, loss_policy, loss_value, entropy, pol
 
 
+def _finite_on_all_ranks(loss: torch.Tensor) -> bool:
+    """isfinite(loss), agreed over the ranks of an initialised process group
+    (MIN all-reduce of the flag: one rank's NaN skips the batch everywhere)."""
+    ok = torch.isfinite(loss.detach()).all()
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dev = loss.device if dist.get_backend() == "nccl" else torch.device("cpu")
+        flag = ok.to(device=dev, dtype=torch.int32).reshape(1)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return bool(flag.item())
+    return bool(ok)
+
+
 def make_scaler(device) -> torch.amp.GradScaler:
     return torch.amp.GradScaler("cuda", enabled=torch.device(device).type == "cuda")
 
@@ -142,7 +155,10 @@ def train_one_epoch(model, data, optimizer, scaler, accumulate_steps: int = ACCU
     total, skipped, correct, seen, steps = 0.0, 0, 0, 0, 0
     for i, b in enumerate(data):
         loss, lp, lv, ent, pol = batch_loss(model, b, entropy_coef, amp)
-        if not torch.isfinite(loss):
+        if not _finite_on_all_ranks(loss):
+            # the reference skips a non-finite batch (train.py:178-180); under DDP every
+            # rank skips together, or the gradient all-reduces of backward would pair up
+            # different batches across ranks (or hang)
             skipped += 1
             continue
         scaler.scale(loss / accumulate_steps).backward()

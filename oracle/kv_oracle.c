@@ -763,6 +763,9 @@ int kvo_sizeof_last(void) { return (int)sizeof(kvo_last); }
  * capacities, same fp32 operation order (-ffp-contract=off), same RNG use:
  * the root priors are the reference's mixed legal weights (self_play.py
  * :147-166) normalised, the move is random.choices over root visit counts.
+ * The root softmax and the leaf priors (legal moves' logits only) use
+ * kvo_det_expf and the device's lane / butterfly summation order, so every
+ * prior equals the device's bit for bit given the same network rows.
  * eval_cb == NULL selects the hash test evaluator (all logits 0, value =
  * dyadic FNV-1a hash of the 64 board codes), which is exact on both sides. */
 typedef struct {
@@ -770,7 +773,82 @@ typedef struct {
     float c_puct;
     int max_moves;
     double eps, alpha;
+    int edge_cap; /* <= 0: KV_MAXM x (sims + 1) (kv_engine.hip kv_create), which cannot overflow */
 } kvo_mcts_cfg;
+
+#define KVO_MAXM 320 /* include/kv.h KV_MAXM */
+
+/* det_expf of kv_engine.h: exp from IEEE double basic operations (this file
+ * is compiled with -ffp-contract=off), Cody-Waite by ln 2, degree-11 Taylor,
+ * exact 2^k scaling, one rounding to float; 0 below e^-87. */
+float kvo_det_expf(float x) {
+    if (!(x >= -87.0f)) return 0.0f;
+    const double xd = (double)x;
+    const double kd = rint(xd * 1.4426950408889634);
+    const double r = (xd - kd * 6.93147180369123816490e-01) - kd * 1.90821492927058770002e-10;
+    double p = 2.5052108385441720e-08;
+    p = p * r + 2.7557319223985893e-07;
+    p = p * r + 2.7557319223985888e-06;
+    p = p * r + 2.4801587301587302e-05;
+    p = p * r + 1.9841269841269841e-04;
+    p = p * r + 1.3888888888888889e-03;
+    p = p * r + 8.3333333333333332e-03;
+    p = p * r + 4.1666666666666664e-02;
+    p = p * r + 1.6666666666666666e-01;
+    p = p * r + 0.5;
+    p = p * r + 1.0;
+    p = p * r + 1.0;
+    const uint64_t bits = (uint64_t)((int64_t)kd + 1023) << 52;
+    double scale;
+    memcpy(&scale, &bits, sizeof scale);
+    return (float)(p * scale);
+}
+
+/* the wave's xor-butterfly sum (kv_engine.h wave_sum) over 64 lane partials */
+static float wave_sum64(float* part) {
+    float t[64];
+    for (int m = 32; m >= 1; m >>= 1) {
+        for (int l = 0; l < 64; ++l) t[l] = part[l] + part[l ^ m];
+        memcpy(part, t, sizeof t);
+    }
+    return part[0];
+}
+
+/* kv_engine.h wave_softmax_4096_det: lane l holds entries j*64+l, j = 0..63 */
+void kvo_softmax_det_4096(const float* lg, float* out) {
+    float m = -INFINITY;
+    for (int i = 0; i < 4096; ++i) m = fmaxf(m, lg[i]);
+    float part[64];
+    static float e[4096];
+    for (int l = 0; l < 64; ++l) {
+        float s = 0.f;
+        for (int j = 0; j < 64; ++j) {
+            e[j * 64 + l] = kvo_det_expf(lg[j * 64 + l] - m);
+            s += e[j * 64 + l];
+        }
+        part[l] = s;
+    }
+    const float inv = 1.0f / wave_sum64(part);
+    for (int i = 0; i < 4096; ++i) out[i] = e[i] * inv;
+}
+
+/* kv_mcts.hip leaf priors: softmax over the n legal moves' logits; lane l
+ * sums entries l, l+64, ... in order, then the butterfly. e[] receives the
+ * unnormalised terms; returns the sum. */
+static float legal_softmax_terms(const float* lg, const int* idx, int n, float* e) {
+    float mx = -INFINITY;
+    for (int j = 0; j < n; ++j) mx = fmaxf(mx, lg[idx[j]]);
+    float part[64];
+    for (int l = 0; l < 64; ++l) {
+        float s = 0.f;
+        for (int j = l; j < n; j += 64) {
+            e[j] = kvo_det_expf(lg[idx[j]] - mx);
+            s += e[j];
+        }
+        part[l] = s;
+    }
+    return wave_sum64(part);
+}
 
 static void hash_eval_board(const int8_t* b, float* logits, float* value) {
     uint32_t h = 2166136261u;
@@ -805,16 +883,18 @@ static int choose_weighted_c(MT* py, const double* w, int n) {
     return k;
 }
 
-static void softmax_any(kvo_softmax_fn smx, void* ctx, const float* lg, float* pr) {
-    if (smx) smx(ctx, lg, pr);
-    else kvo_softmax_f32(lg, 4096, pr);
-}
-
 /* plays one game; rec_moves[ply], visits[ply * maxm + j] = root visit counts
- * in root move-list order (maxm entries per ply, -1 padded). */
-int kvo_mcts_play_game(const kvo_mcts_cfg* cfg, MT* np_mt, MT* py_mt, kvo_eval_fn cb, kvo_softmax_fn smx, void* ctx,
+ * in root move-list order (maxm entries per ply, -1 padded). Returns the
+ * number of plies, or -1 when an expansion did not fit the edge pool (the
+ * device raises KV_EOVERFLOW there). */
+int kvo_mcts_play_game(const kvo_mcts_cfg* cfg, MT* np_mt, MT* py_mt, kvo_eval_fn cb, void* ctx,
                        uint16_t* rec_moves, int cap, int32_t* visits, int maxm, kvo_game_result* res) {
-    const int S = cfg->sims, ncap = S + 2, ecap = 48 * (S + 1) + 320;
+    const int S = cfg->sims, ncap = S + 2;
+    const int full = KVO_MAXM * (S + 1);
+    const int ecap = cfg->edge_cap > 0 && cfg->edge_cap < full ? cfg->edge_cap : full;
+    int overflow = 0;
+    int lidx[MAXMV];
+    float lterm[MAXMV];
     float* sqt = (float*)malloc(sizeof(float) * (size_t)(ncap + 2));
     for (int k = 0; k < ncap + 2; ++k) sqt[k] = (float)sqrt((double)k);
     Mv* e_mv = (Mv*)malloc(sizeof(Mv) * (size_t)ecap);
@@ -840,7 +920,7 @@ int kvo_mcts_play_game(const kvo_mcts_cfg* cfg, MT* np_mt, MT* py_mt, kvo_eval_f
         float root_value;
         eval_one(cb, ctx, &g, logits, &root_value);
         evals++;
-        softmax_any(smx, ctx, logits, probs);
+        kvo_softmax_det_4096(logits, probs);
         kvo_dirichlet(np_mt, cfg->alpha, 4096, noise);
         const float keep = (float)(1.0 - cfg->eps);
         double total = 0.0;
@@ -885,24 +965,22 @@ int kvo_mcts_play_game(const kvo_mcts_cfg* cfg, MT* np_mt, MT* py_mt, kvo_eval_f
                 } else {
                     eval_one(cb, ctx, &b, logits, &v);
                     evals++;
-                    softmax_any(smx, ctx, logits, probs);
-                    float sum = 0.f;
-                    for (int j = 0; j < lm.n; ++j) {
-                        int idx = (lm.m[j].fr * 8 + lm.m[j].fc) * 64 + lm.m[j].tr * 8 + lm.m[j].tc;
-                        sum = sum + probs[idx];
-                    }
+                    for (int j = 0; j < lm.n; ++j)
+                        lidx[j] = (lm.m[j].fr * 8 + lm.m[j].fc) * 64 + lm.m[j].tr * 8 + lm.m[j].tc;
+                    const float sum = legal_softmax_terms(logits, lidx, lm.n, lterm);
                     if (edge_count + lm.n <= ecap && node_count < ncap) {
                         const int id = node_count++;
                         n_first[id] = edge_count; n_cnt[id] = lm.n; n_N[id] = 0;
                         for (int j = 0; j < lm.n; ++j) {
-                            int idx = (lm.m[j].fr * 8 + lm.m[j].fc) * 64 + lm.m[j].tr * 8 + lm.m[j].tc;
                             const int e = edge_count + j;
                             e_mv[e] = lm.m[j];
-                            e_P[e] = sum > 0.f ? probs[idx] / sum : 1.0f / (float)lm.n;
+                            e_P[e] = sum > 0.f ? lterm[j] / sum : 1.0f / (float)lm.n;
                             e_N[e] = 0; e_W[e] = 0.f; e_child[e] = -1;
                         }
                         edge_count += lm.n;
                         e_child[leaf] = id;
+                    } else {
+                        overflow++;
                     }
                 }
             }
@@ -947,5 +1025,5 @@ int kvo_mcts_play_game(const kvo_mcts_cfg* cfg, MT* np_mt, MT* py_mt, kvo_eval_f
     res->n_evals = evals;
     free(sqt); free(e_mv); free(e_P); free(e_N); free(e_W); free(e_child); free(n_first); free(n_cnt); free(n_N);
     free(path); free(logits); free(probs); free(noise); free(w);
-    return move_count;
+    return overflow ? -1 : move_count;
 }

@@ -176,16 +176,37 @@ def play_game(eval_fn, np_mt: MT, py_mt: MT, last: Last, max_moves=None, batch=1
 
 class MctsCfg(C.Structure):
     _fields_ = [("sims", C.c_int), ("c_puct", C.c_float), ("max_moves", C.c_int), ("eps", C.c_double),
-                ("alpha", C.c_double)]
+                ("alpha", C.c_double), ("edge_cap", C.c_int)]
+
+
+class TreeOverflow(RuntimeError):
+    pass
+
+
+def det_expf(x: float) -> float:
+    L = lib()
+    L.kvo_det_expf.argtypes = [C.c_float]
+    L.kvo_det_expf.restype = C.c_float
+    return float(L.kvo_det_expf(x))
+
+
+def softmax_det_4096(logits):
+    L = lib()
+    L.kvo_softmax_det_4096.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_float)]
+    x = np.ascontiguousarray(logits, dtype=np.float32)
+    out = np.zeros(4096, dtype=np.float32)
+    L.kvo_softmax_det_4096(_p(x, C.c_float), _p(out, C.c_float))
+    return out
 
 
 def mcts_play_game(sims, np_mt: MT, py_mt: MT, eval_fn=None, max_moves=None, c_puct=1.5, eps=0.25, alpha=0.3,
-                   softmax_fn=None, cap=2048, maxm=320):
+                   edge_cap=0, cap=2048, maxm=320):
     """Restated PUCT self-play game (build-defined semantics, kv_mcts.hip).
-    eval_fn None = hash test evaluator. Returns dict(moves, visits, ...)."""
+    eval_fn None = hash test evaluator. Returns dict(moves, visits, ...);
+    raises TreeOverflow where the device raises KV_EOVERFLOW."""
     L = lib()
     if not hasattr(L.kvo_mcts_play_game, "_sig"):
-        L.kvo_mcts_play_game.argtypes = [C.POINTER(MctsCfg), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+        L.kvo_mcts_play_game.argtypes = [C.POINTER(MctsCfg), C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_void_p, C.POINTER(C.c_uint16), C.c_int, C.POINTER(C.c_int32), C.c_int,
                                          C.POINTER(GameResult)]
         L.kvo_mcts_play_game._sig = True
@@ -197,17 +218,13 @@ def mcts_play_game(sims, np_mt: MT, py_mt: MT, eval_fn=None, max_moves=None, c_p
             np.ctypeslib.as_array(logits, shape=(n, 4096))[:] = lg
             np.ctypeslib.as_array(values, shape=(n,))[:] = np.asarray(vl).reshape(n)
         cb = EVAL_FN(_cb)
-    smx = None
-    if softmax_fn is not None:
-        def _sm(ctx, lg, pr):
-            np.ctypeslib.as_array(pr, shape=(4096,))[:] = softmax_fn(np.ctypeslib.as_array(lg, shape=(4096,)).copy())
-        smx = SOFTMAX_FN(_sm)
-    cfg = MctsCfg(sims, c_puct, max_moves if max_moves else 0, eps, alpha)
+    cfg = MctsCfg(sims, c_puct, max_moves if max_moves else 0, eps, alpha, int(edge_cap))
     moves = np.zeros(cap, dtype=np.uint16)
     visits = np.full((cap, maxm), -1, dtype=np.int32)
     res = GameResult()
     n = L.kvo_mcts_play_game(C.byref(cfg), np_mt.buf, py_mt.buf, C.cast(cb, C.c_void_p) if cb else None,
-                             C.cast(smx, C.c_void_p) if smx else None, None, _p(moves, C.c_uint16), cap,
-                             _p(visits, C.c_int32), maxm, C.byref(res))
+                             None, _p(moves, C.c_uint16), cap, _p(visits, C.c_int32), maxm, C.byref(res))
+    if n < 0:
+        raise TreeOverflow(f"edge pool of {edge_cap} edges overflowed")
     return dict(moves=moves[:n].copy(), visits=visits[:n].copy(), plies=res.plies, outcome=res.outcome,
                 reward=float(res.reward), reason=res.reason, n_evals=res.n_evals)

@@ -1,6 +1,8 @@
 """World-size-2 gloo test of the multi-GPU path's only collective: the
-end-of-iteration experience gather (knightvision_amd.distributed), and of the
-game-id sharding (rank r plays ids r, r+W, ...)."""
+end-of-iteration experience gather (knightvision_amd.distributed.gather_rows,
+to the root and to all ranks), and of the game-id sharding (rank r plays ids
+r, r+W, ...). The same gather over engine output runs on the GPU box in
+tests/test_shard_gpu.py."""
 import os
 import socket
 
@@ -37,7 +39,11 @@ def _worker(rank, world, port, out_q):
         games[k]["game_id"] = gid
         games[k]["plies"] = n
     recs = np.concatenate(recs)
-    all_r, all_g = gather_experience(recs, games)
+    all_r, all_g = gather_experience(recs, games, dst=None)  # all-gather (the data-parallel learn loop)
+    root_r, root_g = gather_experience(recs, games, dst=0)   # gather to the root (data generation)
+    assert (root_r is None) == (rank != 0) and (root_g is None) == (rank != 0)
+    if rank == 0:
+        assert np.array_equal(root_r, all_r) and np.array_equal(root_g, all_g)
     out_q.put((rank, all_r["game_id"].tolist(), all_r["ply"].tolist(), all_r["move"].tolist(),
                all_g["game_id"].tolist()))
     dist.barrier()

@@ -137,7 +137,6 @@ def _free_port():
 
 def _ddp_worker(rank, world, port, q):
     import torch.distributed as dist
-    from knightvision_amd import learn as L
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(5)
@@ -150,7 +149,8 @@ def _ddp_worker(rank, world, port, q):
     T.train_one_epoch(ddp, mine, opt, T.make_scaler("cpu"), accumulate_steps=2, entropy_coef=0.01)
     # end-of-iteration exchange: all-gather + global decisive filter + round-robin re-shard
     c2, m2, r2 = _data(5 + 3 * rank, 10 + rank)
-    union = [L._all_gather_rows(x) for x in (c2, m2, r2)]
+    from knightvision_amd.distributed import gather_rows
+    union = [gather_rows(x, dst=None) for x in (c2, m2, r2)]
     q.put((rank, {k: v.numpy().copy() for k, v in m.state_dict().items()}, [u.numpy().copy() for u in union]))
     dist.barrier()
     dist.destroy_process_group()
@@ -225,3 +225,102 @@ def test_row_bucketing_is_the_unpadded_update():
     for k in s0:
         assert torch.allclose(s0[k].double(), s1[k].double(), rtol=1e-9, atol=1e-12), k
 
+
+
+def _spawn(target, world=2, timeout=300):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=timeout) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _loop_batch_worker(rank, world, port, q):
+    """The learn loop's update path on one rank: the round-robin shard of the
+    filtered union (learn.extend_dataset) trained with learn.rank_batch_size."""
+    import torch.distributed as dist
+    from knightvision_amd import learn as L
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(5)
+    m = TinyNet()
+    ddp = T.wrap_ddp(m, "cpu")
+    codes, moves, rew = _data(64, 6)
+    shard = (codes[rank::world], moves[rank::world], rew[rank::world])
+    bs = L.rank_batch_size(8, world)
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+    ep = T.train_one_epoch(ddp, T.batches(*shard, bs, False, total=32), opt, T.make_scaler("cpu"),
+                           accumulate_steps=2, entropy_coef=0.01)
+    q.put((rank, bs, ep, {k: v.numpy().copy() for k, v in m.state_dict().items()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_learn_loop_world2_keeps_the_reference_global_batch():
+    """ADVICE r1: with W ranks each micro-batch is W x (batch_size // W) rows --
+    the reference's DataParallel batch (utils/model_utils.py:26-28) -- so an
+    epoch of 64 samples at batch 8, accumulation 2 takes 4 optimizer steps on
+    every rank, and the update equals one process averaging the two ranks'
+    halves of each global batch."""
+    res = _spawn(_loop_batch_worker)
+    for rank, bs, ep, _ in res:
+        assert bs == 4
+        assert ep["batches"] == 8 and ep["optimizer_steps"] == 4 and ep["samples"] == 32
+    torch.manual_seed(5)
+    m = TinyNet()
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+    codes, moves, rew = _data(64, 6)
+    halves = [tuple(x[r::2] for x in (codes, moves, rew)) for r in range(2)]
+    opt.zero_grad()
+    for j in range(8):
+        for r in range(2):
+            c, mv, rw = (x[4 * j:4 * j + 4] for x in halves[r])
+            (T.batch_loss(m, T.Batch(T.codes_to_planes_t(c), mv, rw), 0.01)[0] / 2 / 2).backward()
+        if (j + 1) % 2 == 0:
+            torch.nn.utils.clip_grad_norm_(m.parameters(), max_norm=1.0)
+            opt.step()
+            opt.zero_grad()
+    for rank, _, _, sd in res:
+        for k, v in m.state_dict().items():
+            if "running" in k or "num_batches" in k:
+                continue
+            assert torch.allclose(torch.from_numpy(sd[k]), v, atol=2e-6), (rank, k)
+
+
+def _nan_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(5)
+    m = TinyNet()
+    ddp = T.wrap_ddp(m, "cpu")
+    codes, moves, rew = _data(32, 7 + rank)
+    batches = [T.Batch(T.codes_to_planes_t(codes[i:i + 8]), moves[i:i + 8], rew[i:i + 8].clone())
+               for i in range(0, 32, 8)]
+    if rank == 1:
+        batches[1].outcomes[0] = float("nan")  # one rank's loss of batch 1 is NaN
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+    ep = T.train_one_epoch(ddp, batches, opt, T.make_scaler("cpu"), accumulate_steps=1, entropy_coef=0.01)
+    q.put((rank, ep, {k: v.numpy().copy() for k, v in m.state_dict().items() if "running" not in k}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_nan_batch_is_skipped_on_every_rank():
+    """a non-finite loss on one rank skips that batch on all ranks
+    (MIN all-reduce of the finiteness flag), so DDP's gradient all-reduces
+    stay paired and the replicas stay identical."""
+    res = _spawn(_nan_worker)
+    for rank, ep, _ in res:
+        assert ep["skipped"] == 1 and ep["optimizer_steps"] == 3, (rank, ep)
+    (_, _, a), (_, _, b) = res
+    for k in a:
+        if "num_batches" in k:
+            continue
+        assert np.allclose(a[k], b[k], atol=1e-6), k
