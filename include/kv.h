@@ -218,6 +218,11 @@ int kv_dev_make_move(int device, int8_t* states, const int* index, int n);
  * tail [n] = the stream's next random_sample() after the draws. */
 int kv_dev_dirichlet(int device, const uint64_t* seeds, int n, double alpha, int k, int draws, double* out,
                      int64_t* attempts, double* tail);
+/* The device's restatement of glibc log (op 0: out = log(x)) / pow (op 1:
+ * out = pow(x, y)) (csrc/kv_libm.h, used by the Dirichlet draw), run on the
+ * host CPU: the same source compiled for the host, so tests can pin it against
+ * libm itself without a GPU. */
+int kv_host_libm(int op, const double* x, const double* y, int n, double* out);
 /* CPython random.Random(seed[i]): count random() values -> out [n][count]. */
 int kv_dev_py_random(int device, const uint64_t* seeds, int n, int count, double* out);
 

@@ -84,6 +84,7 @@ def _declare(L):
         "kv_dev_attacks": ([i, P(C.c_int8), i, P(C.c_uint64)], i),
         "kv_dev_dirichlet": ([i, P(C.c_uint64), i, C.c_double, i, i, P(C.c_double), P(i64), P(C.c_double)], i),
         "kv_dev_py_random": ([i, P(C.c_uint64), i, i, P(C.c_double)], i),
+        "kv_host_libm": ([i, P(C.c_double), P(C.c_double), i, P(C.c_double)], i),
         "kv_pgn_extract": ([C.c_char_p, sz, P(PgnRecord), sz, P(sz), P(sz), P(i64)], i),
         "kv_fen_codes": ([C.c_char_p, sz, i, P(C.c_int8)], i),
         "kv_san_move_index": ([C.c_char_p, sz, C.c_char_p, sz, i, P(C.c_int32)], i),
@@ -104,7 +105,7 @@ EXPORTED = ["kv_last_error", "kv_version", "kv_net_packed_size", "kv_net_create"
             "kv_net_forward_boards", "kv_net_set_timing", "kv_net_last_timing", "kv_net_destroy", "kv_net_set_precision", "kv_net_set_algo",
             "kv_create",
             "kv_load_weights", "kv_run", "kv_set_max_moves", "kv_records", "kv_games", "kv_stats_get", "kv_root_visits", "kv_records_device", "kv_sync", "kv_reset_records", "kv_destroy",
-            "kv_dev_valid_moves", "kv_dev_make_move", "kv_dev_attacks", "kv_dev_dirichlet", "kv_dev_py_random",
+            "kv_dev_valid_moves", "kv_dev_make_move", "kv_dev_attacks", "kv_dev_dirichlet", "kv_dev_py_random", "kv_host_libm",
             "kv_pgn_extract", "kv_fen_codes", "kv_san_move_index", "kv_chess_perft", "kv_chess_san", "kv_chess_fen"]
 
 

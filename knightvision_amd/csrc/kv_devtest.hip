@@ -10,6 +10,7 @@
 #include "kv_common.h"
 #include "kv_movegen.h"
 #include "kv_rng.h"
+#include "kv_libm.h"
 
 #pragma clang fp contract(off)
 
@@ -215,6 +216,12 @@ int kv_dev_dirichlet(int device, const uint64_t* seeds, int n, double alpha, int
     KV_HIP(hipMemcpy(out, o.p, (size_t)n * draws * k * sizeof(double), hipMemcpyDeviceToHost));
     KV_HIP(hipMemcpy(attempts, at.p, (size_t)n * draws * sizeof(long long), hipMemcpyDeviceToHost));
     KV_HIP(hipMemcpy(tail, t.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+    return KV_OK;
+}
+
+int kv_host_libm(int op, const double* x, const double* y, int n, double* out) {
+    KV_REQUIRE(x && out && n >= 0 && (op == 0 || (op == 1 && y)), KV_EINVAL, "kv_host_libm: bad arguments");
+    for (int i = 0; i < n; ++i) out[i] = op == 0 ? kv::glibc_log(x[i]) : kv::glibc_pow(x[i], y[i]);
     return KV_OK;
 }
 

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "kv_libm.h"
+
 // numpy/CPython evaluate these expressions without FMA contraction
 #pragma clang fp contract(off)
 
@@ -339,14 +341,16 @@ __device__ inline double block_dirichlet_gamma(BlockMT& w, double alpha, int k, 
             const int a = j * RNG_THREADS + tid;
             const uint32_t w0 = bmt_word(w, 4 * a), w1 = bmt_word(w, 4 * a + 1);
             const uint32_t w2 = bmt_word(w, 4 * a + 2), w3 = bmt_word(w, 4 * a + 3);
+            // legacy_standard_gamma (numpy legacy-distributions.c) with glibc's
+            // log / pow restated bit for bit (kv_libm.h)
             const double U = res53(w0, w1);
-            const double V = -log(1.0 - res53(w2, w3));
+            const double V = -glibc_log(1.0 - res53(w2, w3));
             if (U <= one_m) {
-                X[j] = pow(U, inv_a);
+                X[j] = glibc_pow(U, inv_a);
                 ok[j] = X[j] <= V;
             } else {
-                const double Y = -log((1 - U) / alpha);
-                X[j] = pow(one_m + alpha * Y, inv_a);
+                const double Y = -glibc_log((1 - U) / alpha);
+                X[j] = glibc_pow(one_m + alpha * Y, inv_a);
                 ok[j] = X[j] <= (V + Y);
             }
         }

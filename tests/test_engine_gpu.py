@@ -91,7 +91,9 @@ def test_device_dirichlet_stream_matches_numpy():
         # the stream position after the draws is exact (u32 consumption identical)
         assert tail[i] == rs.random_sample(), s
     print("dirichlet max ulp vs numpy:", max_ulp)
-    assert max_ulp <= 16  # ocml log/pow vs glibc: <= 2 ulp per call; consumption is exact
+    # glibc's log / pow restated bit for bit on the device (csrc/kv_libm.h, pinned on the host by
+    # tests/test_libm_cpu.py) and the serial left-to-right sum: every value identical to numpy's
+    assert max_ulp == 0
 
 
 def test_device_python_random_matches_cpython():
@@ -152,8 +154,10 @@ def test_engine_games_match_reference(golden_dir, group, precision):
         if r == "exact":
             assert reward == pytest.approx(g["reward"])
             assert int(games[k]["n_evals"]) == g["n_evals"]
-    print(precision, group, res)
-    assert sum(r == "exact" for r in res) >= n - max(1, n // 8)
+    ties = [r for r in res if r != "exact"]
+    print(f"{precision} {group}: {n - len(ties)}/{n} games move-for-move identical, near-tie divergences "
+          f"{len(ties)} {ties}")
+    assert len(ties) <= max(1, n // 8)
 
 
 def test_sequential_self_play_api_matches_reference(golden_dir):
