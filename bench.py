@@ -72,6 +72,9 @@ def parse():
                          "enough for games to complete, reported under 'ref_selection' with measured games/hour")
     ap.add_argument("--ref-steps", type=int, default=1200)
     ap.add_argument("--ref-warmup", type=int, default=600)
+    ap.add_argument("--tree-edge-cap", type=int, default=0,
+                    help="MCTS edge pool per slot (0: KV_MAXM x (sims+1), which cannot overflow; an overflow "
+                         "fails the run). Profiling runs under rocprofv3 --pmc use a smaller pool")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     return ap.parse_args()
@@ -214,7 +217,7 @@ def main():
         eng = SelfPlayEngine(synthetic_state_dict(42, "init"), slots=G, n_games=1 << 40, seed=42, max_moves=None,
                              batch=16, sims=sims, game_id_base=rank, game_id_stride=world,
                              record_cap=max(1 << 16, G * (steps + warmup + 8)), device=local, precision=precision,
-                             algo=algo)
+                             algo=algo, tree_edge_cap=args.tree_edge_cap if sims > 0 else 0)
         eng.run(warmup)
         s0 = eng.stats()
         eng.reset_records()

@@ -1,0 +1,158 @@
+"""The learn loop's data bridge and update step on the GPU (SURVEY.md 8f
+ranks 1-2), each against a CPU restatement of the reference.
+
+* Bridge (scripts/train.py:515-521 dataset.extend of self-play tuples): the
+  HIP engine replays golden games (tests/golden/games.npz, identical to the
+  reference move for move); train.records_to_tensors + codes_to_planes_t on
+  the device must give exactly the reference's encode_board planes
+  (ai/ai.py:17-30, via the oracle replay of the same games, pinned to the
+  reference's planes by tests/test_oracle_golden.py), its encode_move indices
+  and the per-game reward on every record (self_play.py:245-253).
+* Update step (scripts/train.py:126-196): one epoch of train.train_one_epoch
+  on the real ChessNet (PyTorch-ROCm autograd, GradScaler, accumulation 2,
+  clip 1.0, Adam) against oracle/torch_ref.reference_epoch in float64 on the
+  CPU from the same weights and batches. The fp32 run pins the step's logic:
+  losses within 1e-4 relative, clipped gradients within 1e-2 per tensor
+  (MIOpen's fp32 3x3 convolutions include Winograd solvers: 4.5e-3 measured),
+  and Adam's first step (~lr * sign(g)) moves at most 0.1 % of the weights
+  whose gradient is not negligible (|g| > 1e-3 max |g| of the tensor) the
+  other way (237 of 24.7 M measured). Under autocast (the reference's
+  torch.cuda.amp.autocast: fp16 convolutions) the same logic runs on fp16
+  arithmetic: losses within 5e-3, gradients within 0.2 (0.11 measured), at
+  most 5 % of the steps reversed (2.3 % measured). Conv biases ahead of a
+  BatchNorm have an exact gradient of 0 and are skipped."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from knightvision_amd import train as T
+from knightvision_amd.engine import SelfPlayEngine
+from knightvision_amd.weights import synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+
+
+def _golden(golden_dir, group="pg_init_mm80", n=4):
+    g = np.load(os.path.join(golden_dir, "games.npz"))
+    cnt = g[f"{group}.n"][:n]
+    offs = np.concatenate([[0], np.cumsum(g[f"{group}.n"])])
+    return [(int(g[f"{group}.seed"][i]), g[f"{group}.moves"][offs[i]:offs[i + 1]], float(g[f"{group}.reward"][i]))
+            for i in range(len(cnt))]
+
+
+def _engine_records(gold):
+    seed0 = gold[0][0]
+    with SelfPlayEngine(synthetic_state_dict(42, "init"), slots=len(gold), n_games=len(gold), seed=seed0,
+                        max_moves=80, batch=16) as eng:
+        eng.run()
+        return eng.records(), eng.games()
+
+
+def test_records_to_tensors_equals_reference_encoding(golden_dir):
+    from oracle import oracle as O
+    from oracle import torch_ref
+    gold = _golden(golden_dir)
+    recs, games = _engine_records(gold)
+    codes, moves, rew = T.records_to_tensors(recs, games, "cuda")
+    planes = T.codes_to_planes_t(codes).cpu().numpy()
+    moves, rew = moves.cpu().numpy(), rew.cpu().numpy()
+    ev = torch_ref.make_eval_fn(synthetic_state_dict(42, "init"))
+    k = 0
+    for gi, (seed, gmoves, greward) in enumerate(gold):
+        r = O.play_game(ev, O.MT(seed, "numpy"), O.MT(seed, "python"), O.Last(), max_moves=80, batch=16,
+                        softmax_fn=torch_ref.torch_softmax)
+        assert np.array_equal(r["moves"], gmoves), "oracle replay differs from the golden game"
+        n = len(gmoves)
+        want = np.stack([O.encode_board(st) for st in r["states"][:n]])
+        assert np.array_equal(planes[k:k + n], want), f"game {gi}: planes differ from encode_board"
+        assert np.array_equal(moves[k:k + n], gmoves.astype(np.int64)), f"game {gi}: move indices"
+        assert np.all(rew[k:k + n] == np.float32(greward)), f"game {gi}: rewards"
+        k += n
+    assert k == len(planes)
+
+
+def _batches(golden_dir, n_batches=4, bs=16):
+    recs, games = _engine_records(_golden(golden_dir))
+    codes, moves, rew = T.records_to_tensors(recs, games, "cuda")
+    g = torch.Generator().manual_seed(7)
+    idx = torch.randperm(codes.shape[0], generator=g)[:n_batches * bs].cuda()
+    return [T.Batch(T.codes_to_planes_t(codes[idx[i:i + bs]]), moves[idx[i:i + bs]], rew[idx[i:i + bs]])
+            for i in range(0, n_batches * bs, bs)]
+
+
+@pytest.mark.parametrize("amp,loss_rtol,grad_tol,flip_frac", [(False, 1e-4, 1e-2, 1e-3), (True, 5e-3, 0.2, 5e-2)])
+def test_update_step_matches_float64_restatement(golden_dir, amp, loss_rtol, grad_tol, flip_frac):
+    from knightvision_amd.model import ChessNet
+    from oracle import torch_ref
+    sd = synthetic_state_dict(42, "bn")
+    lr, accum, coef = 1e-3, 2, 0.01
+    batches = _batches(golden_dir)
+    m = ChessNet()
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    m.cuda().train()
+    opt = torch.optim.Adam(m.parameters(), lr=lr)
+    scaler = T.make_scaler("cuda")
+    losses = []
+    orig = T.batch_loss
+
+    def spy(*a, **kw):  # record each batch's loss as train_one_epoch computes it
+        out = orig(*a, **kw)
+        losses.append(float(out[0].detach()))
+        return out
+    T.batch_loss = spy
+    try:
+        st = T.train_one_epoch(m, batches, opt, scaler, accumulate_steps=accum, entropy_coef=coef, amp=amp)
+    finally:
+        T.batch_loss = orig
+    assert st["optimizer_steps"] == 2 and st["skipped"] == 0
+    cpu_batches = [(b.boards.cpu(), b.moves.cpu(), b.outcomes.cpu()) for b in batches]
+    ref_p, ref_losses, ref_g = torch_ref.reference_epoch(sd, cpu_batches[:accum], lr, accum, coef)
+    # losses of the first optimizer step's micro-batches (identical weights on both sides)
+    for a, b in zip(losses[:accum], ref_losses):
+        assert abs(a - b) <= loss_rtol * abs(b), (a, b)
+    # the first optimizer step's clipped gradients, accumulated as train_one_epoch does
+    m3 = ChessNet()
+    m3.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    m3.cuda().train()
+    for b in batches[:accum]:
+        (T.batch_loss(m3, b, coef, amp)[0] / accum).backward()
+    torch.nn.utils.clip_grad_norm_(m3.parameters(), max_norm=1.0)
+    rel = {}
+    for k, p in m3.named_parameters():
+        g, r = p.grad.detach().double().cpu(), ref_g[k]
+        if float(r.norm()) > 0:
+            rel[k] = float((g - r).norm() / r.norm())
+    rel = {k: v for k, v in rel.items() if not k.endswith(".bias") or "fc" in k}  # conv biases: exact gradient 0
+    worst_g = max(rel.values())
+    print(f"gradients (amp={amp}): worst per-tensor relative error {worst_g:.2e}; "
+          + ", ".join(f"{k} {v:.1e}" for k, v in sorted(rel.items(), key=lambda kv: -kv[1])[:6]))
+    # one optimizer step: redo the GPU epoch up to its first step and compare the moves
+    m2 = ChessNet()
+    m2.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    m2.cuda().train()
+    opt2 = torch.optim.Adam(m2.parameters(), lr=lr)
+    T.train_one_epoch(m2, batches[:accum], opt2, T.make_scaler("cuda"), accumulate_steps=accum, entropy_coef=coef,
+                      amp=amp)
+    worst, worst_k, checked, flips, noise = 0.0, None, 0, 0, []
+    gmax = max(float(g.abs().max()) for g in ref_g.values())
+    for k, p in m2.named_parameters():
+        p0 = torch.from_numpy(np.asarray(sd[k])).double()
+        d_gpu = p.detach().double().cpu() - p0
+        d_ref = ref_p[k] - p0
+        g = ref_g[k].abs()
+        if float(g.max()) < 1e-9 * gmax:
+            # the bias of a conv followed by BatchNorm: its exact gradient is 0 (BN removes the
+            # per-channel mean), so both sides' steps are +-lr on rounding noise
+            noise.append(k)
+            continue
+        sel = g > 1e-3 * g.max()
+        err = (d_gpu[sel] - d_ref[sel]).abs() / lr
+        flips += int((err > 0.5).sum())
+        if float(err.max()) > worst:
+            worst, worst_k = float(err.max()), k
+        checked += int(sel.sum())
+    print(f"update step (amp={amp}): {checked} weights compared, {flips} moved the other way, worst |step - oracle "
+          f"step| = {worst:.2e} lr ({worst_k}); zero-gradient tensors skipped: {len(noise)}")
+    assert worst_g <= grad_tol and flips <= flip_frac * checked
