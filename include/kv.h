@@ -54,6 +54,13 @@ int kv_net_forward(kv_net* net, const float* planes_dev, int B, float* policy_de
  * 7..12 bK bQ bR bB bN bp; square r*8+c, row 0 = rank 8). */
 int kv_net_forward_boards(kv_net* net, const int8_t* boards_dev, int B, float* policy_dev, float* value_dev,
                           void* stream);
+/* The same forward with only the listed moves' logits (the MCTS leaves' legal
+ * moves): moves_dev [B][maxm] move words (from | to << 6, as kv_dev_valid_moves),
+ * n_moves_dev [B] (0: no logits for that board); legal_dev [B][maxm] receives
+ * policy logit (from*64 + to) of each listed move, bit-identical to the
+ * corresponding entry of kv_net_forward_boards; value_dev [B]. */
+int kv_net_forward_boards_legal(kv_net* net, const int8_t* boards_dev, int B, const uint16_t* moves_dev,
+                                const int* n_moves_dev, int maxm, float* legal_dev, float* value_dev, void* stream);
 /* per-launch timing of the last forward (HIP events on `stream`): ms of the
  * residual conv launches summed, and count of those launches. */
 int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv);

@@ -62,6 +62,7 @@ def _declare(L):
         "kv_net_load": ([vp, P(C.c_float), sz], i),
         "kv_net_forward": ([vp, vp, i, vp, vp, vp], i),
         "kv_net_forward_boards": ([vp, vp, i, vp, vp, vp], i),
+        "kv_net_forward_boards_legal": ([vp, vp, i, vp, vp, i, vp, vp, vp], i),
         "kv_net_set_timing": ([vp, i], i),
         "kv_net_last_timing": ([vp, P(C.c_float), P(i)], i),
         "kv_net_destroy": ([vp], None),
@@ -102,7 +103,7 @@ def _declare(L):
 
 
 EXPORTED = ["kv_last_error", "kv_version", "kv_net_packed_size", "kv_net_create", "kv_net_load", "kv_net_forward",
-            "kv_net_forward_boards", "kv_net_set_timing", "kv_net_last_timing", "kv_net_destroy", "kv_net_set_precision", "kv_net_set_algo",
+            "kv_net_forward_boards", "kv_net_forward_boards_legal", "kv_net_set_timing", "kv_net_last_timing", "kv_net_destroy", "kv_net_set_precision", "kv_net_set_algo",
             "kv_create",
             "kv_load_weights", "kv_run", "kv_set_max_moves", "kv_records", "kv_games", "kv_stats_get", "kv_root_visits", "kv_records_device", "kv_sync", "kv_reset_records", "kv_destroy",
             "kv_dev_valid_moves", "kv_dev_make_move", "kv_dev_attacks", "kv_dev_dirichlet", "kv_dev_py_random", "kv_host_libm",

@@ -15,6 +15,8 @@ namespace kv {
 
 int net_forward_boards_internal(kv_net* net, const int8_t* boards_dev, int B, float* policy, float* value,
                                 hipStream_t st);
+int net_forward_boards_legal_internal(kv_net* net, const int8_t* boards_dev, int B, const uint16_t* moves,
+                                      const int* n_moves, int maxm, float* legal, float* value, hipStream_t st);
 int net_set_res_events(kv_net* net, hipEvent_t a, hipEvent_t b);
 void net_dom_info(const kv_net* net, int* algo, int* launches, double* flop);
 
@@ -105,17 +107,21 @@ struct MctsSlot {  // per-slot search scratch (kv_mcts.hip)
     int pad[5];
 };
 
-struct Tree {  // per-slot SoA node / edge pools, slot i at i*ecap / i*ncap
+struct __attribute__((aligned(16))) NodeRec {
+    int first, cnt, N, pad;
+};
+
+struct Tree {  // per-slot SoA edge pools + node records, slot i at i*ecap / i*ncap
     uint16_t* e_move;
     float* e_P;
     int* e_N;
     float* e_W;
     int* e_child;
-    int* n_first;
-    int* n_cnt;
-    int* n_N;
+    NodeRec* node;    // [slot][ncap]: first edge, edge count, visit count (one 16-B load per tree level)
     int* path;        // [slot][ncap]
     uint16_t* leaf_moves;  // [slot][MAXM]
+    int* leaf_cnt;         // [slot]: moves of the leaf in this step's network batch (0: none)
+    float* leaf_logits;    // [slot][MAXM]: their policy logits (kv_net_forward_boards_legal)
     MctsSlot* ms;
     const float* sqrt_tab;  // (float)sqrt((double)n), n < ncap + 2
     int* root_visits;       // optional [record_cap][MAXM]: root visit counts of each committed move (-1 padded)
@@ -326,5 +332,6 @@ int mcts_backup_select(const DevCfg& cfg, const Tree& t, const Slot* slots, cons
 int mcts_choose(const DevCfg& cfg, const Tree& t, Slot* slots, int8_t* boards, uint32_t* py_mt, kv_record* rec,
                 int8_t* last_board, Ctr* ctr, hipStream_t st);
 int hash_eval(const int8_t* boards, int rows, float* logits, float* values, hipStream_t st);
+int hash_legal(const Tree& t, int rows, hipStream_t st);
 
 }  // namespace kv

@@ -458,11 +458,12 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
         ALLOC(t.e_N, E * sizeof(int));
         ALLOC(t.e_W, E * sizeof(float));
         ALLOC(t.e_child, E * sizeof(int));
-        ALLOC(t.n_first, N * sizeof(int));
-        ALLOC(t.n_cnt, N * sizeof(int));
-        ALLOC(t.n_N, N * sizeof(int));
+        ALLOC(t.node, N * sizeof(kv::NodeRec));
         ALLOC(t.path, N * sizeof(int));
         ALLOC(t.leaf_moves, S * kv::MAXM * sizeof(uint16_t));
+        ALLOC(t.leaf_cnt, S * sizeof(int));
+        ALLOC(t.leaf_logits, S * kv::MAXM * sizeof(float));
+        (void)hipMemset(t.leaf_cnt, 0, S * sizeof(int));
         ALLOC(e->ms, S * sizeof(kv::MctsSlot));
         ALLOC(e->nn_boards, S * 64);
         ALLOC(e->probs, S * 4096 * sizeof(float));
@@ -525,13 +526,19 @@ int kv_set_max_moves(kv_engine* e, int max_moves) {
 }
 
 // one network pass over `rows` boards (or the hash test evaluator), with the
-// residual-tower section bracketed by HIP events for the roofline
-static int eng_eval(kv_engine* e, const int8_t* boards, int rows) {
+// residual-tower section bracketed by HIP events for the roofline; `leaf`:
+// the MCTS leaf batch, whose policy is only the leaves' legal moves
+// (kv_net_forward_boards_legal into tree.leaf_logits)
+static int eng_eval(kv_engine* e, const int8_t* boards, int rows, bool leaf = false) {
     kv_net* net = e->net;
     hipStream_t st = e->st;
     float* logits = e->logits;
     float* values = e->values;
-    if (e->dc.eval_mode == KV_EVAL_HASH) return kv::hash_eval(boards, rows, logits, values, st);
+    if (e->dc.eval_mode == KV_EVAL_HASH) {
+        int rc = kv::hash_eval(boards, rows, logits, values, st);
+        if (rc || !leaf) return rc;
+        return kv::hash_legal(e->tree, rows, st);  // its logits (all 0) in the compact layout
+    }
     if ((size_t)e->n_ev_used + 2 > e->ev.size()) {
         for (int k = 0; k < 2; ++k) {
             hipEvent_t x;
@@ -541,7 +548,10 @@ static int eng_eval(kv_engine* e, const int8_t* boards, int rows) {
     }
     kv::net_set_res_events(net, e->ev[e->n_ev_used], e->ev[e->n_ev_used + 1]);
     e->n_ev_used += 2;
-    const int rc = kv::net_forward_boards_internal(net, boards, rows, logits, values, st);
+    const int rc = leaf ? kv::net_forward_boards_legal_internal(net, boards, rows, e->tree.leaf_moves,
+                                                                e->tree.leaf_cnt, kv::MAXM, e->tree.leaf_logits,
+                                                                values, st)
+                        : kv::net_forward_boards_internal(net, boards, rows, logits, values, st);
     kv::net_set_res_events(net, nullptr, nullptr);
     kv::net_dom_info(net, &e->dom_algo, &e->dom_launches, &e->dom_flop);
     return rc;
@@ -586,7 +596,7 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
                 return rc;
             if ((rc = kv::mcts_select(e->dc, t, e->slots, e->boards, e->nn_boards, e->ctr, e->st, 0, S))) return rc;
             for (int k = 0; k < e->dc.sims; ++k) {
-                if ((rc = eng_eval(e, e->nn_boards, S))) return rc;
+                if ((rc = eng_eval(e, e->nn_boards, S, true))) return rc;
                 rc = k + 1 < e->dc.sims
                          ? kv::mcts_backup_select(e->dc, t, e->slots, e->boards, e->logits, e->values, e->probs,
                                                   e->nn_boards, e->ctr, e->st, 0, S)
@@ -717,8 +727,9 @@ void kv_destroy(kv_engine* e) {
     kv::Tree& t = e->tree;
     void* bufs[] = {e->slots, e->boards, e->moves, e->logits, e->values, e->last_probs,
                     e->np_mt, e->py_mt, e->rec, e->games, e->last_board, e->ctr,
-                    t.e_move, t.e_P, t.e_N, t.e_W, t.e_child, t.n_first, t.n_cnt, t.n_N, t.path,
-                    t.leaf_moves, e->ms, e->nn_boards, e->probs, e->sqrt_tab, t.root_visits};
+                    t.e_move, t.e_P, t.e_N, t.e_W, t.e_child, t.node, t.path,
+                    t.leaf_moves, e->ms, e->nn_boards, e->probs, e->sqrt_tab, t.root_visits, t.leaf_cnt,
+                    t.leaf_logits};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (e->ctr_host) (void)hipHostFree(e->ctr_host);

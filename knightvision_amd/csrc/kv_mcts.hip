@@ -24,8 +24,8 @@
 //            caller shrinks it) raises KV_EOVERFLOW.
 //   choose : random.choices over the root visit counts on the CPython stream
 //            (tau = 1), then makeMove / record / termination as the reference.
-// Tree: structure-of-arrays node and edge pools per slot in HBM
-// (move, P, N, W, child per edge; first edge, edge count, N per node).
+// Tree: structure-of-arrays edge pools per slot in HBM (move, P, N, W, child
+// per edge) and one 16-byte record per node (first edge, edge count, N).
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -87,9 +87,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         t.e_child[eb + j] = -1;
     }
     if (lane == 0) {
-        t.n_first[nb] = 0;
-        t.n_cnt[nb] = n;
-        t.n_N[nb] = 1;
+        t.node[nb] = NodeRec{0, n, 1, 0};
         MctsSlot m = t.ms[i];
         m.node_count = 1;
         m.edge_count = n;
@@ -111,7 +109,10 @@ __device__ inline void mcts_select_slot(const DevCfg& cfg, const Tree& t, const 
     __shared__ int s_meta[8];  // wtm wkr wkc bkr bkc flags ep
     const int lane = threadIdx.x;
     const Slot s = slots[i];
-    if (s.status != ST_ACTIVE) return;
+    if (s.status != ST_ACTIVE) {
+        if (lane == 0) t.leaf_cnt[i] = 0;  // no logits for this row of the batch
+        return;
+    }
     bd[lane] = boards[(size_t)i * 64 + lane];
     if (lane == 0) {
         s_meta[0] = s.wtm; s_meta[1] = s.wkr; s_meta[2] = s.wkc; s_meta[3] = s.bkr; s_meta[4] = s.bkc;
@@ -122,8 +123,9 @@ __device__ inline void mcts_select_slot(const DevCfg& cfg, const Tree& t, const 
     int* path = t.path + nb;
     int node = 0, depth = 0, leaf = -1;
     for (;;) {
-        const int first = t.n_first[nb + node], cnt = t.n_cnt[nb + node];
-        const float sq = t.sqrt_tab[t.n_N[nb + node]];
+        const NodeRec nd = t.node[nb + node];
+        const int first = nd.first, cnt = nd.cnt;
+        const float sq = t.sqrt_tab[nd.N];
         float best = -INFINITY;
         int bi = 0x7fffffff;
         for (int j = lane; j < cnt; j += 64) {
@@ -174,7 +176,10 @@ __device__ inline void mcts_select_slot(const DevCfg& cfg, const Tree& t, const 
             m.pad[1] += 1;
         }
     }
-    if (lane == 0) t.ms[i] = m;
+    if (lane == 0) {
+        t.ms[i] = m;
+        t.leaf_cnt[i] = m.leaf_pending ? m.leaf_n : 0;  // the logits the network computes for this slot
+    }
     __syncthreads();
     nn_boards[(size_t)i * 64 + lane] = bd[lane];
 }
@@ -191,16 +196,16 @@ __device__ inline void mcts_backup_slot(const DevCfg& cfg, const Tree& t, const 
     float v = m.leaf_value;
     if (m.leaf_pending) {
         v = values[i];
-        // priors = softmax over the legal moves' logits only (the 16 KB row is
-        // never swept): max, e_j = det_expf(l_j - max) kept in LDS, lane
-        // partial sums over j = lane, lane+64, ... in order, xor butterfly
-        const float* lg = logits + (size_t)i * 4096;
+        // priors = softmax over the legal moves' logits only, which the network
+        // wrote compactly in list order (kv_net_forward_boards_legal):
+        // max, e_j = det_expf(l_j - max) kept in LDS, lane partial sums over
+        // j = lane, lane+64, ... in order, xor butterfly
+        const float* lg = t.leaf_logits + (size_t)i * MAXM;
         const uint16_t* lm = t.leaf_moves + (size_t)i * MAXM;
         const int n = m.leaf_n;
         float mx = -INFINITY;
         for (int j = lane; j < n; j += 64) {
-            const int mv = lm[j];
-            const float l = lg[(mv & 63) * 64 + ((mv >> 6) & 63)];
+            const float l = lg[j];
             pri[j] = l;
             mx = fmaxf(mx, l);
         }
@@ -227,9 +232,7 @@ __device__ inline void mcts_backup_slot(const DevCfg& cfg, const Tree& t, const 
         if (lane == 0) {
             if (fits) {
                 const int id = m.node_count;
-                t.n_first[nb + id] = m.edge_count;
-                t.n_cnt[nb + id] = n;
-                t.n_N[nb + id] = 0;
+                t.node[nb + id] = NodeRec{m.edge_count, n, 0, 0};
                 t.e_child[eb + m.leaf_edge] = id;
                 m.node_count += 1;
                 m.edge_count += n;
@@ -247,14 +250,14 @@ __device__ inline void mcts_backup_slot(const DevCfg& cfg, const Tree& t, const 
         // backup along the path: the mover at depth d is the root side flipped d times
         const int* path = t.path + nb;
         int node = 0;
-        t.n_N[nb + node] += 1;
+        t.node[nb + node].N += 1;
         for (int d = 0; d < m.path_len; ++d) {
             const size_t e = eb + path[d];
             const bool white_moved = ((m.root_wtm != 0) ^ (d & 1)) != 0;
             t.e_N[e] += 1;
             t.e_W[e] = t.e_W[e] + (white_moved ? v : -v);
             node = t.e_child[e];
-            if (node >= 0) t.n_N[nb + node] += 1;
+            if (node >= 0) t.node[nb + node].N += 1;
         }
         t.ms[i] = m;
     }
@@ -294,7 +297,7 @@ __global__ __launch_bounds__(64) void k_mcts_choose(DevCfg cfg, Tree t, Slot* sl
     if (s.status != ST_ACTIVE) return;
     const MctsSlot m = t.ms[i];
     const size_t eb = (size_t)i * t.ecap, nb = (size_t)i * t.ncap;
-    const int n = t.n_cnt[nb];
+    const int n = t.node[nb].cnt;
     for (int j = lane; j < n; j += 64) vals[j] = (double)t.e_N[eb + j];
     __syncthreads();
     if (lane == 0) s_pick = choose_weighted(vals, cum, n, py_mt + (size_t)i * MT_WORDS);
@@ -330,6 +333,18 @@ __global__ void k_hash_eval(const int8_t* boards, int rows, float* logits, float
         }
         values[r] = (float)((int)(h % 129u) - 64) / 64.0f;
     }
+}
+
+// the hash evaluator's leaf logits (all 0) in kv_net_forward_boards_legal's layout
+__global__ void k_hash_legal(int* cnt, float* out) {
+    const int r = blockIdx.x, lane = threadIdx.x;
+    for (int j = lane; j < cnt[r]; j += 64) out[(size_t)r * MAXM + j] = 0.f;
+}
+
+int hash_legal(const Tree& t, int rows, hipStream_t st) {
+    hipLaunchKernelGGL(k_hash_legal, dim3(rows), dim3(64), 0, st, t.leaf_cnt, t.leaf_logits);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
 }
 
 int mcts_root(const DevCfg& cfg, const Tree& t, Slot* slots, const uint16_t* moves, const float* logits,

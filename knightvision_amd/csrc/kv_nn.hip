@@ -552,6 +552,47 @@ __global__ __launch_bounds__(256) void policy_fc_kernel(const float* __restrict_
     }
 }
 
+// Logits of listed moves only (the MCTS leaves' legal moves): out[b][j] =
+// logit of move j of board b, equal bit for bit to policy_fc_kernel's entry:
+// v_mfma_f32_32x32x2_f32 is an exact fmaf chain over its two k (k = 8s + j
+// from lanes 0-31, then 8s + 4 + j from lanes 32-63), so one lane per move
+// replays that chain over s = 0..15, j = 0..3 and adds the bias last. Reads
+// 512 B of W per move instead of writing and re-reading the 16 KB row.
+__global__ __launch_bounds__(64) void policy_legal_kernel(const float* __restrict__ pfeat,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ bias,
+                                                          const uint16_t* __restrict__ moves,
+                                                          const int* __restrict__ nmoves, int maxm,
+                                                          float* __restrict__ out) {
+    __shared__ float a[128];
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const int n = nmoves[b];
+    if (n <= 0) return;
+    a[lane] = pfeat[(size_t)b * 128 + lane];
+    a[lane + 64] = pfeat[(size_t)b * 128 + 64 + lane];
+    __syncthreads();
+    for (int j = lane; j < n; j += 64) {
+        const int mv = moves[(size_t)b * maxm + j];
+        const int idx = (mv & 63) * 64 + ((mv >> 6) & 63);
+        const float* wr = w + (size_t)idx * 128;
+        f32x4 w0[16], w1[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            w0[s] = *(const f32x4*)(wr + 8 * s);
+            w1[s] = *(const f32x4*)(wr + 8 * s + 4);
+        }
+        float acc = 0.f;
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                acc = __builtin_fmaf(a[8 * s + q], w0[s][q], acc);
+                acc = __builtin_fmaf(a[8 * s + 4 + q], w1[s][q], acc);
+            }
+        out[(size_t)b * maxm + j] = acc + bias[idx];
+    }
+}
+
 // ------------------------------------------------------------ encoders --
 // encode_board (ai/ai.py:17-30) straight into the stem's NHWC16 input.
 __global__ void encode_boards_kernel(const int8_t* __restrict__ boards, int nb, int nb_pad, float* __restrict__ x16) {
@@ -730,6 +771,13 @@ struct kv_net {
     float* V = nullptr;     // Winograd workspaces [36][cap*4][512]
     float* V256 = nullptr;  // conv2's input transform [36][cap*4][256]
     float* Mw = nullptr;
+    // kv_net_forward_boards_legal's request for the forward in flight (out == nullptr: full rows)
+    struct {
+        const uint16_t* moves = nullptr;
+        const int* n = nullptr;
+        int maxm = 0;
+        float* out = nullptr;
+    } legal;
     // the dominant kernel bracketed by res_a/res_b in the last forward
     int dom_algo = KV_ALGO_DIRECT;
     int dom_launches = 10;
@@ -1150,8 +1198,13 @@ static int net_heads(kv_net* net, int nb, float* policy, float* value, hipStream
     hipLaunchKernelGGL(kv::heads_kernel, dim3(nb), dim3(1024), 0, st, net->X, W + o.head_w, W + o.head_scale,
                        W + o.head_shift, net->v1wT, W + o.vfc1_b, W + o.vfc2_w, W + o.vfc2_b, net->pfeat, value);
     KV_HIP(hipGetLastError());
-    hipLaunchKernelGGL(kv::policy_fc_kernel, dim3(4096 / 128, (nb + 31) / 32), dim3(256), 0, st, net->pfeat,
-                       W + o.pfc_w, W + o.pfc_b, policy, nb);
+    if (net->legal.out) {  // kv_net_forward_boards_legal: the listed moves' logits only
+        hipLaunchKernelGGL(kv::policy_legal_kernel, dim3(nb), dim3(64), 0, st, net->pfeat, W + o.pfc_w, W + o.pfc_b,
+                           net->legal.moves, net->legal.n, net->legal.maxm, net->legal.out);
+    } else {
+        hipLaunchKernelGGL(kv::policy_fc_kernel, dim3(4096 / 128, (nb + 31) / 32), dim3(256), 0, st, net->pfeat,
+                           W + o.pfc_w, W + o.pfc_b, policy, nb);
+    }
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -1318,6 +1371,24 @@ int kv_net_forward_boards(kv_net* net, const int8_t* boards_dev, int B, float* p
     return net_tower(net, B, nb_pad, boards_dev, policy_dev, value_dev, st);  // stem_kernel encodes on the fly
 }
 
+int kv_net_forward_boards_legal(kv_net* net, const int8_t* boards_dev, int B, const uint16_t* moves_dev,
+                                const int* n_moves_dev, int maxm, float* legal_dev, float* value_dev, void* stream) {
+    KV_REQUIRE(net && net->loaded, KV_EINVAL, "kv_net_forward_boards_legal: net not loaded");
+    KV_REQUIRE(B > 0 && boards_dev && moves_dev && n_moves_dev && legal_dev && value_dev && maxm > 0, KV_EINVAL,
+               "kv_net_forward_boards_legal: bad arguments");
+    hipStream_t st = (hipStream_t)stream;
+    const int nb_pad = net_pad(net, B);
+    int rc = net_reserve(net, nb_pad);
+    if (rc) return rc;
+    net->legal.moves = moves_dev;
+    net->legal.n = n_moves_dev;
+    net->legal.maxm = maxm;
+    net->legal.out = legal_dev;
+    rc = net_tower(net, B, nb_pad, boards_dev, nullptr, value_dev, st);
+    net->legal.out = nullptr;
+    return rc;
+}
+
 int kv_net_set_timing(kv_net* net, int enable) {
     KV_REQUIRE(net, KV_EINVAL, "kv_net_set_timing: NULL");
     net->timing = enable != 0;
@@ -1367,6 +1438,10 @@ namespace kv {
 int net_forward_boards_internal(kv_net* net, const int8_t* boards_dev, int B, float* policy, float* value,
                                 hipStream_t st) {
     return kv_net_forward_boards(net, boards_dev, B, policy, value, (void*)st);
+}
+int net_forward_boards_legal_internal(kv_net* net, const int8_t* boards_dev, int B, const uint16_t* moves,
+                                      const int* n_moves, int maxm, float* legal, float* value, hipStream_t st) {
+    return kv_net_forward_boards_legal(net, boards_dev, B, moves, n_moves, maxm, legal, value, (void*)st);
 }
 int net_set_res_events(kv_net* net, hipEvent_t a, hipEvent_t b) {
     net->res_a = a;

@@ -122,6 +122,19 @@ class KVNet:
                    "kv_net_forward_boards")
         return pol, val
 
+    def forward_boards_legal(self, boards: torch.Tensor, moves: torch.Tensor, n_moves: torch.Tensor):
+        """boards int8 [B,64], moves uint16-as-int16 [B,maxm] (from | to << 6), n_moves int32 [B], all CUDA ->
+        (legal logits [B,maxm], value [B,1]): only the listed moves' logits (kv_net_forward_boards_legal)."""
+        B, maxm = moves.shape
+        boards, moves, n_moves = boards.contiguous(), moves.contiguous(), n_moves.contiguous()
+        out = torch.zeros((B, maxm), dtype=torch.float32, device=boards.device)
+        val = torch.empty((B, 1), dtype=torch.float32, device=boards.device)
+        st = torch.cuda.current_stream(boards.device).cuda_stream
+        _lib.check(_lib.lib().kv_net_forward_boards_legal(self.h, boards.data_ptr(), B, moves.data_ptr(),
+                                                          n_moves.data_ptr(), maxm, out.data_ptr(), val.data_ptr(),
+                                                          st), "kv_net_forward_boards_legal")
+        return out, val
+
     def close(self):
         if getattr(self, "h", None):
             _lib.lib().kv_net_destroy(self.h)

@@ -85,3 +85,28 @@ def test_batch_invariance(precision):
         p1, v1 = m(planes[i:i + 1])
         assert torch.equal(p1[0], p_16[i]) and torch.equal(v1[0], v_16[i])
     assert float((p_16 - p_all[:16]).abs().max()) < 1e-4
+
+
+@pytest.mark.parametrize("B", [17, 300, 2048])
+def test_legal_logits_equal_full_rows(B):
+    """kv_net_forward_boards_legal (the MCTS leaves' policy: listed moves only,
+    one fmaf chain per move) equals the full policy_fc rows bit for bit."""
+    from knightvision_amd.engine import packed_from
+    from knightvision_amd.model import KVNet
+    net = KVNet(0, packed_from(synthetic_state_dict(42, "peaked")))
+    g = torch.Generator().manual_seed(B)
+    codes = (torch.randint(0, 13, (B, 64), generator=g) * (torch.rand(B, 64, generator=g) < 0.4)).to(torch.int8)
+    moves = torch.randint(0, 4096, (B, 320), generator=g, dtype=torch.int32).to(torch.int16)
+    n = torch.randint(0, 321, (B,), generator=g, dtype=torch.int32)
+    n[0], n[-1] = 0, 320
+    pol, val = net.forward_boards(codes.cuda())
+    leg, lval = net.forward_boards_legal(codes.cuda(), moves.cuda(), n.cuda())
+    pol, leg = pol.cpu().numpy(), leg.cpu().numpy()
+    mv = moves.numpy().astype(np.int64) & 0xFFFF
+    idx = (mv & 63) * 64 + ((mv >> 6) & 63)
+    for b in range(B):
+        k = int(n[b])
+        assert np.array_equal(leg[b, :k].view(np.int32), pol[b, idx[b, :k]].view(np.int32)), b
+        assert np.all(leg[b, k:] == 0)
+    assert torch.equal(val.cpu(), lval.cpu())
+    net.close()
