@@ -213,19 +213,32 @@ def main():
     G = args.slots
     dev = torch.device("cuda", local)
 
-    def measure(precision, algo="auto", sims=sims, steps=steps, warmup=warmup, keep=False):
+    def run_chunks(eng, n, chunk, what, t0=None):
+        # kv_run in chunks so a long region prints progress (stderr, rank 0); each kv_run already
+        # synchronises with the device at its end, so the chunking adds no device idle time
+        done = 0
+        while done < n:
+            k = min(chunk, n - done)
+            eng.run(k)
+            done += k
+            if rank == 0 and (done == n or done % max(chunk, 1) == 0):
+                el = f" {time.perf_counter() - t0:.1f}s" if t0 is not None else ""
+                print(f"bench: {what} {done}/{n}{el}", file=sys.stderr, flush=True)
+
+    def measure(precision, algo="auto", sims=sims, steps=steps, warmup=warmup, keep=False, tag="main"):
         eng = SelfPlayEngine(synthetic_state_dict(42, "init"), slots=G, n_games=1 << 40, seed=42, max_moves=None,
                              batch=16, sims=sims, game_id_base=rank, game_id_stride=world,
                              record_cap=max(1 << 16, G * (steps + warmup + 8)), device=local, precision=precision,
                              algo=algo, tree_edge_cap=args.tree_edge_cap if sims > 0 else 0)
-        eng.run(warmup)
+        chunk = 1 if sims > 0 else 100  # one progress line per move (MCTS: ~10 s at C3) or per 100 ply-steps
+        run_chunks(eng, warmup, chunk, f"{tag} warmup")
         s0 = eng.stats()
         eng.reset_records()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        eng.run(steps)
+        run_chunks(eng, steps, chunk, f"{tag} timed", t0)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -263,18 +276,18 @@ def main():
 
     alt = None
     if args.alt_precision and args.alt_precision != args.precision:
-        alt = measure(args.alt_precision, steps=args.alt_steps, warmup=args.alt_warmup)
+        alt = measure(args.alt_precision, steps=args.alt_steps, warmup=args.alt_warmup, tag="alt " + args.alt_precision)
     refsel = None
     if mcts and args.ref_block:
         # C3-ref: the reference's move selection (one network row per ply, sampled move) on the same slots;
         # the warm-up ply-steps fill the slots with games at every stage, the timed ones complete games at
         # the steady-state rate
-        refsel = measure(args.precision, sims=0, steps=args.ref_steps, warmup=args.ref_warmup)
+        refsel = measure(args.precision, sims=0, steps=args.ref_steps, warmup=args.ref_warmup, tag="ref-selection")
     wino44 = direct = None
     if args.compare_direct and args.precision == "fp32" and m["dom_algo"] == 3:
-        wino44 = measure("fp32", "winograd", steps=1, warmup=1)
+        wino44 = measure("fp32", "winograd", steps=1, warmup=1, tag="winograd44")
     if args.compare_direct and args.precision == "fp32" and m["dom_algo"] in (2, 3):
-        direct = measure("fp32", "direct", steps=1, warmup=1)
+        direct = measure("fp32", "direct", steps=1, warmup=1, tag="direct")
 
     # roofline of the dominant kernel, timed with HIP events on the engine stream: the residual-tower
     # Winograd GEMM launch (60 x [2*boards x 512 x 512]) or, for the direct algorithm, the residual conv
@@ -327,14 +340,18 @@ def main():
                        "step": "one move of every slot (the whole search + the committed move)" if mcts else
                                "one ply of every slot"},
             "plies_per_s": plies / dt, "games_per_hour": gph,
-            "games_per_hour_note": ("games completed inside the timed region / its duration" if gph is not None else
-                                    f"no game completed inside the {steps} timed moves (plies {warmup + 1}-"
-                                    f"{warmup + steps} of games from the start position); measured games/hour: "
-                                    f"ref_selection"),
+            "games_per_hour_note": (
+                (f"{int(games_done)} games ended inside the timed region / its duration -- a transient count, not "
+                 f"a steady-state rate: every slot started at ply 0, the region covers plies {warmup + 1}-"
+                 f"{warmup + steps}, so only early endings (resignations after ply 15) are in it; the steady-state "
+                 "games/hour is ref_selection's" if mcts else
+                 "games completed inside the timed region / its duration (slots recycled)") if gph is not None else
+                f"no game completed inside the {steps} timed moves (plies {warmup + 1}-{warmup + steps} of games "
+                f"from the start position); measured games/hour: ref_selection"),
             "games_completed": games_done, "nn_evals_per_s": nn_rows / dt,
             "nn_tflops": nn_rows * FLOP_PER_EVAL / dt / 1e12, "gather_ms": gather_ms,
-            "gather": ("RCCL gather to rank 0 of the timed region's device-resident records" if world > 1 else
-                       "none at N=1 (no collective)"),
+            "gather": ((f"{'RCCL' if backend == 'nccl' else backend} gather to rank 0 of the timed region's "
+                        "device-resident records") if world > 1 else "none at N=1 (no collective)"),
             "records_gathered": n_records, "mean_plies_per_game": mean_len,
             "tree_overflows": m["tree_overflows"],
             "roofline": {"bound": "mfma",
