@@ -127,7 +127,7 @@ typedef struct {
     int batch;            /* SELFPLAY_BATCH_SIZE (self_play.py:34) */
     double eps;           /* DIR_NOISE_EPS */
     double alpha;         /* DIR_NOISE_ALPHA, must be in (0,1) */
-    int sims;             /* 0: reference move selection; >0: PUCT MCTS sims/move */
+    int sims;             /* 0: reference move selection; 1..KV_MAX_SIMS: PUCT MCTS sims/move */
     float c_puct;
     int eval_mode;        /* KV_EVAL_* */
     int64_t record_cap;   /* record buffer capacity */
@@ -140,6 +140,7 @@ typedef struct {
 } kv_config;
 
 #define KV_MAXM 320 /* move-list capacity per position */
+#define KV_MAX_SIMS 65000 /* MCTS edges keep 16-bit visit counts and child node ids */
 
 typedef struct {
     int64_t game_id;

@@ -107,6 +107,8 @@ struct MctsSlot {  // per-slot search scratch (kv_mcts.hip)
     int pad[5];
 };
 
+constexpr uint16_t NO_CHILD = 0xffff;  // e_child of an unexpanded edge
+
 struct __attribute__((aligned(16))) NodeRec {
     int first, cnt, N, pad;
 };
@@ -114,9 +116,9 @@ struct __attribute__((aligned(16))) NodeRec {
 struct Tree {  // per-slot SoA edge pools + node records, slot i at i*ecap / i*ncap
     uint16_t* e_move;
     float* e_P;
-    int* e_N;
+    uint16_t* e_N;      // visit count (<= sims <= KV_MAX_SIMS)
     float* e_W;
-    int* e_child;
+    uint16_t* e_child;  // child node id (< ncap) or NO_CHILD
     NodeRec* node;    // [slot][ncap]: first edge, edge count, visit count (one 16-B load per tree level)
     int* path;        // [slot][ncap]
     uint16_t* leaf_moves;  // [slot][MAXM]

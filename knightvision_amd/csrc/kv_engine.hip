@@ -388,7 +388,9 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
                "kv_create: bad seed_mode");
     KV_REQUIRE(cfg->seed_mode != KV_SEED_SEQUENTIAL || cfg->slots == 1, KV_EINVAL,
                "kv_create: sequential seeding plays games in order on one slot");
-    KV_REQUIRE(cfg->sims >= 0 && cfg->sims <= 100000, KV_EINVAL, "kv_create: sims out of range");
+    KV_REQUIRE(cfg->sims >= 0 && cfg->sims <= KV_MAX_SIMS, KV_EINVAL,
+               "kv_create: sims %d out of range [0, %d] (16-bit edge visit counts and child ids)", cfg->sims,
+               KV_MAX_SIMS);
     KV_REQUIRE(cfg->tree_edge_cap <= 0 || cfg->tree_edge_cap >= kv::MAXM, KV_EINVAL,
                "kv_create: tree_edge_cap %d must be 0 (auto) or >= KV_MAXM (the root's list)", cfg->tree_edge_cap);
     KV_REQUIRE(cfg->sims == 0 || cfg->seed_mode == KV_SEED_PER_GAME, KV_EINVAL,
@@ -446,18 +448,21 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
         kv::Tree& t = e->tree;
         t.ncap = cfg->sims + 2;
         // every expansion adds <= MAXM edges: (sims + 1) x MAXM edges can never
-        // overflow (C3: 2,048 slots x 801 x 320 x 18 B = 9.4 GB of the 288 GB);
+        // overflow (C3: 2,048 slots x 801 x 320 x 14 B = 7.3 GB of the 288 GB);
         // a smaller cap is honoured and an overflow raises KV_EOVERFLOW
         const long long full = (long long)kv::MAXM * (cfg->sims + 1);
-        t.ecap = (int)(cfg->tree_edge_cap > 0 ? std::min<long long>(cfg->tree_edge_cap, full) : full);
+        // node edge blocks start on 16-edge boundaries (kv_mcts.hip), so a
+        // caller's cap is rounded down to a multiple of 16 (MAXM is one) and
+        // every expansion still takes at most MAXM edges
+        t.ecap = (int)(cfg->tree_edge_cap > 0 ? std::min<long long>(cfg->tree_edge_cap & ~15, full) : full);
         t.c_puct = cfg->c_puct > 0.f ? cfg->c_puct : 1.5f;
         t.sims = cfg->sims;
         const size_t E = S * (size_t)t.ecap, N = S * (size_t)t.ncap;
         ALLOC(t.e_move, E * sizeof(uint16_t));
         ALLOC(t.e_P, E * sizeof(float));
-        ALLOC(t.e_N, E * sizeof(int));
+        ALLOC(t.e_N, E * sizeof(uint16_t));
         ALLOC(t.e_W, E * sizeof(float));
-        ALLOC(t.e_child, E * sizeof(int));
+        ALLOC(t.e_child, E * sizeof(uint16_t));
         ALLOC(t.node, N * sizeof(kv::NodeRec));
         ALLOC(t.path, N * sizeof(int));
         ALLOC(t.leaf_moves, S * kv::MAXM * sizeof(uint16_t));

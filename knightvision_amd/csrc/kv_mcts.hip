@@ -24,8 +24,10 @@
 //            caller shrinks it) raises KV_EOVERFLOW.
 //   choose : random.choices over the root visit counts on the CPython stream
 //            (tau = 1), then makeMove / record / termination as the reference.
-// Tree: structure-of-arrays edge pools per slot in HBM (move, P, N, W, child
-// per edge) and one 16-byte record per node (first edge, edge count, N).
+// Tree: structure-of-arrays edge pools per slot in HBM (move u16, P f32, N u16,
+// W f32, child u16 per edge: 14 B; a node's edges start on a 16-edge boundary)
+// and one 16-byte record per node (first edge, edge count; N for the root only:
+// a non-root node's visit count is its parent edge's N).
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -84,7 +86,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         t.e_P[eb + j] = total == 0.0 ? 1.0f / (float)n : (float)(vals[j] / total);
         t.e_N[eb + j] = 0;
         t.e_W[eb + j] = 0.f;
-        t.e_child[eb + j] = -1;
+        t.e_child[eb + j] = NO_CHILD;
     }
     if (lane == 0) {
         t.node[nb] = NodeRec{0, n, 1, 0};
@@ -121,11 +123,13 @@ __device__ inline void mcts_select_slot(const DevCfg& cfg, const Tree& t, const 
     __syncthreads();
     const size_t eb = (size_t)i * t.ecap, nb = (size_t)i * t.ncap;
     int* path = t.path + nb;
-    int node = 0, depth = 0, leaf = -1;
+    int node = 0, depth = 0, leaf = -1, parent_n = 0;
     for (;;) {
         const NodeRec nd = t.node[nb + node];
         const int first = nd.first, cnt = nd.cnt;
-        const float sq = t.sqrt_tab[nd.N];
+        // a non-root node's visit count is its parent edge's (both rise in
+        // the same backups), so only the root keeps one in its record
+        const float sq = t.sqrt_tab[node == 0 ? nd.N : parent_n];
         float best = -INFINITY;
         int bi = 0x7fffffff;
         for (int j = lane; j < cnt; j += 64) {
@@ -146,10 +150,11 @@ __device__ inline void mcts_select_slot(const DevCfg& cfg, const Tree& t, const 
         ++depth;
         __syncthreads();
         const int child = t.e_child[eb + e];
-        if (child < 0 || depth >= t.ncap) {
+        if (child == NO_CHILD || depth >= t.ncap) {
             leaf = e;
             break;
         }
+        parent_n = t.e_N[eb + e];
         node = child;
     }
     MctsSlot m = t.ms[i];
@@ -217,25 +222,27 @@ __device__ inline void mcts_backup_slot(const DevCfg& cfg, const Tree& t, const 
             part += e;
         }
         const float sum = wave_sum(part);
-        const bool fits = m.edge_count + n <= t.ecap && m.node_count < t.ncap;
+        // a node's edges start on a 16-edge boundary, so the descent's P / W
+        // (and N / child / move) reads of one node touch the fewest HBM lines
+        const int first = (m.edge_count + 15) & ~15;
+        const bool fits = first + n <= t.ecap && m.node_count < t.ncap;
         if (fits) {
-            const int first = m.edge_count;
             for (int j = lane; j < n; j += 64) {
                 const size_t e = eb + first + j;
                 t.e_move[e] = lm[j];
                 t.e_P[e] = sum > 0.f ? pri[j] / sum : 1.0f / (float)n;  // sum >= 1 for finite logits
                 t.e_N[e] = 0;
                 t.e_W[e] = 0.f;
-                t.e_child[e] = -1;
+                t.e_child[e] = NO_CHILD;
             }
         }
         if (lane == 0) {
             if (fits) {
                 const int id = m.node_count;
-                t.node[nb + id] = NodeRec{m.edge_count, n, 0, 0};
-                t.e_child[eb + m.leaf_edge] = id;
+                t.node[nb + id] = NodeRec{first, n, 0, 0};
+                t.e_child[eb + m.leaf_edge] = (uint16_t)id;
                 m.node_count += 1;
-                m.edge_count += n;
+                m.edge_count = first + n;
             } else {
                 // the expansion does not fit the slot's pools: counted and
                 // raised as an error (kv_run -> KV_EOVERFLOW), never silent
@@ -248,16 +255,15 @@ __device__ inline void mcts_backup_slot(const DevCfg& cfg, const Tree& t, const 
     }
     if (lane == 0) {
         // backup along the path: the mover at depth d is the root side flipped d times
+        // (a non-root node's visit count is its parent edge's N: only the
+        // root's record is updated)
         const int* path = t.path + nb;
-        int node = 0;
-        t.node[nb + node].N += 1;
+        t.node[nb].N += 1;
         for (int d = 0; d < m.path_len; ++d) {
             const size_t e = eb + path[d];
             const bool white_moved = ((m.root_wtm != 0) ^ (d & 1)) != 0;
             t.e_N[e] += 1;
             t.e_W[e] = t.e_W[e] + (white_moved ? v : -v);
-            node = t.e_child[e];
-            if (node >= 0) t.node[nb + node].N += 1;
         }
         t.ms[i] = m;
     }
