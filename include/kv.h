@@ -270,6 +270,61 @@ int kv_chess_perft(const char* fen, int depth, uint64_t* nodes);
 int kv_chess_san(const char* fen, const char* san_in, char* san_out, size_t san_cap, char* fen_after, size_t fen_cap);
 int kv_chess_fen(const char* fen_in, char* fen_out, size_t cap);
 
+/* --------------------------------------------------------------- train ---
+ * Update-step kernels of the learn loop. The reference
+ * trains ChessNet under torch.cuda.amp.autocast (scripts/train.py:161-184):
+ * its 3x3 convolutions (ai/model.py:34-40, :8-25) run on fp16 operands with
+ * fp32 accumulation and fp16 outputs, its BatchNorms in training mode (fp32
+ * batch statistics, fp16 output). These entry points restate those units for
+ * the tower (conv1, conv2, the 5 residual blocks), replacing the MIOpen
+ * convolutions / BatchNorms torch calls there (knightvision_amd/train_ops.py
+ * wraps them as autograd functions). Activations are NHWC fp16 device arrays
+ * [n boards][64 squares][C]; weights fp16 [co][9][ci] (tap = 3 * row + col of
+ * the 3x3 kernel); every call is asynchronous on `stream`.
+ */
+/* y = bias + conv3x3(x, w), pad 1 on the 8x8 board; ci % 16 == 0, co % 128 == 0;
+ * bias_dev fp32 [co] or NULL. Also the data gradient: x = dy, w = the flipped
+ * image of kv_tr_conv_weights_f16, co = the conv's input channels. */
+int kv_tr_conv3x3_f16(const void* x_dev, int n, int ci, const void* w_dev, const float* bias_dev, int co,
+                      void* y_dev, void* stream);
+/* fp32 torch weight [co][ci_real][3][3] -> fp16 forward image [co][9][ci] (channels >= ci_real zero) and,
+ * if wt_dev != NULL, the data-gradient image [ci][9][co] (taps flipped) */
+int kv_tr_conv_weights_f16(const float* w_dev, int co, int ci_real, int ci, void* wf_dev, void* wt_dev, void* stream);
+/* bytes of workspace kv_tr_conv3x3_wgrad_f16 needs (and the board splits it uses) */
+size_t kv_tr_wgrad_workspace(int n, int ci, int co, int* splits);
+/* dw fp32 [co][ci_real][3][3] = fp16-rounded sum over boards and squares of dy (x) shifted x;
+ * ci % 64 == 0, co % 64 == 0; deterministic (fixed split order) */
+int kv_tr_conv3x3_wgrad_f16(const void* dy_dev, const void* x_dev, int n, int ci, int ci_real, int co, float* dw_dev,
+                            void* ws_dev, size_t ws_bytes, void* stream);
+/* bytes of workspace the BatchNorm / channel-sum calls need for rows x C */
+size_t kv_tr_bn_workspace(int rows, int C);
+/* training BatchNorm statistics over rows (= boards x 64) of fp16 x: mean, biased var, 1/sqrt(var + eps) */
+int kv_tr_bn_stats_f16(const void* x_dev, int rows, int C, float eps, float* mean_dev, float* var_dev,
+                       float* invstd_dev, void* ws_dev, size_t ws_bytes, void* stream);
+/* y = fp16((x - mean) * invstd * gamma + beta); res_dev != NULL: y = fp16(y + res); relu: max(y, 0) */
+int kv_tr_bn_apply_f16(const void* x_dev, int rows, int C, const float* mean_dev, const float* invstd_dev,
+                       const float* gamma_dev, const float* beta_dev, const void* res_dev, int relu, void* y_dev,
+                       void* stream);
+/* backward of kv_tr_bn_apply_f16 (y_dev = its output, for the ReLU mask): dgamma, dbeta fp32 [C], dx fp16 and,
+ * if dres_dev != NULL, the residual's gradient (the masked dy) */
+int kv_tr_bn_backward_f16(const void* x_dev, const void* dy_dev, const void* y_dev, int rows, int C, int relu,
+                          const float* mean_dev, const float* invstd_dev, const float* gamma_dev, float* dgamma_dev,
+                          float* dbeta_dev, void* dx_dev, void* dres_dev, void* ws_dev, size_t ws_bytes, void* stream);
+/* per-channel sum of fp16 rows x C (a conv bias gradient) */
+int kv_tr_channel_sum_f16(const void* x_dev, int rows, int C, float* sum_dev, void* ws_dev, size_t ws_bytes,
+                          void* stream);
+/* the heads' 1x1 convolutions (policy 512 -> 2, value 512 -> 1; ai/model.py:42-49) over rows = boards x 64 of
+ * the tower output h fp16 [rows][512]: w fp16 [3][512] (policy rows 0-1, value row 2), b fp32 [3] (fp16 values);
+ * out fp16 [rows][4] (column 3 unused) */
+int kv_tr_head1x1_f16(const void* h_dev, int rows, const void* w_dev, const float* b_dev, void* out_dev,
+                      void* stream);
+size_t kv_tr_head1x1_workspace(int rows);
+/* its backward from dout fp16 [rows][4]: dh fp16 [rows][512], dw fp32 [3][512], db fp32 [3] (fp16-rounded) */
+int kv_tr_head1x1_backward_f16(const void* h_dev, const void* dout_dev, int rows, const void* w_dev, void* dh_dev,
+                               float* dw_dev, float* db_dev, void* ws_dev, size_t ws_bytes, void* stream);
+/* encode_board planes fp32 [n][12][8][8] (ai/ai.py:17-30) -> NHWC fp16 [n][64][cpad], channels >= 12 zero */
+int kv_tr_planes_to_nhwc(const float* planes_dev, int n, int cpad, void* out_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -4,9 +4,11 @@ HIP kernels of libkv.so (knightvision_amd/csrc/kv_nn.hip).
 
 forward(x[N,12,8,8]) -> (policy logits [N,4096], value [N,1]). In eval mode
 (the self-play path always calls model.eval(), self_play.py:77, :108) the
-forward is the HIP tower with BN folded; in train mode it is PyTorch-ROCm
-autograd over the same parameters (the update step of train.py, see
-knightvision_amd/train.py). The module keeps torch Parameters so checkpoints
+forward is the HIP tower with BN folded; in train mode under autocast fp16 on a
+GPU (the reference's update step, train.py:161-184) the tower runs on the HIP
+training kernels (train_ops.py: fp16 implicit-GEMM convolutions, training
+BatchNorm) with the heads as PyTorch ops; otherwise (fp32, CPU) it is
+PyTorch autograd over the same parameters. The module keeps torch Parameters so checkpoints
 load and save exactly like the reference's; the kernels read a BN-folded packed
 copy that is rebuilt whenever a parameter or BN statistic changes.
 """
@@ -59,6 +61,18 @@ def batch_norm_rows(bn: nn.BatchNorm2d, x, n_real=None):
 # 4096): convolution is per image, so training-mode calls are split into chunks
 # of CONV_CHUNK images (BatchNorm still sees the whole batch).
 CONV_CHUNK = int(os.getenv("KV_TRAIN_CONV_CHUNK", "1024"))
+
+
+# Update step under autocast fp16 on a GPU: "hip" = the tower on the HIP
+# training kernels (train_ops), "miopen" = PyTorch-ROCm's MIOpen convolutions.
+TRAIN_BACKEND = os.getenv("KV_TRAIN_BACKEND", "hip")
+
+
+def _autocast_on() -> bool:
+    try:
+        return torch.is_autocast_enabled("cuda")
+    except TypeError:  # older signature
+        return torch.is_autocast_enabled()
 
 
 def conv_chunked(conv: nn.Conv2d, x):
@@ -210,10 +224,37 @@ class ChessNet(nn.Module):
         val = torch.tanh(self.value_fc2(F.relu(self.value_fc1(v))))
         return pol, val
 
+    def _train_forward_hip(self, x, n_real=None):
+        """Training mode under autocast fp16 on CUDA: the tower on the HIP
+        training kernels (knightvision_amd/train_ops.py, csrc/kv_train.hip),
+        NHWC fp16; the heads' 1x1 convs on HIP kernels too (train_ops.Head1x1),
+        their BatchNorms and FCs as PyTorch ops, in ai/model.py:64-73's order
+        with the NCHW flatten (index c*64 + square). Rows after n_real (padding) are
+        dropped before the tower and returned as zeros."""
+        from . import train_ops
+        n = x.shape[0]
+        xr = x[:n_real] if n_real is not None else x
+        h = train_ops.tower_forward(self, xr)  # [m, 64, 512] fp16
+        m = h.shape[0]
+        bn = batch_norm_rows
+        hv = train_ops.Head1x1.apply(h, self.policy_conv.weight, self.policy_conv.bias, self.value_conv.weight,
+                                     self.value_conv.bias)  # [m, 64, 4] fp16: policy 0-1, value 2
+        pc = hv[..., 0:2].permute(0, 2, 1).reshape(m, 2, 8, 8)
+        pol = self.policy_fc(torch.flatten(F.relu(bn(self.policy_bn, pc)), 1))
+        vc = hv[..., 2:3].permute(0, 2, 1).reshape(m, 1, 8, 8)
+        v = torch.flatten(F.relu(bn(self.value_bn, vc)), 1)
+        val = torch.tanh(self.value_fc2(F.relu(self.value_fc1(v))))
+        if m < n:
+            pol = torch.cat([pol, pol.new_zeros((n - m,) + tuple(pol.shape[1:]))])
+            val = torch.cat([val, val.new_zeros((n - m,) + tuple(val.shape[1:]))])
+        return pol, val
+
     def forward(self, x, n_real=None):
         if self.training:
             if not isinstance(x, torch.Tensor):
                 x = torch.as_tensor(np.asarray(x))
+            if x.is_cuda and TRAIN_BACKEND == "hip" and _autocast_on():
+                return self._train_forward_hip(x, n_real)
             return self._train_forward(x, n_real)
         if not isinstance(x, torch.Tensor):
             x = torch.as_tensor(np.asarray(x))
