@@ -81,12 +81,14 @@ __global__ __launch_bounds__(cv::THREADS) void conv3x3_f16_kernel(const _Float16
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 31, h = lane >> 5;
     const int wb = wave & 3, wc = wave >> 2;
-    // XCD-aware order: the co blocks of one board block run back to back on one XCD (shared halo in L2)
+    // XCD-aware order (block b runs on XCD b % 8): every XCD keeps ONE output-channel block, so its
+    // weights (1.2 MB for 512 input channels) stay in that XCD's L2 for all its board blocks; the
+    // 8 / cblocks XCDs of a channel block interleave the board blocks
     const int cblocks = co / WCO, nblocks = (n + NB - 1) / NB;
-    const int total = cblocks * nblocks, per = (total + 7) >> 3;
-    const int t = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-    if (t >= total) return;
-    const int co0 = (t % cblocks) * WCO, n0 = (t / cblocks) * NB;
+    const int xcd = (int)(blockIdx.x & 7), per_c = 8 / cblocks;
+    const int cb = xcd % cblocks, bb = (int)(blockIdx.x >> 3) * per_c + xcd / cblocks;
+    if (bb >= nblocks) return;
+    const int co0 = cb * WCO, n0 = bb * NB;
 
     // zero both stages' halos (the border stays zero; the interior is rewritten every stage)
     for (int o = tid * 16; o < NB * XBOARD; o += THREADS * 16) {
@@ -140,14 +142,21 @@ __global__ __launch_bounds__(cv::THREADS) void conv3x3_f16_kernel(const _Float16
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[m][q][r] = 0.f;
 
+    // prefetch distance 2: at the top of iteration s the registers hold stage s+1 (loaded during
+    // stage s-1's MFMAs) and go to the free LDS buffer, then stage s+2's global loads are issued;
+    // a whole compute phase covers both latencies; one barrier per stage
     const int ns = ci / CK;
     load(0);
     __syncthreads();  // halo zeroing done before the interior stores
     store(lds);
+    if (ns > 1) load(1);
     __syncthreads();
     for (int s = 0; s < ns; ++s) {
         const unsigned char* cur = lds + (s & 1) * STAGE;
-        if (s + 1 < ns) load(s + 1);
+        if (s + 1 < ns) {
+            store(lds + ((s + 1) & 1) * STAGE);
+            if (s + 2 < ns) load(s + 2);
+        }
 #pragma unroll
         for (int tp = 0; tp < 9; ++tp) {
             const int dr = tp / 3 - 1, dc = tp % 3 - 1;
@@ -161,7 +170,6 @@ __global__ __launch_bounds__(cv::THREADS) void conv3x3_f16_kernel(const _Float16
 #pragma unroll
                 for (int q = 0; q < 2; ++q) acc[m][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[m], b[q], acc[m][q], 0, 0, 0);
         }
-        if (s + 1 < ns) store(lds + ((s + 1) & 1) * STAGE);
         __syncthreads();
     }
 
@@ -223,8 +231,20 @@ __global__ __launch_bounds__(wg::THREADS) void conv3x3_wgrad_f16_kernel(const _F
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63, tap = tid >> 6;
     const int dr = tap / 3 - 1, dc = tap % 3 - 1;
-    const int ct = co / TC, it = ci / TC;
-    const int tile = blockIdx.x % (ct * it), split = blockIdx.x / (ct * it);
+    // XCD-aware order (block b runs on XCD b % 8): the tiles of one board split run side by side on
+    // the same XCD(s), so each board's dY / X pass through HBM once per XCD and the tiles share them in L2
+    const int ct = co / TC, it = ci / TC, tiles = ct * it;
+    const int xcd = (int)(blockIdx.x & 7), k = (int)(blockIdx.x >> 3);
+    int split, tile;
+    if (splits >= 8) {  // splits spread over the XCDs
+        split = (k / tiles) * 8 + xcd;
+        tile = k % tiles;
+    } else {  // 8 / splits XCDs per split, its tiles dealt over them
+        const int xs = 8 / splits;
+        split = xcd / xs;
+        tile = k * xs + xcd % xs;
+    }
+    if (split >= splits || tile >= tiles) return;
     const int co0 = (tile % ct) * TC, ci0 = (tile / ct) * TC;
     const int per = (n + splits - 1) / splits;
     const int b0 = split * per, b1 = min(n, b0 + per);
@@ -275,14 +295,19 @@ __global__ __launch_bounds__(wg::THREADS) void conv3x3_wgrad_f16_kernel(const _F
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[m][j][r] = 0.f;
 
+    // prefetch distance 2, as in conv3x3_f16_kernel
     const int nst = (b1 - b0 + BPS - 1) / BPS;
     if (nst > 0) load(b0);
     __syncthreads();
     if (nst > 0) store(lds);
+    if (nst > 1) load(b0 + BPS);
     __syncthreads();
     for (int s = 0; s < nst; ++s) {
         const unsigned char* cur = lds + (s & 1) * STAGE;
-        if (s + 1 < nst) load(b0 + (s + 1) * BPS);
+        if (s + 1 < nst) {
+            store(lds + ((s + 1) & 1) * STAGE);
+            if (s + 2 < nst) load(b0 + (s + 2) * BPS);
+        }
 #pragma unroll
         for (int b = 0; b < BPS; ++b) {
             const unsigned char* dyi = cur + b * DYB;
@@ -290,19 +315,21 @@ __global__ __launch_bounds__(wg::THREADS) void conv3x3_wgrad_f16_kernel(const _F
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
                 h8 a[2], bv[2];
+                s4 av4[2][2], bv4[2][2];
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     const int k = 16 * ks + 8 * h + q + 4 * e;  // square of this lane's transposed row
                     const int sy = (k >> 3) + 1 + dr, sx = (k & 7) + 1 + dc;
 #pragma unroll
                     for (int m = 0; m < 2; ++m) {
-                        const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(dyi + k * RB + col + m * 64));
-                        const h4 hv = __builtin_bit_cast(h4, v);
-                        a[m][4 * e + 0] = hv[0]; a[m][4 * e + 1] = hv[1]; a[m][4 * e + 2] = hv[2]; a[m][4 * e + 3] = hv[3];
-                        const s4 u = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xi + (sy * 12 + sx) * RB + col + m * 64));
-                        const h4 hu = __builtin_bit_cast(h4, u);
-                        bv[m][4 * e + 0] = hu[0]; bv[m][4 * e + 1] = hu[1]; bv[m][4 * e + 2] = hu[2]; bv[m][4 * e + 3] = hu[3];
+                        av4[m][e] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(dyi + k * RB + col + m * 64));
+                        bv4[m][e] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xi + (sy * 12 + sx) * RB + col + m * 64));
                     }
+                }
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {  // elements 0-3 from the first read, 4-7 from the second
+                    a[m] = __builtin_bit_cast(h8, __builtin_shufflevector(av4[m][0], av4[m][1], 0, 1, 2, 3, 4, 5, 6, 7));
+                    bv[m] = __builtin_bit_cast(h8, __builtin_shufflevector(bv4[m][0], bv4[m][1], 0, 1, 2, 3, 4, 5, 6, 7));
                 }
 #pragma unroll
                 for (int m = 0; m < 2; ++m)
@@ -310,7 +337,6 @@ __global__ __launch_bounds__(wg::THREADS) void conv3x3_wgrad_f16_kernel(const _F
                     for (int j = 0; j < 2; ++j) acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[m], bv[j], acc[m][j], 0, 0, 0);
             }
         }
-        if (s + 1 < nst) store(lds + ((s + 1) & 1) * STAGE);
         __syncthreads();
     }
 
@@ -685,8 +711,10 @@ int kv_tr_conv3x3_f16(const void* x_dev, int n, int ci, const void* w_dev, const
         KV_HIP(hipFuncSetAttribute((const void*)conv3x3_f16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cv::LDS));
         attr = true;
     }
-    const int total = (co / cv::WCO) * ((n + cv::NB - 1) / cv::NB);
-    const int grid = (total + 7) / 8 * 8;
+    const int cblocks = co / cv::WCO, nblocks = (n + cv::NB - 1) / cv::NB;
+    KV_REQUIRE(8 % cblocks == 0, KV_EINVAL, "kv_tr_conv3x3_f16: co %d: at most 1024 output channels, a power of two "
+               "number of 128-channel blocks", co);
+    const int grid = (nblocks + 8 / cblocks - 1) / (8 / cblocks) * 8;
     hipLaunchKernelGGL(conv3x3_f16_kernel, dim3(grid), dim3(cv::THREADS), cv::LDS, (hipStream_t)stream,
                        (const _Float16*)x_dev, n, ci, (const _Float16*)w_dev, bias_dev, co, (_Float16*)y_dev);
     KV_HIP(hipGetLastError());
@@ -708,6 +736,14 @@ size_t kv_tr_wgrad_workspace(int n, int ci, int co, int* splits) {
     int s = (256 + tiles - 1) / tiles;  // about one workgroup per CU
     if (s > (n + 1) / 2) s = (n + 1) / 2;
     if (s < 1) s = 1;
+    // a power of two up to 8 (8 / splits XCDs per split), else a multiple of 8 (splits spread over the XCDs)
+    if (s < 8) {
+        int p = 1;
+        while (p * 2 <= s) p *= 2;
+        s = p;
+    } else {
+        s = s / 8 * 8;
+    }
     if (splits) *splits = s;
     return (size_t)s * co * 9 * ci * sizeof(float);
 }
@@ -727,7 +763,14 @@ int kv_tr_conv3x3_wgrad_f16(const void* dy_dev, const void* x_dev, int n, int ci
         attr = true;
     }
     const int tiles = (co / wg::TC) * (ci / wg::TC);
-    hipLaunchKernelGGL(conv3x3_wgrad_f16_kernel, dim3(tiles * splits), dim3(wg::THREADS), wg::LDS, (hipStream_t)stream,
+    int grid;
+    if (splits >= 8) {
+        grid = splits * tiles;  // splits % 8 == 0
+    } else {
+        const int xs = 8 / splits;
+        grid = (tiles + xs - 1) / xs * 8;
+    }
+    hipLaunchKernelGGL(conv3x3_wgrad_f16_kernel, dim3(grid), dim3(wg::THREADS), wg::LDS, (hipStream_t)stream,
                        (const _Float16*)dy_dev, (const _Float16*)x_dev, n, ci, co, splits, (float*)ws_dev);
     KV_HIP(hipGetLastError());
     const int total = co * ci_real * 9;

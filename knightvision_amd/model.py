@@ -31,14 +31,18 @@ PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "f16x3": 3}
 ALGOS = {"auto": 0, "direct": 1, "winograd": 2, "winograd48": 3}
 
 
-def batch_norm_rows(bn: nn.BatchNorm2d, x, n_real=None):
+def batch_norm_rows(bn: nn.BatchNorm2d, x, n_real=None, explicit: bool = False):
     """Training-mode BatchNorm2d whose batch statistics (and running-statistics
     update) cover only the first n_real rows -- the rows after them are padding
     that gives the update step a bucketed batch shape (knightvision_amd.train);
     those rows are normalised with the real rows' statistics and carry no loss.
-    n_real None / = batch: the module itself."""
-    if n_real is None or n_real >= x.shape[0] or not bn.training:
+    n_real None / = batch: the module itself, unless `explicit` (the same
+    arithmetic as elementwise torch ops: MIOpen compiles a BatchNorm kernel for
+    every new batch shape, tens of seconds on a fresh machine)."""
+    if not explicit and (n_real is None or n_real >= x.shape[0]) or not bn.training:
         return bn(x)
+    if n_real is None:
+        n_real = x.shape[0]
     acc = torch.float32 if x.dtype in (torch.float16, torch.bfloat16) else x.dtype  # statistics at >= fp32
     xr = x[:n_real].to(acc)
     mean = xr.mean(dim=(0, 2, 3))
@@ -236,7 +240,9 @@ class ChessNet(nn.Module):
         xr = x[:n_real] if n_real is not None else x
         h = train_ops.tower_forward(self, xr)  # [m, 64, 512] fp16
         m = h.shape[0]
-        bn = batch_norm_rows
+
+        def bn(mod, t):  # no MIOpen BatchNorm: it compiles a kernel per new batch shape
+            return batch_norm_rows(mod, t, explicit=True)
         hv = train_ops.Head1x1.apply(h, self.policy_conv.weight, self.policy_conv.bias, self.value_conv.weight,
                                      self.value_conv.bias)  # [m, 64, 4] fp16: policy 0-1, value 2
         pc = hv[..., 0:2].permute(0, 2, 1).reshape(m, 2, 8, 8)
