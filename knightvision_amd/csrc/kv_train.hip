@@ -39,37 +39,41 @@ typedef short s4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4 lds_s4;
 
 // ------------------------------------------------------------------ conv --
-// Workgroup: 4 boards x 128 output channels, 8 waves; wave w takes board
-// w & 3 and channels 64 (w >> 2) .. +64 as 2 x 2 MFMA tiles with M = output
-// channel, N = square (so a lane's accumulators are 4 consecutive channels of
-// one square: 8-byte stores). K = 9 taps x input channels, in stages of 16
-// input channels, double-buffered in LDS:
-//   W image : [128 co][9 taps][16 ci] f16, co stride 304 B (19 slots: the
-//             32 rows an A read touches land on distinct 16-B bank slots);
-//   X image : per board a zero-padded 10 x 10 halo at 12 squares per row,
-//             48 B per square (slot = 3 * square), the interior rewritten per
-//             stage, the border zeroed once.
+// Workgroup: 8 boards x 128 output channels, 8 waves; wave w takes board w and
+// all 128 channels as 4 x 2 MFMA tiles with M = output channel, N = square (a
+// lane's accumulators are 4 consecutive channels of one square: 8-byte
+// stores; 0.75 LDS fragment reads per MFMA). K = 9 taps x input channels, in
+// stages of 16 input channels, double-buffered in LDS:
+//   W image : [128 co][9 taps][16 ci] f16, co stride 304 B (19 slots: the 32
+//             rows an A read touches land on distinct 16-B bank slots);
+//   X image : per board the 64 squares at 48 B (32 B data + 16 B pad, row of 8
+//             squares = 24 slots); a tap that leaves the board reads a 16-B
+//             zero slot instead (same address in every such lane: broadcast).
 // Squares are dealt to the lanes of an N tile so that every ds_read_b128 lane
-// group reads board rows {0, 2} or {1, 3} of the tile: 16 distinct bank slots.
+// group reads tile rows {0, 1} or {2, 3}: 16 distinct bank slots for every
+// tap whose squares stay on the board. Global -> LDS through registers with
+// prefetch distance 2, one barrier per stage; each tap's fragments are read
+// while the previous tap's 8 MFMAs issue.
 namespace cv {
-constexpr int WCO = 128, NB = 4, CK = 16;
+constexpr int WCO = 128, NB = 8, CK = 16;
 constexpr int WROW = 9 * 32 + 16;          // 304 B per output channel
-constexpr int XPX = 48, XROW = 12;         // halo: 48 B per square, 12 squares per halo row
-constexpr int XBOARD = 10 * XROW * XPX;    // 5,760 B
+constexpr int XSQ = 48;                    // B per square
+constexpr int XBOARD = 64 * XSQ;           // 3,072 B
 constexpr int WIMG = WCO * WROW;           // 38,912 B
-constexpr int STAGE = WIMG + NB * XBOARD;  // 61,952 B
-constexpr int LDS = 2 * STAGE;             // 123,904 B
+constexpr int STAGE = WIMG + NB * XBOARD;  // 63,488 B
+constexpr int ZERO = 2 * STAGE;            // the zero slot, after both stages
+constexpr int LDS = 2 * STAGE + 16;        // 126,992 B
 constexpr int THREADS = 512;
 constexpr int W_CHUNKS = WCO * 9 * 2;      // 16-B pieces of a stage's W image (2,304)
 }  // namespace cv
 
-// square of an N tile handled by lane li (0..31): lane groups {0-3,12-15,20-27}
-// take tile rows 0 and 2, {4-11,16-19,28-31} rows 1 and 3
+// square of an N tile handled by lane li (0..31): lane group {0-3,12-15,20-27}
+// takes tile rows 0 and 1, {4-11,16-19,28-31} rows 2 and 3
 __device__ inline int conv_lane_square(int li) {
     const bool g0 = li < 4 || (li >= 12 && li < 16) || (li >= 20 && li < 28);
     // rank of li inside its group (0..15): group 0 = 0-3, 12-15, 20-27; group 1 = 4-11, 16-19, 28-31
     const int j = li < 4 ? li : li < 12 ? li - 4 : li < 20 ? li - 8 : li < 28 ? li - 12 : li - 16;
-    return ((j >> 3) * 2 + (g0 ? 0 : 1)) * 8 + (j & 7);
+    return ((j >> 3) + (g0 ? 0 : 2)) * 8 + (j & 7);
 }
 
 __global__ __launch_bounds__(cv::THREADS) void conv3x3_f16_kernel(const _Float16* __restrict__ x, int n, int ci,
@@ -80,7 +84,6 @@ __global__ __launch_bounds__(cv::THREADS) void conv3x3_f16_kernel(const _Float16
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int li = lane & 31, h = lane >> 5;
-    const int wb = wave & 3, wc = wave >> 2;
     // XCD-aware order (block b runs on XCD b % 8): every XCD keeps ONE output-channel block, so its
     // weights (1.2 MB for 512 input channels) stay in that XCD's L2 for all its board blocks; the
     // 8 / cblocks XCDs of a channel block interleave the board blocks
@@ -90,18 +93,10 @@ __global__ __launch_bounds__(cv::THREADS) void conv3x3_f16_kernel(const _Float16
     if (bb >= nblocks) return;
     const int co0 = cb * WCO, n0 = bb * NB;
 
-    // zero both stages' halos (the border stays zero; the interior is rewritten every stage)
-    for (int o = tid * 16; o < NB * XBOARD; o += THREADS * 16) {
-        *(u32x4*)(lds + WIMG + o) = u32x4{0, 0, 0, 0};
-        *(u32x4*)(lds + STAGE + WIMG + o) = u32x4{0, 0, 0, 0};
-    }
+    if (tid == 0) *(u32x4*)(lds + ZERO) = u32x4{0, 0, 0, 0};
 
-    // this thread's global -> LDS pieces
-    u32x4 rw[5], rx;
-    const int xb = tid >> 7, xsq = (tid & 127) >> 1, xhalf = tid & 1;
-    const bool xok = n0 + xb < n;
-    const _Float16* xsrc = x + ((size_t)(n0 + xb) * 64 + xsq) * ci + xhalf * 8;
-    const int xdst = WIMG + xb * XBOARD + (((xsq >> 3) + 1) * XROW + (xsq & 7) + 1) * XPX + xhalf * 16;
+    // this thread's global -> LDS pieces: W chunks tid + 512 i (i < 4, and i = 4 for tid < 256), X chunks tid, tid + 512
+    u32x4 rw[5], rx[2];
     auto load = [&](int s) {
         const int c0 = s * CK;
 #pragma unroll
@@ -112,7 +107,12 @@ __global__ __launch_bounds__(cv::THREADS) void conv3x3_f16_kernel(const _Float16
                 rw[i] = *(const u32x4*)(w + ((size_t)(co0 + o) * 9 + (r >> 1)) * ci + c0 + (r & 1) * 8);
             }
         }
-        rx = xok ? *(const u32x4*)(xsrc + c0) : u32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = tid + i * THREADS, b = c >> 7, sq = (c >> 1) & 63;
+            rx[i] = n0 + b < n ? *(const u32x4*)(x + ((size_t)(n0 + b) * 64 + sq) * ci + c0 + (c & 1) * 8)
+                               : u32x4{0, 0, 0, 0};
+        }
     };
     auto store = [&](unsigned char* st) {
 #pragma unroll
@@ -123,31 +123,38 @@ __global__ __launch_bounds__(cv::THREADS) void conv3x3_f16_kernel(const _Float16
                 *(u32x4*)(st + o * WROW + (r >> 1) * 32 + (r & 1) * 16) = rw[i];
             }
         }
-        *(u32x4*)(st + xdst) = rx;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = tid + i * THREADS, b = c >> 7, sq = (c >> 1) & 63;
+            *(u32x4*)(st + WIMG + b * XBOARD + sq * XSQ + (c & 1) * 16) = rx[i];
+        }
     };
 
-    int abase[2], bbase[2];
+    int abase[4], bbase[2];
+    bool up[2], down[2], left[2], right[2];
 #pragma unroll
-    for (int m = 0; m < 2; ++m) abase[m] = (wc * 64 + m * 32 + li) * WROW + 16 * h;
+    for (int m = 0; m < 4; ++m) abase[m] = (m * 32 + li) * WROW + 16 * h;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-        const int sq = q * 32 + conv_lane_square(li);
-        bbase[q] = WIMG + wb * XBOARD + (((sq >> 3) + 1) * XROW + (sq & 7) + 1) * XPX + 16 * h;
+        const int sq = q * 32 + conv_lane_square(li), sy = sq >> 3, sx = sq & 7;
+        bbase[q] = WIMG + wave * XBOARD + sq * XSQ + 16 * h;
+        up[q] = sy > 0;
+        down[q] = sy < 7;
+        left[q] = sx > 0;
+        right[q] = sx < 7;
     }
-    f32x16 acc[2][2];
+    f32x16 acc[4][2];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int q = 0; q < 2; ++q)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[m][q][r] = 0.f;
 
     // prefetch distance 2: at the top of iteration s the registers hold stage s+1 (loaded during
-    // stage s-1's MFMAs) and go to the free LDS buffer, then stage s+2's global loads are issued;
-    // a whole compute phase covers both latencies; one barrier per stage
+    // stage s-1's MFMAs) and go to the free LDS buffer, then stage s+2's global loads are issued
     const int ns = ci / CK;
     load(0);
-    __syncthreads();  // halo zeroing done before the interior stores
     store(lds);
     if (ns > 1) load(1);
     __syncthreads();
@@ -157,35 +164,43 @@ __global__ __launch_bounds__(cv::THREADS) void conv3x3_f16_kernel(const _Float16
             store(lds + ((s + 1) & 1) * STAGE);
             if (s + 2 < ns) load(s + 2);
         }
+        h8 fa[2][4], fb[2][2];
+        auto frag = [&](int tp, int k) {
+            const int dr = tp / 3 - 1, dc = tp % 3 - 1;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) fa[k][m] = *(const h8*)(cur + abase[m] + tp * 32);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const bool ok = (dr < 0 ? up[q] : dr > 0 ? down[q] : true) && (dc < 0 ? left[q] : dc > 0 ? right[q] : true);
+                fb[k][q] = *(const h8*)(ok ? cur + bbase[q] + (dr * 8 + dc) * XSQ : lds + ZERO);
+            }
+        };
+        frag(0, 0);
 #pragma unroll
         for (int tp = 0; tp < 9; ++tp) {
-            const int dr = tp / 3 - 1, dc = tp % 3 - 1;
-            h8 a[2], b[2];
+            if (tp + 1 < 9) frag(tp + 1, (tp + 1) & 1);
 #pragma unroll
-            for (int m = 0; m < 2; ++m) a[m] = *(const h8*)(cur + abase[m] + tp * 32);
+            for (int m = 0; m < 4; ++m)
 #pragma unroll
-            for (int q = 0; q < 2; ++q) b[q] = *(const h8*)(cur + bbase[q] + (dr * XROW + dc) * XPX);
-#pragma unroll
-            for (int m = 0; m < 2; ++m)
-#pragma unroll
-                for (int q = 0; q < 2; ++q) acc[m][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[m], b[q], acc[m][q], 0, 0, 0);
+                for (int q = 0; q < 2; ++q)
+                    acc[m][q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[tp & 1][m], fb[tp & 1][q], acc[m][q], 0, 0, 0);
         }
         __syncthreads();
     }
 
-    if (n0 + wb >= n) return;
+    if (n0 + wave >= n) return;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int sq = q * 32 + conv_lane_square(li);
-        _Float16* yo = y + ((size_t)(n0 + wb) * 64 + sq) * co + co0 + wc * 64;
+        _Float16* yo = y + ((size_t)(n0 + wave) * 64 + sq) * co + co0;
 #pragma unroll
-        for (int m = 0; m < 2; ++m)
+        for (int m = 0; m < 4; ++m)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int c = m * 32 + 8 * g + 4 * h;  // 4 consecutive channels in registers 4g .. 4g+3
                 f32x4 v = {acc[m][q][4 * g], acc[m][q][4 * g + 1], acc[m][q][4 * g + 2], acc[m][q][4 * g + 3]};
                 if (bias) {
-                    const f32x4 bv = *(const f32x4*)(bias + co0 + wc * 64 + c);
+                    const f32x4 bv = *(const f32x4*)(bias + co0 + c);
                     v = v + bv;
                 }
                 *(h4*)(yo + c) = __builtin_convertvector(v, h4);
