@@ -299,9 +299,13 @@ __global__ __launch_bounds__(wg::THREADS) void conv3x3_wgrad_f16_kernel(const _F
     };
 
     // transposed-read addresses: lane l, group g = l / 16, i = l % 16, q = i / 4, p = i % 4;
-    // rows 8h + q (+4 for elements 4..7), columns 16 (g & 1) + 4p (+32 per tile)
+    // rows 8h + q (+4 for elements 4..7), columns 16 (g & 1) + 4p (+32 per tile). Square k =
+    // 16 ks + 8h + q + 4e sits at board row 2 ks + h, column q + 4e, so every read is a per-lane
+    // base plus a compile-time offset (ks, e, tile, board)
     const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, h = lane >> 5;
     const int col = (16 * (g & 1) + 4 * p) * 2;
+    const int dy_lane = (8 * h + q) * RB + col;                                // + (16 ks + 4 e) RB
+    const int x_lane = BPS * DYB + ((h + 1 + dr) * 12 + q + 1 + dc) * RB + col;  // + (24 ks + 4 e) RB
     f32x16 acc[2][2];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -323,22 +327,22 @@ __global__ __launch_bounds__(wg::THREADS) void conv3x3_wgrad_f16_kernel(const _F
             store(lds + ((s + 1) & 1) * STAGE);
             if (s + 2 < nst) load(b0 + (s + 2) * BPS);
         }
+        const unsigned char* dyl = cur + dy_lane;
+        const unsigned char* xl = cur + x_lane;
 #pragma unroll
         for (int b = 0; b < BPS; ++b) {
-            const unsigned char* dyi = cur + b * DYB;
-            const unsigned char* xi = cur + BPS * DYB + b * XB;
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
                 h8 a[2], bv[2];
                 s4 av4[2][2], bv4[2][2];
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
-                    const int k = 16 * ks + 8 * h + q + 4 * e;  // square of this lane's transposed row
-                    const int sy = (k >> 3) + 1 + dr, sx = (k & 7) + 1 + dc;
 #pragma unroll
                     for (int m = 0; m < 2; ++m) {
-                        av4[m][e] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(dyi + k * RB + col + m * 64));
-                        bv4[m][e] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(xi + (sy * 12 + sx) * RB + col + m * 64));
+                        av4[m][e] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_s4*)(dyl + b * DYB + (16 * ks + 4 * e) * RB + m * 64));
+                        bv4[m][e] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_s4*)(xl + b * XB + (24 * ks + 4 * e) * RB + m * 64));
                     }
                 }
 #pragma unroll
