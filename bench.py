@@ -229,7 +229,8 @@ def main():
         eng = SelfPlayEngine(synthetic_state_dict(42, "init"), slots=G, n_games=1 << 40, seed=42, max_moves=None,
                              batch=16, sims=sims, game_id_base=rank, game_id_stride=world,
                              record_cap=max(1 << 16, G * (steps + warmup + 8)), device=local, precision=precision,
-                             algo=algo, tree_edge_cap=args.tree_edge_cap if sims > 0 else 0)
+                             algo=algo, tree_edge_cap=args.tree_edge_cap if sims > 0 else 0,
+                             keep_root_visits=keep and sims > 0)
         chunk = 1 if sims > 0 else 100  # one progress line per move (MCTS: ~10 s at C3) or per 100 ply-steps
         run_chunks(eng, warmup, chunk, f"{tag} warmup")
         s0 = eng.stats()
@@ -256,8 +257,9 @@ def main():
         out = dict(dt=dt, plies=plies, games_done=games_done, nn_rows=nn_rows, sims=sims_done,
                    conv_ms=d["res_conv_ms"] / max(d["res_conv_launches"], 1), dom_flop=s1["dom_flop"],
                    dom_algo=s1["dom_algo"], tree_overflows=s1["tree_overflows"], steps=steps, warmup=warmup)
-        if keep:  # the timed region's experience, left in HBM for the gather
+        if keep:  # the timed region's experience, left in HBM for the gather (MCTS: with pi)
             out["recs_dev"], out["gms"] = eng.records_device(), eng.games()
+            out["pi_dev"] = eng.root_visits_device() if sims > 0 else None
         eng.close()
         return out
 
@@ -270,9 +272,15 @@ def main():
     if world > 1:
         dist.barrier()
     tg = time.perf_counter()
-    recs_all, gms_all = gather_experience(m.pop("recs_dev"), m["gms"], dst=0)
+    pi_dev = m.pop("pi_dev")
+    if pi_dev is not None:  # (s, pi, z): records + root visit counts (BASELINE config C4)
+        recs_all, gms_all, pi_all = gather_experience(m.pop("recs_dev"), m["gms"], dst=0, pi=pi_dev)
+    else:
+        recs_all, gms_all = gather_experience(m.pop("recs_dev"), m["gms"], dst=0)
+        pi_all = None
     gather_ms = (time.perf_counter() - tg) * 1e3 if world > 1 else None
     n_records = int(len(recs_all)) if recs_all is not None else 0
+    gathered_bytes = n_records * 80 + (int(pi_all.nbytes) if pi_all is not None else 0)
 
     alt = None
     if args.alt_precision and args.alt_precision != args.precision:
@@ -351,8 +359,10 @@ def main():
             "games_completed": games_done, "nn_evals_per_s": nn_rows / dt,
             "nn_tflops": nn_rows * FLOP_PER_EVAL / dt / 1e12, "gather_ms": gather_ms,
             "gather": ((f"{'RCCL' if backend == 'nccl' else backend} gather to rank 0 of the timed region's "
-                        "device-resident records") if world > 1 else "none at N=1 (no collective)"),
-            "records_gathered": n_records, "mean_plies_per_game": mean_len,
+                        "device-resident (s, pi, z): 80-B records + uint16 root visit counts per move slot"
+                        if mcts else f"{'RCCL' if backend == 'nccl' else backend} gather to rank 0 of the timed "
+                        "region's device-resident records") if world > 1 else "none at N=1 (no collective)"),
+            "records_gathered": n_records, "gathered_bytes": gathered_bytes, "mean_plies_per_game": mean_len,
             "tree_overflows": m["tree_overflows"],
             "roofline": {"bound": "mfma",
                          "kernel": kname + kdesc,

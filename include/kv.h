@@ -136,7 +136,7 @@ typedef struct {
     int algo;             /* KV_ALGO_* of the network convs */
     int tree_edge_cap;    /* MCTS edges per slot; <= 0: KV_MAXM x (sims + 1), which cannot overflow. An
                              expansion that does not fit raises KV_EOVERFLOW (kv_stats.tree_overflows) */
-    int keep_root_visits; /* 1: keep each MCTS move's root visit counts for kv_root_visits (tests) */
+    int keep_root_visits; /* 1: keep each MCTS move's root visit counts (pi) for kv_root_visits[_device] */
 } kv_config;
 
 #define KV_MAXM 320 /* move-list capacity per position */
@@ -202,6 +202,10 @@ int kv_stats_get(kv_engine* e, kv_stats* out);
  * order. No reference counterpart (the reference has no search); used by the
  * parity tests against the oracle's PUCT restatement. */
 int kv_root_visits(kv_engine* e, int32_t* out, size_t cap, size_t* n);
+/* the same visit counts (pi of the (s, pi, z) training triple, BASELINE config C4) device to device, uint16
+ * [n][KV_MAXM] in the engine's record order -- row k belongs to record k of kv_records_device (0xffff past the
+ * position's move list); stream as in kv_records_device */
+int kv_root_visits_device(kv_engine* e, uint16_t* out_dev, size_t cap, size_t* n, void* stream);
 int kv_sync(kv_engine* e);
 void kv_destroy(kv_engine* e);
 

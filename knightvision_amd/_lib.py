@@ -76,6 +76,7 @@ def _declare(L):
         "kv_games": ([vp, P(Game), sz, P(sz)], i),
         "kv_stats_get": ([vp, P(Stats)], i),
         "kv_root_visits": ([vp, P(C.c_int32), sz, P(sz)], i),
+        "kv_root_visits_device": ([vp, vp, sz, P(sz), vp], i),
         "kv_records_device": ([vp, vp, sz, P(sz), vp], i),
         "kv_sync": ([vp], i),
         "kv_reset_records": ([vp], i),
@@ -118,7 +119,7 @@ def _declare(L):
 EXPORTED = ["kv_last_error", "kv_version", "kv_net_packed_size", "kv_net_create", "kv_net_load", "kv_net_forward",
             "kv_net_forward_boards", "kv_net_forward_boards_legal", "kv_net_set_timing", "kv_net_last_timing", "kv_net_destroy", "kv_net_set_precision", "kv_net_set_algo",
             "kv_create",
-            "kv_load_weights", "kv_run", "kv_set_max_moves", "kv_records", "kv_games", "kv_stats_get", "kv_root_visits", "kv_records_device", "kv_sync", "kv_reset_records", "kv_destroy",
+            "kv_load_weights", "kv_run", "kv_set_max_moves", "kv_records", "kv_games", "kv_stats_get", "kv_root_visits", "kv_root_visits_device", "kv_records_device", "kv_sync", "kv_reset_records", "kv_destroy",
             "kv_dev_valid_moves", "kv_dev_make_move", "kv_dev_attacks", "kv_dev_dirichlet", "kv_dev_py_random", "kv_host_libm",
             "kv_pgn_extract", "kv_fen_codes", "kv_san_move_index", "kv_chess_perft", "kv_chess_san", "kv_chess_fen",
             "kv_tr_conv3x3_f16", "kv_tr_conv_weights_f16", "kv_tr_wgrad_workspace", "kv_tr_conv3x3_wgrad_f16",

@@ -126,7 +126,7 @@ struct Tree {  // per-slot SoA edge pools + node records, slot i at i*ecap / i*n
     float* leaf_logits;    // [slot][MAXM]: their policy logits (kv_net_forward_boards_legal)
     MctsSlot* ms;
     const float* sqrt_tab;  // (float)sqrt((double)n), n < ncap + 2
-    int* root_visits;       // optional [record_cap][MAXM]: root visit counts of each committed move (-1 padded)
+    uint16_t* root_visits;  // optional [record_cap][MAXM]: root visit counts (pi) of each committed move, 0xffff padded
     int ecap, ncap;
     float c_puct;
     int sims;

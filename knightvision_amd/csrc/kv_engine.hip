@@ -473,7 +473,7 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
         ALLOC(e->nn_boards, S * 64);
         ALLOC(e->probs, S * 4096 * sizeof(float));
         ALLOC(e->sqrt_tab, (size_t)(t.ncap + 2) * sizeof(float));
-        if (cfg->keep_root_visits) ALLOC(t.root_visits, (size_t)e->cfg.record_cap * kv::MAXM * sizeof(int));
+        if (cfg->keep_root_visits) ALLOC(t.root_visits, (size_t)e->cfg.record_cap * kv::MAXM * sizeof(uint16_t));
         t.ms = e->ms;
         std::vector<float> sq(t.ncap + 2);
         for (int k = 0; k < t.ncap + 2; ++k) sq[k] = (float)sqrt((double)k);
@@ -712,16 +712,33 @@ int kv_root_visits(kv_engine* e, int32_t* out, size_t cap, size_t* n) {
     if (!out) return KV_OK;
     KV_REQUIRE(cap >= cnt, KV_EINVAL, "kv_root_visits: buffer holds %zu records, need %zu", cap, cnt);
     std::vector<kv_record> rec(cnt);
-    std::vector<int32_t> vis(cnt * kv::MAXM);
+    std::vector<uint16_t> vis(cnt * kv::MAXM);
     KV_HIP(hipMemcpy(rec.data(), e->rec, cnt * sizeof(kv_record), hipMemcpyDeviceToHost));
-    KV_HIP(hipMemcpy(vis.data(), e->tree.root_visits, vis.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    KV_HIP(hipMemcpy(vis.data(), e->tree.root_visits, vis.size() * sizeof(uint16_t), hipMemcpyDeviceToHost));
     std::vector<size_t> ord(cnt);
     for (size_t k = 0; k < cnt; ++k) ord[k] = k;
     std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {  // kv_records' order
         return rec[a].game_id != rec[b].game_id ? rec[a].game_id < rec[b].game_id : rec[a].ply < rec[b].ply;
     });
     for (size_t k = 0; k < cnt; ++k)
-        memcpy(out + k * kv::MAXM, vis.data() + ord[k] * kv::MAXM, kv::MAXM * sizeof(int32_t));
+        for (int j = 0; j < kv::MAXM; ++j) {
+            const uint16_t v = vis[ord[k] * kv::MAXM + j];
+            out[k * kv::MAXM + j] = v == 0xffff ? -1 : (int32_t)v;
+        }
+    return KV_OK;
+}
+
+int kv_root_visits_device(kv_engine* e, uint16_t* out_dev, size_t cap, size_t* n, void* stream) {
+    KV_REQUIRE(e && n, KV_EINVAL, "kv_root_visits_device: NULL argument");
+    KV_REQUIRE(e->tree.root_visits, KV_EINVAL, "kv_root_visits_device: engine was created without keep_root_visits");
+    int rc = eng_counters(e);
+    if (rc) return rc;
+    const size_t cnt = (size_t)std::min<unsigned long long>(e->ctr_host->rec_count, (unsigned long long)e->cfg.record_cap);
+    *n = cnt;
+    if (!out_dev) return KV_OK;
+    KV_REQUIRE(cap >= cnt, KV_EINVAL, "kv_root_visits_device: buffer holds %zu records, need %zu", cap, cnt);
+    KV_HIP(hipMemcpyAsync(out_dev, e->tree.root_visits, cnt * kv::MAXM * sizeof(uint16_t), hipMemcpyDeviceToDevice,
+                          (hipStream_t)stream));
     return KV_OK;
 }
 

@@ -318,8 +318,8 @@ __global__ __launch_bounds__(64) void k_mcts_choose(DevCfg cfg, Tree t, Slot* sl
     s.n_evals += m.pad[0];
     const unsigned long long ridx = commit_move(cfg, s, i, t.e_move[eb + s_pick], boards, rec, last_board, ctr, lane);
     if (t.root_visits && (long long)ridx < cfg.record_cap) {
-        int* rv = t.root_visits + (size_t)ridx * MAXM;
-        for (int j = lane; j < MAXM; j += 64) rv[j] = j < n ? t.e_N[eb + j] : -1;
+        uint16_t* rv = t.root_visits + (size_t)ridx * MAXM;
+        for (int j = lane; j < MAXM; j += 64) rv[j] = j < n ? t.e_N[eb + j] : (uint16_t)0xffff;
     }
     if (lane == 0) slots[i] = s;
 }

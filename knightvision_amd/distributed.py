@@ -5,7 +5,8 @@ the packed experience records at the end of an iteration.
 
 The gather moves packed 80-byte records (kv_record: game id, ply, move index,
 64 board codes) -- 38x smaller than the (12,8,8) float32 planes the trainer
-expands them into -- straight from HBM: the engine copies its record buffer
+expands them into -- and, for MCTS, each record's root visit counts (pi,
+uint16 per legal move) straight from HBM: the engine copies its record buffer
 device-to-device (kv_records_device) and RCCL (the "nccl" backend on ROCm,
 over xGMI) moves it; "gloo" (CPU tests) moves host tensors.
 
@@ -66,15 +67,20 @@ def gather_rows(t: torch.Tensor, dst: int | None = 0):
     return torch.cat([p[:k] for p, k in zip(parts, counts)])
 
 
-def sort_records(rows: torch.Tensor) -> torch.Tensor:
-    """uint8 [n, 80] kv_record rows -> ordered by (game_id, ply) (two stable sorts, on the rows' device)."""
-    if rows.shape[0] == 0:
-        return rows
+def record_order(rows: torch.Tensor) -> torch.Tensor:
+    """uint8 [n, 80] kv_record rows -> the permutation ordering them by (game_id, ply) (two stable sorts)."""
     gid = rows[:, 0:8].contiguous().view(torch.int64).reshape(-1)
     ply = rows[:, 8:12].contiguous().view(torch.int32).reshape(-1)
     o1 = torch.sort(ply, stable=True).indices
     o2 = torch.sort(gid[o1], stable=True).indices
-    return rows[o1[o2]]
+    return o1[o2]
+
+
+def sort_records(rows: torch.Tensor) -> torch.Tensor:
+    """uint8 [n, 80] kv_record rows -> ordered by (game_id, ply) (on the rows' device)."""
+    if rows.shape[0] == 0:
+        return rows
+    return rows[record_order(rows)]
 
 
 def _as_rows(x, dtype) -> torch.Tensor:
@@ -83,21 +89,30 @@ def _as_rows(x, dtype) -> torch.Tensor:
     return torch.from_numpy(np.ascontiguousarray(x).view(np.uint8).reshape(-1, dtype.itemsize))
 
 
-def gather_experience(records, games, dst: int | None = 0):
+def gather_experience(records, games, dst: int | None = 0, pi=None):
     """End-of-iteration gather of every rank's (records, games), ordered by
     (game_id, ply) / game_id. `records` is a numpy RECORD_DTYPE array or the
     engine's device tensor (SelfPlayEngine.records_device(), uint8 [n, 80]);
-    `games` a GAME_DTYPE array. Returns numpy arrays on `dst` (every rank when
-    dst is None) and (None, None) elsewhere."""
+    `games` a GAME_DTYPE array. MCTS runs also pass `pi`, the root visit counts
+    row for row with `records` (SelfPlayEngine.root_visits_device(), uint8
+    [n, 2 * MAXM]): the (s, pi, z) triple of BASELINE config C4 (s = board,
+    z = the game's reward) then crosses xGMI in the same gather. Returns numpy
+    arrays on `dst` (every rank when dst is None) and Nones elsewhere:
+    (records, games), or (records, games, pi uint16 [n, MAXM]) when pi is given."""
     r = gather_rows(_as_rows(records, RECORD_DTYPE), dst)
     g = gather_rows(_as_rows(games, GAME_DTYPE), dst)
+    p = gather_rows(pi, dst) if pi is not None else None
     if r is None:
-        return None, None
-    r = sort_records(r).cpu().numpy()
+        return (None, None) if pi is None else (None, None, None)
+    order = record_order(r) if r.shape[0] else None
+    r = (r[order] if order is not None else r).cpu().numpy()
     gms = g.cpu().numpy().reshape(-1).view(GAME_DTYPE) if g.numel() else np.zeros(0, GAME_DTYPE)
     recs = np.ascontiguousarray(r).reshape(-1).view(RECORD_DTYPE) if r.size else np.zeros(0, RECORD_DTYPE)
     gms = gms[np.argsort(gms["game_id"], kind="stable")]
-    return recs, gms
+    if pi is None:
+        return recs, gms
+    p = (p[order] if order is not None else p).cpu().numpy()
+    return recs, gms, np.ascontiguousarray(p).view(np.uint16).reshape(p.shape[0], -1)
 
 
 def shard_ids(n_games: int, rank: int, world: int):

@@ -94,6 +94,21 @@ class SelfPlayEngine:
                        "kv_records_device")
         return out
 
+    def root_visits_device(self):
+        """The MCTS root visit counts (pi) as a uint8 CUDA tensor [n, MAXM * 2] (uint16 counts, 0xffff padded),
+        row k belonging to row k of records_device() (needs keep_root_visits=True)."""
+        import torch
+        L = _lib.lib()
+        n = C.c_size_t()
+        _lib.check(L.kv_root_visits_device(self.h, None, 0, C.byref(n), None), "kv_root_visits_device")
+        dev = torch.device("cuda", self.cfg.device)
+        out = torch.empty((n.value, _lib.MAXM * 2), dtype=torch.uint8, device=dev)
+        if n.value:
+            st = torch.cuda.current_stream(dev).cuda_stream
+            _lib.check(L.kv_root_visits_device(self.h, C.c_void_p(out.data_ptr()), n.value, C.byref(n),
+                                               C.c_void_p(st)), "kv_root_visits_device")
+        return out
+
     def root_visits(self) -> np.ndarray:
         """MCTS root visit counts [records, MAXM] (-1 padded), rows in records() order
         (needs keep_root_visits=True)."""

@@ -1,6 +1,7 @@
 """World-size-2 gloo test of the multi-GPU path's only collective: the
 end-of-iteration experience gather (knightvision_amd.distributed.gather_rows,
-to the root and to all ranks), and of the game-id sharding (rank r plays ids
+to the root and to all ranks, with the MCTS root visit counts pi riding
+along row for row), and of the game-id sharding (rank r plays ids
 r, r+W, ...). The same gather over engine output runs on the GPU box in
 tests/test_shard_gpu.py."""
 import os
@@ -44,6 +45,22 @@ def _worker(rank, world, port, out_q):
     assert (root_r is None) == (rank != 0) and (root_g is None) == (rank != 0)
     if rank == 0:
         assert np.array_equal(root_r, all_r) and np.array_equal(root_g, all_g)
+    # MCTS: each record's root visit counts (pi, uint16 per move slot) travel with it and come back in
+    # the records' (game_id, ply) order
+    import torch
+    from knightvision_amd import _lib
+    pi = np.full((len(recs), _lib.MAXM), 0xffff, dtype=np.uint16)
+    pi[:, 0] = recs["move"]
+    pi[:, 1] = recs["ply"]
+    pi_rows = torch.from_numpy(pi.view(np.uint8).reshape(len(recs), -1).copy())
+    pr, pg, pp = gather_experience(recs, games, dst=0, pi=pi_rows)
+    if rank == 0:
+        assert np.array_equal(pr, all_r) and np.array_equal(pg, all_g)
+        assert pp.dtype == np.uint16 and pp.shape == (len(pr), _lib.MAXM)
+        assert np.array_equal(pp[:, 0], pr["move"]) and np.array_equal(pp[:, 1], pr["ply"])
+        assert (pp[:, 2:] == 0xffff).all()
+    else:
+        assert pr is None and pp is None
     out_q.put((rank, all_r["game_id"].tolist(), all_r["ply"].tolist(), all_r["move"].tolist(),
                all_g["game_id"].tolist()))
     dist.barrier()
