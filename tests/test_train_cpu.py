@@ -324,3 +324,29 @@ def test_nan_batch_is_skipped_on_every_rank():
         if "num_batches" in k:
             continue
         assert np.allclose(a[k], b[k], atol=1e-6), k
+
+
+def test_explicit_batch_norm_matches_module():
+    """The HIP update step computes the heads' BatchNorms with elementwise ops
+    (model.batch_norm_rows(explicit=True): MIOpen compiles a BatchNorm kernel for
+    every new batch shape); outputs, gradients and running statistics equal
+    nn.BatchNorm2d's training mode."""
+    from knightvision_amd.model import batch_norm_rows
+    torch.manual_seed(3)
+    for C in (1, 2):
+        a, b = torch.nn.BatchNorm2d(C), torch.nn.BatchNorm2d(C)
+        with torch.no_grad():
+            a.weight.uniform_(0.5, 1.5)
+            a.bias.normal_()
+        b.load_state_dict(a.state_dict())
+        x = (torch.randn(37, C, 8, 8) * 3 + 1).requires_grad_(True)
+        x2 = x.detach().clone().requires_grad_(True)
+        y1, y2 = a(x), batch_norm_rows(b, x2, explicit=True)
+        g = torch.randn_like(y1)
+        y1.backward(g)
+        y2.backward(g)
+        assert torch.allclose(y1, y2, atol=2e-6)
+        assert torch.allclose(x.grad, x2.grad, atol=2e-6)
+        assert torch.allclose(a.weight.grad, b.weight.grad, atol=1e-4)
+        assert torch.allclose(a.running_mean, b.running_mean) and torch.allclose(a.running_var, b.running_var)
+        assert int(a.num_batches_tracked) == int(b.num_batches_tracked) == 1
