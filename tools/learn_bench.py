@@ -31,10 +31,15 @@ def main():
     a = ap.parse_args()
     rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(torch.cuda.device_count(), 1)  # ranks > GPUs (a gloo rehearsal) share the devices
     torch.cuda.set_device(local)
     import torch.distributed as dist
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("KV_LEARN_BACKEND", "nccl")  # gloo: a rehearsal with ranks sharing one GPU
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     from knightvision_amd.learn import reinforcement_loop
     from knightvision_amd.model import ChessNet
     from knightvision_amd.weights import synthetic_state_dict
@@ -52,7 +57,8 @@ def main():
         dist.all_reduce(cnt)
     sp_s, tr_s = vals.tolist()
     if rank == 0:
-        print(json.dumps({"metric": "learn loop: self-play + DDP update per iteration", "n_gpus": world,
+        print(json.dumps({"metric": "learn loop: self-play + DDP update per iteration", "n_ranks": world,
+                          "backend": dist.get_backend() if world > 1 else None,
                           "iterations": a.iterations, "games_per_iteration": a.games, "max_moves": a.max_moves,
                           "sims": a.sims, "selfplay_s": sp_s, "train_s": tr_s,
                           "train_samples_per_s": cnt.item() / tr_s if tr_s else None,
