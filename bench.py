@@ -72,6 +72,9 @@ def parse():
                          "enough for games to complete, reported under 'ref_selection' with measured games/hour")
     ap.add_argument("--ref-steps", type=int, default=1200)
     ap.add_argument("--ref-warmup", type=int, default=600)
+    ap.add_argument("--eval", choices=["faithful", "lazy"], default="faithful",
+                    help="reference-selection network schedule: faithful (every board evaluated, as the reference "
+                         "does) or lazy (only the rows the schedule consumes, identical games)")
     ap.add_argument("--tree-edge-cap", type=int, default=0,
                     help="MCTS edge pool per slot (0: KV_MAXM x (sims+1), which cannot overflow; an overflow "
                          "fails the run). Profiling runs under rocprofv3 --pmc use a smaller pool")
@@ -202,7 +205,7 @@ def main():
             dist.init_process_group(backend)
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
-    from knightvision_amd.engine import SelfPlayEngine
+    from knightvision_amd.engine import EVAL_FAITHFUL, EVAL_LAZY, SelfPlayEngine
     from knightvision_amd.weights import synthetic_state_dict
     from knightvision_amd.distributed import gather_experience
 
@@ -225,9 +228,11 @@ def main():
                 el = f" {time.perf_counter() - t0:.1f}s" if t0 is not None else ""
                 print(f"bench: {what} {done}/{n}{el}", file=sys.stderr, flush=True)
 
-    def measure(precision, algo="auto", sims=sims, steps=steps, warmup=warmup, keep=False, tag="main"):
+    def measure(precision, algo="auto", sims=sims, steps=steps, warmup=warmup, keep=False, tag="main",
+                eval_mode="faithful"):
         eng = SelfPlayEngine(synthetic_state_dict(42, "init"), slots=G, n_games=1 << 40, seed=42, max_moves=None,
                              batch=16, sims=sims, game_id_base=rank, game_id_stride=world,
+                             eval_mode=EVAL_LAZY if (eval_mode == "lazy" and sims == 0) else EVAL_FAITHFUL,
                              record_cap=max(1 << 16, G * (steps + warmup + 8)), device=local, precision=precision,
                              algo=algo, tree_edge_cap=args.tree_edge_cap if sims > 0 else 0,
                              keep_root_visits=keep and sims > 0)
@@ -249,12 +254,14 @@ def main():
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        d = {k: s1[k] - s0[k] for k in ("plies", "games_done", "nn_rows", "sims", "res_conv_ms", "res_conv_launches")}
+        d = {k: s1[k] - s0[k] for k in ("plies", "games_done", "nn_rows", "sims", "res_conv_ms", "res_conv_launches",
+                                        "nn_rows_lazy")}
         tot = torch.tensor([d["plies"], d["games_done"], d["nn_rows"], d["sims"]], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(tot)
         plies, games_done, nn_rows, sims_done = (float(x) for x in tot.tolist())
         out = dict(dt=dt, plies=plies, games_done=games_done, nn_rows=nn_rows, sims=sims_done,
+                   nn_rows_evaluated=float(d["nn_rows_lazy"]) if eval_mode == "lazy" else nn_rows,
                    conv_ms=d["res_conv_ms"] / max(d["res_conv_launches"], 1), dom_flop=s1["dom_flop"],
                    dom_algo=s1["dom_algo"], tree_overflows=s1["tree_overflows"], steps=steps, warmup=warmup)
         if keep:  # the timed region's experience, left in HBM for the gather (MCTS: with pi)
@@ -263,7 +270,7 @@ def main():
         eng.close()
         return out
 
-    m = measure(args.precision, args.algo, keep=True)
+    m = measure(args.precision, args.algo, keep=True, eval_mode=args.eval)
     dt, plies, games_done, nn_rows, sims_done, conv_ms = (m[k] for k in ("dt", "plies", "games_done", "nn_rows",
                                                                           "sims", "conv_ms"))
 
@@ -285,12 +292,16 @@ def main():
     alt = None
     if args.alt_precision and args.alt_precision != args.precision:
         alt = measure(args.alt_precision, steps=args.alt_steps, warmup=args.alt_warmup, tag="alt " + args.alt_precision)
-    refsel = None
+    refsel = reflazy = None
     if mcts and args.ref_block:
         # C3-ref: the reference's move selection (one network row per ply, sampled move) on the same slots;
         # the warm-up ply-steps fill the slots with games at every stage, the timed ones complete games at
         # the steady-state rate
         refsel = measure(args.precision, sims=0, steps=args.ref_steps, warmup=args.ref_warmup, tag="ref-selection")
+        # the same games with the network only on the rows the schedule consumes (KV_EVAL_LAZY): a side
+        # figure, never the measured games/hour -- the reference evaluates every board
+        reflazy = measure(args.precision, sims=0, steps=args.ref_steps, warmup=args.ref_warmup,
+                          tag="ref-selection lazy", eval_mode="lazy")
     wino44 = direct = None
     if args.compare_direct and args.precision == "fp32" and m["dom_algo"] == 3:
         wino44 = measure("fp32", "winograd", steps=1, warmup=1, tag="winograd44")
@@ -430,6 +441,17 @@ def main():
                 "warmup": refsel["warmup"],
                 "reference_cpu": {"plies_per_s": 250.0, "games_per_hour": 2424.0,
                                   "source": "BASELINE.md: reference self_play.py (SELFPLAY_SEQ=1) on 8 Xeon cores"}}
+            if reflazy is not None:
+                out["ref_selection"]["lazy_eval_side_figure"] = {
+                    "note": "NOT the measured games/hour: the same games (identical records, "
+                            "tests/test_engine_gpu.py::test_compact_lazy_eval_matches_faithful) with the network run "
+                            "only on the rows the reference's schedule reads -- self_play.py evaluates a 16-board "
+                            "buffer and uses its last row (:129-150); here those rows alone form one compact batch "
+                            "per ply-step (KV_EVAL_LAZY)",
+                    "plies_per_s": reflazy["plies"] / reflazy["dt"],
+                    "games_per_hour": reflazy["games_done"] / reflazy["dt"] * 3600.0,
+                    "games_completed": reflazy["games_done"], "timed_s": reflazy["dt"],
+                    "network_rows": reflazy["nn_rows_evaluated"], "faithful_network_rows": reflazy["nn_rows"]}
             cal = os.path.join(HERE, "profiles", "r01_cpu_calibration.json")
             if not args.no_cpu_baseline and world == 1:
                 # the reference's selection restated on this box's host cores, and the reference-equivalent rate

@@ -110,9 +110,11 @@ void kv_net_destroy(kv_net* net);
 #define KV_SEED_SEQUENTIAL 1 /* one numpy + one CPython stream seeded SEED, games in order */
 
 #define KV_EVAL_FAITHFUL 0 /* every board evaluated once, as the reference does */
-#define KV_EVAL_LAZY 1     /* the network runs only on the steps whose row the schedule consumes
-                              (reference move selection, <= 16 slots: the sequential drop-in path);
-                              identical outputs, 1/SELFPLAY_BATCH_SIZE of the network work */
+#define KV_EVAL_LAZY 1     /* the network runs only on the rows the schedule consumes (reference move
+                              selection): <= 16 slots, all slots' rows on the steps where one is
+                              consumed (the sequential drop-in path); above, the consumed rows as one
+                              compact batch. Identical outputs, ~1/SELFPLAY_BATCH_SIZE of the network
+                              work -- the reference evaluates every board and reads one row in 16 */
 #define KV_EVAL_HASH 2     /* TEST ONLY: uniform logits + hash value instead of the network */
 
 typedef struct {
@@ -175,6 +177,8 @@ typedef struct {
     double dom_flop;      /* MFMA FLOPs of one measured launch (padded rows included) */
     int64_t dom_algo;     /* KV_ALGO_DIRECT, KV_ALGO_WINOGRAD or KV_ALGO_WINOGRAD48 for those launches */
     int64_t tree_overflows; /* MCTS expansions dropped for a full edge pool (each also fails kv_run) */
+    int64_t nn_rows_lazy;   /* KV_EVAL_LAZY above 16 slots: rows the compact batches sent through the
+                               network (nn_rows counts the rows the reference's schedule evaluates) */
 } kv_stats;
 
 typedef struct kv_engine kv_engine;

@@ -38,7 +38,7 @@ class Stats(C.Structure):
     _fields_ = [("steps", C.c_int64), ("plies", C.c_int64), ("games_done", C.c_int64), ("nn_rows", C.c_int64),
                 ("sims", C.c_int64), ("records", C.c_int64), ("res_conv_ms", C.c_double),
                 ("res_conv_launches", C.c_int64), ("step_ms", C.c_double), ("dom_flop", C.c_double),
-                ("dom_algo", C.c_int64), ("tree_overflows", C.c_int64)]
+                ("dom_algo", C.c_int64), ("tree_overflows", C.c_int64), ("nn_rows_lazy", C.c_int64)]
 
 
 class PgnRecord(C.Structure):

@@ -57,7 +57,7 @@ struct Ctr {
     int active;
     int error;
     int need_eval;  // KV_EVAL_LAZY: some slot consumes a network row this step
-    int pad;
+    int comp_rows;  // KV_EVAL_LAZY above 16 slots: network rows of this step's compact batch
 };
 
 struct DevCfg {

@@ -163,7 +163,7 @@ __global__ __launch_bounds__(64) void k_movegen(DevCfg cfg, Slot* slots, int8_t*
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sample(DevCfg cfg, Slot* slots, int8_t* boards, const uint16_t* moves,
                                                 const float* logits, const float* values, float* last_probs,
                                                 uint32_t* np_mt, uint32_t* py_mt, kv_record* rec, int8_t* last_board,
-                                                Ctr* ctr) {
+                                                Ctr* ctr, const int* row_of) {
     __shared__ uint32_t mt3[MT_RW];
     __shared__ double gam[4096];
     __shared__ double vals[MAXM];
@@ -182,8 +182,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     }
     if (s.consumed) {  // policy/value = _last_outputs[...][-1] (:147-150)
         __syncthreads();
-        if (lane < 64) wave_softmax_4096(logits + (size_t)i * 4096, lp, lane);
-        s.last_value = values[i];
+        const int row = row_of ? row_of[i] : i;  // the compact lazy batch's row of this slot
+        if (lane < 64) wave_softmax_4096(logits + (size_t)row * 4096, lp, lane);
+        s.last_value = values[row];
         s.has_last = 1;
         s.buf = 0;
         s.n_evals += 1;
@@ -304,6 +305,44 @@ __global__ __launch_bounds__(128) void k_finish(DevCfg cfg, Slot* slots, int8_t*
     if (tid == 0) slots[i] = s;
 }
 
+// KV_EVAL_LAZY above 16 slots: the boards of the slots whose network row the
+// schedule consumes this step (the only rows self_play.py reads: :147-150),
+// gathered in slot order into a compact batch; row_of[i] = the slot's row or
+// -1. A batch of 1-16 rows is padded to 17 with copies of its first board: the
+// network is batch-invariant bit for bit inside its > 16-board class (the
+// class of the all-slots batch of faithful mode), so every consumed row equals
+// the faithful row and the games are identical (tests/test_engine_gpu.py).
+__global__ __launch_bounds__(1024) void k_compact(DevCfg cfg, const Slot* slots, const int8_t* boards,
+                                                  int8_t* comp_boards, int* row_of, Ctr* ctr) {
+    __shared__ int wsum[16];
+    __shared__ int base;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) base = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < cfg.slots; c0 += 1024) {
+        const int i = c0 + tid;
+        const bool need = i < cfg.slots && slots[i].status == ST_ACTIVE && slots[i].consumed;
+        const unsigned long long bal = __ballot(need);
+        if (lane == 0) wsum[w] = __popcll(bal);
+        __syncthreads();
+        int off = base;
+        for (int k = 0; k < w; ++k) off += wsum[k];
+        const int row = off + __popcll(bal & ((1ull << lane) - 1));
+        if (i < cfg.slots) row_of[i] = need ? row : -1;
+        if (need)
+            for (int q = 0; q < 4; ++q)
+                ((u32x4*)(comp_boards + (size_t)row * 64))[q] = ((const u32x4*)(boards + (size_t)i * 64))[q];
+        __syncthreads();
+        if (tid == 0)
+            for (int k = 0; k < 16; ++k) base += wsum[k];
+        __syncthreads();
+    }
+    const int cnt = base, padded = cnt > 0 && cnt < 17 ? 17 : cnt;
+    for (int r = cnt + tid / 4; r < padded; r += 256)  // 4 threads per padding row
+        ((u32x4*)(comp_boards + (size_t)r * 64))[tid & 3] = ((const u32x4*)comp_boards)[tid & 3];
+    if (tid == 0) ctr->comp_rows = padded;
+}
+
 // the flush rows of sequential mode: boards [slots, 2*slots) = last appended board
 __global__ void k_flush_rows(DevCfg cfg, const Slot* slots, const int8_t* last_board, int8_t* nn_boards) {
     const int i = blockIdx.x, lane = threadIdx.x;
@@ -325,6 +364,9 @@ struct kv_engine {
     float* logits = nullptr;
     float* values = nullptr;
     float* last_probs = nullptr;
+    int8_t* comp_boards = nullptr;  // KV_EVAL_LAZY above 16 slots: this step's compact batch
+    int* row_of = nullptr;
+    long long lazy_rows = 0;        // rows sent through the network by the compact batches
     uint32_t* np_mt = nullptr;
     uint32_t* py_mt = nullptr;
     kv_record* rec = nullptr;
@@ -396,8 +438,8 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
     KV_REQUIRE(cfg->sims == 0 || cfg->seed_mode == KV_SEED_PER_GAME, KV_EINVAL,
                "kv_create: MCTS mode uses per-game seeding");
     KV_REQUIRE(cfg->eval_mode == KV_EVAL_FAITHFUL || cfg->eval_mode == KV_EVAL_HASH ||
-                   (cfg->eval_mode == KV_EVAL_LAZY && cfg->sims == 0 && cfg->slots <= 16),
-               KV_EINVAL, "kv_create: eval_mode %d not available (lazy: reference move selection, <= 16 slots)",
+                   (cfg->eval_mode == KV_EVAL_LAZY && cfg->sims == 0),
+               KV_EINVAL, "kv_create: eval_mode %d not available (lazy: reference move selection only)",
                cfg->eval_mode);
     KV_HIP(hipSetDevice(cfg->device));
     kv_engine* e = new kv_engine();
@@ -438,6 +480,10 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
     ALLOC(e->logits, R * 4096 * sizeof(float));
     ALLOC(e->values, R * sizeof(float));
     ALLOC(e->last_probs, S * 4096 * sizeof(float));
+    if (cfg->eval_mode == KV_EVAL_LAZY && S > 16) {
+        ALLOC(e->comp_boards, (S + 17) * 64);
+        ALLOC(e->row_of, S * sizeof(int));
+    }
     ALLOC(e->np_mt, S * kv::MT_WORDS * sizeof(uint32_t));
     ALLOC(e->py_mt, S * kv::MT_WORDS * sizeof(uint32_t));
     ALLOC(e->rec, (size_t)e->cfg.record_cap * sizeof(kv_record));
@@ -575,7 +621,8 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
     while ((max_steps < 0 || done < max_steps) && e->ctr_host->active > 0 &&
            (stop_after_games < 0 || (int64_t)e->ctr_host->games_count < stop_after_games)) {
         const bool lazy = e->dc.eval_mode == KV_EVAL_LAZY;
-        if (lazy) KV_HIP(hipMemsetAsync(&e->ctr->need_eval, 0, sizeof(int), e->st));
+        const bool compact = lazy && e->comp_boards != nullptr;  // above 16 slots
+        if (lazy && !compact) KV_HIP(hipMemsetAsync(&e->ctr->need_eval, 0, sizeof(int), e->st));
         hipLaunchKernelGGL(kv::k_movegen, dim3(S), dim3(64), 0, e->st, e->dc, e->slots, e->boards,
                            e->moves, e->ctr);
         KV_HIP(hipGetLastError());
@@ -583,7 +630,18 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
             hipLaunchKernelGGL(kv::k_flush_rows, dim3(S), dim3(64), 0, e->st, e->dc, e->slots, e->last_board,
                                e->boards);
         bool eval_now = true;
-        if (lazy) {  // evaluate only on the steps whose row the schedule consumes (identical outputs)
+        if (compact) {  // only the consumed rows, as one compact batch (identical outputs)
+            hipLaunchKernelGGL(kv::k_compact, dim3(1), dim3(1024), 0, e->st, e->dc, e->slots, e->boards,
+                               e->comp_boards, e->row_of, e->ctr);
+            KV_HIP(hipGetLastError());
+            KV_HIP(hipMemcpyAsync(&e->ctr_host->comp_rows, &e->ctr->comp_rows, sizeof(int), hipMemcpyDeviceToHost,
+                                  e->st));
+            KV_HIP(hipStreamSynchronize(e->st));
+            const int rows = e->ctr_host->comp_rows;
+            if (rows > 0 && (rc = eng_eval(e, e->comp_boards, rows))) return rc;
+            e->lazy_rows += rows;
+            eval_now = false;
+        } else if (lazy) {  // evaluate only on the steps whose row the schedule consumes (identical outputs)
             KV_HIP(hipMemcpyAsync(&e->ctr_host->need_eval, &e->ctr->need_eval, sizeof(int), hipMemcpyDeviceToHost,
                                   e->st));
             KV_HIP(hipStreamSynchronize(e->st));
@@ -593,7 +651,7 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
         if (!mcts) {
             hipLaunchKernelGGL(kv::k_sample, dim3(S), dim3(256), 0, e->st, e->dc, e->slots, e->boards, e->moves,
                                e->logits, e->values, e->last_probs, e->np_mt, e->py_mt, e->rec, e->last_board,
-                               e->ctr);
+                               e->ctr, compact ? (const int*)e->row_of : (const int*)nullptr);
             KV_HIP(hipGetLastError());
         } else {
             const kv::Tree& t = e->tree;
@@ -699,6 +757,7 @@ int kv_stats_get(kv_engine* e, kv_stats* out) {
     out->dom_flop = e->dom_flop;
     out->dom_algo = e->dom_algo;
     out->tree_overflows = (int64_t)e->ctr_host->tree_overflows;
+    out->nn_rows_lazy = e->lazy_rows;
     return KV_OK;
 }
 
@@ -747,7 +806,7 @@ void kv_destroy(kv_engine* e) {
     (void)hipSetDevice(e->cfg.device);
     if (e->st) (void)hipStreamSynchronize(e->st);
     kv::Tree& t = e->tree;
-    void* bufs[] = {e->slots, e->boards, e->moves, e->logits, e->values, e->last_probs,
+    void* bufs[] = {e->slots, e->boards, e->moves, e->logits, e->values, e->last_probs, e->comp_boards, e->row_of,
                     e->np_mt, e->py_mt, e->rec, e->games, e->last_board, e->ctr,
                     t.e_move, t.e_P, t.e_N, t.e_W, t.e_child, t.node, t.path,
                     t.leaf_moves, e->ms, e->nn_boards, e->probs, e->sqrt_tab, t.root_visits, t.leaf_cnt,

@@ -53,10 +53,11 @@ def selfplay_shard(model, n_games: int, iteration: int, device, *, sims=0, max_m
     if not ids:
         return None, None
     base = iteration * n_games + rank
+    from .self_play import batched_eval_mode
     with SelfPlayEngine(packed_from(model), slots=min(slots, len(ids)), n_games=len(ids), seed=SEED,
                         max_moves=max_moves, batch=SELFPLAY_BATCH, eps=EPSILON, alpha=ALPHA, sims=sims,
                         game_id_base=base, game_id_stride=world, device=dev.index or 0,
-                        precision=precision) as eng:
+                        precision=precision, eval_mode=batched_eval_mode() if sims == 0 else 0) as eng:
         eng.run()
         return eng.records(), eng.games()
 

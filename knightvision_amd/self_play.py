@@ -27,7 +27,7 @@ import numpy as np
 import torch
 
 from .ai import codes_to_planes
-from .engine import EVAL_LAZY, SEED_PER_GAME, SEED_SEQUENTIAL, REASONS, SelfPlayEngine, packed_from, records_by_game
+from .engine import EVAL_FAITHFUL, EVAL_LAZY, SEED_PER_GAME, SEED_SEQUENTIAL, REASONS, SelfPlayEngine, packed_from, records_by_game
 
 EPSILON = float(os.getenv("DIR_NOISE_EPS", "0.25"))
 ALPHA = float(os.getenv("DIR_NOISE_ALPHA", "0.3"))
@@ -172,11 +172,22 @@ def self_play(model, num_games, device, max_moves=None, model_path=None):
     return data
 
 
+def batched_eval_mode() -> int:
+    """Network schedule of the many-slot paths (play_batched, learn.selfplay_shard): KV_SELFPLAY_EVAL=faithful
+    (default: every board evaluated, as the reference does) or lazy (only the rows the schedule consumes, one
+    compact batch per ply-step: identical games, ~1/16 of the network work)."""
+    mode = os.getenv("KV_SELFPLAY_EVAL", "faithful")
+    if mode not in ("faithful", "lazy"):
+        raise ValueError(f"KV_SELFPLAY_EVAL must be 'faithful' or 'lazy', got {mode!r}")
+    return EVAL_LAZY if mode == "lazy" else EVAL_FAITHFUL
+
+
 def play_batched(model, num_games, max_moves=None, slots=None, seed=None, device_index=None):
     """num_games concurrent-slot games on one GPU, game g seeded SEED+g."""
     slots = slots or min(int(os.getenv("KV_SELFPLAY_SLOTS", "256")), max(1, num_games))
     with SelfPlayEngine(packed_from(model), slots=slots, n_games=num_games, seed=SEED if seed is None else seed,
                         seed_mode=SEED_PER_GAME, max_moves=max_moves, batch=BATCH_SIZE, eps=EPSILON, alpha=ALPHA,
+                        eval_mode=batched_eval_mode(),
                         device=_device_index(device) if device_index is None else device_index) as eng:
         eng.run()
         return _to_records(eng.records(), eng.games())

@@ -195,3 +195,26 @@ def test_lazy_eval_matches_faithful():
     assert len(ra) == len(rb) > 0 and np.array_equal(ra["move"], rb["move"])
     assert np.array_equal(ra["board"], rb["board"])
     assert np.array_equal(ga["reward"], gb["reward"]) and np.array_equal(ga["n_evals"], gb["n_evals"])
+
+
+@pytest.mark.parametrize("slots,n_games,max_moves", [(20, 40, 60), (96, 96, None)])
+def test_compact_lazy_eval_matches_faithful(slots, n_games, max_moves):
+    """KV_EVAL_LAZY above 16 slots: only the rows the schedule consumes (self_play.py:147-150 reads one
+    row of every 16-board batch) go through the network, as one compact batch per ply-step (padded to
+    17 rows when 1-16 are consumed: the > 16-board network class is batch-invariant bit for bit). The
+    games equal the faithful all-slots run record for record, on ~1/16 of the network rows."""
+    from knightvision_amd.engine import EVAL_FAITHFUL, EVAL_LAZY, SelfPlayEngine
+    out = {}
+    for mode in (EVAL_FAITHFUL, EVAL_LAZY):
+        with SelfPlayEngine(synthetic_state_dict(42, "peaked"), slots=slots, n_games=n_games, seed=42,
+                            max_moves=max_moves, batch=16, eval_mode=mode) as eng:
+            eng.run()
+            out[mode] = (eng.records(), eng.games(), eng.stats())
+    (ra, ga, sa), (rb, gb, sb) = out[EVAL_FAITHFUL], out[EVAL_LAZY]
+    assert len(ra) == len(rb) > 0 and len(ga) == len(gb) == n_games
+    assert np.array_equal(ra, rb), "compact lazy records differ from the faithful run"
+    assert np.array_equal(ga, gb), "compact lazy game results differ from the faithful run"
+    assert sb["nn_rows_lazy"] > 0 and sa["nn_rows_lazy"] == 0
+    print(f"compact lazy: {sb['nn_rows_lazy']} network rows for {sa['nn_rows']} faithful rows "
+          f"({sb['nn_rows_lazy'] / sa['nn_rows']:.3f})")
+    assert sb["nn_rows_lazy"] < 0.25 * sa["nn_rows"]

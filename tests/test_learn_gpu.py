@@ -36,3 +36,19 @@ def test_learn_loop_two_iterations():
     rp, rv = torch_ref.forward({k: torch.from_numpy(x) for k, x in sd.items()}, planes)
     assert np.abs(p.cpu().numpy() - rp.numpy()).max() <= 1e-4
     assert np.abs(v.cpu().numpy() - rv.numpy()).max() <= 1e-5
+
+
+def test_selfplay_shard_lazy_equals_faithful(monkeypatch):
+    """KV_SELFPLAY_EVAL=lazy (the compact schedule: only the consumed network rows) plays the learn
+    loop's self-play shard record for record like the default faithful schedule."""
+    from knightvision_amd.learn import selfplay_shard
+    from knightvision_amd.model import ChessNet
+    from knightvision_amd.weights import synthetic_state_dict
+    m = ChessNet()
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(42, "peaked").items()})
+    out = {}
+    for mode in ("faithful", "lazy"):
+        monkeypatch.setenv("KV_SELFPLAY_EVAL", mode)
+        out[mode] = selfplay_shard(m, 48, 0, "cuda:0", max_moves=40, slots=24)
+    (ra, ga), (rb, gb) = out["faithful"], out["lazy"]
+    assert len(ra) > 0 and np.array_equal(ra, rb) and np.array_equal(ga, gb)
