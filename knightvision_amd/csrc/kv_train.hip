@@ -14,7 +14,7 @@
 //       kernel on dy with the weights flipped and transposed
 //       (w'[ci][8 - t][co] = w[co][t][ci]).
 //   conv3x3_wgrad_f16_kernel : dw[co][t][ci] = sum_{n,p} dy[n][p][co] x[n][p + off(t)][ci],
-//       one wave per tap, split over boards (fp32 partials, reduced in a fixed
+//       12 waves (channel halves x a row of 3 taps), split over boards (fp32 partials, reduced in a fixed
 //       order: deterministic), both operands read transposed from LDS with
 //       ds_read_b64_tr_b16.
 //   bn_* : per-channel sums in fp32 per row block, combined in fp64 in block
@@ -221,7 +221,8 @@ __global__ void conv_weights_f16_kernel(const float* __restrict__ w, int co, int
 }
 
 // ----------------------------------------------------------------- wgrad --
-// Workgroup: 64 output x 64 input channels, all 9 taps (wave = tap), boards
+// Workgroup: 64 output x 64 input channels, all 9 taps (12 waves: output half x
+// input half x a kernel row of 3 taps, the dY fragment shared by the row), boards
 // [b0, b1) of this split, 2 boards per LDS stage (double-buffered). Images
 // (rows 192 B = 64 channels + 64 B pad: the 4 rows x 64 B of a transposed
 // read's 32-lane half land on 4 distinct quarter bank rows):
@@ -234,7 +235,7 @@ constexpr int DYB = 64 * RB;                // 12,288 B per board
 constexpr int XB = 10 * 12 * RB;            // 23,040 B per board
 constexpr int STAGE = BPS * (DYB + XB);     // 70,656 B
 constexpr int LDS = 2 * STAGE;              // 141,312 B
-constexpr int THREADS = 9 * 64;
+constexpr int THREADS = 12 * 64;          // 3 waves per SIMD
 constexpr int CHUNKS = BPS * 2 * 64 * 8;    // 16-B pieces per stage (dY + X interiors): 2,048
 }  // namespace wg
 
@@ -244,8 +245,12 @@ __global__ __launch_bounds__(wg::THREADS) void conv3x3_wgrad_f16_kernel(const _F
                                                                         float* __restrict__ part) {
     using namespace wg;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int tid = threadIdx.x, lane = tid & 63, tap = tid >> 6;
-    const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+    // wave w: output-channel half m, input-channel half jn, taps 3 gt .. 3 gt + 2 (kernel row dr = gt - 1,
+    // columns dc = -1, 0, 1): one 32 x 32 MFMA block per tap, the dY fragment shared by the three taps.
+    // 12 waves = 3 per SIMD (9 waves, one per tap, left one SIMD a third wave: 3/2/2/2)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int m = wave & 1, jn = (wave >> 1) & 1, gt = wave >> 2;
+    const int dr = gt - 1;
     // XCD-aware order (block b runs on XCD b % 8): the tiles of one board split run side by side on
     // the same XCD(s), so each board's dY / X pass through HBM once per XCD and the tiles share them in L2
     const int ct = co / TC, it = ci / TC, tiles = ct * it;
@@ -269,10 +274,11 @@ __global__ __launch_bounds__(wg::THREADS) void conv3x3_wgrad_f16_kernel(const _F
         *(u32x4*)(lds + STAGE + BPS * DYB + o) = u32x4{0, 0, 0, 0};
     }
 
-    u32x4 reg[4];
+    constexpr int PER = (CHUNKS + THREADS - 1) / THREADS;
+    u32x4 reg[PER];
     auto load = [&](int bb) {  // boards bb, bb+1
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < PER; ++i) {
             const int c = tid + i * THREADS;
             if (c < CHUNKS) {
                 const int isx = c >= CHUNKS / 2, cc = c & (CHUNKS / 2 - 1);
@@ -286,7 +292,7 @@ __global__ __launch_bounds__(wg::THREADS) void conv3x3_wgrad_f16_kernel(const _F
     };
     auto store = [&](unsigned char* st) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < PER; ++i) {
             const int c = tid + i * THREADS;
             if (c < CHUNKS) {
                 const int isx = c >= CHUNKS / 2, cc = c & (CHUNKS / 2 - 1);
@@ -304,15 +310,13 @@ __global__ __launch_bounds__(wg::THREADS) void conv3x3_wgrad_f16_kernel(const _F
     // base plus a compile-time offset (ks, e, tile, board)
     const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, h = lane >> 5;
     const int col = (16 * (g & 1) + 4 * p) * 2;
-    const int dy_lane = (8 * h + q) * RB + col;                                // + (16 ks + 4 e) RB
-    const int x_lane = BPS * DYB + ((h + 1 + dr) * 12 + q + 1 + dc) * RB + col;  // + (24 ks + 4 e) RB
-    f32x16 acc[2][2];
+    const int dy_lane = (8 * h + q) * RB + col + m * 64;                              // + (16 ks + 4 e) RB
+    const int x_lane = BPS * DYB + ((h + 1 + dr) * 12 + q + 1) * RB + col + jn * 64;   // + (24 ks + 4 e + dc) RB
+    f32x16 acc[3];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int t = 0; t < 3; ++t)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[m][j][r] = 0.f;
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
     // prefetch distance 2, as in conv3x3_f16_kernel
     const int nst = (b1 - b0 + BPS - 1) / BPS;
@@ -333,44 +337,37 @@ __global__ __launch_bounds__(wg::THREADS) void conv3x3_wgrad_f16_kernel(const _F
         for (int b = 0; b < BPS; ++b) {
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
-                h8 a[2], bv[2];
-                s4 av4[2][2], bv4[2][2];
+                s4 av4[2], bv4[3][2];
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
+                    av4[e] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(dyl + b * DYB + (16 * ks + 4 * e) * RB));
 #pragma unroll
-                    for (int m = 0; m < 2; ++m) {
-                        av4[m][e] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                            (lds_s4*)(dyl + b * DYB + (16 * ks + 4 * e) * RB + m * 64));
-                        bv4[m][e] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                            (lds_s4*)(xl + b * XB + (24 * ks + 4 * e) * RB + m * 64));
-                    }
+                    for (int t = 0; t < 3; ++t)
+                        bv4[t][e] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_s4*)(xl + b * XB + (24 * ks + 4 * e + t - 1) * RB));
                 }
+                // elements 0-3 from the first read, 4-7 from the second
+                const h8 a = __builtin_bit_cast(h8, __builtin_shufflevector(av4[0], av4[1], 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
-                for (int m = 0; m < 2; ++m) {  // elements 0-3 from the first read, 4-7 from the second
-                    a[m] = __builtin_bit_cast(h8, __builtin_shufflevector(av4[m][0], av4[m][1], 0, 1, 2, 3, 4, 5, 6, 7));
-                    bv[m] = __builtin_bit_cast(h8, __builtin_shufflevector(bv4[m][0], bv4[m][1], 0, 1, 2, 3, 4, 5, 6, 7));
+                for (int t = 0; t < 3; ++t) {
+                    const h8 bv = __builtin_bit_cast(h8, __builtin_shufflevector(bv4[t][0], bv4[t][1], 0, 1, 2, 3, 4, 5, 6, 7));
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bv, acc[t], 0, 0, 0);
                 }
-#pragma unroll
-                for (int m = 0; m < 2; ++m)
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[m], bv[j], acc[m][j], 0, 0, 0);
             }
         }
         __syncthreads();
     }
 
-    // D[row = co][col = ci]: lane li holds ci = 32 j + li, rows (r&3) + 8 (r>>2) + 4h of tile m
+    // D[row = co][col = ci]: lane li holds ci = 32 jn + li, rows (r&3) + 8 (r>>2) + 4h of half m
     const int li = lane & 31;
     float* po = part + (size_t)split * co * 9 * ci;
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int t = 0; t < 3; ++t)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int o = co0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                po[((size_t)o * 9 + tap) * ci + ci0 + j * 32 + li] = acc[m][j][r];
-            }
+        for (int r = 0; r < 16; ++r) {
+            const int o = co0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            po[((size_t)o * 9 + 3 * gt + t) * ci + ci0 + jn * 32 + li] = acc[t][r];
+        }
 }
 
 // sum of the split partials in split order -> fp16 rounding (the gradient of
