@@ -211,3 +211,42 @@ def test_head1x1_forward_backward():
     _close16(torch.cat([params[0].grad.reshape(2, 512), params[2].grad.reshape(1, 512)]), dw, "head 1x1 weight grad")
     db = d.sum(dim=(0, 1))
     assert torch.allclose(torch.cat([params[1].grad, params[3].grad]).cpu(), db.half().float(), rtol=1e-3, atol=1e-3)
+
+
+def test_training_trajectory_matches_miopen():
+    """30 update steps (autocast fp16, GradScaler, accumulation 2, clip 1.0, Adam; train.py:126-196) on the
+    same engine-played records with the HIP training kernels and with torch's MIOpen path: the loss
+    trajectories agree to fp16-rounding drift and both fall (the HIP step trains the network as the
+    reference's does)."""
+    from knightvision_amd import model as KM
+    from knightvision_amd import train as T
+    from knightvision_amd.engine import SelfPlayEngine
+    from knightvision_amd.weights import synthetic_state_dict
+    sd = synthetic_state_dict(42, "init")
+    with SelfPlayEngine(sd, slots=64, n_games=64, seed=42, max_moves=60, batch=16) as eng:
+        eng.run()
+        recs, games = eng.records(), eng.games()
+    codes, moves, rew = T.records_to_tensors(recs, games, "cuda")
+    curves = {}
+    for backend in ("hip", "miopen"):
+        KM.TRAIN_BACKEND = backend
+        try:
+            m = KM.ChessNet()
+            m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+            m.cuda().train()
+            opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+            scaler = T.make_scaler("cuda")
+            gen = torch.Generator().manual_seed(5)
+            losses = []
+            for _ in range(15):  # 15 epochs of 4 batches of 256, accumulation 2: 30 optimizer steps
+                st = T.train_one_epoch(m, T.batches(codes[:1024], moves[:1024], rew[:1024], 256, True, gen), opt,
+                                       scaler, accumulate_steps=2)
+                losses.append(st["loss"] / st["batches"])
+            curves[backend] = np.array(losses)
+        finally:
+            KM.TRAIN_BACKEND = "hip"
+    h, mi = curves["hip"], curves["miopen"]
+    print("loss per epoch  HIP:", np.round(h, 4).tolist())
+    print("loss per epoch MIOp:", np.round(mi, 4).tolist())
+    assert h[-1] < 0.8 * h[0] and mi[-1] < 0.8 * mi[0], "the loss did not fall"
+    assert np.abs(h - mi).max() <= 0.03 * np.abs(mi).max(), "HIP and MIOpen loss trajectories diverge"
