@@ -106,6 +106,11 @@ def test_mcts_network_visits_identical_to_oracle_c2_first_move():
     _compare_network_games("init", slots=256, n_check=16, sims=400, max_moves=None, steps=1)
 
 
+def test_mcts_network_visits_identical_to_oracle_c3_first_move():
+    """C3, the headline config (2,048 slots x 800 sims): the first move of the first 8 games."""
+    _compare_network_games("init", slots=2048, n_check=8, sims=800, max_moves=None, steps=1)
+
+
 def test_mcts_network_games_run():
     """The real network path: games complete, sims are counted per backup."""
     with SelfPlayEngine(synthetic_state_dict(42, "init"), slots=8, n_games=8, seed=42, max_moves=6,
