@@ -62,7 +62,8 @@ def main():
                           "iterations": a.iterations, "games_per_iteration": a.games, "max_moves": a.max_moves,
                           "sims": a.sims, "selfplay_s": sp_s, "train_s": tr_s,
                           "train_samples_per_s": cnt.item() / tr_s if tr_s else None,
-                          "records_per_rank": last["records"], "wall_s": wall, "data": "synthetic"}), flush=True)
+                          "val_loss": last.get("val_loss"), "records": last["records"], "wall_s": wall,
+                          "data": "synthetic"}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
