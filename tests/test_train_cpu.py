@@ -350,3 +350,36 @@ def test_explicit_batch_norm_matches_module():
         assert torch.allclose(a.weight.grad, b.weight.grad, atol=1e-4)
         assert torch.allclose(a.running_mean, b.running_mean) and torch.allclose(a.running_var, b.running_var)
         assert int(a.num_batches_tracked) == int(b.num_batches_tracked) == 1
+
+
+def _val_worker(rank, world, port, q):
+    """learn.split_train_val / evaluate_sharded on two gloo ranks."""
+    import torch.distributed as dist
+    from knightvision_amd import learn as L
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(5)
+    m = TinyNet()
+    data = _data(57, 3)
+    tr, va = L.split_train_val(57, torch.Generator().manual_seed(0))
+    loss = L.evaluate_sharded(m, data, va, 8, torch.device("cpu"))
+    q.put((rank, tr.tolist(), va.tolist(), loss))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_validation_split_and_sharded_evaluate_world2():
+    """The learn loop's random_split (learn.py:162-165: int(0.9 n) train samples) is the same on every
+    rank, and the validation loss of the ranks' round-robin shards (sums all-reduced) equals train.evaluate
+    over the whole validation subset on one process (train.py:109-124)."""
+    from knightvision_amd import learn as L
+    res = _spawn(_val_worker)
+    (r0, tr0, va0, l0), (r1, tr1, va1, l1) = res
+    assert tr0 == tr1 and va0 == va1 and len(tr0) == int(0.9 * 57) and len(va0) == 57 - int(0.9 * 57)
+    assert sorted(tr0 + va0) == list(range(57))
+    torch.manual_seed(5)
+    m = TinyNet()
+    data = _data(57, 3)
+    va = torch.tensor(va0)
+    want = T.evaluate(m, list(T.batches(*(x[va] for x in data), 8, False)))
+    assert abs(l0 - want) < 1e-5 * abs(want) and l0 == l1
