@@ -295,6 +295,11 @@ int kv_chess_fen(const char* fen_in, char* fen_out, size_t cap);
  * image of kv_tr_conv_weights_f16, co = the conv's input channels. */
 int kv_tr_conv3x3_f16(const void* x_dev, int n, int ci, const void* w_dev, const float* bias_dev, int co,
                       void* y_dev, void* stream);
+/* the same with a fused fp16 addend: y = fp16(float(fp16(bias + conv3x3(x, w))) + float(add)) -- the data
+ * gradient of a residual block's first conv plus the residual branch's gradient, rounded as autograd's
+ * fp16 gradient accumulation rounds it; add_dev [n][64][co] (not y_dev) or NULL */
+int kv_tr_conv3x3_add_f16(const void* x_dev, int n, int ci, const void* w_dev, const float* bias_dev, int co,
+                          const void* add_dev, void* y_dev, void* stream);
 /* fp32 torch weight [co][ci_real][3][3] -> fp16 forward image [co][9][ci] (channels >= ci_real zero) and,
  * if wt_dev != NULL, the data-gradient image [ci][9][co] (taps flipped) */
 int kv_tr_conv_weights_f16(const float* w_dev, int co, int ci_real, int ci, void* wf_dev, void* wt_dev, void* stream);
@@ -314,10 +319,12 @@ int kv_tr_bn_apply_f16(const void* x_dev, int rows, int C, const float* mean_dev
                        const float* gamma_dev, const float* beta_dev, const void* res_dev, int relu, void* y_dev,
                        void* stream);
 /* backward of kv_tr_bn_apply_f16 (y_dev = its output, for the ReLU mask): dgamma, dbeta fp32 [C], dx fp16 and,
- * if dres_dev != NULL, the residual's gradient (the masked dy) */
+ * if dres_dev != NULL, the residual's gradient (the masked dy); if dxsum_dev != NULL, the channel sums of dx
+ * fp32 [C] (the bias gradient of the conv that produced x, without a second pass over dx) */
 int kv_tr_bn_backward_f16(const void* x_dev, const void* dy_dev, const void* y_dev, int rows, int C, int relu,
                           const float* mean_dev, const float* invstd_dev, const float* gamma_dev, float* dgamma_dev,
-                          float* dbeta_dev, void* dx_dev, void* dres_dev, void* ws_dev, size_t ws_bytes, void* stream);
+                          float* dbeta_dev, void* dx_dev, void* dres_dev, float* dxsum_dev, void* ws_dev,
+                          size_t ws_bytes, void* stream);
 /* per-channel sum of fp16 rows x C (a conv bias gradient) */
 int kv_tr_channel_sum_f16(const void* x_dev, int rows, int C, float* sum_dev, void* ws_dev, size_t ws_bytes,
                           void* stream);

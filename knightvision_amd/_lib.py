@@ -94,13 +94,14 @@ def _declare(L):
         "kv_chess_san": ([C.c_char_p, C.c_char_p, C.c_char_p, sz, C.c_char_p, sz], i),
         "kv_chess_fen": ([C.c_char_p, C.c_char_p, sz], i),
         "kv_tr_conv3x3_f16": ([vp, i, i, vp, vp, i, vp, vp], i),
+        "kv_tr_conv3x3_add_f16": ([vp, i, i, vp, vp, i, vp, vp, vp], i),
         "kv_tr_conv_weights_f16": ([vp, i, i, i, vp, vp, vp], i),
         "kv_tr_wgrad_workspace": ([i, i, i, P(i)], sz),
         "kv_tr_conv3x3_wgrad_f16": ([vp, vp, i, i, i, i, vp, vp, sz, vp], i),
         "kv_tr_bn_workspace": ([i, i], sz),
         "kv_tr_bn_stats_f16": ([vp, i, i, C.c_float, vp, vp, vp, vp, sz, vp], i),
         "kv_tr_bn_apply_f16": ([vp, i, i, vp, vp, vp, vp, vp, i, vp, vp], i),
-        "kv_tr_bn_backward_f16": ([vp, vp, vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp], i),
+        "kv_tr_bn_backward_f16": ([vp, vp, vp, i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp], i),
         "kv_tr_channel_sum_f16": ([vp, i, i, vp, vp, sz, vp], i),
         "kv_tr_planes_to_nhwc": ([vp, i, i, vp, vp], i),
         "kv_tr_head1x1_f16": ([vp, i, vp, vp, vp, vp], i),
@@ -122,7 +123,7 @@ EXPORTED = ["kv_last_error", "kv_version", "kv_net_packed_size", "kv_net_create"
             "kv_load_weights", "kv_run", "kv_set_max_moves", "kv_records", "kv_games", "kv_stats_get", "kv_root_visits", "kv_root_visits_device", "kv_records_device", "kv_sync", "kv_reset_records", "kv_destroy",
             "kv_dev_valid_moves", "kv_dev_make_move", "kv_dev_attacks", "kv_dev_dirichlet", "kv_dev_py_random", "kv_host_libm",
             "kv_pgn_extract", "kv_fen_codes", "kv_san_move_index", "kv_chess_perft", "kv_chess_san", "kv_chess_fen",
-            "kv_tr_conv3x3_f16", "kv_tr_conv_weights_f16", "kv_tr_wgrad_workspace", "kv_tr_conv3x3_wgrad_f16",
+            "kv_tr_conv3x3_f16", "kv_tr_conv3x3_add_f16", "kv_tr_conv_weights_f16", "kv_tr_wgrad_workspace", "kv_tr_conv3x3_wgrad_f16",
             "kv_tr_bn_workspace", "kv_tr_bn_stats_f16", "kv_tr_bn_apply_f16", "kv_tr_bn_backward_f16",
             "kv_tr_channel_sum_f16", "kv_tr_planes_to_nhwc", "kv_tr_head1x1_f16", "kv_tr_head1x1_workspace",
             "kv_tr_head1x1_backward_f16"]

@@ -79,6 +79,7 @@ __device__ inline int conv_lane_square(int li) {
 __global__ __launch_bounds__(cv::THREADS) void conv3x3_f16_kernel(const _Float16* __restrict__ x, int n, int ci,
                                                                   const _Float16* __restrict__ w,
                                                                   const float* __restrict__ bias, int co,
+                                                                  const _Float16* __restrict__ add,
                                                                   _Float16* __restrict__ y) {
     using namespace cv;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(cv::THREADS) void conv3x3_f16_kernel(const _Float16
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const int sq = q * 32 + conv_lane_square(li);
-        _Float16* yo = y + ((size_t)(n0 + wave) * 64 + sq) * co + co0;
+        const size_t o = ((size_t)(n0 + wave) * 64 + sq) * co + co0;
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -203,7 +204,13 @@ __global__ __launch_bounds__(cv::THREADS) void conv3x3_f16_kernel(const _Float16
                     const f32x4 bv = *(const f32x4*)(bias + co0 + c);
                     v = v + bv;
                 }
-                *(h4*)(yo + c) = __builtin_convertvector(v, h4);
+                h4 hv = __builtin_convertvector(v, h4);
+                if (add) {  // autograd's gradient accumulation: fp16(float(dx) + float(other))
+                    const h4 av = *(const h4*)(add + o + c);
+                    hv = __builtin_convertvector(__builtin_convertvector(hv, f32x4) + __builtin_convertvector(av, f32x4),
+                                                 h4);
+                }
+                *(h4*)(y + o + c) = hv;
             }
     }
 }
@@ -402,11 +409,16 @@ __device__ inline void h8_to_f(const u32x4 v, float* f) {
     for (int e = 0; e < 8; ++e) f[e] = (float)hv[e];
 }
 
+// MODE is a template argument so the row loop can keep U rows' loads in flight
+// (U 16-B loads per operand issued before the first is consumed); the sums
+// still take the rows in the same order.
+template <int MODE>
 __global__ __launch_bounds__(256) void bn_partial_kernel(const _Float16* __restrict__ x, const _Float16* __restrict__ dy,
-                                                         const _Float16* __restrict__ yout, int rows, int C, int mode,
-                                                         int relu, const float* __restrict__ mean,
+                                                         const _Float16* __restrict__ yout, int rows, int C, int relu,
+                                                         const float* __restrict__ mean,
                                                          const float* __restrict__ invstd, float* __restrict__ p0,
                                                          float* __restrict__ p1) {
+    constexpr int U = MODE == 1 ? 4 : 8;
     __shared__ float red[2][256 * 8];
     const int cg = C / 8, rl = 256 / cg;  // channel groups, row lanes
     const int tid = threadIdx.x, g = tid % cg, lr = tid / cg;
@@ -421,36 +433,52 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const _Float16* __restr
         m[e] = 0.f;
         iv[e] = 0.f;
     }
-    if (mode == 0) h8_to_f(*(const u32x4*)(x + c), k);
-    if (mode == 1) {
+    if (MODE == 0) h8_to_f(*(const u32x4*)(x + c), k);
+    if (MODE == 1) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             m[e] = mean[c + e];
             iv[e] = invstd[c + e];
         }
     }
-    for (int r = r0 + lr; r < r1; r += rl) {
-        float xv[8];
-        h8_to_f(*(const u32x4*)(x + (size_t)r * C + c), xv);
-        if (mode == 0) {
+    for (int r = r0 + lr; r < r1; r += U * rl) {
+        u32x4 xa[U], ga[U], ya[U];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float d = xv[e] - k[e];
-                s0[e] += d;
-                s1[e] += d * d;
+        for (int u = 0; u < U; ++u) {
+            const int rr = r + u * rl;
+            if (rr < r1) {
+                xa[u] = *(const u32x4*)(x + (size_t)rr * C + c);
+                if (MODE == 1) {
+                    ga[u] = *(const u32x4*)(dy + (size_t)rr * C + c);
+                    if (relu) ya[u] = *(const u32x4*)(yout + (size_t)rr * C + c);
+                }
             }
-        } else if (mode == 2) {
+        }
 #pragma unroll
-            for (int e = 0; e < 8; ++e) s0[e] += xv[e];
-        } else {
-            float gv[8], yv[8];
-            h8_to_f(*(const u32x4*)(dy + (size_t)r * C + c), gv);
-            if (relu) h8_to_f(*(const u32x4*)(yout + (size_t)r * C + c), yv);
+        for (int u = 0; u < U; ++u) {
+            if (r + u * rl >= r1) break;
+            float xv[8];
+            h8_to_f(xa[u], xv);
+            if (MODE == 0) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float gg = (relu && !(yv[e] > 0.f)) ? 0.f : gv[e];
-                s0[e] += gg;
-                s1[e] += gg * ((xv[e] - m[e]) * iv[e]);
+                for (int e = 0; e < 8; ++e) {
+                    const float d = xv[e] - k[e];
+                    s0[e] += d;
+                    s1[e] += d * d;
+                }
+            } else if (MODE == 2) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) s0[e] += xv[e];
+            } else {
+                float gv[8], yv[8];
+                h8_to_f(ga[u], gv);
+                if (relu) h8_to_f(ya[u], yv);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float gg = (relu && !(yv[e] > 0.f)) ? 0.f : gv[e];
+                    s0[e] += gg;
+                    s1[e] += gg * ((xv[e] - m[e]) * iv[e]);
+                }
             }
         }
     }
@@ -469,34 +497,40 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const _Float16* __restr
             b2 += red[1][(l * cg + gg) * 8 + e];
         }
         p0[(size_t)blockIdx.x * C + ch] = a;
-        p1[(size_t)blockIdx.x * C + ch] = b2;
+        if (MODE != 2) p1[(size_t)blockIdx.x * C + ch] = b2;
     }
 }
 
-// block partials -> per-channel results (fp64; thread (channel, group j) adds
-// blocks j, j+16, ... then the 16 groups are added in order):
+// block partials -> per-channel results (fp64; block = 16 channels x 64
+// groups, thread (channel, group j) adds blocks j, j+64, ... then the 64 groups
+// are added in order):
 //   mode 0: mean, biased var, invstd = 1/sqrt(var + eps) (out0, out1, out2)
-//   mode 1: sum g, sum g*xhat (out0, out1 if given)
+//   mode 1: sum g, sum g*xhat (out0, out1 if given); p1 is not read without out1
+constexpr int BNF_CH = 16, BNF_GROUPS = 64;
+
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restrict__ p0, const float* __restrict__ p1,
                                                            int blocks, int C, int rows, int mode, float eps,
                                                            const _Float16* __restrict__ shift, float* __restrict__ out0,
                                                            float* __restrict__ out1, float* __restrict__ out2) {
-    __shared__ double ra[16][64], rb[16][64];
-    const int cl = threadIdx.x & 63, j = threadIdx.x >> 6;
-    const int c = blockIdx.x * 64 + cl;
+    __shared__ double ra[BNF_GROUPS][BNF_CH], rb[BNF_GROUPS][BNF_CH];
+    const int cl = threadIdx.x % BNF_CH, j = threadIdx.x / BNF_CH;
+    const int c = blockIdx.x * BNF_CH + cl;
+    const bool two = mode == 0 || out1 != nullptr;
     double a = 0.0, b = 0.0;
-    if (c < C)
-        for (int k = j; k < blocks; k += 16) {
+    if (c < C) {
+#pragma unroll 4
+        for (int k = j; k < blocks; k += BNF_GROUPS) {
             a += (double)p0[(size_t)k * C + c];
-            b += (double)p1[(size_t)k * C + c];
+            if (two) b += (double)p1[(size_t)k * C + c];
         }
+    }
     ra[j][cl] = a;
     rb[j][cl] = b;
     __syncthreads();
     if (j != 0 || c >= C) return;
     a = 0.0;
     b = 0.0;
-    for (int q = 0; q < 16; ++q) {
+    for (int q = 0; q < BNF_GROUPS; ++q) {
         a += ra[q][cl];
         b += rb[q][cl];
     }
@@ -561,7 +595,8 @@ __global__ __launch_bounds__(256) void bn_backward_kernel(const _Float16* __rest
                                                           const float* __restrict__ invstd,
                                                           const float* __restrict__ gamma, const float* __restrict__ sg,
                                                           const float* __restrict__ sgx, _Float16* __restrict__ dx,
-                                                          _Float16* __restrict__ dres) {
+                                                          _Float16* __restrict__ dres, float* __restrict__ dsp) {
+    __shared__ float red[256 * 8];
     const int cg = C / 8, rl = 256 / cg;
     const int g = threadIdx.x % cg, lr = threadIdx.x / cg, c = g * 8;
     const float inv_m = 1.0f / (float)rows;
@@ -574,6 +609,7 @@ __global__ __launch_bounds__(256) void bn_backward_kernel(const _Float16* __rest
         mgx[e] = sgx[c + e] * inv_m;
         sc[e] = gamma[c + e] * iv[e];
     }
+    float ds[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const int r0 = blockIdx.x * BN_EW_ROWS, r1 = min(rows, r0 + BN_EW_ROWS);
     for (int r = r0 + lr; r < r1; r += rl) {
         const size_t i = (size_t)r * C + c;
@@ -588,9 +624,20 @@ __global__ __launch_bounds__(256) void bn_backward_kernel(const _Float16* __rest
             const float xh = (xv[e] - m[e]) * iv[e];
             o[e] = (_Float16)((gg - mg[e] - xh * mgx[e]) * sc[e]);
             rr[e] = (_Float16)gg;
+            ds[e] += (float)o[e];
         }
         *(h8*)(dx + i) = o;
         if (dres) *(h8*)(dres + i) = rr;
+    }
+    if (!dsp) return;
+    // the channel sums of dx (the producing conv's bias gradient): block partials [block][C], row lanes in order
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[threadIdx.x * 8 + e] = ds[e];
+    __syncthreads();
+    for (int ch = threadIdx.x; ch < C; ch += 256) {
+        float a = 0.f;
+        for (int l = 0; l < rl; ++l) a += red[(l * cg + ch / 8) * 8 + ch % 8];
+        dsp[(size_t)blockIdx.x * C + ch] = a;
     }
 }
 
@@ -719,7 +766,12 @@ extern "C" {
 
 int kv_tr_conv3x3_f16(const void* x_dev, int n, int ci, const void* w_dev, const float* bias_dev, int co,
                       void* y_dev, void* stream) {
-    KV_REQUIRE(x_dev && w_dev && y_dev && n > 0, KV_EINVAL, "kv_tr_conv3x3_f16: bad arguments");
+    return kv_tr_conv3x3_add_f16(x_dev, n, ci, w_dev, bias_dev, co, nullptr, y_dev, stream);
+}
+
+int kv_tr_conv3x3_add_f16(const void* x_dev, int n, int ci, const void* w_dev, const float* bias_dev, int co,
+                          const void* add_dev, void* y_dev, void* stream) {
+    KV_REQUIRE(x_dev && w_dev && y_dev && n > 0 && add_dev != y_dev, KV_EINVAL, "kv_tr_conv3x3_f16: bad arguments");
     KV_REQUIRE(ci > 0 && ci % cv::CK == 0 && co > 0 && co % cv::WCO == 0, KV_EINVAL,
                "kv_tr_conv3x3_f16: ci %d must be a multiple of %d, co %d of %d", ci, cv::CK, co, cv::WCO);
     static bool attr = false;
@@ -732,7 +784,8 @@ int kv_tr_conv3x3_f16(const void* x_dev, int n, int ci, const void* w_dev, const
                "number of 128-channel blocks", co);
     const int grid = (nblocks + 8 / cblocks - 1) / (8 / cblocks) * 8;
     hipLaunchKernelGGL(conv3x3_f16_kernel, dim3(grid), dim3(cv::THREADS), cv::LDS, (hipStream_t)stream,
-                       (const _Float16*)x_dev, n, ci, (const _Float16*)w_dev, bias_dev, co, (_Float16*)y_dev);
+                       (const _Float16*)x_dev, n, ci, (const _Float16*)w_dev, bias_dev, co, (const _Float16*)add_dev,
+                       (_Float16*)y_dev);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -797,7 +850,9 @@ int kv_tr_conv3x3_wgrad_f16(const void* dy_dev, const void* x_dev, int n, int ci
 }
 
 size_t kv_tr_bn_workspace(int rows, int C) {
-    return 2 * (size_t)((rows + BN_ROWS - 1) / BN_ROWS) * C * sizeof(float);
+    // two partial sums per BN_ROWS block, or (backward) the dx sums per BN_EW_ROWS block after them
+    const size_t a = 2 * (size_t)((rows + BN_ROWS - 1) / BN_ROWS), b = (size_t)((rows + BN_EW_ROWS - 1) / BN_EW_ROWS);
+    return std::max(a, b) * C * sizeof(float);
 }
 
 int kv_tr_bn_stats_f16(const void* x_dev, int rows, int C, float eps, float* mean_dev, float* var_dev,
@@ -808,11 +863,11 @@ int kv_tr_bn_stats_f16(const void* x_dev, int rows, int C, float eps, float* mea
     const int blocks = (rows + BN_ROWS - 1) / BN_ROWS;
     float* p0 = (float*)ws_dev;
     float* p1 = p0 + (size_t)blocks * C;
-    hipLaunchKernelGGL(bn_partial_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const _Float16*)x_dev,
-                       (const _Float16*)nullptr, (const _Float16*)nullptr, rows, C, 0, 0, (const float*)nullptr,
+    hipLaunchKernelGGL(bn_partial_kernel<0>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const _Float16*)x_dev,
+                       (const _Float16*)nullptr, (const _Float16*)nullptr, rows, C, 0, (const float*)nullptr,
                        (const float*)nullptr, p0, p1);
     KV_HIP(hipGetLastError());
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, (hipStream_t)stream, p0, p1, blocks, C,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + BNF_CH - 1) / BNF_CH), dim3(1024), 0, (hipStream_t)stream, p0, p1, blocks, C,
                        rows, 0, eps, (const _Float16*)x_dev, mean_dev, var_dev, invstd_dev);
     KV_HIP(hipGetLastError());
     return KV_OK;
@@ -832,7 +887,8 @@ int kv_tr_bn_apply_f16(const void* x_dev, int rows, int C, const float* mean_dev
 
 int kv_tr_bn_backward_f16(const void* x_dev, const void* dy_dev, const void* y_dev, int rows, int C, int relu,
                           const float* mean_dev, const float* invstd_dev, const float* gamma_dev, float* dgamma_dev,
-                          float* dbeta_dev, void* dx_dev, void* dres_dev, void* ws_dev, size_t ws_bytes, void* stream) {
+                          float* dbeta_dev, void* dx_dev, void* dres_dev, float* dxsum_dev, void* ws_dev,
+                          size_t ws_bytes, void* stream) {
     KV_REQUIRE(x_dev && dy_dev && (y_dev || !relu) && mean_dev && invstd_dev && gamma_dev && dgamma_dev && dbeta_dev &&
                    dx_dev && ws_dev && rows > 0 && C % 64 == 0 && C <= 512,
                KV_EINVAL, "kv_tr_bn_backward_f16: bad arguments");
@@ -840,17 +896,24 @@ int kv_tr_bn_backward_f16(const void* x_dev, const void* dy_dev, const void* y_d
     const int blocks = (rows + BN_ROWS - 1) / BN_ROWS;
     float* p0 = (float*)ws_dev;
     float* p1 = p0 + (size_t)blocks * C;
-    hipLaunchKernelGGL(bn_partial_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const _Float16*)x_dev,
-                       (const _Float16*)dy_dev, (const _Float16*)y_dev, rows, C, 1, relu, mean_dev, invstd_dev, p0, p1);
+    hipLaunchKernelGGL(bn_partial_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const _Float16*)x_dev,
+                       (const _Float16*)dy_dev, (const _Float16*)y_dev, rows, C, relu, mean_dev, invstd_dev, p0, p1);
     KV_HIP(hipGetLastError());
     // sum g -> dbeta, sum g * xhat -> dgamma
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, (hipStream_t)stream, p0, p1, blocks, C,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + BNF_CH - 1) / BNF_CH), dim3(1024), 0, (hipStream_t)stream, p0, p1, blocks, C,
                        rows, 1, 0.f, (const _Float16*)nullptr, dbeta_dev, dgamma_dev, (float*)nullptr);
     KV_HIP(hipGetLastError());
     hipLaunchKernelGGL(bn_backward_kernel, dim3((rows + BN_EW_ROWS - 1) / BN_EW_ROWS), dim3(256), 0, (hipStream_t)stream,
                        (const _Float16*)x_dev, (const _Float16*)dy_dev, (const _Float16*)y_dev, rows, C, relu,
-                       mean_dev, invstd_dev, gamma_dev, dbeta_dev, dgamma_dev, (_Float16*)dx_dev, (_Float16*)dres_dev);
+                       mean_dev, invstd_dev, gamma_dev, dbeta_dev, dgamma_dev, (_Float16*)dx_dev, (_Float16*)dres_dev,
+                       dxsum_dev ? p0 : nullptr);  // p0 / p1 are consumed: the dx partials reuse the workspace
     KV_HIP(hipGetLastError());
+    if (dxsum_dev) {
+        hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + BNF_CH - 1) / BNF_CH), dim3(1024), 0, (hipStream_t)stream, p0,
+                           p0, (rows + BN_EW_ROWS - 1) / BN_EW_ROWS, C, rows, 1, 0.f, (const _Float16*)nullptr,
+                           dxsum_dev, (float*)nullptr, (float*)nullptr);
+        KV_HIP(hipGetLastError());
+    }
     return KV_OK;
 }
 
@@ -862,11 +925,11 @@ int kv_tr_channel_sum_f16(const void* x_dev, int rows, int C, float* sum_dev, vo
     const int blocks = (rows + BN_ROWS - 1) / BN_ROWS;
     float* p0 = (float*)ws_dev;
     float* p1 = p0 + (size_t)blocks * C;
-    hipLaunchKernelGGL(bn_partial_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const _Float16*)x_dev,
-                       (const _Float16*)nullptr, (const _Float16*)nullptr, rows, C, 2, 0, (const float*)nullptr,
+    hipLaunchKernelGGL(bn_partial_kernel<2>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const _Float16*)x_dev,
+                       (const _Float16*)nullptr, (const _Float16*)nullptr, rows, C, 0, (const float*)nullptr,
                        (const float*)nullptr, p0, p1);
     KV_HIP(hipGetLastError());
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, (hipStream_t)stream, p0, p1, blocks, C,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + BNF_CH - 1) / BNF_CH), dim3(1024), 0, (hipStream_t)stream, p0, p1, blocks, C,
                        rows, 1, 0.f, (const _Float16*)nullptr, sum_dev, (float*)nullptr, (float*)nullptr);
     KV_HIP(hipGetLastError());
     return KV_OK;

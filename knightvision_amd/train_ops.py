@@ -16,6 +16,13 @@ on those kernels with NHWC fp16 activations [boards, 64 squares, C]:
     ReLU, in the reference's rounding order; backward in one reduction and
     one elementwise kernel. Running statistics are updated as
     nn.BatchNorm2d does (momentum, unbiased variance);
+  * fusions across the two (FUSE, on by default): the BatchNorm backward
+    also sums its dx per channel -- the producing conv's bias gradient, so
+    dy is not read a second time -- and hands it to that conv through a
+    shared dict; a residual block's second BatchNorm hands the residual
+    branch's gradient to the block's first conv, whose data-gradient kernel
+    adds it in its epilogue, rounded as autograd's fp16 accumulation of the
+    two would be (the same bits, one fewer pass over the activations);
   * Head1x1: the heads' policy / value 1x1 convolutions over the tower output.
 
 Only the fp16 autocast path runs here; an fp32 (autocast off) update uses the
@@ -28,6 +35,7 @@ import torch
 from . import _lib
 
 STEM_CI = 64  # encode_board's 12 planes padded to the weight-gradient kernel's 64-channel tile
+FUSE = True   # the BatchNorm -> conv backward fusions (module docstring); False: separate passes
 
 _ws = {}
 
@@ -72,13 +80,15 @@ def conv_weight_images(weight: torch.Tensor, ci: int, flipped: bool):
     return wf, wt
 
 
-def conv3x3_f16(x: torch.Tensor, wf: torch.Tensor, bias32) -> torch.Tensor:
-    """Raw kernel call: x fp16 [n,64,ci], wf fp16 [co,9,ci] -> fp16 [n,64,co]."""
+def conv3x3_f16(x: torch.Tensor, wf: torch.Tensor, bias32, add=None) -> torch.Tensor:
+    """Raw kernel call: x fp16 [n,64,ci], wf fp16 [co,9,ci] -> fp16 [n,64,co] (+ fp16 `add`, fused)."""
     n, _, ci = x.shape
     co = wf.shape[0]
     y = torch.empty((n, 64, co), dtype=torch.float16, device=x.device)
-    _lib.check(_lib.lib().kv_tr_conv3x3_f16(x.data_ptr(), n, ci, wf.data_ptr(), _ptr(bias32), co, y.data_ptr(),
-                                            _stream(x)), "kv_tr_conv3x3_f16")
+    if add is not None:
+        assert add.dtype == torch.float16 and add.shape == y.shape and add.is_contiguous()
+    _lib.check(_lib.lib().kv_tr_conv3x3_add_f16(x.data_ptr(), n, ci, wf.data_ptr(), _ptr(bias32), co, _ptr(add),
+                                                y.data_ptr(), _stream(x)), "kv_tr_conv3x3_f16")
     return y
 
 
@@ -107,10 +117,12 @@ def channel_sum_f16(t: torch.Tensor) -> torch.Tensor:
 
 class Conv3x3(torch.autograd.Function):
     """y fp16 [n,64,co] = conv3x3(x fp16 [n,64,ci], weight fp32 [co,ci_real,3,3]) + bias, as an
-    autocast fp16 convolution (weight and bias rounded to fp16, fp32 accumulation)."""
+    autocast fp16 convolution (weight and bias rounded to fp16, fp32 accumulation).
+    bias_link: dict the consuming BNAct's backward leaves the bias gradient in ("db");
+    dx_link: dict a residual BNAct's backward leaves x's other gradient in ("dres"), added to dx here."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, need_dx: bool):
+    def forward(ctx, x, weight, bias, need_dx: bool, bias_link=None, dx_link=None):
         x = x.contiguous()
         ci = x.shape[2]
         wf, wt = conv_weight_images(weight, ci, need_dx)
@@ -120,26 +132,38 @@ class Conv3x3(torch.autograd.Function):
         ctx.need_dx = need_dx
         ctx.ci_real = weight.shape[1]
         ctx.has_bias = bias is not None
+        ctx.links = (bias_link, dx_link)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, wt = ctx.saved_tensors
+        bias_link, dx_link = ctx.links
         dy = dy.to(torch.float16).contiguous()
-        dx = conv3x3_f16(dy, wt, None) if (ctx.need_dx and ctx.needs_input_grad[0]) else None
+        dres = dx_link.pop("dres", None) if dx_link is not None else None
+        dx = None
+        if ctx.need_dx and ctx.needs_input_grad[0]:
+            dx = conv3x3_f16(dy, wt, None, dres)
+        elif dres is not None and ctx.needs_input_grad[0]:
+            dx = dres
         dw = conv3x3_wgrad_f16(dy, x, ctx.ci_real) if ctx.needs_input_grad[1] else None
-        db = None
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = channel_sum_f16(dy).to(torch.float16).to(torch.float32)
-        return dx, dw, db, None
+        db = bias_link.pop("db", None) if bias_link is not None else None
+        if db is None and ctx.has_bias and ctx.needs_input_grad[2]:
+            db = channel_sum_f16(dy)
+        if db is not None:
+            db = db.to(torch.float16).to(torch.float32)
+        return dx, dw, db, None, None, None
 
 
 class BNAct(torch.autograd.Function):
     """Training BatchNorm over boards x squares of fp16 x [n,64,C] (+ fp16 residual) (+ ReLU) -> fp16.
-    `stats` (a list) receives (mean, biased var) for the running-statistics update."""
+    `stats` (a list) receives (mean, biased var) for the running-statistics update.
+    bias_link: the producing Conv3x3's dict -- the backward leaves the channel sums of dx there ("db");
+    res_link: the dict of the Conv3x3 that consumes `res` -- the backward leaves res's gradient there
+    ("dres") for that conv's data-gradient kernel to add, and returns none of its own."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, relu: bool, eps: float, stats: list):
+    def forward(ctx, x, gamma, beta, res, relu: bool, eps: float, stats: list, bias_link=None, res_link=None):
         x = x.contiguous()
         n, _, C = x.shape
         rows = n * 64
@@ -161,6 +185,7 @@ class BNAct(torch.autograd.Function):
         ctx.save_for_backward(x, y, mean, invstd, g32)
         ctx.relu = relu
         ctx.has_res = res is not None
+        ctx.links = (bias_link, res_link)
         return y
 
     @staticmethod
@@ -172,14 +197,21 @@ class BNAct(torch.autograd.Function):
         L = _lib.lib()
         ws = _workspace(x.device, L.kv_tr_bn_workspace(rows, C))
         dx = torch.empty_like(x)
+        bias_link, res_link = ctx.links
         dres = torch.empty_like(x) if ctx.has_res else None
         dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
         dbeta = torch.empty_like(dgamma)
+        dxsum = torch.empty_like(dgamma) if bias_link is not None else None
         _lib.check(L.kv_tr_bn_backward_f16(x.data_ptr(), dy.data_ptr(), y.data_ptr(), rows, C, int(ctx.relu),
                                            mean.data_ptr(), invstd.data_ptr(), g32.data_ptr(), dgamma.data_ptr(),
-                                           dbeta.data_ptr(), dx.data_ptr(), _ptr(dres), ws.data_ptr(), ws.numel(),
-                                           _stream(x)), "kv_tr_bn_backward_f16")
-        return dx, dgamma, dbeta, dres, None, None, None
+                                           dbeta.data_ptr(), dx.data_ptr(), _ptr(dres), _ptr(dxsum), ws.data_ptr(),
+                                           ws.numel(), _stream(x)), "kv_tr_bn_backward_f16")
+        if dxsum is not None:
+            bias_link["db"] = dxsum
+        if dres is not None and res_link is not None:
+            res_link["dres"] = dres
+            dres = None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None
 
 
 class Head1x1(torch.autograd.Function):
@@ -225,11 +257,14 @@ def update_running_stats(bn: torch.nn.BatchNorm2d, mean: torch.Tensor, var: torc
         bn.running_var.mul_(1 - mom).add_(var * (count / max(count - 1, 1)), alpha=mom)
 
 
-def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, res=None, need_dx: bool = True):
-    """relu(bn(conv(x)) [+ res]) on the HIP kernels (training mode)."""
-    y = Conv3x3.apply(x, conv.weight, conv.bias, need_dx)
+def conv_bn_act(x, conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, res=None, need_dx: bool = True,
+                dx_link=None, res_link=None):
+    """relu(bn(conv(x)) [+ res]) on the HIP kernels (training mode). dx_link / res_link: the
+    residual-gradient hand-over (BNAct, Conv3x3)."""
+    bias_link = {} if FUSE else None
+    y = Conv3x3.apply(x, conv.weight, conv.bias, need_dx, bias_link, dx_link)
     stats = []
-    out = BNAct.apply(y, bn.weight, bn.bias, res, True, bn.eps, stats)
+    out = BNAct.apply(y, bn.weight, bn.bias, res, True, bn.eps, stats, bias_link, res_link)
     update_running_stats(bn, stats[0][0], stats[0][1], y.shape[0] * 64)
     return out
 
@@ -241,6 +276,7 @@ def tower_forward(net, planes: torch.Tensor) -> torch.Tensor:
     h = conv_bn_act(x, net.conv1, net.bn1, need_dx=False)
     h = conv_bn_act(h, net.conv2, net.bn2)
     for blk in net.res_blocks:
-        a = conv_bn_act(h, blk.conv1, blk.bn1)
-        h = conv_bn_act(a, blk.conv2, blk.bn2, res=h)
+        link = {} if FUSE else None  # bn2's residual gradient -> conv1's data gradient (both take h)
+        a = conv_bn_act(h, blk.conv1, blk.bn1, dx_link=link)
+        h = conv_bn_act(a, blk.conv2, blk.bn2, res=h, res_link=link)
     return h

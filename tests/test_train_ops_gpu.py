@@ -73,6 +73,11 @@ def test_conv_forward_and_grads(n, ci_real, ci, co):
     db = TO.channel_sum_f16(dyc)
     assert torch.allclose(db.cpu(), dy.float().sum(dim=(0, 1)), rtol=1e-5, atol=1e-3)
 
+    # the fused addend (a residual block's data gradient + the residual branch's): autograd's fp16 add, bit for bit
+    add = torch.randn(y.shape, generator=g).half().cuda()
+    ya = TO.conv3x3_f16(xc, wf, bc.half().float(), add)
+    assert torch.equal(ya, (y.float() + add.float()).half())
+
 
 def test_wgrad_is_deterministic():
     g = torch.Generator().manual_seed(3)
@@ -187,6 +192,42 @@ def test_tower_matches_miopen_autocast():
             assert torch.allclose(bh[k], bm[k], rtol=2e-2, atol=2e-3), k
         else:
             assert torch.equal(bh[k], bm[k]), k
+
+
+def test_fused_backward_is_the_unfused_one():
+    """train_ops.FUSE: the BatchNorm backward's dx channel sums (conv bias gradients) and the residual
+    gradient added inside the data-gradient kernel give the same gradients as the separate passes:
+    every weight / BatchNorm gradient bit for bit, the conv biases to their summation noise (the channel
+    sums add the same fp16 values in another order)."""
+    from knightvision_amd import model as KM
+    from knightvision_amd.weights import synthetic_state_dict
+    sd = synthetic_state_dict(7, "bn")
+    g = torch.Generator().manual_seed(5)
+    codes = torch.randint(0, 13, (40, 64), generator=g)
+    planes = F.one_hot(codes, 13)[..., 1:].permute(0, 2, 1).reshape(-1, 12, 8, 8).float().cuda()
+    moves = torch.randint(0, 4096, (40,), generator=g).cuda()
+    grads = {}
+    for fuse in (False, True):
+        TO.FUSE = fuse
+        try:
+            m = KM.ChessNet()
+            m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+            m.cuda().train()
+            with torch.autocast("cuda"):
+                pol, val = m(planes)
+            loss = F.cross_entropy(pol.float(), moves) + (val.float() ** 2).mean()
+            (loss * 65536.0).backward()
+            grads[fuse] = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+        finally:
+            TO.FUSE = True
+    for k, a in grads[False].items():
+        b = grads[True][k]
+        if k.endswith(".bias") and "conv" in k:
+            # exact value 0 (BatchNorm removes the bias): both sides are the cancellation noise of the same
+            # fp16 dx values summed in another order, ~2^-12 of the largest here
+            assert torch.allclose(a, b, rtol=0.0, atol=float(a.abs().max()) * 2.0 ** -8), k
+        else:
+            assert torch.equal(a, b), k
 
 
 def test_head1x1_forward_backward():
