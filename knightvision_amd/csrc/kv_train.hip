@@ -423,7 +423,8 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const _Float16* __restr
     const int cg = C / 8, rl = 256 / cg;  // channel groups, row lanes
     const int tid = threadIdx.x, g = tid % cg, lr = tid / cg;
     const int c = g * 8;
-    const int r0 = blockIdx.x * BN_ROWS, r1 = min(rows, r0 + BN_ROWS);
+    // threads past rl * cg (C / 8 not a divisor of 256) take no rows
+    const int r0 = blockIdx.x * BN_ROWS, r1 = lr < rl ? min(rows, r0 + BN_ROWS) : r0;
     float k[8], m[8], iv[8], s0[8], s1[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -568,7 +569,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const _Float16* __restric
         ga[e] = gamma[c + e];
         be[e] = beta[c + e];
     }
-    const int r0 = blockIdx.x * BN_EW_ROWS, r1 = min(rows, r0 + BN_EW_ROWS);
+    const int r0 = blockIdx.x * BN_EW_ROWS, r1 = lr < rl ? min(rows, r0 + BN_EW_ROWS) : r0;
     for (int r = r0 + lr; r < r1; r += rl) {
         const size_t i = (size_t)r * C + c;
         float xv[8], rv[8];
@@ -610,7 +611,7 @@ __global__ __launch_bounds__(256) void bn_backward_kernel(const _Float16* __rest
         sc[e] = gamma[c + e] * iv[e];
     }
     float ds[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const int r0 = blockIdx.x * BN_EW_ROWS, r1 = min(rows, r0 + BN_EW_ROWS);
+    const int r0 = blockIdx.x * BN_EW_ROWS, r1 = lr < rl ? min(rows, r0 + BN_EW_ROWS) : r0;
     for (int r = r0 + lr; r < r1; r += rl) {
         const size_t i = (size_t)r * C + c;
         float xv[8], gv[8], yv[8];

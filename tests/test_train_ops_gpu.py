@@ -88,7 +88,7 @@ def test_wgrad_is_deterministic():
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("res,C", [(False, 256), (True, 512)])
+@pytest.mark.parametrize("res,C", [(False, 256), (True, 512), (True, 192)])  # 192: C/8 does not divide 256
 def test_bn_act_forward_backward(res, C):
     g = torch.Generator().manual_seed(C + res)
     n = 7
@@ -118,7 +118,9 @@ def test_bn_act_forward_backward(res, C):
     y16 = yb.detach().half().float()
     mag = None
     if res:
-        mag = y16.abs() + rf.abs()  # the BN output is rounded before the residual add
+        # two fp16 roundings (the BN output, then the sum), each may land one ulp off when the fp32 values
+        # differ in their last bits
+        mag = 2 * (y16.abs() + rf.abs())
         y16 = (y16 + rf).half().float()
     yref = torch.relu(y16)
     _close16(y, yref, "BN forward", mag)
