@@ -1,4 +1,4 @@
-"""World-size-2 gloo test of the multi-GPU path's only collective: the
+"""World-size-2 and -3 gloo tests of the multi-GPU path's only collective: the
 end-of-iteration experience gather (knightvision_amd.distributed.gather_rows,
 to the root and to all ranks, with the MCTS root visit counts pi riding
 along row for row), and of the game-id sharding (rank r plays ids
@@ -8,6 +8,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 
@@ -19,13 +20,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_q):
+def _worker(rank, world, n_games, port, out_q):
     import torch.distributed as dist
     from knightvision_amd.distributed import gather_experience
     from knightvision_amd.engine import GAME_DTYPE, RECORD_DTYPE
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    ids = list(range(rank, 10, world))  # sharded global ids
+    ids = list(range(rank, n_games, world))  # sharded global ids (none for ranks >= n_games)
     rng = np.random.default_rng(rank)
     recs = []
     games = np.zeros(len(ids), dtype=GAME_DTYPE)
@@ -39,7 +40,7 @@ def _worker(rank, world, port, out_q):
         recs.append(r)
         games[k]["game_id"] = gid
         games[k]["plies"] = n
-    recs = np.concatenate(recs)
+    recs = np.concatenate(recs) if recs else np.zeros(0, dtype=RECORD_DTYPE)
     all_r, all_g = gather_experience(recs, games, dst=None)  # all-gather (the data-parallel learn loop)
     root_r, root_g = gather_experience(recs, games, dst=0)   # gather to the root (data generation)
     assert (root_r is None) == (rank != 0) and (root_g is None) == (rank != 0)
@@ -52,7 +53,7 @@ def _worker(rank, world, port, out_q):
     pi = np.full((len(recs), _lib.MAXM), 0xffff, dtype=np.uint16)
     pi[:, 0] = recs["move"]
     pi[:, 1] = recs["ply"]
-    pi_rows = torch.from_numpy(pi.view(np.uint8).reshape(len(recs), -1).copy())
+    pi_rows = torch.from_numpy(pi.view(np.uint8).reshape(len(recs), 2 * _lib.MAXM).copy())
     pr, pg, pp = gather_experience(recs, games, dst=0, pi=pi_rows)
     if rank == 0:
         assert np.array_equal(pr, all_r) and np.array_equal(pg, all_g)
@@ -67,20 +68,21 @@ def _worker(rank, world, port, out_q):
     dist.destroy_process_group()
 
 
-def test_gather_experience_world2():
+@pytest.mark.parametrize("world,n_games", [(2, 10), (3, 2)])  # (3, 2): rank 2 plays no game
+def test_gather_experience(world, n_games):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, n_games, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    want_ids = [g for g in range(10) for _ in range(3 + g)]
-    want_ply = [p for g in range(10) for p in range(3 + g)]
+    want_ids = [g for g in range(n_games) for _ in range(3 + g)]
+    want_ply = [p for g in range(n_games) for p in range(3 + g)]
     for rank, ids, ply, move, gids in res:
         assert ids == want_ids and ply == want_ply
-        assert move == [g * 100 + p for g in range(10) for p in range(3 + g)]
-        assert gids == list(range(10))
+        assert move == [g * 100 + p for g in range(n_games) for p in range(3 + g)]
+        assert gids == list(range(n_games))
