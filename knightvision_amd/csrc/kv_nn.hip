@@ -437,14 +437,28 @@ __global__ void split_weights_kernel(const float* __restrict__ w, size_t n, uint
     lo[i] = (uint16_t)bf16_rne(x - __uint_as_float(hb << 16));
 }
 
-// split-K combine: fixed-order sum of the slabs + folded BN (+ residual) + ReLU
-__global__ void splitk_reduce_kernel(const float* __restrict__ slab, int splits, size_t n4, int cout,
-                                     const float* __restrict__ scale, const float* __restrict__ shift,
-                                     const float* resid, float* out) {
+// split-K combine: fixed-order sum of the slabs + folded BN (+ residual) + ReLU.
+// The slab loads go out 16 at a time (a small batch has few outputs per split:
+// 64-thread blocks over every CU, and the 48 partials of an output are latency,
+// not bandwidth); the adds keep the order s = 0, 1, ..., splits - 1.
+constexpr int kReduceBatch = 16;
+__global__ __launch_bounds__(64) void splitk_reduce_kernel(const float* __restrict__ slab, int splits, size_t n4,
+                                                           int cout, const float* __restrict__ scale,
+                                                           const float* __restrict__ shift, const float* resid,
+                                                           float* out) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // float4 index
     if (i >= n4) return;
-    f32x4 v = ((const f32x4*)slab)[i];
-    for (int s = 1; s < splits; ++s) v += ((const f32x4*)slab)[(size_t)s * n4 + i];
+    const f32x4* sl = (const f32x4*)slab + i;
+    f32x4 v = sl[0];
+    for (int s0 = 1; s0 < splits; s0 += kReduceBatch) {
+        f32x4 p[kReduceBatch];
+#pragma unroll
+        for (int k = 0; k < kReduceBatch; ++k)
+            if (s0 + k < splits) p[k] = sl[(size_t)(s0 + k) * n4];
+#pragma unroll
+        for (int k = 0; k < kReduceBatch; ++k)
+            if (s0 + k < splits) v += p[k];
+    }
     const int c = (int)((i * 4) % (size_t)cout);
     const f32x4 sc = *(const f32x4*)(scale + c), sh = *(const f32x4*)(shift + c);
     f32x4 o = v * sc + sh;
@@ -795,7 +809,7 @@ static int split_kt(int nb_pad) { return nb_pad <= kSplitMaxBoards ? kSplitKt : 
 static int launch_reduce(const float* slab, int splits, int rows, int cout, const float* sc, const float* sh,
                          const float* resid, float* out, hipStream_t st) {
     const size_t n4 = (size_t)rows * cout / 4;
-    hipLaunchKernelGGL(kv::splitk_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, slab, splits,
+    hipLaunchKernelGGL(kv::splitk_reduce_kernel, dim3((unsigned)((n4 + 63) / 64)), dim3(64), 0, st, slab, splits,
                        n4, cout, sc, sh, resid, out);
     KV_HIP(hipGetLastError());
     return KV_OK;
