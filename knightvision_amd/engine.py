@@ -41,7 +41,11 @@ class SelfPlayEngine:
                  algo="auto", tree_edge_cap=0, keep_root_visits=False):
         L = _lib.lib()
         if record_cap is None:
-            record_cap = max(1 << 16, min(1 << 26, int(n_games) * 400))
+            # one record per committed ply: a capped game holds at most max_moves; an uncapped one
+            # (the reference default) is given 1,024 plies (its random-init games run 116-660). A
+            # run that still fills the buffer fails with KV_EOVERFLOW ("record buffer full").
+            per_game = int(max_moves) if max_moves else 1024
+            record_cap = max(1 << 16, min(1 << (22 if keep_root_visits else 27), int(n_games) * per_game))
         cfg = _lib.Config(device=device, slots=slots, n_games=n_games, game_id_base=game_id_base,
                           game_id_stride=game_id_stride, seed=seed, seed_mode=seed_mode,
                           max_moves=max_moves if max_moves else 0, batch=batch, eps=eps, alpha=alpha, sims=sims,

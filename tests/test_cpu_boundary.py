@@ -85,3 +85,58 @@ def test_chessnet_state_dict_keys_match_reference_layout():
     assert list(sd.keys()) == [n for n, _ in spec]
     for n, shape in spec:
         assert tuple(sd[n].shape) == tuple(shape), n
+
+
+def _cfg(**kw):
+    from knightvision_amd import _lib
+    base = dict(device=0, slots=4, n_games=4, game_id_base=0, game_id_stride=1, seed=42, seed_mode=0, max_moves=0,
+                batch=16, eps=0.25, alpha=0.3, sims=0, c_puct=1.5, eval_mode=0, record_cap=1 << 16, recycle=1,
+                precision=0, algo=0, tree_edge_cap=0, keep_root_visits=0)
+    base.update(kw)
+    return _lib.Config(**base)
+
+
+@pytest.mark.parametrize("kw, msg", [
+    (dict(slots=0), "slots must be > 0"),
+    (dict(n_games=-1), "slots must be > 0"),
+    (dict(alpha=0.0), "DIR_NOISE_ALPHA"),
+    (dict(alpha=1.5), "DIR_NOISE_ALPHA"),
+    (dict(batch=0), "SELFPLAY_BATCH_SIZE"),
+    (dict(seed_mode=7), "bad seed_mode"),
+    (dict(seed_mode=1, slots=2), "sequential seeding"),
+    (dict(sims=-1), "out of range"),
+    (dict(sims=65001), "out of range"),
+    (dict(sims=64, tree_edge_cap=100), "tree_edge_cap"),
+    (dict(sims=64, seed_mode=1, slots=1), "per-game seeding"),
+    (dict(sims=64, eval_mode=1), "eval_mode 1 not available"),
+    (dict(eval_mode=5), "eval_mode 5 not available"),
+])
+def test_kv_create_rejects_bad_configs(kw, msg):
+    """kv_create validates its kv_config before touching the device (include/kv.h conventions: KV_EINVAL
+    and the reason in kv_last_error()), so these run without a GPU."""
+    from knightvision_amd import _lib
+    L = _lib.lib()
+    h = C.c_void_p()
+    cfg = _cfg(**kw)
+    assert L.kv_create(C.byref(cfg), C.byref(h)) == -1  # KV_EINVAL
+    assert msg in L.kv_last_error().decode()
+    assert not h.value
+
+
+def test_null_engine_arguments_are_einval():
+    """Every engine entry point refuses a NULL engine / output pointer with KV_EINVAL (no device call)."""
+    from knightvision_amd import _lib
+    L = _lib.lib()
+    n = C.c_size_t()
+    assert L.kv_create(None, None) == -1 and "NULL" in L.kv_last_error().decode()
+    assert L.kv_load_weights(None, None, 0) == -1
+    assert L.kv_run(None, -1, -1) == -1 and "no weights" in L.kv_last_error().decode()
+    assert L.kv_set_max_moves(None, 10) == -1
+    assert L.kv_records(None, None, 0, C.byref(n)) == -1
+    assert L.kv_records_device(None, None, 0, C.byref(n), None) == -1
+    assert L.kv_games(None, None, 0, C.byref(n)) == -1
+    assert L.kv_stats_get(None, None) == -1
+    assert L.kv_root_visits(None, None, 0, C.byref(n)) == -1
+    assert L.kv_root_visits_device(None, None, 0, C.byref(n), None) == -1
+    assert L.kv_reset_records(None) == -1
+    assert L.kv_sync(None) == -1
