@@ -83,6 +83,11 @@ def parse():
     return ap.parse_args()
 
 
+# mean plies of complete MCTS games at C3's settings (800 sims/move, uncapped, per-game seeds 42+id,
+# random-init weights seed 42): 64 games played to the end, profiles/r02_mcts_game_length_c3.log
+C3_MCTS_GAME_PLIES = 148.328125
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -362,11 +367,19 @@ def main():
             "games_per_hour_note": (
                 (f"{int(games_done)} games ended inside the timed region / its duration -- a transient count, not "
                  f"a steady-state rate: every slot started at ply 0, the region covers plies {warmup + 1}-"
-                 f"{warmup + steps}, so only early endings (resignations after ply 15) are in it; the steady-state "
-                 "games/hour is ref_selection's" if mcts else
+                 f"{warmup + steps}, so only early endings are in it; see games_per_hour_steady_derived and "
+                 "ref_selection" if mcts else
                  "games completed inside the timed region / its duration (slots recycled)") if gph is not None else
                 f"no game completed inside the {steps} timed moves (plies {warmup + 1}-{warmup + steps} of games "
                 f"from the start position); measured games/hour: ref_selection"),
+            "games_per_hour_steady_derived": (plies / dt * 3600.0 / C3_MCTS_GAME_PLIES
+                                              if mcts and G == 2048 and sims == 800 else None),
+            "games_per_hour_steady_note": (
+                f"this run's measured plies/s x 3600 / {C3_MCTS_GAME_PLIES} plies, the measured mean length of "
+                "complete games at these settings (game ids 0-63 played to the end: 57 checkmates, 6 draws, 1 "
+                "stalemate; median 115, range 8-611 plies; standard error of the mean ~15 plies) -- "
+                "profiles/r02_mcts_game_length_c3.log, tools/mcts_game_length.py"
+                if mcts and G == 2048 and sims == 800 else None),
             "games_completed": games_done, "nn_evals_per_s": nn_rows / dt,
             "nn_tflops": nn_rows * FLOP_PER_EVAL / dt / 1e12, "gather_ms": gather_ms,
             "gather": ((f"{'RCCL' if backend == 'nccl' else backend} gather to rank 0 of the timed region's "

@@ -1,0 +1,61 @@
+"""Length of complete MCTS self-play games at the C3 settings (800 sims/move,
+uncapped, per-game seeds 42 + id, random-init weights seed 42), played to
+the end on fewer slots. Games are per-game seeded and the > 16-board network
+class is batch-invariant, so game g here is move for move game g of the C3
+bench run (tests/test_fullsize_gpu.py checks that a small run equals the first
+games of a big one). The C3 bench times 20 moves of games that started
+together, so its own games/hour is a transient count; this gives the game
+lengths the steady-state figure needs.
+
+    python tools/mcts_game_length.py [--games 64] [--seconds 420]
+
+Prints a progress line per 20 plies and one JSON line: per-game plies, end
+reasons, games still running at the time limit (censored).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--games", type=int, default=64)
+    ap.add_argument("--sims", type=int, default=800)
+    ap.add_argument("--seconds", type=float, default=420.0)
+    a = ap.parse_args()
+    import torch  # noqa: F401
+    from knightvision_amd.engine import REASONS, SelfPlayEngine
+    from knightvision_amd.weights import synthetic_state_dict
+    t0 = time.perf_counter()
+    with SelfPlayEngine(synthetic_state_dict(42, "init"), slots=a.games, n_games=a.games, seed=42, max_moves=None,
+                        sims=a.sims, recycle=False, record_cap=a.games * 2048) as eng:
+        ply = 0
+        while time.perf_counter() - t0 < a.seconds:
+            eng.run(max_steps=20)
+            ply += 20
+            st = eng.stats()
+            print(f"ply {ply}: {st['games_done']}/{a.games} games done, {time.perf_counter() - t0:.0f} s",
+                  file=sys.stderr, flush=True)
+            if st["games_done"] >= a.games:
+                break
+        games = eng.games()
+        st = eng.stats()
+    plies = np.sort(games["plies"]).tolist()
+    reasons = {REASONS.get(int(r), "?"): int((games["reason"] == r).sum()) for r in np.unique(games["reason"])}
+    print(json.dumps({"what": "complete MCTS games at the C3 settings (game ids 0..n-1 of the C3 run)",
+                      "sims": a.sims, "games": a.games, "finished": len(plies),
+                      "still_running": a.games - len(plies), "plies_played_by_running_games": ply,
+                      "mean_plies_finished": float(np.mean(plies)) if plies else None,
+                      "median_plies_finished": float(np.median(plies)) if plies else None,
+                      "plies": plies, "reasons": reasons, "wall_s": time.perf_counter() - t0,
+                      "total_sims": int(st["sims"])}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
