@@ -132,7 +132,8 @@ typedef struct {
     int sims;             /* 0: reference move selection; 1..KV_MAX_SIMS: PUCT MCTS sims/move */
     float c_puct;
     int eval_mode;        /* KV_EVAL_* */
-    int64_t record_cap;   /* record buffer capacity */
+    int64_t record_cap;   /* record buffer capacity (records, one per committed ply; <= 0: 2^20); a run that
+                             fills it fails with KV_EOVERFLOW ("record buffer full"), never a silent drop */
     int recycle;          /* 1: a finished slot starts the next game id */
     int precision;        /* KV_PREC_* of the network convs */
     int algo;             /* KV_ALGO_* of the network convs */
