@@ -634,14 +634,13 @@ __global__ void encode_boards_kernel(const int8_t* __restrict__ boards, int nb, 
 // 0..31 / 32..63. WINO: the activated 8x8 planes go through LDS to the tile
 // transforms -- wave w writes board w/2's tile w%2 (F(4x8)) or tiles 2(w%2),
 // 2(w%2)+1 (F(4x4)) of conv2's Winograd input V [points][rows][256]; else
-// NHWC T [board][64][256].
+// NHWC T [board][64][256]. F(4x8) skips the plane (below).
 template <int WINO>  // 0: NHWC out, 1: F(4x4) V of conv2, 2: F(4x8) V of conv2
 __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ boards, int nb,
                                                    const float* __restrict__ wT, const float* __restrict__ scale,
                                                    const float* __restrict__ shift, float* __restrict__ out,
                                                    int rows, unsigned* vmax) {
     __shared__ float wl[9 * 13][64];    // [tap][code 0..12][channel], code 0 = empty = 0
-    __shared__ float plane[2][64][64];  // [board][pixel][channel]
     __shared__ int codes[2][100];       // the boards with a one-square empty border (10x10)
     const int cl = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + cl, b0 = blockIdx.y * 2;
@@ -664,6 +663,49 @@ __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ bo
     __syncthreads();
     const float sc = scale[c], sh = shift[c];
     const int bb = w >> 1, b = b0 + bb;
+    if constexpr (WINO == 2) {
+        // no plane exchange: wave w computes the conv1 outputs of its own tile's 6x10 patch (the
+        // 40 on-board pixels; rows 3-4 are computed by both tiles' waves, same sums, same bits).
+        // 25 % more LDS reads than sharing the 64 pixels through a plane, but no 32 KB plane:
+        // 4 workgroups per CU instead of 2 (VGPR-bound at 106), so one workgroup's V stores
+        // overlap another's sums (forward 12.40 -> 12.35 ms at 2,048 boards), bit-identical
+        const int tile = w & 1;
+        float d48[60];
+        // the tile as a compile-time constant: every patch position's on-board test and LDS
+        // offset are then static
+        auto patch = [&](auto T) {
+            constexpr int TILE = decltype(T)::value;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const int py = TILE * 4 - 1 + i;
+#pragma unroll
+                for (int j = 0; j < 10; ++j) {
+                    const int px = j - 1;
+                    float y = 0.f;
+                    if (py >= 0 && py < 8 && px >= 0 && px < 8) {
+                        float acc = 0.f;
+#pragma unroll
+                        for (int t = 0; t < 9; ++t)
+                            acc += wl[t * 13 + codes[bb][(py + t / 3) * 10 + px + t % 3]][cl];
+                        const float v = acc * sc + sh;
+                        y = v > 0.f ? v : 0.f;
+                    }
+                    d48[i * 10 + j] = y;
+                }
+            }
+        };
+        if (tile == 0)
+            patch(std::integral_constant<int, 0>{});
+        else
+            patch(std::integral_constant<int, 1>{});
+        float mx = wino48_input_tile(d48, out, ((size_t)b * 2 + tile) * 256 + c, (size_t)rows * 256);
+        if (vmax) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+            if (cl == 0) atomicMax(vmax + b, __float_as_uint(mx));
+        }
+    } else {
+    __shared__ float plane[2][64][64];  // [board][pixel][channel]
     // branch-free: an empty or off-board neighbour adds +0 (exact, acc starts at +0),
     // so every pixel issues its 9 independent LDS reads back to back
 #pragma unroll 4
@@ -712,6 +754,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ bo
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
         if (cl == 0) atomicMax(vmax + b, __float_as_uint(mx));
+    }
     }
 }
 
