@@ -996,7 +996,9 @@ static int launch_wino_gemm(const float* V, const float* U, float* M, int rows, 
 // 64x64 (3,840 tiles: an equal share per CU) 1.87 / 13.49; 64x128 as 8 waves of 32x32 1.89 / 13.18;
 // 128x128 as 4 waves of 64x64 1.82 / 13.06 (k-tile 16: 1.85 / 13.20), as 8 waves of 64x32 1.79 / 12.60
 // (re-measured A/B on the final out kernels: 8 waves of 32x64 1.78 / 12.55, of 64x32 1.80 / 12.77,
-// 4 waves of 64x64 1.84 / 13.07)
+// 4 waves of 64x64 1.84 / 13.07); larger tiles, round 2 (bit-identical, two alternating runs on one box,
+// profiles/r02_gemm_tile_ab.log): 256x128 as 8 waves of 64x64, k-tile 16 (2 per CU) 1.74 / 12.83;
+// 128x256 the same way 1.73 / 12.89; 256x128 k-tile 32 (1 per CU) 1.78 / 13.35 -- against 1.65 / 12.22
 template <int K>
 static int launch_wino48_gemm(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
     if (rows % 128 == 0) return launch_wino_gemm_t<K, 4, 2, 1, 2, 32, 0, kv::W48_XI>(V, U, M, rows, stride, st);
