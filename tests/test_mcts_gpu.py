@@ -106,9 +106,16 @@ def test_mcts_network_visits_identical_to_oracle_c2_first_move():
     _compare_network_games("init", slots=256, n_check=16, sims=400, max_moves=None, steps=1)
 
 
-def test_mcts_network_visits_identical_to_oracle_c3_first_move():
+def test_mcts_network_visits_identical_to_oracle_c2_peaked_three_moves():
+    """C2 with the peaked weight set (priors the search follows, not near-uniform
+    ones): the first three moves of the first 8 games."""
+    _compare_network_games("peaked", slots=256, n_check=8, sims=400, max_moves=None, steps=3)
+
+
+@pytest.mark.parametrize("variant", ["init", "peaked"])
+def test_mcts_network_visits_identical_to_oracle_c3_first_move(variant):
     """C3, the headline config (2,048 slots x 800 sims): the first move of the first 8 games."""
-    _compare_network_games("init", slots=2048, n_check=8, sims=800, max_moves=None, steps=1)
+    _compare_network_games(variant, slots=2048, n_check=8, sims=800, max_moves=None, steps=1)
 
 
 def test_mcts_network_games_run():
