@@ -133,16 +133,21 @@ GROUPS = {"pg_init_mm80": ("init", 80, 16), "pg_peaked_mm80": ("peaked", 80, 16)
           "pg_init_b1_mm60": ("init", 60, 1), "pg_init_full": ("init", None, 16)}
 
 
-@pytest.mark.parametrize("precision", ["fp32", "f16x3", "bf16x6", "bf16x3"])
+@pytest.mark.parametrize("precision,algo", [("fp32", "auto"), ("f16x3", "auto"), ("bf16x6", "auto"),
+                                            ("bf16x3", "auto"), ("fp32", "winograd48")])
 @pytest.mark.parametrize("group", list(GROUPS))
-def test_engine_games_match_reference(golden_dir, group, precision):
+def test_engine_games_match_reference(golden_dir, group, precision, algo):
+    """Complete games vs the reference's golden games. The slot counts here put
+    the network in the <= 16-board class; ("fp32", "winograd48") forces the
+    headline's F(4x8) Winograd tower (the > 16-board class of C2 / C3) on the
+    same games."""
     from knightvision_amd.engine import SelfPlayEngine, records_by_game
     variant, mm, batch = GROUPS[group]
     gold = _golden_games(golden_dir, group)
     n = len(gold)
     slots = max(1, n // 2)  # fewer slots than games: exercises slot recycling
     with SelfPlayEngine(synthetic_state_dict(42, variant), slots=slots, n_games=n, seed=gold[0]["seed"],
-                        max_moves=mm, batch=batch, precision=precision) as eng:
+                        max_moves=mm, batch=batch, precision=precision, algo=algo) as eng:
         eng.run()
         recs, games = eng.records(), eng.games()
     by = records_by_game(recs, games)
@@ -155,7 +160,7 @@ def test_engine_games_match_reference(golden_dir, group, precision):
             assert reward == pytest.approx(g["reward"])
             assert int(games[k]["n_evals"]) == g["n_evals"]
     ties = [r for r in res if r != "exact"]
-    print(f"{precision} {group}: {n - len(ties)}/{n} games move-for-move identical, near-tie divergences "
+    print(f"{precision}/{algo} {group}: {n - len(ties)}/{n} games move-for-move identical, near-tie divergences "
           f"{len(ties)} {ties}")
     assert len(ties) <= max(1, n // 8)
 
