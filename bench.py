@@ -83,9 +83,18 @@ def parse():
     return ap.parse_args()
 
 
-# mean plies of complete MCTS games at C3's settings (800 sims/move, uncapped, per-game seeds 42+id,
-# random-init weights seed 42): 64 games played to the end, profiles/r02_mcts_game_length_c3.log
-C3_MCTS_GAME_PLIES = 148.328125
+def _mcts_game_length(sims: int):
+    """The newest committed game-length run at these search settings (tools/mcts_game_length.py: complete
+    MCTS games at C3's settings, game ids 0..n-1 of the C3 run played to the end), or (None, None)."""
+    d = os.path.join(HERE, "profiles")
+    for f in sorted((x for x in os.listdir(d) if "mcts_game_length" in x and x.endswith(".json")), reverse=True):
+        try:
+            gl = json.loads(open(os.path.join(d, f)).read().splitlines()[-1])
+        except (OSError, ValueError, IndexError):
+            continue
+        if gl.get("sims") == sims and gl.get("still_running") == 0 and gl.get("finished", 0) >= 2:
+            return gl, f
+    return None, None
 
 
 def _free_port() -> int:
@@ -292,7 +301,10 @@ def main():
         pi_all = None
     gather_ms = (time.perf_counter() - tg) * 1e3 if world > 1 else None
     n_records = int(len(recs_all)) if recs_all is not None else 0
-    gathered_bytes = n_records * 80 + (int(pi_all.nbytes) if pi_all is not None else 0)
+    # wire bytes: 80-B records + pi as legal-move prefixes (2 B per legal move + a 2-B count per record,
+    # distributed.pack_pi); the padded uint16 [n, MAXM] form would be 640 B per record
+    pi_wire = (2 * int(pi_all.shape[0]) + 2 * int((pi_all != 0xffff).sum())) if pi_all is not None else 0
+    gathered_bytes = n_records * 80 + pi_wire
 
     alt = None
     if args.alt_precision and args.alt_precision != args.precision:
@@ -344,6 +356,7 @@ def main():
                     "source": "profiles/" + tf,
                     "note": "latency-bound: one wave per game (select descent + leaf getValidMoves, backup)"}
 
+    gl, gl_file = _mcts_game_length(sims) if (mcts and G == 2048) else (None, None)
     if rank == 0:
         if mcts:
             metric, unit, value = "MCTS simulations/sec + self-play games/hour", "sims/s", sims_done / dt
@@ -372,21 +385,28 @@ def main():
                  "games completed inside the timed region / its duration (slots recycled)") if gph is not None else
                 f"no game completed inside the {steps} timed moves (plies {warmup + 1}-{warmup + steps} of games "
                 f"from the start position); measured games/hour: ref_selection"),
-            "games_per_hour_steady_derived": (plies / dt * 3600.0 / C3_MCTS_GAME_PLIES
-                                              if mcts and G == 2048 and sims == 800 else None),
+            "games_per_hour_steady_derived": (plies / dt * 3600.0 / gl["mean_plies_finished"]
+                                              if gl is not None else None),
+            "games_per_hour_steady_ci95": ([plies / dt * 3600.0 / gl["ci95_mean_plies"][1],
+                                            plies / dt * 3600.0 / gl["ci95_mean_plies"][0]]
+                                           if gl is not None and gl.get("ci95_mean_plies") else None),
             "games_per_hour_steady_note": (
-                f"this run's measured plies/s x 3600 / {C3_MCTS_GAME_PLIES} plies, the measured mean length of "
-                "complete games at these settings (game ids 0-63 played to the end: 57 checkmates, 6 draws, 1 "
-                "stalemate; median 115, range 8-611 plies; standard error of the mean ~15 plies) -- "
-                "profiles/r02_mcts_game_length_c3.log, tools/mcts_game_length.py"
-                if mcts and G == 2048 and sims == 800 else None),
+                f"this run's measured plies/s x 3600 / the mean length of complete games at these settings, "
+                f"{gl['mean_plies_finished']:.1f} plies (game ids 0-{gl['games'] - 1} played to the end: "
+                f"{gl['reasons']}; median {gl['median_plies_finished']:.0f}, range {gl['plies'][0]}-"
+                f"{gl['plies'][-1]}, standard error {100 * gl['se_frac']:.1f} %; the 95 % interval of the mean "
+                f"gives games_per_hour_steady_ci95) -- profiles/{gl_file}, tools/mcts_game_length.py"
+                if gl is not None else None),
             "games_completed": games_done, "nn_evals_per_s": nn_rows / dt,
             "nn_tflops": nn_rows * FLOP_PER_EVAL / dt / 1e12, "gather_ms": gather_ms,
             "gather": ((f"{'RCCL' if backend == 'nccl' else backend} gather to rank 0 of the timed region's "
-                        "device-resident (s, pi, z): 80-B records + uint16 root visit counts per move slot"
+                        "device-resident (s, pi, z): 80-B records + the root visit counts of each record's "
+                        "legal moves (uint16 each, plus a 2-B count)"
                         if mcts else f"{'RCCL' if backend == 'nccl' else backend} gather to rank 0 of the timed "
                         "region's device-resident records") if world > 1 else "none at N=1 (no collective)"),
-            "records_gathered": n_records, "gathered_bytes": gathered_bytes, "mean_plies_per_game": mean_len,
+            "records_gathered": n_records, "gathered_bytes": gathered_bytes,
+            "gathered_bytes_per_record": (gathered_bytes / n_records) if n_records else None,
+            "mean_plies_per_game": mean_len,
             "tree_overflows": m["tree_overflows"],
             "roofline": {"bound": "mfma",
                          "kernel": kname + kdesc,

@@ -56,7 +56,8 @@ int kv_net_forward_boards(kv_net* net, const int8_t* boards_dev, int B, float* p
                           void* stream);
 /* The same forward with only the listed moves' logits (the MCTS leaves' legal
  * moves): moves_dev [B][maxm] move words (from | to << 6, as kv_dev_valid_moves),
- * n_moves_dev [B] (0: no logits for that board); legal_dev [B][maxm] receives
+ * n_moves_dev [B] (0: no logits for that board; values above maxm are read as
+ * maxm -- a row holds maxm moves); legal_dev [B][maxm] receives
  * policy logit (from*64 + to) of each listed move, bit-identical to the
  * corresponding entry of kv_net_forward_boards; value_dev [B]. */
 int kv_net_forward_boards_legal(kv_net* net, const int8_t* boards_dev, int B, const uint16_t* moves_dev,
@@ -128,7 +129,10 @@ typedef struct {
     int max_moves;        /* <= 0: None */
     int batch;            /* SELFPLAY_BATCH_SIZE (self_play.py:34) */
     double eps;           /* DIR_NOISE_EPS */
-    double alpha;         /* DIR_NOISE_ALPHA, must be in (0,1) */
+    double alpha;         /* DIR_NOISE_ALPHA, a normal double in (0,1) (numpy's legacy gamma shape < 1
+                             branch, restated exactly down to subnormal / zero draws; a ply whose 4096
+                             draws are all 0 fails kv_run with KV_EINVAL, as the reference's
+                             random.choices raises ValueError on the NaN weights) */
     int sims;             /* 0: reference move selection; 1..KV_MAX_SIMS: PUCT MCTS sims/move */
     float c_puct;
     int eval_mode;        /* KV_EVAL_* */
@@ -195,7 +199,9 @@ int kv_records(kv_engine* e, kv_record* out, size_t cap, size_t* n);
 /* The same records, unsorted (allocation order), copied device-to-device into
  * out_dev (a device buffer of cap records on the engine's GPU) on `stream`:
  * the experience stays in HBM for the RCCL gather. out_dev
- * NULL: only *n. */
+ * NULL: only *n. The engine's next kv_run / kv_reset_records waits for the
+ * copy on its own stream (an event recorded on `stream`), and kv_destroy
+ * waits for it before freeing the buffer. */
 int kv_records_device(kv_engine* e, kv_record* out_dev, size_t cap, size_t* n, void* stream);
 /* finished games (the last 2^20 at most), ordered by game id */
 int kv_games(kv_engine* e, kv_game* out, size_t cap, size_t* n);

@@ -198,7 +198,7 @@ int kv_dev_dirichlet(int device, const uint64_t* seeds, int n, double alpha, int
                      int64_t* attempts, double* tail) {
     KV_REQUIRE(n > 0 && k > 0 && draws > 0 && seeds && out && attempts && tail, KV_EINVAL,
                "kv_dev_dirichlet: bad arguments");
-    KV_REQUIRE(alpha > 0.0 && alpha < 1.0, KV_EINVAL, "kv_dev_dirichlet: alpha must be in (0,1)");
+    KV_REQUIRE(alpha >= 2.2250738585072014e-308 && alpha < 1.0, KV_EINVAL, "kv_dev_dirichlet: alpha must be a normal double in (0,1)");
     KV_HIP(hipSetDevice(device));
     kv::DevBuf<unsigned long long> sd;
     kv::DevBuf<double> o, t;

@@ -321,7 +321,7 @@ __device__ inline unsigned long long commit_move(const DevCfg& cfg, Slot& s, int
 
 // MCTS launches (kv_mcts.hip), all on `st`
 int mcts_root(const DevCfg& cfg, const Tree& t, Slot* slots, const uint16_t* moves, const float* logits,
-              const float* values, float* probs_scratch, uint32_t* np_mt, hipStream_t st);
+              const float* values, float* probs_scratch, uint32_t* np_mt, Ctr* ctr, hipStream_t st);
 // select / backup for slots [slot0, slot0 + count)
 int mcts_select(const DevCfg& cfg, const Tree& t, const Slot* slots, const int8_t* boards, int8_t* nn_boards,
                 Ctr* ctr, hipStream_t st, int slot0, int count);

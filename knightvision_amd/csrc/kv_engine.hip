@@ -204,6 +204,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     }
     __syncthreads();
     uint32_t* py = py_mt + (size_t)i * MT_WORDS;
+    if (!isfinite(s_total)) {
+        // every gamma draw of the ply was 0 (only a tiny alpha can do this):
+        // noise = 0 * (1/0) = NaN, and the reference's random.choices raises
+        // ValueError('Total of weights must be finite') -- an error, not a move
+        if (lane == 0) atomicOr(&ctr->error, 8);
+        return;
+    }
     if (s_total == 0.0) {
         if (lane == 0) s_pick = mt_randbelow_serial(py, n);  // random.choice
     } else {
@@ -343,6 +350,66 @@ __global__ __launch_bounds__(1024) void k_compact(DevCfg cfg, const Slot* slots,
     if (tid == 0) ctr->comp_rows = padded;
 }
 
+// MCTS with fewer active slots than slots (a finite run whose game queue has
+// run dry: its last games, a test's tail): the leaf batches carry only the
+// active slots' rows. slot_of[r] = the r-th active slot in slot order, rows
+// past the count (padding up to the > 16-board class) repeat row 0; row_of[i]
+// = the slot's row or -1. The network is batch-invariant bit for bit inside a
+// class, so every active slot's leaf row equals its row in the full batch and
+// the searches are unchanged (tests/test_mcts_gpu.py).
+__global__ __launch_bounds__(1024) void k_compact_active(DevCfg cfg, const Slot* slots, int rows, int* slot_of,
+                                                         int* row_of) {
+    __shared__ int wsum[16];
+    __shared__ int base;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) base = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < cfg.slots; c0 += 1024) {
+        const int i = c0 + tid;
+        const bool act = i < cfg.slots && slots[i].status == ST_ACTIVE;
+        const unsigned long long bal = __ballot(act);
+        if (lane == 0) wsum[w] = __popcll(bal);
+        __syncthreads();
+        int off = base;
+        for (int k = 0; k < w; ++k) off += wsum[k];
+        const int row = off + __popcll(bal & ((1ull << lane) - 1));
+        if (i < cfg.slots) row_of[i] = act && row < rows ? row : -1;
+        if (act && row < rows) slot_of[row] = i;
+        __syncthreads();
+        if (tid == 0)
+            for (int k = 0; k < 16; ++k) base += wsum[k];
+        __syncthreads();
+    }
+    const int cnt = base < rows ? base : rows;
+    __syncthreads();
+    const int first = cnt > 0 ? slot_of[0] : 0;
+    for (int r = cnt + tid; r < rows; r += 1024) slot_of[r] = first;  // padding rows
+}
+
+// this sim-step's leaves of the active slots -> the compact batch (one wave per row)
+__global__ __launch_bounds__(64) void k_gather_leaves(const int* slot_of, const int8_t* nn_boards,
+                                                      const uint16_t* leaf_moves, const int* leaf_cnt, int8_t* cb,
+                                                      uint16_t* cm, int* cc) {
+    const int r = blockIdx.x, lane = threadIdx.x;
+    const int s = slot_of[r];
+    cb[(size_t)r * 64 + lane] = nn_boards[(size_t)s * 64 + lane];
+    const int n = min(leaf_cnt[s], MAXM);
+    if (lane == 0) cc[r] = n;
+    for (int j = lane; j < n; j += 64) cm[(size_t)r * MAXM + j] = leaf_moves[(size_t)s * MAXM + j];
+}
+
+// the compact batch's outputs back to the slots' rows (padding rows dropped)
+__global__ __launch_bounds__(64) void k_scatter_leaves(const int* slot_of, const int* row_of, const float* cl,
+                                                       const float* cv, const int* cc, float* leaf_logits,
+                                                       float* values) {
+    const int r = blockIdx.x, lane = threadIdx.x;
+    const int s = slot_of[r];
+    if (row_of[s] != r) return;
+    if (lane == 0) values[s] = cv[r];
+    const int n = cc[r];
+    for (int j = lane; j < n; j += 64) leaf_logits[(size_t)s * MAXM + j] = cl[(size_t)r * MAXM + j];
+}
+
 // the flush rows of sequential mode: boards [slots, 2*slots) = last appended board
 __global__ void k_flush_rows(DevCfg cfg, const Slot* slots, const int8_t* last_board, int8_t* nn_boards) {
     const int i = blockIdx.x, lane = threadIdx.x;
@@ -389,7 +456,36 @@ struct kv_engine {
     int8_t* nn_boards = nullptr;
     float* probs = nullptr;
     float* sqrt_tab = nullptr;
+    // MCTS leaf batches of the active slots only (k_compact_active)
+    int* mc_slot_of = nullptr;
+    int* mc_row_of = nullptr;
+    int8_t* mc_boards = nullptr;
+    uint16_t* mc_moves = nullptr;
+    int* mc_cnt = nullptr;
+    float* mc_logits = nullptr;
+    float* mc_values = nullptr;
+    long long mc_rows = 0;  // leaf rows the compact batches sent through the network
+    // kv_records_device / kv_root_visits_device copy out of e->rec / root_visits on the caller's
+    // stream; the next write to those buffers (kv_run, kv_reset_records) or their release
+    // (kv_destroy) waits for that copy on e->st
+    hipEvent_t copy_done = nullptr;
+    bool copy_pending = false;
 };
+
+// order e->st after an outstanding device-to-device copy of the engine's buffers on a caller stream
+static int eng_wait_copies(kv_engine* e) {
+    if (!e->copy_pending) return KV_OK;
+    KV_HIP(hipStreamWaitEvent(e->st, e->copy_done, 0));
+    e->copy_pending = false;
+    return KV_OK;
+}
+
+static int eng_note_copy(kv_engine* e, hipStream_t caller) {
+    if (!e->copy_done) KV_HIP(hipEventCreateWithFlags(&e->copy_done, hipEventDisableTiming));
+    KV_HIP(hipEventRecord(e->copy_done, caller));
+    e->copy_pending = true;
+    return KV_OK;
+}
 
 static int eng_counters(kv_engine* e, bool check_error = true) {
     // active slots / plies / rows are summed from the slots only when the host reads them
@@ -399,9 +495,11 @@ static int eng_counters(kv_engine* e, bool check_error = true) {
     KV_HIP(hipStreamSynchronize(e->st));
     if (check_error && e->ctr_host->error) {
         kv::set_error("engine device error flags 0x%x (1: move list overflow, 2: record buffer full, "
-                      "4: MCTS tree pool full, %llu expansions dropped -- raise kv_config.tree_edge_cap)",
+                      "4: MCTS tree pool full, %llu expansions dropped -- raise kv_config.tree_edge_cap; "
+                      "8: move weights not finite -- every Dirichlet gamma draw of a ply was 0, where the "
+                      "reference's random.choices raises ValueError)",
                       e->ctr_host->error, (unsigned long long)e->ctr_host->tree_overflows);
-        return KV_EOVERFLOW;
+        return (e->ctr_host->error & 8) ? KV_EINVAL : KV_EOVERFLOW;
     }
     return KV_OK;
 }
@@ -423,8 +521,12 @@ extern "C" {
 int kv_create(const kv_config* cfg, kv_engine** out) {
     KV_REQUIRE(cfg && out, KV_EINVAL, "kv_create: NULL argument");
     KV_REQUIRE(cfg->slots > 0 && cfg->n_games >= 0, KV_EINVAL, "kv_create: slots must be > 0");
-    KV_REQUIRE(cfg->alpha > 0.0 && cfg->alpha < 1.0, KV_EINVAL,
-               "kv_create: DIR_NOISE_ALPHA must be in (0,1) (legacy gamma shape<1 branch), got %g", cfg->alpha);
+    // numpy's legacy gamma for shape < 1 (the branch restated on the device); a
+    // normal double keeps 1/alpha finite, and kv_libm.h's pow is exact over the
+    // whole range, subnormal / zero gamma draws of a small alpha included
+    KV_REQUIRE(cfg->alpha >= 2.2250738585072014e-308 && cfg->alpha < 1.0, KV_EINVAL,
+               "kv_create: DIR_NOISE_ALPHA must be a normal double in (0,1) (legacy gamma shape<1 branch), got %g",
+               cfg->alpha);
     KV_REQUIRE(cfg->batch >= 1, KV_EINVAL, "kv_create: SELFPLAY_BATCH_SIZE must be >= 1");
     KV_REQUIRE(cfg->seed_mode == KV_SEED_PER_GAME || cfg->seed_mode == KV_SEED_SEQUENTIAL, KV_EINVAL,
                "kv_create: bad seed_mode");
@@ -520,6 +622,16 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
         ALLOC(e->probs, S * 4096 * sizeof(float));
         ALLOC(e->sqrt_tab, (size_t)(t.ncap + 2) * sizeof(float));
         if (cfg->keep_root_visits) ALLOC(t.root_visits, (size_t)e->cfg.record_cap * kv::MAXM * sizeof(uint16_t));
+        const char* mc_env = getenv("KV_MCTS_COMPACT");  // "0": always the full-slot leaf batch (A/B timing)
+        if (cfg->eval_mode != KV_EVAL_HASH && S > 1 && !(mc_env && mc_env[0] == '0')) {
+            ALLOC(e->mc_slot_of, S * sizeof(int));
+            ALLOC(e->mc_row_of, S * sizeof(int));
+            ALLOC(e->mc_boards, S * 64);
+            ALLOC(e->mc_moves, S * kv::MAXM * sizeof(uint16_t));
+            ALLOC(e->mc_cnt, S * sizeof(int));
+            ALLOC(e->mc_logits, S * kv::MAXM * sizeof(float));
+            ALLOC(e->mc_values, S * sizeof(float));
+        }
         t.ms = e->ms;
         std::vector<float> sq(t.ncap + 2);
         for (int k = 0; k < t.ncap + 2; ++k) sq[k] = (float)sqrt((double)k);
@@ -580,11 +692,12 @@ int kv_set_max_moves(kv_engine* e, int max_moves) {
 // residual-tower section bracketed by HIP events for the roofline; `leaf`:
 // the MCTS leaf batch, whose policy is only the leaves' legal moves
 // (kv_net_forward_boards_legal into tree.leaf_logits)
-static int eng_eval(kv_engine* e, const int8_t* boards, int rows, bool leaf = false) {
+// `comp`: the leaf batch is the compact active-slot batch (e->mc_*) instead of the slots' rows
+static int eng_eval(kv_engine* e, const int8_t* boards, int rows, bool leaf = false, bool comp = false) {
     kv_net* net = e->net;
     hipStream_t st = e->st;
     float* logits = e->logits;
-    float* values = e->values;
+    float* values = comp ? e->mc_values : e->values;
     if (e->dc.eval_mode == KV_EVAL_HASH) {
         int rc = kv::hash_eval(boards, rows, logits, values, st);
         if (rc || !leaf) return rc;
@@ -599,8 +712,10 @@ static int eng_eval(kv_engine* e, const int8_t* boards, int rows, bool leaf = fa
     }
     kv::net_set_res_events(net, e->ev[e->n_ev_used], e->ev[e->n_ev_used + 1]);
     e->n_ev_used += 2;
-    const int rc = leaf ? kv::net_forward_boards_legal_internal(net, boards, rows, e->tree.leaf_moves,
-                                                                e->tree.leaf_cnt, kv::MAXM, e->tree.leaf_logits,
+    const int rc = leaf ? kv::net_forward_boards_legal_internal(net, boards, rows,
+                                                                comp ? e->mc_moves : e->tree.leaf_moves,
+                                                                comp ? e->mc_cnt : e->tree.leaf_cnt, kv::MAXM,
+                                                                comp ? e->mc_logits : e->tree.leaf_logits,
                                                                 values, st)
                         : kv::net_forward_boards_internal(net, boards, rows, logits, values, st);
     kv::net_set_res_events(net, nullptr, nullptr);
@@ -615,7 +730,9 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
     const int S = e->cfg.slots;
     const bool mcts = e->dc.sims > 0;
     const int check_every = (S >= 64 && stop_after_games < 0 && !mcts) ? 4 : 1;
-    int rc = eng_counters(e);
+    int rc = eng_wait_copies(e);
+    if (rc) return rc;
+    rc = eng_counters(e);
     if (rc) return rc;
     long long done = 0;
     while ((max_steps < 0 || done < max_steps) && e->ctr_host->active > 0 &&
@@ -655,11 +772,33 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
             KV_HIP(hipGetLastError());
         } else {
             const kv::Tree& t = e->tree;
-            if ((rc = kv::mcts_root(e->dc, t, e->slots, e->moves, e->logits, e->values, e->probs, e->np_mt, e->st)))
+            // fewer active slots than slots (no game left to start): compact leaf batches of the active
+            // slots, padded to the network class of the full batch (> 16 boards: at least 17 rows)
+            const int act = e->ctr_host->active;
+            const bool comp = e->mc_slot_of != nullptr && act < S;
+            const int R = comp ? (S > 16 ? std::max(act, 17) : act) : S;
+            if (comp) {
+                hipLaunchKernelGGL(kv::k_compact_active, dim3(1), dim3(1024), 0, e->st, e->dc, e->slots, R,
+                                   e->mc_slot_of, e->mc_row_of);
+                KV_HIP(hipGetLastError());
+            }
+            if ((rc = kv::mcts_root(e->dc, t, e->slots, e->moves, e->logits, e->values, e->probs, e->np_mt, e->ctr, e->st)))
                 return rc;
             if ((rc = kv::mcts_select(e->dc, t, e->slots, e->boards, e->nn_boards, e->ctr, e->st, 0, S))) return rc;
             for (int k = 0; k < e->dc.sims; ++k) {
-                if ((rc = eng_eval(e, e->nn_boards, S, true))) return rc;
+                if (comp) {
+                    hipLaunchKernelGGL(kv::k_gather_leaves, dim3(R), dim3(64), 0, e->st, e->mc_slot_of, e->nn_boards,
+                                       t.leaf_moves, t.leaf_cnt, e->mc_boards, e->mc_moves, e->mc_cnt);
+                    KV_HIP(hipGetLastError());
+                    if ((rc = eng_eval(e, e->mc_boards, R, true, true))) return rc;
+                    hipLaunchKernelGGL(kv::k_scatter_leaves, dim3(R), dim3(64), 0, e->st, e->mc_slot_of,
+                                       e->mc_row_of, e->mc_logits, e->mc_values, e->mc_cnt, t.leaf_logits,
+                                       e->values);
+                    KV_HIP(hipGetLastError());
+                    e->mc_rows += R;
+                } else if ((rc = eng_eval(e, e->nn_boards, S, true))) {
+                    return rc;
+                }
                 rc = k + 1 < e->dc.sims
                          ? kv::mcts_backup_select(e->dc, t, e->slots, e->boards, e->logits, e->values, e->probs,
                                                   e->nn_boards, e->ctr, e->st, 0, S)
@@ -688,6 +827,8 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
 
 int kv_reset_records(kv_engine* e) {
     KV_REQUIRE(e, KV_EINVAL, "kv_reset_records: NULL");
+    const int rc = eng_wait_copies(e);
+    if (rc) return rc;
     KV_HIP(hipMemsetAsync(&e->ctr->rec_count, 0, sizeof(unsigned long long), e->st));
     KV_HIP(hipStreamSynchronize(e->st));
     return KV_OK;
@@ -723,9 +864,10 @@ int kv_records_device(kv_engine* e, kv_record* out_dev, size_t cap, size_t* n, v
     *n = cnt;
     if (!out_dev) return KV_OK;
     KV_REQUIRE(cap >= cnt, KV_EINVAL, "kv_records_device: buffer holds %zu, need %zu", cap, cnt);
-    // the engine stream is idle after eng_counters; the copy runs on the caller's stream
+    // the engine stream is idle after eng_counters; the copy runs on the caller's stream, and the
+    // engine's next write to e->rec waits for it (eng_wait_copies)
     KV_HIP(hipMemcpyAsync(out_dev, e->rec, cnt * sizeof(kv_record), hipMemcpyDeviceToDevice, (hipStream_t)stream));
-    return KV_OK;
+    return eng_note_copy(e, (hipStream_t)stream);
 }
 
 int kv_games(kv_engine* e, kv_game* out, size_t cap, size_t* n) {
@@ -798,23 +940,26 @@ int kv_root_visits_device(kv_engine* e, uint16_t* out_dev, size_t cap, size_t* n
     KV_REQUIRE(cap >= cnt, KV_EINVAL, "kv_root_visits_device: buffer holds %zu records, need %zu", cap, cnt);
     KV_HIP(hipMemcpyAsync(out_dev, e->tree.root_visits, cnt * kv::MAXM * sizeof(uint16_t), hipMemcpyDeviceToDevice,
                           (hipStream_t)stream));
-    return KV_OK;
+    return eng_note_copy(e, (hipStream_t)stream);
 }
 
 void kv_destroy(kv_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->cfg.device);
+    if (e->copy_pending) (void)hipEventSynchronize(e->copy_done);  // a caller-stream copy out of e->rec
     if (e->st) (void)hipStreamSynchronize(e->st);
     kv::Tree& t = e->tree;
     void* bufs[] = {e->slots, e->boards, e->moves, e->logits, e->values, e->last_probs, e->comp_boards, e->row_of,
                     e->np_mt, e->py_mt, e->rec, e->games, e->last_board, e->ctr,
                     t.e_move, t.e_P, t.e_N, t.e_W, t.e_child, t.node, t.path,
                     t.leaf_moves, e->ms, e->nn_boards, e->probs, e->sqrt_tab, t.root_visits, t.leaf_cnt,
-                    t.leaf_logits};
+                    t.leaf_logits, e->mc_slot_of, e->mc_row_of, e->mc_boards, e->mc_moves, e->mc_cnt,
+                    e->mc_logits, e->mc_values};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (e->ctr_host) (void)hipHostFree(e->ctr_host);
     for (auto x : e->ev) (void)hipEventDestroy(x);
+    if (e->copy_done) (void)hipEventDestroy(e->copy_done);
     if (e->net) kv_net_destroy(e->net);
     if (e->st) (void)hipStreamDestroy(e->st);
     delete e;

@@ -13,10 +13,17 @@
 // host by tests/test_libm_cpu.py (kv_host_libm through the C ABI) and on the
 // GPU by tests/test_engine_gpu.py (Dirichlet values identical to numpy).
 //
-// Domain: what legacy gamma with 0 < shape < 1 feeds them -- log(x) for
-// 0 < x < 2^1024 finite (the subnormal branch is not restated), pow(x, y) for
-// x in [0, 2^1024), y = 1/shape in (1, 2^63) finite; results that would be
-// subnormal or overflow are outside it (x^y < 2^-1022 needs x < 2^-306).
+// Domain: what legacy gamma with 0 < shape < 1 feeds them.
+//  * log(x): x in [2^-53, 1] -- 1 - res53 and (1 - U) / shape with
+//    U > 1 - shape, both >= 2^-53 -- and the tests' wider normal range; the
+//    subnormal / zero / negative input branch of e_log.c is never reached and
+//    is not restated.
+//  * pow(x, y): x = 0 or x in [2^-53, 2^1024) normal, y = 1/shape > 1 (shape a
+//    normal double, kv_create). Every result is restated, including the
+//    underflowing ones a small shape produces (U^(1/shape) < 2^-1022 once
+//    shape < 53/1022): exp_inline's specialcase() (scaled subnormal result with
+//    the double-rounding fix, and the scaled overflow side), the total
+//    underflow / overflow for |y log x| >= 1024, and pow's |y| >= 2^63 case.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -78,9 +85,40 @@ __host__ __device__ inline double glibc_log(double x) {
     return fma(r3, q, fma(r2, A[0], lo)) + hi;
 }
 
+// exp_inline's specialcase() (e_pow.c), for 512 <= |ehi| < 1024, where the
+// table scale 2^(k/N) has left the normal range. As the resolved __pow_fma
+// evaluates it (0x76b88..0x76cd9 and 0x76e08 in this image's libm): the
+// overflow side contracts scale + scale*tmp into one fma; the underflow side
+// keeps scale * tmp separately rounded and, for |y| < 1, re-rounds y to the
+// precision of the subnormal result before the final scaling (no double
+// rounding).
+__host__ __device__ inline double glibc_exp_specialcase(double tmp, uint64_t sbits, uint64_t ki) {
+    if ((ki & 0x80000000ull) == 0) {  // k > 0: the exponent of scale overflowed by <= 460
+        const double scale = libm_asdouble(sbits - (1009ull << 52));
+        return fma(scale, tmp, scale) * 0x1p1009;
+    }
+    sbits += 1022ull << 52;  // k < 0: scale 2^1022 too large, the result lands in the subnormal range
+    const double scale = libm_asdouble(sbits);
+    const double st = scale * tmp;
+    double y = scale + st;
+    if (fabs(y) < 1.0) {
+        const double one = y < 0.0 ? -1.0 : 1.0;
+        double lo = (scale - y) + st;
+        const double hi = y + one;
+        lo = ((one - hi) + y) + lo;
+        y = (lo + hi) - one;
+        if (y == 0.0) y = libm_asdouble(sbits & 0x8000000000000000ull);  // the sign of 0
+    }
+    return y * 0x1p-1022;
+}
+
 // pow (e_pow.c with __FP_FAST_FMA), glibc 2.35 __pow_fma: log_inline -> exp_inline
 __host__ __device__ inline double glibc_pow(double x, double y) {
     if (x == 0.0) return 0.0;  // y > 0 (the special-case path's result for +0)
+    // pow's special-y path (e_pow.c: |y| >= 2^63, y > 0 here): 1 at x == 1,
+    // else __math_oflow(0) = +inf for x > 1 and __math_uflow(0) = +0 for x < 1
+    if (((uint32_t)(libm_asuint64(y) >> 52) & 0x7ff) >= 0x43e)
+        return x == 1.0 ? 1.0 : (x > 1.0 ? libm_asdouble(0x7ff0000000000000ull) : 0.0);
     const double* P = kv_pow_log_hdr;  // ln2hi ln2lo A[0..6]
     const double* A = P + 2;
     const uint64_t ix = libm_asuint64(x);
@@ -111,7 +149,13 @@ __host__ __device__ inline double glibc_pow(double x, double y) {
     const double ehi = y * lhi;
     const double elo = fma(y, ltail, fma(lhi, y, -ehi));
     const uint32_t abstop = (uint32_t)(libm_asuint64(ehi) >> 52) & 0x7ff;
-    if (abstop < 0x3c9) return ehi + 1.0;  // |ehi| < 2^-54 (abstop - top12(0x1p-54) wraps)
+    bool special = false;
+    if (abstop - 0x3c9u >= 0x408u - 0x3c9u) {  // |ehi| < 2^-54 or |ehi| >= 512
+        if (abstop < 0x3c9) return ehi + 1.0;  // |ehi| < 2^-54 (abstop - top12(0x1p-54) wraps)
+        if (abstop > 0x408)                    // |ehi| >= 1024: __math_uflow(0) / __math_oflow(0)
+            return (libm_asuint64(ehi) >> 63) ? 0.0 : libm_asdouble(0x7ff0000000000000ull);
+        special = true;                        // 512 <= |ehi| < 1024: specialcase() below
+    }
     const double* E = kv_exp_hdr;  // invln2N shift negln2hiN negln2loN C2..C5
     const double kz = fma(ehi, E[0], E[1]);
     const uint64_t ki = libm_asuint64(kz);
@@ -126,6 +170,7 @@ __host__ __device__ inline double glibc_pow(double x, double y) {
     const double re2 = re * re;
     const double c45 = fma(re, E[7], E[6]);
     const double tmpv = fma(c45, re2 * re2, fma(c23, re2, tr));
+    if (special) return glibc_exp_specialcase(tmpv, sbits, ki);
     const double scale = libm_asdouble(sbits);
     return fma(tmpv, scale, scale);
 }

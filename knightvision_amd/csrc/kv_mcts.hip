@@ -58,7 +58,7 @@ __device__ inline float puct(float c_puct, float P, float sq, int N, float W) {
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_mcts_root(DevCfg cfg, Tree t, Slot* slots, const uint16_t* moves,
                                                    const float* logits, const float* values, float* probs,
-                                                   uint32_t* np_mt) {
+                                                   uint32_t* np_mt, Ctr* ctr) {
     __shared__ uint32_t mt3[MT_RW];
     __shared__ double gam[4096];
     __shared__ double vals[MAXM];
@@ -80,6 +80,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     }
     __syncthreads();
     const double total = s_total;
+    if (!isfinite(total)) {  // all-zero gamma draws: NaN weights (k_sample's error 8)
+        if (lane == 0) atomicOr(&ctr->error, 8);
+        return;
+    }
     const size_t eb = (size_t)i * t.ecap, nb = (size_t)i * t.ncap;
     for (int j = lane; j < n; j += 256) {
         t.e_move[eb + j] = ml[j];
@@ -354,9 +358,9 @@ int hash_legal(const Tree& t, int rows, hipStream_t st) {
 }
 
 int mcts_root(const DevCfg& cfg, const Tree& t, Slot* slots, const uint16_t* moves, const float* logits,
-              const float* values, float* probs, uint32_t* np_mt, hipStream_t st) {
+              const float* values, float* probs, uint32_t* np_mt, Ctr* ctr, hipStream_t st) {
     hipLaunchKernelGGL(k_mcts_root, dim3(cfg.slots), dim3(256), 0, st, cfg, t, slots, moves, logits, values, probs,
-                       np_mt);
+                       np_mt, ctr);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }

@@ -580,7 +580,7 @@ __global__ __launch_bounds__(64) void policy_legal_kernel(const float* __restric
                                                           float* __restrict__ out) {
     __shared__ float a[128];
     const int b = blockIdx.x, lane = threadIdx.x;
-    const int n = nmoves[b];
+    const int n = min(nmoves[b], maxm);  // a row holds maxm moves (kv.h); never read / write past it
     if (n <= 0) return;
     a[lane] = pfeat[(size_t)b * 128 + lane];
     a[lane + 64] = pfeat[(size_t)b * 128 + 64 + lane];

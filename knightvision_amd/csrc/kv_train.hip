@@ -762,6 +762,21 @@ __global__ void planes_to_nhwc_kernel(const float* __restrict__ planes, int n, i
 
 using namespace kv::tr;
 
+// The large-LDS opt-in of a kernel is per device: done once per (kernel, device)
+// and recorded in a per-kernel bitset of devices (atomic, so concurrent host
+// threads at worst set the attribute twice, which is harmless).
+#include <atomic>
+static std::atomic<unsigned long long> g_lds_opted[2];
+static hipError_t lds_opt_in(const void* fn, int bytes, int which) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (g_lds_opted[which].load(std::memory_order_acquire) & bit) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) g_lds_opted[which].fetch_or(bit, std::memory_order_acq_rel);
+    return e;
+}
 
 extern "C" {
 
@@ -775,11 +790,7 @@ int kv_tr_conv3x3_add_f16(const void* x_dev, int n, int ci, const void* w_dev, c
     KV_REQUIRE(x_dev && w_dev && y_dev && n > 0 && add_dev != y_dev, KV_EINVAL, "kv_tr_conv3x3_f16: bad arguments");
     KV_REQUIRE(ci > 0 && ci % cv::CK == 0 && co > 0 && co % cv::WCO == 0, KV_EINVAL,
                "kv_tr_conv3x3_f16: ci %d must be a multiple of %d, co %d of %d", ci, cv::CK, co, cv::WCO);
-    static bool attr = false;
-    if (!attr) {
-        KV_HIP(hipFuncSetAttribute((const void*)conv3x3_f16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, cv::LDS));
-        attr = true;
-    }
+    KV_HIP(lds_opt_in((const void*)conv3x3_f16_kernel, cv::LDS, 0));
     const int cblocks = co / cv::WCO, nblocks = (n + cv::NB - 1) / cv::NB;
     KV_REQUIRE(8 % cblocks == 0, KV_EINVAL, "kv_tr_conv3x3_f16: co %d: at most 1024 output channels, a power of two "
                "number of 128-channel blocks", co);
@@ -826,12 +837,7 @@ int kv_tr_conv3x3_wgrad_f16(const void* dy_dev, const void* x_dev, int n, int ci
     int splits = 0;
     const size_t need = kv_tr_wgrad_workspace(n, ci, co, &splits);
     KV_REQUIRE(ws_bytes >= need, KV_EINVAL, "kv_tr_conv3x3_wgrad_f16: workspace %zu < %zu B", ws_bytes, need);
-    static bool attr = false;
-    if (!attr) {
-        KV_HIP(hipFuncSetAttribute((const void*)conv3x3_wgrad_f16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   wg::LDS));
-        attr = true;
-    }
+    KV_HIP(lds_opt_in((const void*)conv3x3_wgrad_f16_kernel, wg::LDS, 1));
     const int tiles = (co / wg::TC) * (ci / wg::TC);
     int grid;
     if (splits >= 8) {

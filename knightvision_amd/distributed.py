@@ -39,13 +39,15 @@ def comm_device(t: torch.Tensor | None = None) -> torch.device:
     return torch.device("cpu")
 
 
-def gather_rows(t: torch.Tensor, dst: int | None = 0):
+def gather_rows(t: torch.Tensor, dst: int | None = 0, force_collective: bool = False):
     """Concatenation over ranks (rank order) of a tensor whose first dimension
     differs per rank: per-rank row counts are all-gathered (int64), then the
     rows padded to the largest count are gathered to `dst` (None: to every
-    rank). Returns the concatenation on `dst` / every rank, None elsewhere."""
+    rank). Returns the concatenation on `dst` / every rank, None elsewhere.
+    A world of one returns `t` itself unless force_collective (tests: the
+    collectives then run on a one-rank group, e.g. RCCL on one GPU)."""
     rank, world = rank_world()
-    if world == 1:
+    if world == 1 and not (force_collective and dist.is_initialized()):
         return t
     dev = comm_device(t)
     src = t.to(dev)
@@ -89,19 +91,60 @@ def _as_rows(x, dtype) -> torch.Tensor:
     return torch.from_numpy(np.ascontiguousarray(x).view(np.uint8).reshape(-1, dtype.itemsize))
 
 
-def gather_experience(records, games, dst: int | None = 0, pi=None):
+def pack_pi(pi_rows: torch.Tensor):
+    """Root visit counts as they cross xGMI: uint8 [n, 2 * MAXM] rows (uint16 per
+    move slot, 0xffff past the position's move list -- kv_root_visits_device)
+    -> (counts int16 [n], packed int16 [sum counts]): each row's legal-move
+    prefix only, rows concatenated in order. 2 B per legal move + 2 B per record
+    instead of 640 B per record (MAXM 320, ~23 legal moves on average)."""
+    if pi_rows.shape[0] == 0:
+        z = torch.zeros(0, dtype=torch.int16, device=pi_rows.device)
+        return z, z.clone()
+    v = pi_rows.contiguous().view(torch.int16)  # 2-D rows of bytes -> int16 per move slot
+    valid = v != -1
+    counts = valid.sum(1, dtype=torch.int32)
+    return counts.to(torch.int16), v[valid]
+
+
+def unpack_pi(counts: torch.Tensor, packed: torch.Tensor, maxm: int) -> torch.Tensor:
+    """pack_pi's inverse: int16 [n, maxm] rows, -1 (0xffff) past each row's count."""
+    n = int(counts.shape[0])
+    out = torch.full((n, maxm), -1, dtype=torch.int16, device=packed.device)
+    if n == 0 or packed.numel() == 0:
+        return out
+    c = counts.to(device=packed.device, dtype=torch.int64)
+    row = torch.repeat_interleave(torch.arange(n, device=packed.device), c)
+    start = torch.cumsum(c, 0) - c
+    col = torch.arange(packed.numel(), device=packed.device) - start[row]
+    out[row, col] = packed
+    return out
+
+
+def gather_experience(records, games, dst: int | None = 0, pi=None, force_collective: bool = False):
     """End-of-iteration gather of every rank's (records, games), ordered by
     (game_id, ply) / game_id. `records` is a numpy RECORD_DTYPE array or the
     engine's device tensor (SelfPlayEngine.records_device(), uint8 [n, 80]);
     `games` a GAME_DTYPE array. MCTS runs also pass `pi`, the root visit counts
     row for row with `records` (SelfPlayEngine.root_visits_device(), uint8
     [n, 2 * MAXM]): the (s, pi, z) triple of BASELINE config C4 (s = board,
-    z = the game's reward) then crosses xGMI in the same gather. Returns numpy
-    arrays on `dst` (every rank when dst is None) and Nones elsewhere:
-    (records, games), or (records, games, pi uint16 [n, MAXM]) when pi is given."""
-    r = gather_rows(_as_rows(records, RECORD_DTYPE), dst)
-    g = gather_rows(_as_rows(games, GAME_DTYPE), dst)
-    p = gather_rows(pi, dst) if pi is not None else None
+    z = the game's reward) then crosses xGMI in the same gather, as each
+    record's legal-move prefix (pack_pi: 2 B per legal move + a 2-B count) and
+    is re-padded on the receiver. Returns numpy arrays on `dst` (every rank
+    when dst is None) and Nones elsewhere: (records, games), or (records,
+    games, pi uint16 [n, MAXM]) when pi is given."""
+    fc = force_collective
+    r = gather_rows(_as_rows(records, RECORD_DTYPE), dst, fc)
+    g = gather_rows(_as_rows(games, GAME_DTYPE), dst, fc)
+    p = None
+    if pi is not None:
+        maxm = pi.shape[-1] // 2
+        counts, packed = pack_pi(pi)
+        # int16 travels as byte pairs (gloo has no int16 collectives; RCCL moves the same bytes)
+        c_all = gather_rows(counts.view(torch.uint8).reshape(-1, 2), dst, fc)
+        k_all = gather_rows(packed.view(torch.uint8).reshape(-1, 2), dst, fc)
+        if c_all is not None:
+            p = unpack_pi(c_all.contiguous().view(torch.int16).reshape(-1),
+                          k_all.contiguous().view(torch.int16).reshape(-1), maxm)
     if r is None:
         return (None, None) if pi is None else (None, None, None)
     order = record_order(r) if r.shape[0] else None
@@ -113,6 +156,12 @@ def gather_experience(records, games, dst: int | None = 0, pi=None):
         return recs, gms
     p = (p[order] if order is not None else p).cpu().numpy()
     return recs, gms, np.ascontiguousarray(p).view(np.uint16).reshape(p.shape[0], -1)
+
+
+def pi_wire_bytes(pi) -> int:
+    """Bytes the compact (s, pi, z) gather moves for these root visit rows (pack_pi)."""
+    counts, packed = pack_pi(pi)
+    return 2 * int(counts.numel()) + 2 * int(packed.numel())
 
 
 def shard_ids(n_games: int, rank: int, world: int):

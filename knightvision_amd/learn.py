@@ -45,6 +45,8 @@ LEARN_BATCH_SIZE = int(os.getenv("BATCH_SIZE", "2048"))
 LEARN_LR = float(os.getenv("LR", "1e-3"))
 PATIENCE = int(os.getenv("PATIENCE", "5"))
 LR_GAMMA = float(os.getenv("LR_GAMMA", "0.1"))
+LR_STEP_SIZE = int(os.getenv("LR_STEP_SIZE", "10"))  # train.py:463
+COSINE_T0 = int(os.getenv("COSINE_T0", "10"))        # train.py:295
 VAL_FRAC = 0.1
 
 
@@ -143,20 +145,26 @@ def evaluate_sharded(model, data, idx, batch_size: int, dev) -> float:
 def train_with_validation(ddp, model, optimizer, data, epochs: int, batch_size: int, accumulate_steps: int,
                           gen: torch.Generator, split_gen: torch.Generator, dev) -> dict:
     """train.py train_with_validation (:293-420) as the learn loop calls it (TRAIN_EPOCHS = 2 <
-    NUM_PGN_EPOCHS, so no self-play inside it): a fresh GradScaler and ReduceLROnPlateau(mode='min',
-    factor=LR_GAMMA, patience=PATIENCE) per call; per epoch one pass of _train_one_epoch over the train
-    split, then evaluate() on the validation split, the plateau step on the validation loss, and early
-    stopping after PATIENCE epochs without improvement. Checkpoints, TensorBoard and Telegram are not
-    reproduced."""
+    NUM_PGN_EPOCHS, so no self-play inside it). Per call, as the reference: a fresh GradScaler and the
+    three LR schedulers in its order -- CosineAnnealingWarmRestarts(T_0=COSINE_T0, T_mult=1) (:293-297;
+    constructing it resets the LR to the optimizer's initial LR, so the cosine schedule restarts every
+    iteration), ReduceLROnPlateau(mode='min', factor=LR_GAMMA, patience=PATIENCE) (:298-304) and
+    StepLR(LR_STEP_SIZE, LR_GAMMA) (:306-307). Per epoch one pass of _train_one_epoch over the train
+    split, evaluate() on the validation split and the plateau step on its loss (_run_validation
+    :198-218), early stopping after PATIENCE epochs without improvement (before the other two
+    schedulers step), then cos.step(epoch + 1) and step.step() (:421-423). Checkpoints, TensorBoard
+    and Telegram are not reproduced."""
+    import warnings
     dist, rank, world = _dist()
     tr, va = split_train_val(int(data[0].shape[0]), split_gen)
     mine = tr[rank::world].to(dev)
     n_max = _max_over_ranks(int(mine.numel()), dev)
     scaler = T.make_scaler(dev)
-    plateau = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, mode="min", factor=LR_GAMMA, patience=PATIENCE)
+    cos, plateau, step = make_lr_schedulers(optimizer)
     best, no_improve, ep, val_loss, done = math.inf, 0, None, math.inf, 0
     shard = tuple(x[mine] for x in data)
-    for _ in range(epochs):
+    lrs = []
+    for epoch in range(epochs):
         ep = T.train_one_epoch(ddp, T.batches(*shard, rank_batch_size(batch_size, world), True, gen, total=n_max),
                                optimizer, scaler, accumulate_steps=accumulate_steps)
         val_loss = evaluate_sharded(model, data, va, batch_size, dev)
@@ -168,8 +176,21 @@ def train_with_validation(ddp, model, optimizer, data, epochs: int, batch_size: 
             no_improve += 1
             if no_improve >= PATIENCE:
                 break
+        with warnings.catch_warnings():  # the reference passes the epoch to step() (deprecated form)
+            warnings.simplefilter("ignore")
+            cos.step(epoch + 1)
+        step.step()
+        lrs.append(optimizer.param_groups[0]["lr"])
     return {"ep": ep, "val_loss": val_loss, "epochs_run": done, "train_split": int(tr.numel()),
-            "val_split": int(va.numel()), "lr": optimizer.param_groups[0]["lr"]}
+            "val_split": int(va.numel()), "lr": optimizer.param_groups[0]["lr"], "lr_per_epoch": lrs}
+
+
+def make_lr_schedulers(optimizer):
+    """The three schedulers train_with_validation builds per call (train.py:293-307), in its order."""
+    cos = torch.optim.lr_scheduler.CosineAnnealingWarmRestarts(optimizer, T_0=COSINE_T0, T_mult=1)
+    plateau = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, mode="min", factor=LR_GAMMA, patience=PATIENCE)
+    step = torch.optim.lr_scheduler.StepLR(optimizer, step_size=LR_STEP_SIZE, gamma=LR_GAMMA)
+    return cos, plateau, step
 
 
 def reinforcement_loop(model, iterations: int, games_per_iter: int, device, *, epochs: int = TRAIN_EPOCHS,

@@ -86,3 +86,26 @@ def test_gather_experience(world, n_games):
         assert ids == want_ids and ply == want_ply
         assert move == [g * 100 + p for g in range(n_games) for p in range(3 + g)]
         assert gids == list(range(n_games))
+
+
+def test_pi_travels_as_legal_move_prefixes():
+    """VERDICT r2 #3c: the root visit counts cross the interconnect as each record's legal-move prefix
+    (2 B per legal move + a 2-B count) and are re-padded to the kv_root_visits_device form on the receiver."""
+    import torch
+    from knightvision_amd import _lib
+    from knightvision_amd.distributed import pack_pi, pi_wire_bytes, unpack_pi
+    rng = np.random.default_rng(3)
+    n = 500
+    cnt = rng.integers(0, 60, n)
+    cnt[:3] = [0, _lib.MAXM, 1]  # no legal move, a full list, a single move
+    pi = np.full((n, _lib.MAXM), 0xffff, dtype=np.uint16)
+    for i, c in enumerate(cnt):
+        pi[i, :c] = rng.integers(0, 801, c)
+    rows = torch.from_numpy(pi.view(np.uint8).reshape(n, 2 * _lib.MAXM).copy())
+    counts, packed = pack_pi(rows)
+    assert counts.tolist() == cnt.tolist() and packed.numel() == cnt.sum()
+    back = unpack_pi(counts, packed, _lib.MAXM).numpy().view(np.uint16)
+    assert np.array_equal(back, pi)
+    assert pi_wire_bytes(rows) == 2 * n + 2 * int(cnt.sum()) < pi.nbytes / 10
+    empty = unpack_pi(*pack_pi(rows[:0]), _lib.MAXM)
+    assert empty.shape == (0, _lib.MAXM)

@@ -79,6 +79,48 @@ def test_pow_bit_identical_to_libm(seed):
     assert bad.size == 0, f"{bad.size}/{xs.size} differ, e.g. x={xs[bad[:3]]} y={ys[bad[:3]]}"
 
 
+@pytest.mark.parametrize("alpha", [0.05, 0.03, 0.01, 0.003, 0.001])
+def test_pow_underflow_bit_identical_to_libm(alpha):
+    """Small DIR_NOISE_ALPHA (scripts/self_play.py:13): U^(1/alpha) with U down
+    to 2^-53 falls below 2^-1022 (alpha < 53/1022) -- glibc pow's specialcase
+    (scaled subnormal result, the re-rounding for |y| < 1, total underflow for
+    y log x <= -1024) -- and the second branch's (1 - alpha + alpha Y)^(1/alpha)
+    reaches large finite results (the overflow-side specialcase)."""
+    rng = np.random.default_rng(int(alpha * 1e6))
+    u = _res53(rng, 100_000)
+    inv = 1.0 / alpha
+    # first branch U <= 1 - alpha, log-uniform down to 2^-53 so that every
+    # result range (normal, specialcase subnormal, total underflow) is hit
+    lu = np.exp2(rng.uniform(-53, 0, 100_000)) * (1 - alpha)
+    # edges of the subnormal range: x with x^(1/alpha) near 2^-1022 and 2^-1074
+    edge = np.concatenate([2.0 ** (e * alpha) * (1 + rng.uniform(-1e-3, 1e-3, 5_000)) for e in (-1022, -1050, -1074, -1075)])
+    y2 = -np.log((1.0 - (1 - alpha + alpha * u)) / alpha)
+    xs = np.concatenate([u * (1 - alpha), lu, edge, 1 - alpha + alpha * y2,
+                         np.array([2.0 ** -53, 0.0, 1.0 - alpha, np.nextafter(1.0, 0)])])
+    xs = xs[(xs >= 0) & (xs < 2.0 ** 1000)]
+    ys = np.full(xs.size, inv)
+    want = np.array([libm.pow(float(x), float(y)) for x, y in zip(xs, ys)])
+    got = _host(1, xs, ys)
+    bad = _mismatch(got, want)
+    n_sub = int(np.count_nonzero((want > 0) & (want < 2.2250738585072014e-308)))
+    assert n_sub > 100, "the subnormal range was not exercised"
+    assert bad.size == 0, f"{bad.size}/{xs.size} differ, e.g. x={xs[bad[:3]]} got {got[bad[:3]]} want {want[bad[:3]]}"
+
+
+def test_pow_large_y_and_overflow_side_bit_identical_to_libm():
+    """pow's |y| >= 2^63 path and exp_inline's k > 0 specialcase (results in
+    [2^738, 2^1024)) and total overflow, for positive x and y."""
+    rng = np.random.default_rng(7)
+    xs = np.concatenate([1 + rng.uniform(0, 1, 20_000), rng.uniform(0, 1, 2_000), np.array([1.0, 0.5, 2.0, 0.0])])
+    ys = np.concatenate([rng.uniform(738, 1500, 20_000) / np.log2(xs[:20_000]),
+                         np.full(2_000, 2.0 ** 63), np.array([2.0 ** 63, 2.0 ** 64, 2.0 ** 64, 2.0 ** 70])])
+    want = np.array([libm.pow(float(x), float(y)) for x, y in zip(xs, ys)])
+    got = _host(1, xs, ys)
+    bad = _mismatch(got, want)
+    assert np.isinf(want).sum() > 100 and ((want > 2.0 ** 738) & np.isfinite(want)).sum() > 100
+    assert bad.size == 0, f"{bad.size}/{xs.size} differ, e.g. x={xs[bad[:3]]} y={ys[bad[:3]]}"
+
+
 def test_numpy_dirichlet_uses_this_libm():
     """The pin above is against the libm numpy's legacy gamma links: replay
     RandomState(42).dirichlet([0.3]*64) with libm log/pow in Python and

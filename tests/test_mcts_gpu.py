@@ -144,3 +144,31 @@ def test_mcts_tree_overflow_is_an_error():
         O.mcts_play_game(64, O.MT(42, "numpy"), O.MT(42, "python"), None, max_moves=4, edge_cap=cap)
     with pytest.raises(_lib.KVError, match="tree_edge_cap"):
         SelfPlayEngine(synthetic_state_dict(42, "init"), slots=1, n_games=1, sims=8, tree_edge_cap=100)
+
+
+def test_mcts_compact_tail_batches_identical_to_oracle():
+    """Games that end at different plies (mates / draws before max_moves) leave fewer active slots than
+    slots; their leaf batches then carry the active slots only (k_compact_active, padded to the > 16-board
+    class). Full games of the first 4 slots -- the tails included -- equal the oracle's PUCT restatement
+    root vector for root vector."""
+    slots, sims, mm = 20, 16, 120
+    from oracle import oracle as O
+    sd = synthetic_state_dict(42, "peaked")
+    with SelfPlayEngine(sd, slots=slots, n_games=slots, seed=42, max_moves=mm, sims=sims, c_puct=1.5,
+                        keep_root_visits=True) as eng:
+        eng.run()
+        recs, visits, games = eng.records(), eng.root_visits(), eng.games()
+    ends = np.sort(games["plies"])
+    print("game lengths:", ends.tolist())
+    assert ends[0] < ends[-1], "every game ended on the same ply: no compact tail was exercised"
+    ev, net = _hip_eval(sd)
+    compared = 0
+    for g in range(4):
+        sel = recs["game_id"] == g
+        r = O.mcts_play_game(sims, O.MT(42 + g, "numpy"), O.MT(42 + g, "python"), ev, max_moves=mm, c_puct=1.5)
+        assert np.array_equal(recs["move"][sel], r["moves"]), f"game {g}: moves differ"
+        for p in range(len(r["moves"])):
+            assert np.array_equal(visits[sel][p], r["visits"][p]), (g, p)
+            compared += 1
+    net.close()
+    print(f"compact-tail MCTS parity: {compared} root vectors identical")

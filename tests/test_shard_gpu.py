@@ -119,3 +119,44 @@ def test_gather_of_mcts_shards_with_pi_to_root():
     want_p = np.where(whole_p < 0, 0xffff, whole_p).astype(np.uint16)
     assert np.array_equal(got_p, want_p)
     assert (got_p[:, 0] != 0xffff).all() and (np.where(got_p == 0xffff, 0, got_p).sum(axis=1) == 16).all()
+
+
+def _rccl_world1(port, q):
+    """One rank on RCCL ('nccl' backend = RCCL on ROCm) with the collectives forced: the all_gather of the
+    per-rank counts and the gather / all_gather of device-resident records and pi run through RCCL on
+    device tensors -- the code path of the driver's 8-GPU run, on the one GPU this box has."""
+    import torch
+    import torch.distributed as dist
+    from knightvision_amd.distributed import comm_device, gather_experience
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl" and comm_device().type == "cuda"
+    with SelfPlayEngine(SD, slots=20, n_games=20, seed=42, max_moves=4, sims=16, keep_root_visits=True) as eng:
+        eng.run()
+        host_r, host_g, host_p = eng.records(), eng.games(), eng.root_visits()
+        dev_r, dev_p = eng.records_device(), eng.root_visits_device()
+        assert dev_r.is_cuda and dev_p.is_cuda
+        out = []
+        for dst in (0, None):
+            r, g, p = gather_experience(dev_r, host_g, dst=dst, pi=dev_p, force_collective=True)
+            out.append((r.tobytes(), g.tobytes(), p.tobytes()))
+    want_p = np.where(host_p < 0, 0xffff, host_p).astype(np.uint16)
+    q.put((out, host_r.tobytes(), host_g.tobytes(), want_p.tobytes()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rccl_gather_path_world1():
+    """VERDICT r2 #3a: the experience gather over RCCL on device tensors (the all_gather of counts and the
+    gather / all_gather of packed records and legal-move pi), forced through the collectives at world
+    size 1, equals the engine's own host-side records and visit counts."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_world1, args=(_free_port(), q))
+    p.start()
+    out, hr, hg, hp = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    for rb, gb, pb in out:
+        assert rb == hr and gb == hg and pb == hp

@@ -383,3 +383,47 @@ def test_validation_split_and_sharded_evaluate_world2():
     va = torch.tensor(va0)
     want = T.evaluate(m, list(T.batches(*(x[va] for x in data), 8, False)))
     assert abs(l0 - want) < 1e-5 * abs(want) and l0 == l1
+
+
+def test_train_with_validation_steps_the_reference_lr_schedulers():
+    """train.py train_with_validation builds CosineAnnealingWarmRestarts(T_0=10), ReduceLROnPlateau
+    and StepLR(10, 0.1) per call (:293-307) and steps the cosine schedule with epoch + 1, then StepLR, after
+    each epoch's validation (:421-423); a second call restarts the cosine schedule from the initial LR. With
+    lr 1e-3 the LR after epochs 1, 2, 3 is 1e-3 (1 + cos(k pi / 10)) / 2."""
+    import math
+    from knightvision_amd import learn as L
+    torch.manual_seed(5)
+    m = TinyNet()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    data = _data(40, 11)
+    want = [1e-3 * (1 + math.cos(k * math.pi / L.COSINE_T0)) / 2 for k in (1, 2, 3)]
+    for call in range(2):
+        tv = L.train_with_validation(m, m, opt, data, 3, 8, 2, torch.Generator().manual_seed(call),
+                                     torch.Generator().manual_seed(0), torch.device("cpu"))
+        assert tv["epochs_run"] == 3
+        assert np.allclose(tv["lr_per_epoch"], want, rtol=1e-12, atol=0), (call, tv["lr_per_epoch"])
+
+
+def test_lr_schedulers_match_the_reference_over_a_step_boundary():
+    """Epochs 1..12 of one call: the cosine restart at T_0 and StepLR's x gamma at epoch 10 compose in the
+    reference's order (cos.step(epoch + 1) then step.step()); the plateau scheduler is fed a falling loss."""
+    from knightvision_amd import learn as L
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.Adam([p], lr=1e-3)
+    cos, plateau, step = L.make_lr_schedulers(opt)
+    # the same schedulers, built directly as train.py:293-307 builds them
+    p2 = torch.nn.Parameter(torch.zeros(1))
+    opt2 = torch.optim.Adam([p2], lr=1e-3)
+    c2 = torch.optim.lr_scheduler.CosineAnnealingWarmRestarts(opt2, T_0=10, T_mult=1)
+    r2 = torch.optim.lr_scheduler.ReduceLROnPlateau(opt2, mode="min", factor=0.1, patience=5)
+    s2 = torch.optim.lr_scheduler.StepLR(opt2, step_size=10, gamma=0.1)
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for epoch in range(12):
+            for o, (c, r, s) in ((opt, (cos, plateau, step)), (opt2, (c2, r2, s2))):
+                r.step(1.0 / (epoch + 1))
+                c.step(epoch + 1)
+                s.step()
+            assert opt.param_groups[0]["lr"] == opt2.param_groups[0]["lr"], epoch
+    assert opt.param_groups[0]["lr"] != 1e-3

@@ -7,10 +7,14 @@ games of a big one). The C3 bench times 20 moves of games that started
 together, so its own games/hour is a transient count; this gives the game
 lengths the steady-state figure needs.
 
-    python tools/mcts_game_length.py [--games 64] [--seconds 420]
+    python tools/mcts_game_length.py [--games 384] [--seconds 1000] [--out profiles/r03_mcts_game_length_c3.json]
 
-Prints a progress line per 20 plies and one JSON line: per-game plies, end
-reasons, games still running at the time limit (censored).
+Prints a progress line per 20 plies and one JSON line (also written to --out):
+per-game plies, end reasons, the mean with its standard error and 95 %
+interval, games still running at the time limit (censored; none when the run
+completes). bench.py reads the newest such file for its steady-state MCTS
+games/hour. Once games start to end, the engine's leaf batches carry only the
+active slots (k_compact_active), so the tail of long games is cheap.
 """
 import argparse
 import json
@@ -25,9 +29,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--games", type=int, default=64)
+    ap.add_argument("--games", type=int, default=384)
     ap.add_argument("--sims", type=int, default=800)
-    ap.add_argument("--seconds", type=float, default=420.0)
+    ap.add_argument("--seconds", type=float, default=1000.0)
+    ap.add_argument("--out", default=None)
     a = ap.parse_args()
     import torch  # noqa: F401
     from knightvision_amd.engine import REASONS, SelfPlayEngine
@@ -48,13 +53,24 @@ def main():
         st = eng.stats()
     plies = np.sort(games["plies"]).tolist()
     reasons = {REASONS.get(int(r), "?"): int((games["reason"] == r).sum()) for r in np.unique(games["reason"])}
-    print(json.dumps({"what": "complete MCTS games at the C3 settings (game ids 0..n-1 of the C3 run)",
-                      "sims": a.sims, "games": a.games, "finished": len(plies),
-                      "still_running": a.games - len(plies), "plies_played_by_running_games": ply,
-                      "mean_plies_finished": float(np.mean(plies)) if plies else None,
-                      "median_plies_finished": float(np.median(plies)) if plies else None,
-                      "plies": plies, "reasons": reasons, "wall_s": time.perf_counter() - t0,
-                      "total_sims": int(st["sims"])}), flush=True)
+    n = len(plies)
+    mean = float(np.mean(plies)) if plies else None
+    sd = float(np.std(plies, ddof=1)) if n > 1 else None
+    se = sd / np.sqrt(n) if sd is not None else None
+    res = {"what": "complete MCTS games at the C3 settings (game ids 0..n-1 of the C3 run: 800 sims/move, "
+                   "uncapped, per-game seeds 42+id, random-init weights seed 42, c_puct 1.5)",
+           "sims": a.sims, "games": a.games, "finished": n, "still_running": a.games - n,
+           "plies_played_by_running_games": ply if n < a.games else None,
+           "mean_plies_finished": mean, "median_plies_finished": float(np.median(plies)) if plies else None,
+           "sd_plies": sd, "se_mean_plies": se, "se_frac": (se / mean) if se else None,
+           "ci95_mean_plies": [mean - 1.96 * se, mean + 1.96 * se] if se else None,
+           "plies": plies, "reasons": reasons, "wall_s": time.perf_counter() - t0,
+           "total_sims": int(st["sims"])}
+    line = json.dumps(res)
+    print(line, flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(line + "\n")
 
 
 if __name__ == "__main__":
