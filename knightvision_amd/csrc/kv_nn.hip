@@ -1128,12 +1128,28 @@ static int wino48_gemm_layer(kv_net* net, int l, const float* V, float* M, int r
     return launch_wino48_gemm<K>(V, net->U48 + o, M, rows, stride, st);
 }
 
+// KV_DEBUG_SKIP_TRANSFORMS=1: the F(4x8) tower's output/input transform launches are skipped (timing
+// probe only: the GEMM-only forward bounds what fusing the transforms away could gain; outputs invalid)
+static bool debug_skip_transforms() {
+    static const int v = [] {
+        const char* e = getenv("KV_DEBUG_SKIP_TRANSFORMS");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    return v != 0;
+}
+
 // conv2 + the 5 residual blocks for boards [0, nb), F(4x8)
 static int wino48_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     const int rows = nb * 2, stride = rows;
     float* V = net->V;
     float* M = net->Mw;
     int rc;
+    if (debug_skip_transforms()) {
+        if ((rc = wino48_gemm_layer<256>(net, 1, net->V256, M, rows, stride, st))) return rc;
+        for (int l = 2; l < 12; ++l)
+            if ((rc = wino48_gemm_layer<512>(net, l, V, M, rows, stride, st))) return rc;
+        return KV_OK;
+    }
     if ((rc = wino48_gemm_layer<256>(net, 1, net->V256, M, rows, stride, st))) return rc;
     if ((rc = launch_wino48_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st))) return rc;
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));

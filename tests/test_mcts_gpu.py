@@ -151,7 +151,7 @@ def test_mcts_compact_tail_batches_identical_to_oracle():
     slots; their leaf batches then carry the active slots only (k_compact_active, padded to the > 16-board
     class). Full games of the first 4 slots -- the tails included -- equal the oracle's PUCT restatement
     root vector for root vector."""
-    slots, sims, mm = 20, 16, 120
+    slots, sims, mm = 17, 16, 120  # 17: once a game ends the batch is padded (16 active + 1)
     from oracle import oracle as O
     sd = synthetic_state_dict(42, "peaked")
     with SelfPlayEngine(sd, slots=slots, n_games=slots, seed=42, max_moves=mm, sims=sims, c_puct=1.5,

@@ -18,8 +18,9 @@ ranks 1-2), each against a CPU restatement of the reference.
   whose gradient is not negligible (|g| > 1e-3 max |g| of the tensor) the
   other way (237 of 24.7 M measured). Under autocast (the reference's
   torch.cuda.amp.autocast: fp16 convolutions) the same logic runs on fp16
-  arithmetic: losses within 5e-3, gradients within 0.2 (0.11 measured), at
-  most 5 % of the steps reversed (2.3 % measured). Conv biases ahead of a
+  arithmetic: losses within 5e-3, gradients within 0.15 (0.11 measured), at
+  most 3.5 % of the steps reversed (2.3 % measured); every tensor's gradient
+  error is printed. Conv biases ahead of a
   BatchNorm have an exact gradient of 0 and are skipped."""
 import os
 
@@ -82,7 +83,9 @@ def _batches(golden_dir, n_batches=4, bs=16):
             for i in range(0, n_batches * bs, bs)]
 
 
-@pytest.mark.parametrize("amp,loss_rtol,grad_tol,flip_frac", [(False, 1e-4, 1e-2, 1e-3), (True, 5e-3, 0.2, 5e-2)])
+# autocast bounds: 0.11 gradient error and 2.3 % reversed steps measured (deterministic kernels, fixed
+# batches), bounds at ~1.4x / 1.5x of that for a different MIOpen / hipBLASLt solver choice on another box
+@pytest.mark.parametrize("amp,loss_rtol,grad_tol,flip_frac", [(False, 1e-4, 1e-2, 1e-3), (True, 5e-3, 0.15, 3.5e-2)])
 def test_update_step_matches_float64_restatement(golden_dir, amp, loss_rtol, grad_tol, flip_frac):
     from knightvision_amd.model import ChessNet
     from oracle import torch_ref
@@ -126,8 +129,9 @@ def test_update_step_matches_float64_restatement(golden_dir, amp, loss_rtol, gra
             rel[k] = float((g - r).norm() / r.norm())
     rel = {k: v for k, v in rel.items() if not k.endswith(".bias") or "fc" in k}  # conv biases: exact gradient 0
     worst_g = max(rel.values())
-    print(f"gradients (amp={amp}): worst per-tensor relative error {worst_g:.2e}; "
-          + ", ".join(f"{k} {v:.1e}" for k, v in sorted(rel.items(), key=lambda kv: -kv[1])[:6]))
+    print(f"gradients (amp={amp}): worst per-tensor relative error {worst_g:.2e} (bound {grad_tol}); per tensor:")
+    for k, v in sorted(rel.items(), key=lambda kv: -kv[1]):
+        print(f"  {k:40s} {v:.3e}")
     # one optimizer step: redo the GPU epoch up to its first step and compare the moves
     m2 = ChessNet()
     m2.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})

@@ -10,7 +10,11 @@ Reference: scripts/self_play.py `self_play(model, N, cpu, 64)` (model-instance
 path = sequential, :283-287). Port: oracle.play_game per game with the same
 schedule (test infrastructure, as in bench.py's cpu_baseline).
 
-    PYTHONDONTWRITEBYTECODE=1 python tools/calibrate_cpu.py [N] > profiles/r01_cpu_calibration.json
+    PYTHONDONTWRITEBYTECODE=1 python tools/calibrate_cpu.py [N] [THREADS] > profiles/r01_cpu_calibration.json
+
+THREADS (default: torch's default, all cores) sets the torch threads of both
+sides; 1 matches bench.py's cpu_baseline pool (one thread per worker process):
+    PYTHONDONTWRITEBYTECODE=1 python tools/calibrate_cpu.py 12 1 > profiles/r03_cpu_calibration_1thread.json
 """
 from __future__ import annotations
 
@@ -41,6 +45,8 @@ def cpu_model():
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 12
+    if len(sys.argv) > 2:
+        torch.set_num_threads(int(sys.argv[2]))
     from make_golden import import_reference
     from knightvision_amd.weights import synthetic_state_dict
     from oracle import oracle as O

@@ -5,7 +5,7 @@ correction, MI355X_MICROARCH.md), achieved GB/s = bytes / average duration.
 Narrow (4-16 B per lane) accesses are not calibrated by the guide; treat the
 absolute figure as an estimate.
 
-    python tools/tree_hbm.py FETCH_CSV_GLOB WRITE_CSV_GLOB TRACE_DB SLOTS > profiles/rNN_pmc_tree.json
+    python tools/tree_hbm.py FETCH_CSV_GLOB WRITE_CSV_GLOB TRACE_DB SLOTS [SIMS_PER_MOVE [NOTE]] > profiles/rNN_pmc_tree.json
 """
 import csv
 import glob
@@ -44,6 +44,10 @@ def main():
     fetch, write, dur = pmc(sys.argv[1], "FETCH_SIZE"), pmc(sys.argv[2], "WRITE_SIZE"), durations(sys.argv[3])
     slots = int(sys.argv[4])
     res = {"slots": slots, "peak_GBps": PEAK_GBPS, "kernels": {}}
+    if len(sys.argv) > 5:
+        res["sims_per_move"] = int(sys.argv[5])
+    if len(sys.argv) > 6:
+        res["note"] = sys.argv[6]
     for k in KERNELS:
         if k in fetch and k in write and k in dur:
             b = (2 * fetch[k] + write[k]) * 1024
