@@ -30,6 +30,10 @@ from .ai import codes_to_planes
 from .engine import EVAL_FAITHFUL, EVAL_LAZY, SEED_PER_GAME, SEED_SEQUENTIAL, REASONS, SelfPlayEngine, packed_from, records_by_game
 
 EPSILON = float(os.getenv("DIR_NOISE_EPS", "0.25"))
+# DIR_NOISE_ALPHA (scripts/self_play.py:13): any normal double in (0, 1) -- numpy's legacy gamma branch for
+# shape < 1, which the device restates bit for bit down to subnormal and zero draws (glibc pow's underflow
+# special case, csrc/kv_libm.h); shape >= 1 (a different numpy branch) is rejected by kv_create (KV_EINVAL),
+# and a ply whose 4096 draws are all 0 fails the run as the reference's random.choices raises ValueError
 ALPHA = float(os.getenv("DIR_NOISE_ALPHA", "0.3"))
 SEED = int(os.getenv("SEED", "42"))
 BATCH_SIZE = int(os.getenv("SELFPLAY_BATCH_SIZE", "16"))

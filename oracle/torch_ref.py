@@ -85,7 +85,7 @@ def forward_train(params, planes):
     return pol, val
 
 
-def reference_epoch(sd, batches, lr, accumulate_steps, entropy_coef, clip=1.0, dtype=torch.float64):
+def reference_epoch(sd, batches, lr, accumulate_steps, entropy_coef, clip=1.0, dtype=torch.float64, trace=None):
     """scripts/train.py _train_one_epoch (:126-196) restated on the CPU in
     `dtype`: per batch the loss of :169-176 (cross entropy + MSE - coef *
     entropy), NaN/Inf skip (:178-180), loss / accumulate_steps backward, and
@@ -93,7 +93,9 @@ def reference_epoch(sd, batches, lr, accumulate_steps, entropy_coef, clip=1.0, d
     step (GradScaler's scale / unscale is the identity in exact arithmetic).
     batches: list of (planes [B,12,8,8], moves [B], outcomes [B]).
     Returns (parameters after the epoch, per-batch losses, gradients of the
-    first optimizer step after clipping)."""
+    first optimizer step after clipping). `trace` (a dict) also receives every
+    step's clipped gradients ("grads") and the parameters after the first step
+    ("after1")."""
     params = {k: torch.tensor(np.asarray(v), dtype=dtype).requires_grad_(True) for k, v in sd.items()
               if not (k.endswith("running_mean") or k.endswith("running_var") or k.endswith("num_batches_tracked"))}
     opt = torch.optim.Adam(list(params.values()), lr=lr)
@@ -117,6 +119,10 @@ def reference_epoch(sd, batches, lr, accumulate_steps, entropy_coef, clip=1.0, d
             torch.nn.utils.clip_grad_norm_(list(params.values()), max_norm=clip)
             if first_grads is None:
                 first_grads = {k: p.grad.detach().clone() for k, p in params.items()}
+            if trace is not None:
+                trace.setdefault("grads", []).append({k: p.grad.detach().clone() for k, p in params.items()})
             opt.step()
             opt.zero_grad()
+            if trace is not None and "after1" not in trace:
+                trace["after1"] = {k: p.detach().clone() for k, p in params.items()}
     return {k: p.detach() for k, p in params.items()}, losses, first_grads

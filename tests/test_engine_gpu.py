@@ -168,7 +168,10 @@ def test_engine_games_match_reference(golden_dir, group, precision, algo):
     ties = [r for r in res if r != "exact"]
     print(f"{precision}/{algo} {group}: {n - len(ties)}/{n} games move-for-move identical, near-tie divergences "
           f"{len(ties)} {ties}")
-    assert len(ties) <= max(1, n // 8)
+    # fp32 towers: every golden game identical (0 near-tie divergences measured on every run, the kernels are
+    # deterministic and the fixtures fixed); the split precisions keep the near-tie allowance (a divergence
+    # only where the reference's own decision margin is < MARGIN_TOL, see _compare)
+    assert len(ties) <= (0 if precision == "fp32" else max(1, n // 8))
 
 
 def test_sequential_self_play_api_matches_reference(golden_dir):

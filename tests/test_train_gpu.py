@@ -160,3 +160,41 @@ def test_update_step_matches_float64_restatement(golden_dir, amp, loss_rtol, gra
     print(f"update step (amp={amp}): {checked} weights compared, {flips} moved the other way, worst |step - oracle "
           f"step| = {worst:.2e} lr ({worst_k}); zero-gradient tensors skipped: {len(noise)}")
     assert worst_g <= grad_tol and flips <= flip_frac * checked
+
+
+# vs the REFERENCE's own update step (tests/golden/train_epoch.npz, written by running scripts/train.py
+# _train_one_epoch itself: tests/golden/make_train_golden.py). fp32: MIOpen's fp32 convolutions include
+# Winograd solvers (4.5e-3 of the norm measured against float64); autocast: the reference's fp16 AMP on the
+# HIP training kernels, compared with its fp32 CPU run (bounds as above)
+@pytest.mark.parametrize("amp,loss_rtol,grad_tol,flip_frac", [(False, 1e-4, (1e-2, 3e-2), 1e-2),
+                                                         (True, 5e-3, (0.15, 0.2), 3.5e-2)])
+def test_update_step_matches_reference_epoch(golden_dir, amp, loss_rtol, grad_tol, flip_frac):
+    from knightvision_amd.model import ChessNet
+    from test_train_golden_cpu import batches_of, check_against_reference
+    g = dict(np.load(os.path.join(golden_dir, "train_epoch.npz")))
+    sd = synthetic_state_dict(42, "bn")
+    _, _, accum, coef, lr = g["meta"]
+    m = ChessNet()
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    m.cuda().train()
+    opt = torch.optim.Adam(m.parameters(), lr=float(lr))
+    grads, after1 = [], {}
+    inner = opt.step
+
+    def step(*a, **kw):
+        grads.append({k: p.grad.detach().double().cpu().numpy() for k, p in m.named_parameters()})
+        r = inner(*a, **kw)
+        if not after1:
+            after1.update({k: p.detach().double().cpu().numpy() for k, p in m.named_parameters()})
+        return r
+    opt.step = step
+    batches = [T.Batch(torch.from_numpy(x).cuda(), torch.from_numpy(mv).cuda(), torch.from_numpy(oc).cuda())
+               for x, mv, oc in batches_of(g)]
+    st = T.train_one_epoch(m, batches, opt, T.make_scaler("cuda"), accumulate_steps=int(accum),
+                           entropy_coef=float(coef), amp=amp)
+    assert st["optimizer_steps"] == 2 and st["skipped"] == 0
+    delta1 = {k: v - np.asarray(sd[k], dtype=np.float64) for k, v in after1.items()}
+    # GradScaler on the GPU scales the loss by 2^16 and unscales before the clip: the recorded gradients are
+    # the unscaled, clipped ones the optimizer steps with, as in the reference
+    check_against_reference(g, grads, delta1, st["loss"], f"GPU update step (amp={amp})",
+                            grad_tol=grad_tol, flip_frac=flip_frac, loss_rtol=loss_rtol)
