@@ -72,9 +72,12 @@ def parse():
                          "enough for games to complete, reported under 'ref_selection' with measured games/hour")
     ap.add_argument("--ref-steps", type=int, default=1200)
     ap.add_argument("--ref-warmup", type=int, default=600)
-    ap.add_argument("--eval", choices=["faithful", "lazy"], default="faithful",
+    ap.add_argument("--eval", choices=["faithful", "lazy", "hash"], default="faithful",
                     help="reference-selection network schedule: faithful (every board evaluated, as the reference "
-                         "does) or lazy (only the rows the schedule consumes, identical games)")
+                         "does) or lazy (only the rows the schedule consumes, identical games); hash: PROFILING "
+                         "ONLY -- the MCTS test evaluator (uniform priors, hashed values) instead of the network, "
+                         "3 launches per sim-step, so a tree-kernel counter run of a whole 800-sim move stays under "
+                         "rocprofv3's dispatch limit (tools/r03_tree.sh); its line is not a measurement")
     ap.add_argument("--tree-edge-cap", type=int, default=0,
                     help="MCTS edge pool per slot (0: KV_MAXM x (sims+1), which cannot overflow; an overflow "
                          "fails the run). Profiling runs under rocprofv3 --pmc use a smaller pool")
@@ -256,7 +259,7 @@ def main():
             dist.init_process_group(backend)
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
-    from knightvision_amd.engine import EVAL_FAITHFUL, EVAL_LAZY, SelfPlayEngine
+    from knightvision_amd.engine import EVAL_FAITHFUL, EVAL_HASH, EVAL_LAZY, SelfPlayEngine
     from knightvision_amd.weights import synthetic_state_dict
     from knightvision_amd.distributed import gather_experience
 
@@ -283,7 +286,8 @@ def main():
                 eval_mode="faithful"):
         eng = SelfPlayEngine(synthetic_state_dict(42, "init"), slots=G, n_games=1 << 40, seed=42, max_moves=None,
                              batch=16, sims=sims, game_id_base=rank, game_id_stride=world,
-                             eval_mode=EVAL_LAZY if (eval_mode == "lazy" and sims == 0) else EVAL_FAITHFUL,
+                             eval_mode=(EVAL_LAZY if (eval_mode == "lazy" and sims == 0) else
+                                        EVAL_HASH if (eval_mode == "hash" and sims > 0) else EVAL_FAITHFUL),
                              record_cap=max(1 << 16, G * (steps + warmup + 8)), device=local, precision=precision,
                              algo=algo, tree_edge_cap=args.tree_edge_cap if sims > 0 else 0,
                              keep_root_visits=keep and sims > 0)
@@ -402,7 +406,9 @@ def main():
                 "plies/s", plies / dt
         mean_len = float(gms_all["plies"].mean()) if gms_all is not None and len(gms_all) else None
         gph = games_done / dt * 3600.0 if games_done > 0 else None
-        wl = (f"{G} concurrent games/GPU, {sims} sims/move, batch-{G} NN eval, fp32" if mcts else
+        wl = (f"{G} concurrent games/GPU, {sims} sims/move, batch-{G} NN eval, fp32" +
+              (" [hash test evaluator instead of the network: PROFILING ONLY, not a measurement]"
+               if args.eval == "hash" else "") if mcts else
               f"{G} concurrent games/GPU, reference move selection (sims=0), batch-{G} NN eval, fp32")
         out = {
             "metric": metric, "value": value, "unit": unit, "n_gpus": world, "steps": steps, "warmup": warmup,

@@ -22,8 +22,8 @@ O=$R/gpurun_out/${1:-tree}
 mkdir -p $O
 cd /tmp
 export TMPDIR=/tmp
-ARGS="--steps 1 --warmup 0 --sims 800 --alt-precision= --ref-block 0 --no-cpu-baseline"
-RANGE="[1-799]"
+ARGS="--steps 1 --warmup 0 --sims 800 --alt-precision= --ref-block 0 --no-cpu-baseline ${EXTRA_ARGS:-}"
+RANGE="${RANGE:-[1-799]}"
 if [ "${SKIP_TRACE:-0}" != 1 ]; then
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o t -- python3 $R/bench.py $ARGS > $O/trace.log 2>&1
 echo trace-done
