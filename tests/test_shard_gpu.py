@@ -160,3 +160,30 @@ def test_rccl_gather_path_world1():
     assert p.exitcode == 0
     for rb, gb, pb in out:
         assert rb == hr and gb == hg and pb == hp
+
+
+def test_bench_json_line_contract():
+    """bench.py's one JSON line (the driver's contract) on a tiny MCTS config, run as the driver runs it (a
+    child process): every required key, value = completed backups / timed seconds, roofline + cpu_baseline
+    objects present."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, KV_CPU_WORKERS="2")
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--slots", "32", "--sims", "8",
+                          "--steps", "2", "--warmup", "1", "--alt-precision=", "--ref-block", "0",
+                          "--cpu-seconds", "2"], capture_output=True, text=True, timeout=240, env=env, cwd=repo)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["unit"] == "sims/s"
+    assert d["value"] > 0 and abs(d["value"] * d["ms_per_step"] * 1e-3 * 2 - 32 * 8 * 2) < 1e-6 * 32 * 8 * 2
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in d["roofline"], k
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in d["cpu_baseline"], k
