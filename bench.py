@@ -139,7 +139,7 @@ def _cpu_worker(wid: int, workers: int, sims: int, seconds: float, threads: int,
     from knightvision_amd.weights import synthetic_state_dict
     ev = torch_ref.make_eval_fn(synthetic_state_dict(42, "init"))
     ev(np.zeros((1, 12, 8, 8), dtype=np.float32))  # first-call setup outside the timed loop
-    barrier.wait()
+    barrier.wait(timeout=600)
     t0 = time.perf_counter()
     units = games = 0
     seed = 42 + wid
@@ -180,7 +180,18 @@ def cpu_baseline(seconds: float, sims: int):
     procs = [ctx.Process(target=_cpu_worker, args=(w, workers, sims, seconds, 1, barrier, q)) for w in range(workers)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=seconds + 600) for _ in procs]
+    import queue
+    res, deadline = [], time.perf_counter() + seconds + 900
+    while len(res) < workers:  # fail loudly (not after a long block) if a worker dies
+        try:
+            res.append(q.get(timeout=5))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead or time.perf_counter() > deadline:
+                for p in procs:
+                    if p.is_alive():
+                        p.terminate()
+                raise RuntimeError(f"cpu_baseline: worker exit codes {dead or 'timeout'}")
     for p in procs:
         p.join(timeout=60)
     units = sum(r[1] for r in res)

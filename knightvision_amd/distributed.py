@@ -96,7 +96,10 @@ def pack_pi(pi_rows: torch.Tensor):
     move slot, 0xffff past the position's move list -- kv_root_visits_device)
     -> (counts int16 [n], packed int16 [sum counts]): each row's legal-move
     prefix only, rows concatenated in order. 2 B per legal move + 2 B per record
-    instead of 640 B per record (MAXM 320, ~23 legal moves on average)."""
+    instead of 640 B per record (MAXM 320, ~23 legal moves on average).
+    The valid entries of a row are a prefix (kv_root_visits_device pads past
+    the move list) and never 0xffff themselves (visit counts <= KV_MAX_SIMS =
+    65000)."""
     if pi_rows.shape[0] == 0:
         z = torch.zeros(0, dtype=torch.int16, device=pi_rows.device)
         return z, z.clone()
