@@ -42,9 +42,10 @@ def test_mcts_hash_games_identical_to_oracle(sims, max_moves, n):
         assert reward == pytest.approx(r["reward"])
 
 
-def _hip_eval(sd):
+def _hip_eval(sd, class_rows=CLASS_ROWS):
     """Oracle evaluator: the HIP network's row for one board, computed in a
-    batch of CLASS_ROWS copies (the engine's batch class)."""
+    batch of class_rows copies (the engine's batch class: 17 = the > 16-board
+    Winograd class, 1 = the <= 16-board direct class of a one-slot engine)."""
     from knightvision_amd.model import KVNet
     net = KVNet(0, packed_from(sd))
 
@@ -54,10 +55,10 @@ def _hip_eval(sd):
         codes = np.zeros((n, 64), dtype=np.int8)
         b, c, sq = np.nonzero(planes)
         codes[b, sq] = c + 1
-        rows = torch.from_numpy(np.repeat(codes, CLASS_ROWS, axis=0)).cuda()
+        rows = torch.from_numpy(np.repeat(codes, class_rows, axis=0)).cuda()
         pol, val = net.forward_boards(rows)
         torch.cuda.synchronize()
-        return pol.cpu().numpy()[::CLASS_ROWS], val.cpu().numpy().reshape(-1)[::CLASS_ROWS]
+        return pol.cpu().numpy()[::class_rows], val.cpu().numpy().reshape(-1)[::class_rows]
 
     return ev, net
 
@@ -99,6 +100,25 @@ def _compare_network_games(variant, slots, n_check, sims, max_moves, steps=-1):
 def test_mcts_network_visits_identical_to_oracle_c1(variant):
     """C1-sized search (64 sims/move) with the real network, 8 games x 6 plies."""
     _compare_network_games(variant, slots=20, n_check=8, sims=64, max_moves=6)
+
+
+@pytest.mark.parametrize("variant", ["init", "peaked"])
+def test_mcts_network_c1_single_game(variant):
+    """BASELINE config C1 itself: ONE game, 64 sims/move (a one-slot engine, so every leaf batch is one board
+    in the <= 16-board direct class), 10 moves, root visit vectors identical to the oracle's PUCT."""
+    from oracle import oracle as O
+    sd = synthetic_state_dict(42, variant)
+    with SelfPlayEngine(sd, slots=1, n_games=1, seed=42, max_moves=10, sims=64, c_puct=1.5,
+                        keep_root_visits=True) as eng:
+        eng.run()
+        recs, visits = eng.records(), eng.root_visits()
+    ev, net = _hip_eval(sd, class_rows=1)
+    r = O.mcts_play_game(64, O.MT(42, "numpy"), O.MT(42, "python"), ev, max_moves=10, c_puct=1.5)
+    net.close()
+    assert np.array_equal(recs["move"], r["moves"])
+    for p in range(len(r["moves"])):
+        assert np.array_equal(visits[p], r["visits"][p]), p
+    print(f"C1 ({variant}): {len(r['moves'])} root visit vectors identical")
 
 
 def test_mcts_network_visits_identical_to_oracle_c2_first_move():
