@@ -101,6 +101,9 @@ def _cfg(**kw):
     (dict(n_games=-1), "slots must be > 0"),
     (dict(alpha=0.0), "DIR_NOISE_ALPHA"),
     (dict(alpha=1.5), "DIR_NOISE_ALPHA"),
+    (dict(alpha=1.0), "DIR_NOISE_ALPHA"),          # shape 1: numpy's exponential branch, not restated
+    (dict(alpha=1e-310), "DIR_NOISE_ALPHA"),       # subnormal: 1/alpha overflows
+    (dict(alpha=float("nan")), "DIR_NOISE_ALPHA"),
     (dict(batch=0), "SELFPLAY_BATCH_SIZE"),
     (dict(seed_mode=7), "bad seed_mode"),
     (dict(seed_mode=1, slots=2), "sequential seeding"),

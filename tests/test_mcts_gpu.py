@@ -198,3 +198,22 @@ def test_mcts_compact_tail_batches_identical_to_oracle():
             compared += 1
     net.close()
     print(f"compact-tail MCTS parity: {compared} root vectors identical")
+
+
+def test_mcts_recycled_slots_then_compact_tail_identical_to_oracle():
+    """Slot recycling (more games than slots) followed by the compact tail once the game queue is empty:
+    games 0..19 on 17 slots, each equal to the oracle's game of the same id move for move."""
+    from oracle import oracle as O
+    slots, n, sims, mm = 17, 20, 16, 40
+    sd = synthetic_state_dict(42, "peaked")
+    with SelfPlayEngine(sd, slots=slots, n_games=n, seed=42, max_moves=mm, sims=sims, c_puct=1.5) as eng:
+        eng.run()
+        by = records_by_game(eng.records(), eng.games())
+    assert len(by) == n
+    ev, net = _hip_eval(sd)
+    for g in range(n):
+        r = O.mcts_play_game(sims, O.MT(42 + g, "numpy"), O.MT(42 + g, "python"), ev, max_moves=mm, c_puct=1.5)
+        moves, _, reward = by[g]
+        assert np.array_equal(moves, r["moves"]), f"game {g}"
+        assert reward == pytest.approx(r["reward"])
+    net.close()
