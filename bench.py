@@ -408,7 +408,9 @@ def main():
                     "source": "profiles/" + tf,
                     "note": "latency-bound: one wave per game (select descent + leaf getValidMoves, backup)"}
 
-    gl, gl_file = _mcts_game_length(sims) if (mcts and G == 2048) else (None, None)
+    # complete-game length at these search settings (per-game seeds: the same distribution at any slot count)
+    gl, gl_file = _mcts_game_length(sims) if mcts else (None, None)
+    steady = bool(gl) and warmup >= 2 * gl["mean_plies_finished"]  # slots have cycled through whole games
     if rank == 0:
         if mcts:
             metric, unit, value = "MCTS simulations/sec + self-play games/hour", "sims/s", sims_done / dt
@@ -432,7 +434,10 @@ def main():
                                "one ply of every slot"},
             "plies_per_s": plies / dt, "games_per_hour": gph,
             "games_per_hour_note": (
-                (f"{int(games_done)} games ended inside the timed region / its duration -- a transient count, not "
+                (f"{int(games_done)} games ended inside the timed region / its duration, slots recycled; the "
+                 f"warm-up ({warmup} moves) is >= 2 mean game lengths, so the slots hold games at every stage: a "
+                 "steady-state rate" if (mcts and steady) else
+                 f"{int(games_done)} games ended inside the timed region / its duration -- a transient count, not "
                  f"a steady-state rate: every slot started at ply 0, the region covers plies {warmup + 1}-"
                  f"{warmup + steps}, so only early endings are in it; see games_per_hour_steady_derived and "
                  "ref_selection" if mcts else
