@@ -213,3 +213,25 @@ def test_datasets(tmp_path, monkeypatch):
     assert codes.shape == (5, 64) and float(outs.abs().sum()) == 0.0
     pds.extend([("b", 1, 1.0)])
     assert pds[5] == ("b", 1, 1.0)
+
+
+def test_san_edge_cases():
+    """More python-chess parse_san / san / push semantics (hand-checked positions; python-chess itself is not
+    installed here, so these are pinned by the rules, not by the library)."""
+    # capture-promotion giving check: the SAN carries "x", "=Q" and "+"; halfmove clock reset
+    san, after = _chess.san_push("3r2k1/4P3/8/8/8/8/8/4K3 w - - 0 1", "exd8=Q")
+    assert san == "exd8=Q+" and after == "3Q2k1/8/8/8/8/8/8/4K3 b - - 0 1"
+    # castling through an attacked square is illegal
+    with pytest.raises(Exception, match="illegal"):
+        _chess.san_push("4k3/8/8/8/8/8/5r2/4K2R w K - 0 1", "O-O")
+    # an en-passant capture that exposes the own king along the rank is illegal
+    with pytest.raises(Exception, match="illegal"):
+        _chess.san_push("8/8/8/KPp4r/8/8/8/7k w - c6 0 1", "bxc6")
+    # long-algebraic pawn capture spelling, canonical SAN out; en-passant square cleared after the push
+    san, after = _chess.san_push("rnbqkbnr/ppp1pppp/8/3p4/4P3/8/PPPP1PPP/RNBQKBNR w KQkq - 0 2", "e4xd5")
+    assert san == "exd5" and after == "rnbqkbnr/ppp1pppp/8/3P4/8/8/PPPP1PPP/RNBQKBNR b KQkq - 0 2"
+    # a king move drops both castling rights of its side; a rook capture on a corner drops the opponent's right
+    san, after = _chess.san_push("r3k2r/8/8/8/8/8/8/R3K2R w KQkq - 0 1", "Rxa8+")
+    assert san == "Rxa8+" and after == "R3k2r/8/8/8/8/8/8/4K2R b Kk - 0 1"
+    san, after = _chess.san_push("r3k2r/8/8/8/8/8/8/R3K2R w KQkq - 0 1", "Kd1")
+    assert san == "Kd1" and after == "r3k2r/8/8/8/8/8/8/R2K3R b kq - 1 1"
