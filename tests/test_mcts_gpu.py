@@ -138,10 +138,11 @@ def test_mcts_network_visits_identical_to_oracle_c3_first_move(variant):
     _compare_network_games(variant, slots=2048, n_check=8, sims=800, max_moves=None, steps=1)
 
 
-def test_mcts_network_visits_identical_to_oracle_c3_three_moves():
+@pytest.mark.parametrize("variant", ["init", "peaked"])
+def test_mcts_network_visits_identical_to_oracle_c3_three_moves(variant):
     """C3, the headline config (2,048 slots x 800 sims): the first three moves of the first 8 games -- trees
     that start from positions the search itself chose."""
-    _compare_network_games("init", slots=2048, n_check=8, sims=800, max_moves=None, steps=3)
+    _compare_network_games(variant, slots=2048, n_check=8, sims=800, max_moves=None, steps=3)
 
 
 def test_mcts_network_games_run():
