@@ -45,6 +45,7 @@ FLOP_PER_EVAL = 3175744512            # SURVEY.md 8d, ChessNet forward per posit
 FLOP_RES_CONV_PER_BOARD = 301989888   # one 3x3 512->512 conv on 8x8 (2*64*512*4608)
 FLOP_WINO_GEMM_PER_BOARD = 75497472   # its Winograd F(4x4,3x3) GEMMs: 2 * 4 tiles * 36 * 512 * 512
 FLOP_WINO48_GEMM_PER_BOARD = 62914560  # its Winograd F(4x8,3x3) GEMMs: 2 * 2 tiles * 60 * 512 * 512
+FLOP_WINO88_GEMM_PER_BOARD = 52428800  # opt-in F(8x8,3x3) GEMMs: 2 * 1 tile * 100 * 512 * 512
 FP32_MFMA_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md, f32-input MFMA (dense)
 BF16_MFMA_PEAK_TFLOPS = 2500.0        # dense bf16 MFMA
 
@@ -58,13 +59,16 @@ def parse():
     ap.add_argument("--slots", type=int, default=2048)
     ap.add_argument("--sims", type=int, default=800)
     ap.add_argument("--precision", choices=["fp32", "f16x3", "bf16x6", "bf16x3"], default="fp32")
-    ap.add_argument("--algo", choices=["auto", "direct", "winograd", "winograd48"], default="auto",
+    ap.add_argument("--algo", choices=["auto", "direct", "winograd", "winograd48", "winograd88"], default="auto",
                     help="conv algorithm of the fp32 tower (auto: Winograd F(4x8,3x3) above 16 boards)")
     ap.add_argument("--compare-direct", type=int, default=0,
                     help="also measure the fp32 direct implicit-GEMM and F(4x4) towers ('fp32_direct', "
                          "'fp32_winograd44'; ~40 s per step at C3)")
     ap.add_argument("--alt-precision", default="f16x3",
                     help="also measure this network precision (reported under 'alt_precision'; '' to skip)")
+    ap.add_argument("--alt-algo", default="winograd48",
+                    help="fp32 only: also time this conv algorithm for --alt-steps moves when the headline runs "
+                         "F(8x8) (the fp32 default); '' to skip")
     ap.add_argument("--alt-steps", type=int, default=2)
     ap.add_argument("--alt-warmup", type=int, default=1)
     ap.add_argument("--ref-block", type=int, default=1,
@@ -361,6 +365,10 @@ def main():
     alt = None
     if args.alt_precision and args.alt_precision != args.precision:
         alt = measure(args.alt_precision, steps=args.alt_steps, warmup=args.alt_warmup, tag="alt " + args.alt_precision)
+    alt_algo = None
+    if args.alt_algo and args.precision == "fp32" and m["dom_algo"] == 4:
+        alt_algo = measure("fp32", args.alt_algo, steps=args.alt_steps, warmup=args.alt_warmup,
+                           tag="alt " + args.alt_algo)
     refsel = reflazy = None
     if mcts and args.ref_block:
         # C3-ref: the reference's move selection (one network row per ply, sampled move) on the same slots;
@@ -372,21 +380,27 @@ def main():
         reflazy = measure(args.precision, sims=0, steps=args.ref_steps, warmup=args.ref_warmup,
                           tag="ref-selection lazy", eval_mode="lazy")
     wino44 = direct = None
-    if args.compare_direct and args.precision == "fp32" and m["dom_algo"] == 3:
+    if args.compare_direct and args.precision == "fp32" and m["dom_algo"] in (3, 4):
         wino44 = measure("fp32", "winograd", steps=1, warmup=1, tag="winograd44")
-    if args.compare_direct and args.precision == "fp32" and m["dom_algo"] in (2, 3):
+    if args.compare_direct and args.precision == "fp32" and m["dom_algo"] in (2, 3, 4):
         direct = measure("fp32", "direct", steps=1, warmup=1, tag="direct")
 
     # roofline of the dominant kernel, timed with HIP events on the engine stream: the residual-tower
     # Winograd GEMM launch (60 x [2*boards x 512 x 512]) or, for the direct algorithm, the residual conv
-    algo = m["dom_algo"]  # 1 direct, 2 Winograd F(4x4), 3 Winograd F(4x8)
-    per_board = {2: FLOP_WINO_GEMM_PER_BOARD, 3: FLOP_WINO48_GEMM_PER_BOARD}.get(algo, FLOP_RES_CONV_PER_BOARD)
+    algo = m["dom_algo"]  # 1 direct, 2 Winograd F(4x4), 3 Winograd F(4x8), 4 Winograd F(8x8) (the fp32 default)
+    per_board = {2: FLOP_WINO_GEMM_PER_BOARD, 3: FLOP_WINO48_GEMM_PER_BOARD,
+                 4: FLOP_WINO88_GEMM_PER_BOARD}.get(algo, FLOP_RES_CONV_PER_BOARD)
     bpl = min(G, int(round(m["dom_flop"] / per_board))) if m["dom_flop"] else G
     flop_alg = per_board * bpl
     achieved = flop_alg / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
     # the library picks the GEMM tile by rows (knightvision_amd/csrc/kv_nn.hip launch_wino_gemm / launch_wino48_gemm)
     pad = (bpl + 31) // 32 * 32
-    if algo == 3:
+    if algo == 4:
+        pad88 = (bpl + 63) // 64 * 64
+        kname = ("wino_gemm_kernel<512,4,2,1,2,32,100>" if pad88 % 128 == 0
+                 else "wino_gemm_kernel<512,2,2,1,2,16,100>")
+        kdesc = " (residual-tower Winograd F(8x8,3x3) GEMMs, 100 points)"
+    elif algo == 3:
         kname = ("wino_gemm_kernel<512,4,2,1,2,32,60>" if (pad * 2) % 128 == 0
                  else "wino_gemm_kernel<512,2,2,1,2,16,60>")
         kdesc = " (residual-tower Winograd F(4x8,3x3) GEMMs, 60 points)"
@@ -494,6 +508,21 @@ def main():
                 "value": (wino44["sims"] if mcts else wino44["plies"]) / wino44["dt"], "unit": unit,
                 "ms_per_step": wino44["dt"] * 1e3 / wino44["steps"], "res_gemm_avg_launch_ms": wino44["conv_ms"],
                 "res_gemm_tflops": w_ach, "res_gemm_frac": (w_ach / FP32_MFMA_PEAK_TFLOPS) if w_ach else None}
+        if alt_algo is not None:
+            aa = alt_algo
+            per = {3: FLOP_WINO48_GEMM_PER_BOARD, 2: FLOP_WINO_GEMM_PER_BOARD}.get(aa["dom_algo"],
+                                                                                 FLOP_RES_CONV_PER_BOARD)
+            aa_ach = (per * bpl / (aa["conv_ms"] * 1e-3) / 1e12) if aa["conv_ms"] > 0 else None
+            out["fp32_" + args.alt_algo] = {
+                "note": ("the same fp32 network with the Winograd F(4x8,3x3) tower (60 points, 2 tiles per board, "
+                         "KV_ALGO_WINOGRAD48): about half the logit error of the default F(8x8) (max |dlogit| vs "
+                         "float64 over 1,024 random boards on the peaked weights 2.3e-5 against 5.1e-5, "
+                         "profiles/r03_wino88_accuracy_speed.log) for 20 % more GEMM FLOPs and transform bytes"
+                         if aa["dom_algo"] == 3 else f"the same fp32 network with algo {args.alt_algo}"),
+                "value": (aa["sims"] if mcts else aa["plies"]) / aa["dt"], "unit": unit,
+                "steps": aa["steps"], "warmup": aa["warmup"], "ms_per_step": aa["dt"] * 1e3 / aa["steps"],
+                "res_gemm_avg_launch_ms": aa["conv_ms"], "res_gemm_tflops": aa_ach,
+                "res_gemm_frac": (aa_ach / FP32_MFMA_PEAK_TFLOPS) if aa_ach else None}
         if alt is not None:
             # dominant launch of the alternate run (Winograd GEMM or direct residual conv), fp32-equivalent FLOPs
             a_ach = (alt["dom_flop"] / (alt["conv_ms"] * 1e-3) / 1e12) if alt["conv_ms"] > 0 else None

@@ -86,19 +86,25 @@ int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv);
 #define KV_PREC_F16X3 3
 int kv_net_set_precision(kv_net* net, int precision);
 /* Algorithm of the fp32 3x3 convs with Cin 256/512:
- * KV_ALGO_AUTO      Winograd for batches > 16 boards (F(4x8) in fp32, F(4x4)
- *                   for the split precisions), direct (split-K) below
+ * KV_ALGO_AUTO      Winograd for batches > 16 boards (F(8x8) in fp32, F(4x8)
+ *                   for f16x3, F(4x4) for bf16x6), direct (split-K) below
  * KV_ALGO_DIRECT    implicit GEMM over the 9 taps (exact fp32 products)
  * KV_ALGO_WINOGRAD  F(4x4,3x3): 36 GEMMs of 4 tiles x Cin x Cout per board, 4x
  *                   fewer FLOPs, fp32 transforms (logits within 1e-4)
  * KV_ALGO_WINOGRAD48 F(4x8,3x3): 60 GEMMs of 2 tiles x Cin x Cout per board,
- *                   4.8x fewer FLOPs than direct (fp32 only; the split
- *                   precisions run F(4x4) under this setting)
+ *                   4.8x fewer FLOPs than direct (fp32 and f16x3; bf16x6
+ *                   runs F(4x4) under this setting); about half the logit
+ *                   error of F(8x8) for 18 % more time at 2,048 boards
+ * KV_ALGO_WINOGRAD88 F(8x8,3x3): 100 GEMMs of 1 tile x Cin x Cout per board,
+ *                   5.76x fewer FLOPs than direct (fp32; the fp32 AUTO choice
+ *                   above 16 boards; f16x3 runs F(4x8) under it, bf16x6
+ *                   F(4x4))
  * Results are batch-invariant inside a class (<= 16 boards, > 16 boards). */
 #define KV_ALGO_AUTO 0
 #define KV_ALGO_DIRECT 1
 #define KV_ALGO_WINOGRAD 2
 #define KV_ALGO_WINOGRAD48 3
+#define KV_ALGO_WINOGRAD88 4
 int kv_net_set_algo(kv_net* net, int algo);
 int kv_net_set_timing(kv_net* net, int enable);
 void kv_net_destroy(kv_net* net);
@@ -180,7 +186,7 @@ typedef struct {
     int64_t res_conv_launches;
     double step_ms;       /* wall time inside kv_run */
     double dom_flop;      /* MFMA FLOPs of one measured launch (padded rows included) */
-    int64_t dom_algo;     /* KV_ALGO_DIRECT, KV_ALGO_WINOGRAD or KV_ALGO_WINOGRAD48 for those launches */
+    int64_t dom_algo;     /* KV_ALGO_DIRECT, _WINOGRAD, _WINOGRAD48 or _WINOGRAD88 for those launches */
     int64_t tree_overflows; /* MCTS expansions dropped for a full edge pool (each also fails kv_run) */
     int64_t nn_rows_lazy;   /* KV_EVAL_LAZY above 16 slots: rows the compact batches sent through the
                                network (nn_rows counts the rows the reference's schedule evaluates) */

@@ -21,6 +21,7 @@
 #include "kv_common.h"
 #include "kv_wino.h"
 #include "kv_wino48.h"
+#include "kv_wino88.h"
 
 namespace kv {
 
@@ -815,6 +816,8 @@ struct kv_net {
     float* U = nullptr;     // Winograd weights [36][Cout][Cin] of convs 1..11
     float* U48 = nullptr;   // F(4x8) weights [60][Cout][Cin] of convs 1..11
     size_t uoff48[12] = {};
+    float* U88 = nullptr;   // F(8x8) weights [100][Cout][Cin] of convs 1..11 (KV_ALGO_WINOGRAD88)
+    size_t uoff88[12] = {};
     uint16_t* Uf48[2] = {};  // fp16 pieces of U48 * 2^ut48[l] (KV_PREC_F16X3 on F(4x8))
     int ut48[12] = {};
     uint16_t* Up[3] = {};   // the same split into bf16 h / m / l (KV_PREC_BF16X6)
@@ -918,18 +921,29 @@ static int launch_conv(const float* in, const float* w, const float* sc, const f
 // Winograd for the fp32 tower when the batch is past the split-K class
 static bool use_wino(const kv_net* net, int B) {
     if (net->precision == KV_PREC_BF16X3) return false;
-    if (net->algo == KV_ALGO_WINOGRAD || net->algo == KV_ALGO_WINOGRAD48) return true;
+    if (net->algo == KV_ALGO_WINOGRAD || net->algo == KV_ALGO_WINOGRAD48 || net->algo == KV_ALGO_WINOGRAD88)
+        return true;
     return net->algo == KV_ALGO_AUTO && B > kSplitMaxBoards;
 }
 
-// the F(4x8) variant: fp32 and f16x3 (AUTO and WINOGRAD48); bf16x6 keeps F(4x4)
-static bool use_wino48(const kv_net* net, int B) {
-    return use_wino(net, B) && (net->precision == KV_PREC_FP32 || net->precision == KV_PREC_F16X3) &&
-           net->algo != KV_ALGO_WINOGRAD;
+// the F(8x8) variant: fp32 under KV_ALGO_AUTO (the fp32 default above 16 boards) and WINOGRAD88
+static bool use_wino88(const kv_net* net, int B) {
+    return use_wino(net, B) && net->precision == KV_PREC_FP32 &&
+           (net->algo == KV_ALGO_WINOGRAD88 || net->algo == KV_ALGO_AUTO);
 }
 
-// padded batch: a multiple of 4 boards (direct tiles) or 32 (128-row GEMM tiles)
-static int net_pad(const kv_net* net, int B) { return use_wino(net, B) ? (B + 31) & ~31 : (B + 3) & ~3; }
+// the F(4x8) variant: fp32 under WINOGRAD48, f16x3 under AUTO / WINOGRAD48 / WINOGRAD88; bf16x6 keeps F(4x4)
+static bool use_wino48(const kv_net* net, int B) {
+    return use_wino(net, B) && (net->precision == KV_PREC_FP32 || net->precision == KV_PREC_F16X3) &&
+           net->algo != KV_ALGO_WINOGRAD && !use_wino88(net, B);
+}
+
+// padded batch: a multiple of 4 boards (direct tiles), 32 (128-row GEMM tiles of 2 rows per
+// board) or 64 (F(8x8): one row per board, 64- or 128-row tiles)
+static int net_pad(const kv_net* net, int B) {
+    if (use_wino88(net, B)) return (B + 63) & ~63;
+    return use_wino(net, B) ? (B + 31) & ~31 : (B + 3) & ~3;
+}
 
 static int net_reserve(kv_net* net, int nb_pad) {
     if (nb_pad <= net->cap) return KV_OK;
@@ -1169,10 +1183,71 @@ static int wino48_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     return KV_OK;
 }
 
+// F(8x8) GEMMs (100 points, rows = 1 per board, a multiple of 64): 128x128 tiles when the
+// rows allow, else 64x128; same k order, same bits
+template <int K>
+static int launch_wino88_gemm(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
+    if (rows % 128 == 0) return launch_wino_gemm_t<K, 4, 2, 1, 2, 32, 0, kv::W88_XI>(V, U, M, rows, stride, st);
+    return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720, kv::W88_XI>(V, U, M, rows, stride, st);
+}
+
+template <bool RESID, bool WRITE_Y, bool NEXT_V>
+static int launch_wino88_out(kv_net* net, int l, const float* M, int nb, int stride, const float* resid, float* Y,
+                             float* Vn, hipStream_t st) {
+    const float* W = net->w;
+    hipLaunchKernelGGL((kv::wino88_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 256, nb), dim3(256), 0, st, M,
+                       stride, W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+// conv2 + the 5 residual blocks for boards [0, nb), F(8x8)
+static int wino88_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
+    const int rows = nb, stride = rows;
+    float* V = net->V;
+    float* M = net->Mw;
+    int rc;
+    if (debug_skip_transforms()) {
+        if ((rc = launch_wino88_gemm<256>(net->V256, net->U88 + net->uoff88[1], M, rows, stride, st))) return rc;
+        for (int l = 2; l < 12; ++l)
+            if ((rc = launch_wino88_gemm<512>(V, net->U88 + net->uoff88[l], M, rows, stride, st))) return rc;
+        return KV_OK;
+    }
+    if ((rc = launch_wino88_gemm<256>(net->V256, net->U88 + net->uoff88[1], M, rows, stride, st))) return rc;
+    if ((rc = launch_wino88_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st))) return rc;
+    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
+    for (int r = 0; r < 5; ++r) {
+        const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
+        const bool m = mark && r == 2;  // one representative residual GEMM for the engine's timing hook
+        if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
+        if ((rc = launch_wino88_gemm<512>(V, net->U88 + net->uoff88[l1], M, rows, stride, st))) return rc;
+        if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
+        if ((rc = launch_wino88_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st))) return rc;
+        if ((rc = launch_wino88_gemm<512>(V, net->U88 + net->uoff88[l2], M, rows, stride, st))) return rc;
+        rc = r < 4 ? launch_wino88_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
+                   : launch_wino88_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
+        if (rc) return rc;
+    }
+    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
+    return KV_OK;
+}
+
 // Winograd tower: conv2 and the 5 residual blocks (conv1 output in net->T,
 // or conv2's input transform already in net->V256 when v256_ready)
 static int net_tower_wino(kv_net* net, int nb_pad, bool v256_ready, hipStream_t st) {
     int rc;
+    if (use_wino88(net, nb_pad)) {
+        if (!v256_ready) {
+            hipLaunchKernelGGL(kv::wino88_in_kernel<256>, dim3(1, nb_pad), dim3(256), 0, st, net->T, nb_pad,
+                               net->V256);
+            KV_HIP(hipGetLastError());
+        }
+        if ((rc = wino88_blocks(net, nb_pad, true, st))) return rc;
+        net->dom_flop = 2.0 * kv::W88_XI * nb_pad * 512.0 * 512.0;
+        net->dom_algo = KV_ALGO_WINOGRAD88;
+        net->dom_launches = 1;
+        return KV_OK;
+    }
     if (use_wino48(net, nb_pad)) {
         const int rows48 = nb_pad * 2;
         if (!v256_ready) {
@@ -1211,8 +1286,13 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
     if (wino && net->precision == KV_PREC_F16X3)
         KV_HIP(hipMemsetAsync(net->vmax, 0, (size_t)12 * net->cap * sizeof(unsigned), st));
+    // F(8x8): the stem writes NHWC and wino88_in_kernel builds conv2's V
+    const bool w88 = wino && use_wino88(net, nb);
     if (boards) {
-        if (wino && use_wino48(net, nb))
+        if (w88)
+            hipLaunchKernelGGL(kv::stem_kernel<0>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
+                               W + o.scale[0], W + o.shift[0], net->T, nb_pad * 4, nullptr);
+        else if (wino && use_wino48(net, nb))
             hipLaunchKernelGGL(kv::stem_kernel<2>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], net->V256, nb_pad * 2, net_vmax(net, 1));
         else if (wino)
@@ -1227,7 +1307,7 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
         return rc;
     }
     if (wino) {
-        if ((rc = net_tower_wino(net, nb_pad, boards != nullptr, st))) return rc;
+        if ((rc = net_tower_wino(net, nb_pad, boards != nullptr && !w88, st))) return rc;
         return net_heads(net, nb, policy, value, st);
     }
     const bool bf3 = net->precision == KV_PREC_BF16X3;
@@ -1389,6 +1469,20 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
                        net->utot, net->Up[0], net->Up[1], net->Up[2]);
     KV_HIP(hipGetLastError());
     int rc;
+    if (!net->U88) {
+        size_t tot = 0;
+        for (int l = 1; l < 12; ++l) {
+            net->uoff88[l] = tot;
+            tot += (size_t)kv::W88_XI * kv::kConv[l].cout * kv::kConv[l].cin;
+        }
+        KV_HIP(hipMalloc(&net->U88, tot * sizeof(float)));
+    }
+    for (int l = 1; l < 12; ++l) {
+        const size_t n = (size_t)kv::kConv[l].cout * kv::kConv[l].cin;
+        hipLaunchKernelGGL(kv::wino88_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0,
+                           net->w + net->off.w[l], kv::kConv[l].cout, kv::kConv[l].cin, net->U88 + net->uoff88[l]);
+        KV_HIP(hipGetLastError());
+    }
     if ((rc = split_f16_set(net->U, net->uoff, kv::WN_XI, net->Uf, net->ut))) return rc;
     if ((rc = split_f16_set(net->U48, net->uoff48, kv::W48_XI, net->Uf48, net->ut48))) return rc;
     if (!net->stemT) KV_HIP(hipMalloc(&net->stemT, 9 * 12 * 256 * sizeof(float)));
@@ -1405,7 +1499,7 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
 int kv_net_set_algo(kv_net* net, int algo) {
     KV_REQUIRE(net, KV_EINVAL, "kv_net_set_algo: NULL");
     KV_REQUIRE(algo == KV_ALGO_AUTO || algo == KV_ALGO_DIRECT || algo == KV_ALGO_WINOGRAD ||
-                   algo == KV_ALGO_WINOGRAD48,
+                   algo == KV_ALGO_WINOGRAD48 || algo == KV_ALGO_WINOGRAD88,
                KV_EINVAL,
                "kv_net_set_algo: unknown algo %d", algo);
     net->algo = algo;
@@ -1493,6 +1587,7 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->pfeat);
     (void)hipFree(net->U);
     (void)hipFree(net->U48);
+    (void)hipFree(net->U88);
     (void)hipFree(net->stemT);
     (void)hipFree(net->v1wT);
     for (int p = 0; p < 3; ++p) (void)hipFree(net->Up[p]);

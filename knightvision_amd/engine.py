@@ -31,7 +31,7 @@ def packed_from(weights) -> np.ndarray:
     return pack_weights(state_dict_to_numpy(weights))[0]
 
 
-ALGOS = {"auto": 0, "direct": 1, "winograd": 2, "winograd48": 3}
+ALGOS = {"auto": 0, "direct": 1, "winograd": 2, "winograd48": 3, "winograd88": 4}
 
 
 class SelfPlayEngine:

@@ -28,7 +28,7 @@ from .weights import pack_weights, state_dict_to_numpy
 
 
 PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "f16x3": 3}
-ALGOS = {"auto": 0, "direct": 1, "winograd": 2, "winograd48": 3}
+ALGOS = {"auto": 0, "direct": 1, "winograd": 2, "winograd48": 3, "winograd88": 4}
 
 
 def batch_norm_rows(bn: nn.BatchNorm2d, x, n_real=None, explicit: bool = False):

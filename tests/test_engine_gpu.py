@@ -140,13 +140,13 @@ GROUPS = {"pg_init_mm80": ("init", 80, 16), "pg_peaked_mm80": ("peaked", 80, 16)
 
 
 @pytest.mark.parametrize("precision,algo", [("fp32", "auto"), ("f16x3", "auto"), ("bf16x6", "auto"),
-                                            ("bf16x3", "auto"), ("fp32", "winograd48")])
+                                            ("bf16x3", "auto"), ("fp32", "winograd48"), ("fp32", "winograd88")])
 @pytest.mark.parametrize("group", list(GROUPS))
 def test_engine_games_match_reference(golden_dir, group, precision, algo):
     """Complete games vs the reference's golden games. The slot counts here put
     the network in the <= 16-board class; ("fp32", "winograd48") forces the
-    headline's F(4x8) Winograd tower (the > 16-board class of C2 / C3) on the
-    same games."""
+    F(4x8) Winograd tower and ("fp32", "winograd88") the F(8x8) one (the
+    > 16-board class of C2 / C3) on the same games."""
     from knightvision_amd.engine import SelfPlayEngine, records_by_game
     variant, mm, batch = GROUPS[group]
     gold = _golden_games(golden_dir, group)

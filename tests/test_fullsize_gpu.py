@@ -3,7 +3,7 @@
 
   * slot-count invariance: with per-game seeds a game's trajectory depends only
     on its seed and on the network rows of its own boards, and the Winograd
-    towers (F(4x8), the fp32 default, and F(4x4)) are batch-invariant bit for
+    towers (F(8x8), the fp32 default, F(4x8) and F(4x4)) are batch-invariant bit for
     bit (tests/test_nn_gpu.py), so the first
     16 games of a 256- or 2,048-slot run must equal a 16-slot run move for move;
   * every recorded game replays legally on the oracle rules from the start
@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 SD = synthetic_state_dict(42, "init")
 
 
-def _run(slots, n_games, sims, max_moves, steps=-1, algo="winograd48"):
+def _run(slots, n_games, sims, max_moves, steps=-1, algo="winograd88"):
     with SelfPlayEngine(SD, slots=slots, n_games=n_games, seed=42, max_moves=max_moves, batch=16, sims=sims,
                         algo=algo) as eng:
         eng.run(steps)
@@ -76,7 +76,7 @@ def test_c3_2048x800_one_move():
         _replay(by[g][0], by[g][1], None)
 
 
-@pytest.mark.parametrize("algo", ["winograd48", "winograd"])
+@pytest.mark.parametrize("algo", ["winograd88", "winograd48", "winograd"])
 def test_c2_256x400_three_moves(algo):
     big = _run(256, 256, 400, 3, algo=algo)
     assert big[2]["sims"] == 256 * 3 * 400 and len(big[1]) == 256

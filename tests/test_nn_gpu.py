@@ -13,10 +13,10 @@ pytestmark = pytest.mark.gpu
 TOL_P, TOL_V = 1e-4, 1e-5
 
 
-# (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x4,3x3) / fp32 Winograd F(4x8,3x3) (the fp32
-# default above 16 boards) / f16x3 Winograd F(4x4) and F(4x8) (its default) / bf16x6 Winograd F(4x4) / bf16x3 direct
-MODES = [("fp32", "direct"), ("fp32", "winograd"), ("fp32", "winograd48"), ("f16x3", "winograd"),
-         ("f16x3", "winograd48"), ("bf16x6", "winograd"), ("bf16x3", "auto")]
+# (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x4,3x3) / fp32 Winograd F(4x8,3x3) / fp32
+# Winograd F(8x8,3x3) (the fp32 default above 16 boards) / f16x3 Winograd F(4x4) and F(4x8) (its default) / bf16x6 Winograd F(4x4) / bf16x3 direct
+MODES = [("fp32", "direct"), ("fp32", "winograd"), ("fp32", "winograd48"), ("fp32", "winograd88"),
+         ("f16x3", "winograd"), ("f16x3", "winograd48"), ("bf16x6", "winograd"), ("bf16x3", "auto")]
 
 
 def _net(variant, precision="fp32", algo="auto"):
@@ -75,7 +75,7 @@ def test_batch_invariance(precision):
     p_all, v_all = m(planes)  # 40 boards: whole-K class
     p_20, v_20 = m(planes[20:])
     assert torch.equal(p_20, p_all[20:]) and torch.equal(v_20, v_all[20:])
-    if precision in ("fp32", "f16x3"):  # fp32: 300 boards run the 128x128 GEMM tile, 40 the 64x128 tile: same bits
+    if precision in ("fp32", "f16x3"):  # f16x3 (F(4x8)): 300 boards run the 128-row GEMM tile, 40 the 64-row one
         codes_l = rng.integers(0, 13, size=(300, 64)) * (rng.random((300, 64)) < 0.4)
         codes_l[:40] = codes
         p_l, v_l = m(torch.from_numpy(codes_to_planes(codes_l)).cuda())
@@ -85,6 +85,21 @@ def test_batch_invariance(precision):
         p1, v1 = m(planes[i:i + 1])
         assert torch.equal(p1[0], p_16[i]) and torch.equal(v1[0], v_16[i])
     assert float((p_16 - p_all[:16]).abs().max()) < 1e-4
+
+
+def test_wino88_batch_invariance():
+    """F(8x8) (one row per board, batches padded to 64): a board's outputs are
+    the same bits at 20 / 40 / 300 boards (64x128 GEMM tiles) and 512 boards
+    (128x128 tiles)."""
+    from knightvision_amd.ai import codes_to_planes
+    rng = np.random.default_rng(88)
+    codes = rng.integers(0, 13, size=(512, 64)) * (rng.random((512, 64)) < 0.4)
+    planes = torch.from_numpy(codes_to_planes(codes)).cuda()
+    m = _net("peaked", "fp32", "winograd88")
+    p_l, v_l = m(planes)
+    for lo, hi in ((0, 40), (20, 40), (0, 300)):
+        p, v = m(planes[lo:hi])
+        assert torch.equal(p, p_l[lo:hi]) and torch.equal(v, v_l[lo:hi]), (lo, hi)
 
 
 @pytest.mark.parametrize("B", [17, 300, 2048])

@@ -28,7 +28,13 @@ F32 = np.float32
 
 
 def toom_cook(P, m, r=3):
-    """A^T [m][n], G [n][r], B^T [n][n] (exact) for points P + infinity, n = m + r - 1."""
+    """A^T [m][n], G [n][r], B^T [n][n] as float64 arrays for points P + infinity."""
+    f = lambda T: np.array([[float(x) for x in row] for row in T])  # noqa: E731
+    return tuple(f(T) for T in toom_cook_exact(P, m, r))
+
+
+def toom_cook_exact(P, m, r=3):
+    """A^T [m][n], G [n][r], B^T [n][n] (exact rationals) for points P + infinity, n = m + r - 1."""
     n = m + r - 1
     assert len(P) == n - 1
     AT = [[Fr(0)] * n for _ in range(m)]
@@ -75,8 +81,7 @@ def toom_cook(P, m, r=3):
     BT = [[sol[j * n + l] for l in range(n)] for j in range(n)]
     for i, k, l in itertools.product(range(m), range(r), range(n)):
         assert sum(AT[i][j] * G[j][k] * BT[j][l] for j in range(n)) == (1 if l == i + k else 0)
-    f = lambda T: np.array([[float(x) for x in row] for row in T])  # noqa: E731
-    return f(AT), f(G), f(BT)
+    return AT, G, BT
 
 
 P4 = [Fr(0), Fr(1), Fr(-1), Fr(2), Fr(-2)]
