@@ -45,7 +45,7 @@ FLOP_PER_EVAL = 3175744512            # SURVEY.md 8d, ChessNet forward per posit
 FLOP_RES_CONV_PER_BOARD = 301989888   # one 3x3 512->512 conv on 8x8 (2*64*512*4608)
 FLOP_WINO_GEMM_PER_BOARD = 75497472   # its Winograd F(4x4,3x3) GEMMs: 2 * 4 tiles * 36 * 512 * 512
 FLOP_WINO48_GEMM_PER_BOARD = 62914560  # its Winograd F(4x8,3x3) GEMMs: 2 * 2 tiles * 60 * 512 * 512
-FLOP_WINO88_GEMM_PER_BOARD = 52428800  # opt-in F(8x8,3x3) GEMMs: 2 * 1 tile * 100 * 512 * 512
+FLOP_WINO88_GEMM_PER_BOARD = 52428800  # the fp32 default, F(8x8,3x3) GEMMs: 2 * 1 tile * 100 * 512 * 512
 FP32_MFMA_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md, f32-input MFMA (dense)
 BF16_MFMA_PEAK_TFLOPS = 2500.0        # dense bf16 MFMA
 
@@ -60,7 +60,7 @@ def parse():
     ap.add_argument("--sims", type=int, default=800)
     ap.add_argument("--precision", choices=["fp32", "f16x3", "bf16x6", "bf16x3"], default="fp32")
     ap.add_argument("--algo", choices=["auto", "direct", "winograd", "winograd48", "winograd88"], default="auto",
-                    help="conv algorithm of the fp32 tower (auto: Winograd F(4x8,3x3) above 16 boards)")
+                    help="conv algorithm of the fp32 tower (auto: Winograd F(8x8,3x3) above 16 boards)")
     ap.add_argument("--compare-direct", type=int, default=0,
                     help="also measure the fp32 direct implicit-GEMM and F(4x4) towers ('fp32_direct', "
                          "'fp32_winograd44'; ~40 s per step at C3)")
@@ -224,6 +224,22 @@ def cpu_model() -> str:
     except OSError:
         pass
     return "unknown"
+
+
+def _w88_split_points(rows: int) -> int:
+    """Points of the F(8x8) GEMM layer run as 128x128 tiles (the rest as 64x128 tiles in a second launch):
+    the rule of kv_nn.hip wino88_split_points."""
+    if rows % 128 or os.environ.get("KV_W88_SPLIT", "1") == "0":
+        return 100
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    per_xi, slots = (rows // 128) * 4, 2 * cus
+    if (100 * per_xi) % slots % cus == 0:
+        return 100
+    xa = (100 * per_xi) // slots * slots // per_xi
+    while xa > 0 and (xa * per_xi) % slots:
+        xa -= 1
+    return xa if xa > 0 else 100
 
 
 def _pmc_traffic(kname: str, bpl: int):
@@ -400,6 +416,10 @@ def main():
         kname = ("wino_gemm_kernel<512,4,2,1,2,32,100>" if pad88 % 128 == 0
                  else "wino_gemm_kernel<512,2,2,1,2,16,100>")
         kdesc = " (residual-tower Winograd F(8x8,3x3) GEMMs, 100 points)"
+        xa = _w88_split_points(pad88)
+        if xa < 100:  # launch_wino88_gemm splits the points over two tile shapes (kv_nn.hip wino88_split_points)
+            kdesc = (f" points 0-{xa - 1} + wino_gemm_kernel<512,2,2,1,2,16,100> points {xa}-99 (residual-tower "
+                     "Winograd F(8x8,3x3) GEMM layer: two launches, both inside the timed events)")
     elif algo == 3:
         kname = ("wino_gemm_kernel<512,4,2,1,2,32,60>" if (pad * 2) % 128 == 0
                  else "wino_gemm_kernel<512,2,2,1,2,16,60>")

@@ -635,8 +635,11 @@ __global__ void encode_boards_kernel(const int8_t* __restrict__ boards, int nb, 
 // 0..31 / 32..63. WINO: the activated 8x8 planes go through LDS to the tile
 // transforms -- wave w writes board w/2's tile w%2 (F(4x8)) or tiles 2(w%2),
 // 2(w%2)+1 (F(4x4)) of conv2's Winograd input V [points][rows][256]; else
-// NHWC T [board][64][256]. F(4x8) skips the plane (below).
-template <int WINO>  // 0: NHWC out, 1: F(4x4) V of conv2, 2: F(4x8) V of conv2
+// NHWC T [board][64][256]. F(4x8) skips the plane (below). F(8x8): thread
+// (w % 2) of a (board, channel) plane stores rows 5(w % 2) .. 5(w % 2) + 4 of its
+// 10x10 transform (the column pass is done by both: same operations, same bits
+// as wino88_in_kernel over T).
+template <int WINO>  // 0: NHWC out, 1: F(4x4) V of conv2, 2: F(4x8) V of conv2, 3: F(8x8) V of conv2
 __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ boards, int nb,
                                                    const float* __restrict__ wT, const float* __restrict__ scale,
                                                    const float* __restrict__ shift, float* __restrict__ out,
@@ -725,7 +728,15 @@ __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ bo
     if (!WINO) return;
     __syncthreads();
     float mx = 0.f;
-    if (WINO == 2) {
+    if constexpr (WINO == 3) {
+        const auto px = [&](int p) { return plane[bb][p][cl]; };
+        const size_t off = (size_t)b * 256 + c, xs = (size_t)rows * 256;
+        if (w & 1)
+            wino88_input_rows<5, 5>(px, out, off, xs);
+        else
+            wino88_input_rows<0, 5>(px, out, off, xs);
+        return;
+    } else if (WINO == 2) {
         const int tile = w & 1;
         float d48[60];
 #pragma unroll
@@ -971,7 +982,8 @@ static int net_heads(kv_net* net, int nb, float* policy, float* value, hipStream
 
 // LDS_PAD: dynamic LDS requested beyond the tiles' need, to cap workgroups per CU
 template <int K, int WR, int WC, int MT, int NT, int CK = 32, int LDS_PAD = 0, int XI = kv::WN_XI>
-static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
+static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st,
+                              int xi0 = 0, int nxi = XI) {
     using T = kv::WinoTile<WR, WC, MT, NT, CK>;
     constexpr size_t bytes = T::BYTES + LDS_PAD;
     static bool attr_set = false;
@@ -980,10 +992,11 @@ static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
         attr_set = true;
     }
-    const int nwg = XI * (rows / T::WM) * (512 / T::WN);
-    KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0, KV_EINVAL, "wino gemm: rows %d vs tile %d", rows, T::WM);
+    const int nwg = nxi * (rows / T::WM) * (512 / T::WN);
+    KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0 && xi0 >= 0 && nxi > 0 && xi0 + nxi <= XI, KV_EINVAL,
+               "wino gemm: rows %d vs tile %d, points [%d, %d)", rows, T::WM, xi0, xi0 + nxi);
     hipLaunchKernelGGL((kv::wino_gemm_kernel<K, WR, WC, MT, NT, CK, XI>), dim3(nwg), dim3(T::THREADS), bytes, st, V,
-                       U, M, rows, 512, stride);
+                       U, M, rows, 512, stride, xi0);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -1185,9 +1198,44 @@ static int wino48_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 
 // F(8x8) GEMMs (100 points, rows = 1 per board, a multiple of 64): 128x128 tiles when the
 // rows allow, else 64x128; same k order, same bits
+// Round filling: the 128x128 tiles of the first points fill whole rounds of the resident
+// slots (2 per CU); the points left over run as 64x128 tiles (3 per CU) in a second launch
+// when the one-launch grid would end on a last round that leaves CUs idle or doubles up on a
+// few of them. 256 boards: 800 tiles = 1.56 rounds (288 tiles in the last: 32 CUs run two)
+// -> points 0-63 in one round + points 64-99 as 576 half tiles: forward 1.64 -> 1.53 ms;
+// 1,024 boards: 6.25 rounds (128 CUs idle in the last) -> 96 points + 256 half tiles: 5.36
+// -> 5.31 ms. At 2,048 boards the last round is one tile per CU, which the half tiles do
+// not beat (10.25 vs 10.32 ms), so it stays one launch. Same k order, same bits
+// (profiles/r03_w88split_ab.log). KV_W88_SPLIT=0 turns it off.
+static int wino88_split_points(int rows) {
+    static int mode = -1, cus = 0;
+    if (mode < 0) {
+        const char* e = getenv("KV_W88_SPLIT");
+        mode = e ? atoi(e) : 1;
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 0;
+    }
+    if (!mode || cus <= 0) return kv::W88_XI;
+    const int per_xi = (rows / 128) * 4, slots = 2 * cus;
+    const int rem = (kv::W88_XI * per_xi) % slots;  // tiles of the last round
+    if (rem % cus == 0) return kv::W88_XI;           // whole rounds, or one tile on every CU
+    const int full = (kv::W88_XI * per_xi) / slots * slots;  // tiles in whole rounds
+    int xa = full / per_xi;
+    while (xa > 0 && (xa * per_xi) % slots) --xa;
+    return xa > 0 ? xa : kv::W88_XI;
+}
+
 template <int K>
 static int launch_wino88_gemm(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
-    if (rows % 128 == 0) return launch_wino_gemm_t<K, 4, 2, 1, 2, 32, 0, kv::W88_XI>(V, U, M, rows, stride, st);
+    if (rows % 128 == 0) {
+        const int xa = wino88_split_points(rows);
+        int rc = launch_wino_gemm_t<K, 4, 2, 1, 2, 32, 0, kv::W88_XI>(V, U, M, rows, stride, st, 0, xa);
+        if (rc || xa == kv::W88_XI) return rc;
+        return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720, kv::W88_XI>(V, U, M, rows, stride, st, xa,
+                                                                                   kv::W88_XI - xa);
+    }
     return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720, kv::W88_XI>(V, U, M, rows, stride, st);
 }
 
@@ -1286,12 +1334,12 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
     if (wino && net->precision == KV_PREC_F16X3)
         KV_HIP(hipMemsetAsync(net->vmax, 0, (size_t)12 * net->cap * sizeof(unsigned), st));
-    // F(8x8): the stem writes NHWC and wino88_in_kernel builds conv2's V
+    // F(8x8): the stem builds conv2's V itself (stem_kernel<3>)
     const bool w88 = wino && use_wino88(net, nb);
     if (boards) {
         if (w88)
-            hipLaunchKernelGGL(kv::stem_kernel<0>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
-                               W + o.scale[0], W + o.shift[0], net->T, nb_pad * 4, nullptr);
+            hipLaunchKernelGGL(kv::stem_kernel<3>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
+                               W + o.scale[0], W + o.shift[0], net->V256, nb_pad, nullptr);
         else if (wino && use_wino48(net, nb))
             hipLaunchKernelGGL(kv::stem_kernel<2>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], net->V256, nb_pad * 2, net_vmax(net, 1));
@@ -1307,7 +1355,7 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
         return rc;
     }
     if (wino) {
-        if ((rc = net_tower_wino(net, nb_pad, boards != nullptr && !w88, st))) return rc;
+        if ((rc = net_tower_wino(net, nb_pad, boards != nullptr, st))) return rc;
         return net_heads(net, nb, policy, value, st);
     }
     const bool bf3 = net->precision == KV_PREC_BF16X3;

@@ -230,7 +230,7 @@ template <int K, int WR, int WC, int MT, int NT, int CK = 32, int XI = WN_XI>
 __global__ __launch_bounds__(WR * WC * 64) void wino_gemm_kernel(const float* __restrict__ V,
                                                                    const float* __restrict__ U,
                                                                    float* __restrict__ M, int rows, int cout,
-                                                                   int stride) {
+                                                                   int stride, int xi0 = 0) {
     using T = WinoTile<WR, WC, MT, NT, CK>;
     constexpr int WM = T::WM, WN = T::WN, TH = T::THREADS;
     constexpr int PS = T::PS;
@@ -253,11 +253,13 @@ __global__ __launch_bounds__(WR * WC * 64) void wino_gemm_kernel(const float* __
     // XCD-aware tile order: blocks b and b+8 share an XCD (round-robin
     // dealing), so each group of 8 gets a contiguous run of the xi-major tile
     // order -- the 4 column tiles of a row panel and the row panels of one xi
-    // run on one XCD and re-read V / U from its L2 instead of HBM.
+    // run on one XCD and re-read V / U from its L2 instead of HBM. A launch
+    // covers the points [xi0, xi0 + gridDim.x / (RT * CT)) (F(8x8) splits its
+    // 100 points over two tile shapes so that no round of tiles is left half full).
     const int CT = cout / WN, RT = rows / WM;
-    const int nwg = XI * RT * CT;  // a multiple of 8 (36 or 60 points x 4 column tiles x RT)
+    const int nwg = (int)gridDim.x;  // a multiple of 8 (points x 4 column tiles x RT)
     const int idx = (int)(blockIdx.x & 7) * (nwg >> 3) + (int)(blockIdx.x >> 3);
-    const int xi = idx / (CT * RT);
+    const int xi = xi0 + idx / (CT * RT);
     const int n_base = (idx % CT) * WN;
     const int r_base = ((idx / CT) % RT) * WM;
     const float* Va = V + ((size_t)xi * stride + r_base) * K;

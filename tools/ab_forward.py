@@ -18,15 +18,16 @@ m = ChessNet()
 m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(42, "bn").items()})
 m.eval()
 net = m.kv_net(0)
-os.makedirs("gpurun_out", exist_ok=True)
+OUT = os.environ.get("AB_DIR", "gpurun_out")  # the saved outputs: 2048-board logits are 32 MB each
+os.makedirs(OUT, exist_ok=True)
 for B in [int(a) for a in sys.argv[2:]]:
     g = torch.Generator().manual_seed(B)
     codes = torch.randint(0, 13, (B, 64), dtype=torch.int8, generator=g).cuda()
     for _ in range(3):
         p, v = net.forward_boards(codes)
     torch.cuda.synchronize()
-    np.save(f"gpurun_out/ab_{tag}_{B}_p.npy", p.cpu().numpy())
-    np.save(f"gpurun_out/ab_{tag}_{B}_v.npy", v.cpu().numpy())
+    np.save(f"{OUT}/ab_{tag}_{B}_p.npy", p.cpu().numpy())
+    np.save(f"{OUT}/ab_{tag}_{B}_v.npy", v.cpu().numpy())
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     best = []
     for rep in range(3):

@@ -2,7 +2,7 @@
 (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950: FETCH_SIZE counts half of a wide
 coalesced read, MI355X_MICROARCH.md HBM section).
 
-    python tools/pmc_summary.py FETCH_GLOB WRITE_GLOB BATCH [resconv|wino_gemm|wino48_gemm]
+    python tools/pmc_summary.py FETCH_GLOB WRITE_GLOB BATCH [resconv|wino_gemm|wino48_gemm|wino88_gemm]
 """
 import csv
 import glob
@@ -13,6 +13,7 @@ KERNELS = {
     "resconv": ("conv3x3_kernel<512,32", "conv3x3_kernel<512,32,*>"),
     "wino_gemm": ("wino_gemm_kernel<512,2,2,1,2,16,36>", "wino_gemm_kernel<512,2,2,1,2,16,36>"),
     "wino48_gemm": ("wino_gemm_kernel<512,4,2,1,2,32,60>", "wino_gemm_kernel<512,4,2,1,2,32,60>"),
+    "wino88_gemm": ("wino_gemm_kernel<512,4,2,1,2,32,100>", "wino_gemm_kernel<512,4,2,1,2,32,100>"),
 }
 
 
@@ -28,7 +29,7 @@ def load(pattern, counter, sub):
 def algorithmic_bytes(kind, B):
     if kind == "resconv":  # activations in + out, weights once
         return B * 64 * 512 * 4 * 2 + 512 * 9 * 512 * 4
-    xi, rows = (60, 2 * B) if kind == "wino48_gemm" else (36, 4 * B)  # V read + M write over the GEMMs, U once
+    xi, rows = {"wino48_gemm": (60, 2 * B), "wino88_gemm": (100, B)}.get(kind, (36, 4 * B))  # V read + M write over the GEMMs, U once
     return xi * rows * 512 * 4 * 2 + xi * 512 * 512 * 4
 
 
