@@ -18,6 +18,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+#include <set>
+#include <utility>
+
 #include "kv_common.h"
 #include "kv_wino.h"
 #include "kv_wino48.h"
@@ -872,19 +876,30 @@ static int launch_reduce(const float* slab, int splits, int rows, int cout, cons
     return KV_OK;
 }
 
+// Large dynamic-LDS opt-in, per (kernel, device): hipFuncSetAttribute applies to
+// the current device only, so a process that uses several GPUs opts in on each
+// (a process-wide flag would leave the second device without it). Guarded by a
+// mutex; a launch pays one map lookup.
+static hipError_t lds_opt_in(const void* fn, int bytes) {
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> g(mu);
+    if (done.count({fn, dev})) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done.insert({fn, dev});
+    return e;
+}
+
 template <int CIN, bool RESID>
 static int launch_conv_bf3(const float* in, const uint16_t* whi, const uint16_t* wlo, const float* sc,
                            const float* sh, const float* resid, float* out, int cout, int nb_pad, float* slab,
                            hipStream_t st) {
     using G = kv::Bf3Lds<CIN>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        KV_HIP(hipFuncSetAttribute((const void*)kv::conv3x3_bf16x3_kernel<CIN, RESID>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::BYTES));
-        KV_HIP(hipFuncSetAttribute((const void*)kv::conv3x3_bf16x3_kernel<CIN, false>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::BYTES));
-        attr_set = true;
-    }
+    KV_HIP(lds_opt_in((const void*)kv::conv3x3_bf16x3_kernel<CIN, RESID>, (int)G::BYTES));
+    KV_HIP(lds_opt_in((const void*)kv::conv3x3_bf16x3_kernel<CIN, false>, (int)G::BYTES));
     const int nk = 9 * (CIN / 32);
     const int kt_per = slab ? split_kt(nb_pad) : 0;
     if (kt_per) {
@@ -905,14 +920,8 @@ template <int CIN, int CK, bool RESID>
 static int launch_conv(const float* in, const float* w, const float* sc, const float* sh, const float* resid,
                        float* out, int cout, int nb_pad, float* slab, hipStream_t st) {
     using G = kv::ConvLds<CIN, CK>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        KV_HIP(hipFuncSetAttribute((const void*)kv::conv3x3_kernel<CIN, CK, RESID>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::BYTES));
-        KV_HIP(hipFuncSetAttribute((const void*)kv::conv3x3_kernel<CIN, CK, false>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::BYTES));
-        attr_set = true;
-    }
+    KV_HIP(lds_opt_in((const void*)kv::conv3x3_kernel<CIN, CK, RESID>, (int)G::BYTES));
+    KV_HIP(lds_opt_in((const void*)kv::conv3x3_kernel<CIN, CK, false>, (int)G::BYTES));
     const int nk = 9 * (CIN / CK);
     const int kt_per = slab ? split_kt(nb_pad) : 0;
     if (kt_per) {
@@ -986,12 +995,7 @@ static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows
                               int xi0 = 0, int nxi = XI) {
     using T = kv::WinoTile<WR, WC, MT, NT, CK>;
     constexpr size_t bytes = T::BYTES + LDS_PAD;
-    static bool attr_set = false;
-    if (!attr_set) {
-        KV_HIP(hipFuncSetAttribute((const void*)kv::wino_gemm_kernel<K, WR, WC, MT, NT, CK, XI>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-        attr_set = true;
-    }
+    KV_HIP(lds_opt_in((const void*)kv::wino_gemm_kernel<K, WR, WC, MT, NT, CK, XI>, (int)bytes));
     const int nwg = nxi * (rows / T::WM) * (512 / T::WN);
     KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0 && xi0 >= 0 && nxi > 0 && xi0 + nxi <= XI, KV_EINVAL,
                "wino gemm: rows %d vs tile %d, points [%d, %d)", rows, T::WM, xi0, xi0 + nxi);
@@ -1036,12 +1040,7 @@ template <int K, int TM, int XI = kv::WN_XI, int RSH = 2>
 static int launch_wino_gemm_h3_t(const float* V, const uint16_t* Uh, const uint16_t* Ul, const unsigned* vmax,
                                  float* M, int rows, int stride, hipStream_t st) {
     using T = kv::WinoH3<TM>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        KV_HIP(hipFuncSetAttribute((const void*)kv::wino_gemm_h3_kernel<K, TM, XI, RSH>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::BYTES));
-        attr_set = true;
-    }
+    KV_HIP(lds_opt_in((const void*)kv::wino_gemm_h3_kernel<K, TM, XI, RSH>, (int)T::BYTES));
     const int nwg = XI * (rows / T::WM) * (512 / T::WN);
     KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0, KV_EINVAL, "wino gemm f16x3: rows %d", rows);
     hipLaunchKernelGGL((kv::wino_gemm_h3_kernel<K, TM, XI, RSH>), dim3(nwg), dim3(256), T::BYTES, st, V, Uh, Ul, vmax,
@@ -1064,12 +1063,7 @@ template <int K>
 static int launch_wino_gemm_bf6(const float* V, const uint16_t* Uh, const uint16_t* Um, const uint16_t* Ul, float* M,
                                 int rows, int stride, hipStream_t st) {
     using T = kv::WinoBf6;
-    static bool attr_set = false;
-    if (!attr_set) {
-        KV_HIP(hipFuncSetAttribute((const void*)kv::wino_gemm_bf6_kernel<K>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)T::BYTES));
-        attr_set = true;
-    }
+    KV_HIP(lds_opt_in((const void*)kv::wino_gemm_bf6_kernel<K>, (int)T::BYTES));
     const int nwg = kv::WN_XI * (rows / T::WM) * (512 / T::WN);
     KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0, KV_EINVAL, "wino gemm bf16x6: rows %d", rows);
     hipLaunchKernelGGL((kv::wino_gemm_bf6_kernel<K>), dim3(nwg), dim3(256), T::BYTES, st, V, Uh, Um, Ul, M, rows, 512,
@@ -1208,15 +1202,14 @@ static int wino48_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 // not beat (10.25 vs 10.32 ms), so it stays one launch. Same k order, same bits
 // (profiles/r03_w88split_ab.log). KV_W88_SPLIT=0 turns it off.
 static int wino88_split_points(int rows) {
-    static int mode = -1, cus = 0;
-    if (mode < 0) {
+    static const int mode = [] {  // thread-safe one-time initialisation
         const char* e = getenv("KV_W88_SPLIT");
-        mode = e ? atoi(e) : 1;
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 0;
-    }
+        return e ? atoi(e) : 1;
+    }();
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 0;
     if (!mode || cus <= 0) return kv::W88_XI;
     const int per_xi = (rows / 128) * 4, slots = 2 * cus;
     const int rem = (kv::W88_XI * per_xi) % slots;  // tiles of the last round
