@@ -226,13 +226,14 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def _w88_split_points(rows: int) -> int:
+def _w88_split_points(rows: int, cus: int = 0) -> int:
     """Points of the F(8x8) GEMM layer run as 128x128 tiles (the rest as 64x128 tiles in a second launch):
-    the rule of kv_nn.hip wino88_split_points."""
+    the rule of kv_nn.hip wino88_split_points (cus = the device's CU count; 0: ask the device)."""
     if rows % 128 or os.environ.get("KV_W88_SPLIT", "1") == "0":
         return 100
-    import torch
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    if not cus:
+        import torch
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
     per_xi, slots = (rows // 128) * 4, 2 * cus
     if (100 * per_xi) % slots % cus == 0:
         return 100

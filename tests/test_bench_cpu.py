@@ -32,6 +32,22 @@ def test_tree_summary_is_at_c3_sims():
 def test_gemm_traffic_summary_present():
     t, f = bench._pmc_traffic("wino_gemm_kernel<512,4,2,1,2,32,60>", 2048)
     assert t is not None and t > 1.0e9
+    # the default fp32 tower's GEMM (F(8x8)) at C3's 2,048 boards: 0.94 GB algorithmic per launch
+    t, f = bench._pmc_traffic("wino_gemm_kernel<512,4,2,1,2,32,100>", 2048)
+    assert t is not None and 0.94e9 <= t < 1.2e9
+
+
+@pytest.mark.parametrize("rows,cus,xa", [(2048, 256, 100), (1024, 256, 96), (512, 256, 96), (256, 256, 64),
+                                         (384, 256, 100), (128, 256, 100), (64, 256, 100), (2048, 304, 95)])
+def test_w88_split_rule(monkeypatch, rows, cus, xa):
+    """bench.py's label of the F(8x8) GEMM layer mirrors kv_nn.hip wino88_split_points: the points whose
+    128x128 tiles fill whole rounds of 2 workgroups per CU, unless the last round of the one-launch grid is
+    empty or puts exactly one tile on every CU (then one launch)."""
+    monkeypatch.delenv("KV_W88_SPLIT", raising=False)
+    got = bench._w88_split_points(rows, cus)
+    assert got == xa
+    if got < 100:
+        assert (got * (rows // 128) * 4) % (2 * cus) == 0
 
 
 @pytest.mark.parametrize("sims", [0, 8])
