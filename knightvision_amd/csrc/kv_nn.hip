@@ -1224,7 +1224,11 @@ template <int K>
 static int launch_wino88_gemm(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
     if (rows % 128 == 0) {
         const int xa = wino88_split_points(rows);
+#ifdef KV_W88_K16  // A/B probe: 128x128 tiles with k-tiles of 16 (40 KB of LDS: 3 workgroups per CU)
+        int rc = launch_wino_gemm_t<K, 4, 2, 1, 2, 16, 0, kv::W88_XI>(V, U, M, rows, stride, st, 0, xa);
+#else
         int rc = launch_wino_gemm_t<K, 4, 2, 1, 2, 32, 0, kv::W88_XI>(V, U, M, rows, stride, st, 0, xa);
+#endif
         if (rc || xa == kv::W88_XI) return rc;
         return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720, kv::W88_XI>(V, U, M, rows, stride, st, xa,
                                                                                    kv::W88_XI - xa);
