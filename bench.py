@@ -413,9 +413,12 @@ def main():
     # the library picks the GEMM tile by rows (knightvision_amd/csrc/kv_nn.hip launch_wino_gemm / launch_wino48_gemm)
     pad = (bpl + 31) // 32 * 32
     if algo == 4:
-        pad88 = (bpl + 63) // 64 * 64
+        pad88 = (bpl + 31) // 32 * 32
+        pad88 = pad88 if pad88 in (32, 96) else (bpl + 63) // 64 * 64  # kv_nn.hip net_pad
         kname = ("wino_gemm_kernel<512,4,2,1,2,32,100>" if pad88 % 128 == 0
-                 else "wino_gemm_kernel<512,2,2,1,2,16,100>")
+                 else "wino_gemm_kernel<512,2,2,1,2,16,100>" if pad88 % 64 == 0
+                 else "wino_gemm_kernel<512,1,2,1,2,32,100>" if pad88 == 32
+                 else "wino_gemm_kernel<512,1,2,1,2,16,100>")
         kdesc = " (residual-tower Winograd F(8x8,3x3) GEMMs, 100 points)"
         xa = _w88_split_points(pad88)
         if xa < 100:  # launch_wino88_gemm splits the points over two tile shapes (kv_nn.hip wino88_split_points)

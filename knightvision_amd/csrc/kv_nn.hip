@@ -959,9 +959,14 @@ static bool use_wino48(const kv_net* net, int B) {
 }
 
 // padded batch: a multiple of 4 boards (direct tiles), 32 (128-row GEMM tiles of 2 rows per
-// board) or 64 (F(8x8): one row per board, 64- or 128-row tiles)
+// board) or F(8x8)'s one row per board: 32 / 96 boards (32-row tiles: forward 0.556 -> 0.522 ms at
+// <= 32 boards, 0.895 -> 0.783 at 65-96) else a multiple of 64 (at 160 boards the 32-row tiles were
+// 1.26 -> 1.38 ms slower than padding to 192; profiles/r03_w88_rows32_ab.log)
 static int net_pad(const kv_net* net, int B) {
-    if (use_wino88(net, B)) return (B + 63) & ~63;
+    if (use_wino88(net, B)) {  // 32 and 96 rows run 32-row GEMM tiles: faster there, slower at 160 (measured)
+        const int p32 = (B + 31) & ~31;
+        return (p32 == 32 || p32 == 96) ? p32 : (B + 63) & ~63;
+    }
     return use_wino(net, B) ? (B + 31) & ~31 : (B + 3) & ~3;
 }
 
@@ -1224,16 +1229,18 @@ template <int K>
 static int launch_wino88_gemm(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
     if (rows % 128 == 0) {
         const int xa = wino88_split_points(rows);
-#ifdef KV_W88_K16  // A/B probe: 128x128 tiles with k-tiles of 16 (40 KB of LDS: 3 workgroups per CU)
-        int rc = launch_wino_gemm_t<K, 4, 2, 1, 2, 16, 0, kv::W88_XI>(V, U, M, rows, stride, st, 0, xa);
-#else
         int rc = launch_wino_gemm_t<K, 4, 2, 1, 2, 32, 0, kv::W88_XI>(V, U, M, rows, stride, st, 0, xa);
-#endif
         if (rc || xa == kv::W88_XI) return rc;
         return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720, kv::W88_XI>(V, U, M, rows, stride, st, xa,
                                                                                    kv::W88_XI - xa);
     }
-    return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720, kv::W88_XI>(V, U, M, rows, stride, st);
+    if (rows % 64 == 0)
+        return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720, kv::W88_XI>(V, U, M, rows, stride, st);
+    // 32-row tiles (2 waves of 32x64): batches of <= 32 and 65-96 boards (net_pad), below one round of
+    // tiles, where the time is the padded work per CU; k-tiles of 32 at 32 rows (forward 0.537 -> 0.522
+    // ms), of 16 at 96 (0.783 vs 0.915 ms; profiles/r03_w88_rows32_ck_ab.log)
+    if (rows == 32) return launch_wino_gemm_t<K, 1, 2, 1, 2, 32, 0, kv::W88_XI>(V, U, M, rows, stride, st);
+    return launch_wino_gemm_t<K, 1, 2, 1, 2, 16, 0, kv::W88_XI>(V, U, M, rows, stride, st);
 }
 
 template <bool RESID, bool WRITE_Y, bool NEXT_V>
