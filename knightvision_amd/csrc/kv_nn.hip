@@ -22,6 +22,10 @@
 #include <set>
 #include <utility>
 
+#ifndef KV_STEM88
+#define KV_STEM88 4
+#endif
+
 #include "kv_common.h"
 #include "kv_wino.h"
 #include "kv_wino48.h"
@@ -643,7 +647,7 @@ __global__ void encode_boards_kernel(const int8_t* __restrict__ boards, int nb, 
 // (w % 2) of a (board, channel) plane stores rows 5(w % 2) .. 5(w % 2) + 4 of its
 // 10x10 transform (the column pass is done by both: same operations, same bits
 // as wino88_in_kernel over T).
-template <int WINO>  // 0: NHWC out, 1: F(4x4) V of conv2, 2: F(4x8) V of conv2, 3: F(8x8) V of conv2
+template <int WINO>  // 0: NHWC out, 1: F(4x4) V of conv2, 2: F(4x8) V of conv2, 3 / 4: F(8x8) V of conv2
 __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ boards, int nb,
                                                    const float* __restrict__ wT, const float* __restrict__ scale,
                                                    const float* __restrict__ shift, float* __restrict__ out,
@@ -669,6 +673,27 @@ __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ bo
     for (int it = 0; it < 30; ++it)
         if (w + 4 * it < 9 * 13) wl[w + 4 * it][cl] = wv[it];
     __syncthreads();
+    if constexpr (WINO == 4) {
+        // F(8x8) without the plane exchange: a wave holds 32 channels of one board, lane half h the
+        // plane rows 4h .. 4h+3 of its channel (the same sums as below), and the two halves finish the
+        // transform by lane swaps (wino88_input_half): no 32 KB plane in LDS, so more workgroups per CU
+        const int h = cl >> 5, bb4 = w >> 1, b4 = b0 + bb4;
+        const int ch = (w & 1) * 32 + (cl & 31), c4 = blockIdx.x * 64 + ch;
+        const float sc4 = scale[c4], sh4 = shift[c4];
+        float x2[4][8];
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+            for (int px = 0; px < 8; ++px) {
+                const int py = 4 * h + ii;
+                float acc = 0.f;
+#pragma unroll
+                for (int t = 0; t < 9; ++t) acc += wl[t * 13 + codes[bb4][(py + t / 3) * 10 + px + t % 3]][ch];
+                const float v = acc * sc4 + sh4;
+                x2[ii][px] = v > 0.f ? v : 0.f;
+            }
+        wino88_input_half(x2, h, out, (size_t)b4 * 256 + c4, (size_t)rows * 256);
+    } else {
     const float sc = scale[c], sh = shift[c];
     const int bb = w >> 1, b = b0 + bb;
     if constexpr (WINO == 2) {
@@ -770,6 +795,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ bo
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
         if (cl == 0) atomicMax(vmax + b, __float_as_uint(mx));
+    }
     }
     }
 }
@@ -1342,7 +1368,7 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     const bool w88 = wino && use_wino88(net, nb);
     if (boards) {
         if (w88)
-            hipLaunchKernelGGL(kv::stem_kernel<3>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
+            hipLaunchKernelGGL(kv::stem_kernel<KV_STEM88>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], net->V256, nb_pad, nullptr);
         else if (wino && use_wino48(net, nb))
             hipLaunchKernelGGL(kv::stem_kernel<2>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
