@@ -1230,7 +1230,8 @@ static int wino48_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 // -> points 0-63 in one round + points 64-99 as 576 half tiles: forward 1.64 -> 1.53 ms;
 // 1,024 boards: 6.25 rounds (128 CUs idle in the last) -> 96 points + 256 half tiles: 5.36
 // -> 5.31 ms. At 2,048 boards the last round is one tile per CU, which the half tiles do
-// not beat (10.25 vs 10.32 ms), so it stays one launch. Same k order, same bits
+// not beat (10.25 vs 10.32 ms), so it stays one launch; nor do 64x64 or 128x64 tiles for its last
+// 4 points (10.42-10.49 vs 10.39-10.42 ms, profiles/r03_w88_tail_ab.log). Same k order, same bits
 // (profiles/r03_w88split_ab.log). KV_W88_SPLIT=0 turns it off.
 static int wino88_split_points(int rows) {
     static const int mode = [] {  // thread-safe one-time initialisation
