@@ -88,16 +88,17 @@ def test_batch_invariance(precision):
 
 
 def test_wino88_batch_invariance():
-    """F(8x8) (one row per board, batches padded to 64): a board's outputs are
-    the same bits at 20 / 40 / 300 boards (64x128 GEMM tiles) and 512 boards
-    (128x128 tiles)."""
+    """F(8x8) (one row per board): a board's outputs are the same bits at 20
+    boards (padded to 32: 32-row GEMM tiles, k-tiles of 32), 80 / 96 (padded to
+    96: 32-row tiles, k-tiles of 16), 40 / 300 (padded to 64 / 320: 64x128
+    tiles) and 512 boards (128x128 tiles for points 0-95, 64x128 for 96-99)."""
     from knightvision_amd.ai import codes_to_planes
     rng = np.random.default_rng(88)
     codes = rng.integers(0, 13, size=(512, 64)) * (rng.random((512, 64)) < 0.4)
     planes = torch.from_numpy(codes_to_planes(codes)).cuda()
     m = _net("peaked", "fp32", "winograd88")
     p_l, v_l = m(planes)
-    for lo, hi in ((0, 40), (20, 40), (0, 300)):
+    for lo, hi in ((0, 40), (20, 40), (0, 300), (0, 96), (16, 96)):
         p, v = m(planes[lo:hi])
         assert torch.equal(p, p_l[lo:hi]) and torch.equal(v, v_l[lo:hi]), (lo, hi)
 
