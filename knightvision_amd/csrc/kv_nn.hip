@@ -1365,7 +1365,7 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
     if (wino && net->precision == KV_PREC_F16X3)
         KV_HIP(hipMemsetAsync(net->vmax, 0, (size_t)12 * net->cap * sizeof(unsigned), st));
-    // F(8x8): the stem builds conv2's V itself (stem_kernel<3>)
+    // F(8x8): the stem builds conv2's V itself (stem_kernel<KV_STEM88>: 4, the lane-swap form; 3, the LDS-plane form)
     const bool w88 = wino && use_wino88(net, nb);
     if (boards) {
         if (w88)
