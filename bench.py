@@ -43,10 +43,12 @@ sys.path.insert(0, HERE)
 
 FLOP_PER_EVAL = 3175744512            # SURVEY.md 8d, ChessNet forward per position
 FLOP_RES_CONV_PER_BOARD = 301989888   # one 3x3 512->512 conv on 8x8 (2*64*512*4608)
-FLOP_WINO_GEMM_PER_BOARD = 75497472   # its Winograd F(4x4,3x3) GEMMs: 2 * 4 tiles * 36 * 512 * 512
 FLOP_WINO48_GEMM_PER_BOARD = 62914560  # its Winograd F(4x8,3x3) GEMMs: 2 * 2 tiles * 60 * 512 * 512
 FLOP_WINO88_GEMM_PER_BOARD = 52428800  # the fp32 default, F(8x8,3x3) GEMMs: 2 * 1 tile * 100 * 512 * 512
 FP32_MFMA_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md, f32-input MFMA (dense)
+FP64_MFMA_PEAK_TFLOPS = 78.6          # AMD's MI355X FP64 matrix figure (the guides give no f64 row; measured in
+                                      # profiles/r04_f64_mfma_peak.log)
+PATH_NAMES = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3"}  # KV_PATH_*
 BF16_MFMA_PEAK_TFLOPS = 2500.0        # dense bf16 MFMA
 
 
@@ -58,12 +60,15 @@ def parse():
     ap.add_argument("--mode", choices=["mcts", "ref"], default=os.environ.get("KV_BENCH_MODE", "mcts"))
     ap.add_argument("--slots", type=int, default=2048)
     ap.add_argument("--sims", type=int, default=800)
-    ap.add_argument("--precision", choices=["fp32", "f16x3", "bf16x6", "bf16x3"], default="fp32")
-    ap.add_argument("--algo", choices=["auto", "direct", "winograd", "winograd48", "winograd88"], default="auto",
-                    help="conv algorithm of the fp32 tower (auto: Winograd F(8x8,3x3) above 16 boards)")
+    ap.add_argument("--precision", choices=["fp32", "f16x3", "f64w"], default="fp32")
+    ap.add_argument("--algo", choices=["auto", "direct", "winograd48", "winograd88"], default="auto",
+                    help="conv algorithm of the fp32 tower (auto: the library's calibrated choice per weight load -- "
+                         "Winograd F(8x8,3x3) fp32 for the random-init weights)")
     ap.add_argument("--compare-direct", type=int, default=0,
-                    help="also measure the fp32 direct implicit-GEMM and F(4x4) towers ('fp32_direct', "
-                         "'fp32_winograd44'; ~40 s per step at C3)")
+                    help="also measure the fp32 direct implicit-GEMM tower ('fp32_direct'; ~40 s per step at C3)")
+    ap.add_argument("--f64w-steps", type=int, default=2,
+                    help="fp32 headline: also time this many moves with the fp64 Winograd domain (KV_PREC_F64W, the "
+                         "AUTO path for trained-magnitude weights), reported under 'trained_weights_path'; 0 to skip")
     ap.add_argument("--alt-precision", default="f16x3",
                     help="also measure this network precision (reported under 'alt_precision'; '' to skip)")
     ap.add_argument("--alt-algo", default="winograd48",
@@ -121,6 +126,26 @@ def launch_ranks(n: int) -> int:
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     return subprocess.call(cmd, env=env)
+
+
+def process_group_info(rank: int, world: int, local: int, backend: str) -> dict:
+    """What the N-rank run actually was: the process group's size and backend and, per rank, its host and GPU
+    (PCI domain / bus / device of the device it bound). Under nccl (RCCL) two ranks on one GPU are an error:
+    the scaling line must come from N distinct GPUs."""
+    import torch.distributed as dist
+    props = torch.cuda.get_device_properties(local)
+    pci = [int(getattr(props, k, -1)) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id")]
+    me = {"rank": rank, "host": socket.gethostname(), "local_device": local, "pci": pci, "name": props.name}
+    ranks = [None] * world
+    dist.all_gather_object(ranks, me)
+    if backend == "nccl":
+        seen = {}
+        for r in ranks:
+            key = (r["host"], tuple(r["pci"])) if -1 not in r["pci"] else (r["host"], "device", r["local_device"])
+            if key in seen:
+                raise SystemExit(f"bench.py: ranks {seen[key]} and {r['rank']} share one GPU {key} under nccl")
+            seen[key] = r["rank"]
+    return {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "ranks": ranks}
 
 
 def host_cpu() -> dict:
@@ -226,21 +251,33 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def _w88_split_points(rows: int, cus: int = 0) -> int:
-    """Points of the F(8x8) GEMM layer run as 128x128 tiles (the rest as 64x128 tiles in a second launch):
-    the rule of kv_nn.hip wino88_split_points (cus = the device's CU count; 0: ask the device)."""
-    if rows % 128 or os.environ.get("KV_W88_SPLIT", "1") == "0":
-        return 100
-    if not cus:
-        import torch
-        cus = torch.cuda.get_device_properties(0).multi_processor_count
-    per_xi, slots = (rows // 128) * 4, 2 * cus
-    if (100 * per_xi) % slots % cus == 0:
-        return 100
-    xa = (100 * per_xi) // slots * slots // per_xi
-    while xa > 0 and (xa * per_xi) % slots:
-        xa -= 1
-    return xa if xa > 0 else 100
+def gemm_label(path: int, rows: int, split: int):
+    """(kernel name, description) of the dominant Winograd GEMM launch at `rows` rows per point, as
+    knightvision_amd/csrc/kv_nn.hip launches it; `split` = the engine's kv_stats.dom_split (F(8x8) fp32:
+    points in the 128x128-tile launch)."""
+    if path == 2:
+        if rows % 128 == 0:
+            name = "wino_gemm_kernel<512,4,2,1,2,32,100>"
+        elif rows % 64 == 0:
+            name = "wino_gemm_kernel<512,2,2,1,2,16,100>"
+        else:
+            name = "wino_gemm_kernel<512,1,2,1,2,32,100>" if rows == 32 else "wino_gemm_kernel<512,1,2,1,2,16,100>"
+        desc = " (residual-tower Winograd F(8x8,3x3) GEMMs, 100 points)"
+        if 0 < split < 100:
+            desc = (f" points 0-{split - 1} + wino_gemm_kernel<512,2,2,1,2,16,100> points {split}-99 (residual-tower "
+                    "Winograd F(8x8,3x3) GEMM layer: two launches, both inside the timed events)")
+        return name, desc
+    if path == 3:
+        name = ("wino88d_gemm_kernel<512,2,4,4,2>" if rows % 128 == 0 else
+                "wino88d_gemm_kernel<512,1,4,4,2>" if rows % 64 == 0 else "wino88d_gemm_kernel<512,1,4,2,2>")
+        return name, " (residual-tower Winograd F(8x8,3x3) GEMMs in fp64, 100 points, v_mfma_f64_16x16x4_f64)"
+    if path in (1, 4):
+        if path == 4:
+            return ("wino_gemm_h3_kernel<512,2,60,1>" if rows % 128 == 0 else "wino_gemm_h3_kernel<512,1,60,1>",
+                    " (residual-tower Winograd F(4x8,3x3) GEMMs, f16x3 split)")
+        return ("wino_gemm_kernel<512,4,2,1,2,32,60>" if rows % 128 == 0 else "wino_gemm_kernel<512,2,2,1,2,16,60>",
+                " (residual-tower Winograd F(4x8,3x3) GEMMs, 60 points)")
+    return "conv3x3_kernel<512,32>", " (residual-tower 3x3 conv, implicit GEMM)"
 
 
 def _pmc_traffic(kname: str, bpl: int):
@@ -291,6 +328,7 @@ def main():
             dist.init_process_group(backend)
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+    pg_info = process_group_info(rank, world, local, backend) if world > 1 else None
     from knightvision_amd.engine import EVAL_FAITHFUL, EVAL_HASH, EVAL_LAZY, SelfPlayEngine
     from knightvision_amd.weights import synthetic_state_dict
     from knightvision_amd.distributed import gather_experience
@@ -350,7 +388,10 @@ def main():
         out = dict(dt=dt, plies=plies, games_done=games_done, nn_rows=nn_rows, sims=sims_done,
                    nn_rows_evaluated=float(d["nn_rows_lazy"]) if eval_mode == "lazy" else nn_rows,
                    conv_ms=d["res_conv_ms"] / max(d["res_conv_launches"], 1), dom_flop=s1["dom_flop"],
-                   dom_algo=s1["dom_algo"], tree_overflows=s1["tree_overflows"], steps=steps, warmup=warmup)
+                   dom_algo=s1["dom_algo"], dom_path=s1["dom_path"], dom_split=s1["dom_split"],
+                   tree_overflows=s1["tree_overflows"], steps=steps, warmup=warmup)
+        if tag == "main":
+            out["calibration"] = eng.calibration()
         if keep:  # the timed region's experience, left in HBM for the gather (MCTS: with pi)
             out["recs_dev"], out["gms"] = eng.records_device(), eng.games()
             out["pi_dev"] = eng.root_visits_device() if sims > 0 else None
@@ -383,7 +424,7 @@ def main():
     if args.alt_precision and args.alt_precision != args.precision:
         alt = measure(args.alt_precision, steps=args.alt_steps, warmup=args.alt_warmup, tag="alt " + args.alt_precision)
     alt_algo = None
-    if args.alt_algo and args.precision == "fp32" and m["dom_algo"] == 4:
+    if args.alt_algo and args.precision == "fp32" and m["dom_path"] == 2:
         alt_algo = measure("fp32", args.alt_algo, steps=args.alt_steps, warmup=args.alt_warmup,
                            tag="alt " + args.alt_algo)
     refsel = reflazy = None
@@ -396,43 +437,25 @@ def main():
         # figure, never the measured games/hour -- the reference evaluates every board
         reflazy = measure(args.precision, sims=0, steps=args.ref_steps, warmup=args.ref_warmup,
                           tag="ref-selection lazy", eval_mode="lazy")
-    wino44 = direct = None
-    if args.compare_direct and args.precision == "fp32" and m["dom_algo"] in (3, 4):
-        wino44 = measure("fp32", "winograd", steps=1, warmup=1, tag="winograd44")
-    if args.compare_direct and args.precision == "fp32" and m["dom_algo"] in (2, 3, 4):
+    direct = None
+    if args.compare_direct and args.precision == "fp32" and m["dom_path"] != 0:
         direct = measure("fp32", "direct", steps=1, warmup=1, tag="direct")
+    f64w = None
+    if args.f64w_steps > 0 and args.precision == "fp32" and m["dom_path"] != 3:
+        f64w = measure("f64w", steps=args.f64w_steps, warmup=args.alt_warmup, tag="f64w")
 
-    # roofline of the dominant kernel, timed with HIP events on the engine stream: the residual-tower
-    # Winograd GEMM launch (60 x [2*boards x 512 x 512]) or, for the direct algorithm, the residual conv
-    algo = m["dom_algo"]  # 1 direct, 2 Winograd F(4x4), 3 Winograd F(4x8), 4 Winograd F(8x8) (the fp32 default)
-    per_board = {2: FLOP_WINO_GEMM_PER_BOARD, 3: FLOP_WINO48_GEMM_PER_BOARD,
-                 4: FLOP_WINO88_GEMM_PER_BOARD}.get(algo, FLOP_RES_CONV_PER_BOARD)
+    # roofline of the dominant kernel, timed with HIP events on the engine stream: one residual-tower
+    # Winograd GEMM layer per forward (fp32 F(8x8) by default; [boards x 512] x [512 x 512] per point) or, for
+    # the direct algorithm, the residual convs
+    path = m["dom_path"]  # KV_PATH_*: 0 direct, 1 F(4x8), 2 F(8x8) fp32 (the fp32 default), 3 F(8x8) fp64, 4 f16x3
+    per_board = {1: FLOP_WINO48_GEMM_PER_BOARD, 2: FLOP_WINO88_GEMM_PER_BOARD, 3: FLOP_WINO88_GEMM_PER_BOARD,
+                 4: FLOP_WINO48_GEMM_PER_BOARD}.get(path, FLOP_RES_CONV_PER_BOARD)
     bpl = min(G, int(round(m["dom_flop"] / per_board))) if m["dom_flop"] else G
     flop_alg = per_board * bpl
     achieved = flop_alg / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
-    # the library picks the GEMM tile by rows (knightvision_amd/csrc/kv_nn.hip launch_wino_gemm / launch_wino48_gemm)
-    pad = (bpl + 31) // 32 * 32
-    if algo == 4:
-        pad88 = (bpl + 31) // 32 * 32
-        pad88 = pad88 if pad88 in (32, 96) else (bpl + 63) // 64 * 64  # kv_nn.hip net_pad
-        kname = ("wino_gemm_kernel<512,4,2,1,2,32,100>" if pad88 % 128 == 0
-                 else "wino_gemm_kernel<512,2,2,1,2,16,100>" if pad88 % 64 == 0
-                 else "wino_gemm_kernel<512,1,2,1,2,32,100>" if pad88 == 32
-                 else "wino_gemm_kernel<512,1,2,1,2,16,100>")
-        kdesc = " (residual-tower Winograd F(8x8,3x3) GEMMs, 100 points)"
-        xa = _w88_split_points(pad88)
-        if xa < 100:  # launch_wino88_gemm splits the points over two tile shapes (kv_nn.hip wino88_split_points)
-            kdesc = (f" points 0-{xa - 1} + wino_gemm_kernel<512,2,2,1,2,16,100> points {xa}-99 (residual-tower "
-                     "Winograd F(8x8,3x3) GEMM layer: two launches, both inside the timed events)")
-    elif algo == 3:
-        kname = ("wino_gemm_kernel<512,4,2,1,2,32,60>" if (pad * 2) % 128 == 0
-                 else "wino_gemm_kernel<512,2,2,1,2,16,60>")
-        kdesc = " (residual-tower Winograd F(4x8,3x3) GEMMs, 60 points)"
-    elif algo == 2:
-        kname = "wino_gemm_kernel<512,2,2,1,2,16,36>" if pad * 4 <= 1024 else "wino_gemm_kernel<512,4,2,1,2,32,36>"
-        kdesc = " (residual-tower Winograd F(4x4,3x3) GEMMs)"
-    else:
-        kname, kdesc = "conv3x3_kernel<512,32>", " (residual-tower 3x3 conv, implicit GEMM)"
+    rows = int(round(m["dom_flop"] / (2 * 512 * 512 * (100 if path in (2, 3) else 60)))) if path else bpl
+    kname, kdesc = gemm_label(path, rows, m["dom_split"])
+    peak = FP64_MFMA_PEAK_TFLOPS if path == 3 else FP32_MFMA_PEAK_TFLOPS
     traffic, traffic_src = _pmc_traffic(kname, bpl)
 
     # HBM side of the search (north_star: tree kernels as a fraction of the HBM roofline), from the
@@ -507,8 +530,8 @@ def main():
             "tree_overflows": m["tree_overflows"],
             "roofline": {"bound": "mfma",
                          "kernel": kname + kdesc,
-                         "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None,
+                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": (achieved / peak) if achieved else None,
                          "traffic": traffic, "traffic_source": ("profiles/" + traffic_src) if traffic_src else None,
                          "avg_launch_ms": conv_ms, "boards_per_launch": bpl,
                          "flop_per_launch": flop_alg, "mfma_flop_per_launch_incl_padding": m["dom_flop"],
@@ -525,24 +548,35 @@ def main():
                 "ms_per_step": direct["dt"] * 1e3 / direct["steps"],
                 "res_conv_avg_launch_ms": direct["conv_ms"], "res_conv_tflops": d_ach,
                 "res_conv_frac": (d_ach / FP32_MFMA_PEAK_TFLOPS) if d_ach else None}
-        if wino44 is not None:
-            w_ach = (FLOP_WINO_GEMM_PER_BOARD * G / (wino44["conv_ms"] * 1e-3) / 1e12) if wino44["conv_ms"] > 0 else None
-            out["fp32_winograd44"] = {
-                "note": "same fp32 network with the Winograd F(4x4,3x3) tower (36 points, 4 tiles per board)",
-                "value": (wino44["sims"] if mcts else wino44["plies"]) / wino44["dt"], "unit": unit,
-                "ms_per_step": wino44["dt"] * 1e3 / wino44["steps"], "res_gemm_avg_launch_ms": wino44["conv_ms"],
-                "res_gemm_tflops": w_ach, "res_gemm_frac": (w_ach / FP32_MFMA_PEAK_TFLOPS) if w_ach else None}
+        out["calibration"] = dict(m["calibration"], note=(
+            "the network's conv paths for these weights: fp32 + AUTO measures its candidates at load time against an "
+            "fp64 forward on 64 seeded boards and keeps the fastest within max |dlogit| 4e-5 / |dvalue| 4e-6 "
+            "(F(8x8) fp32, then F(4x8) fp32, else F(8x8) with the fp64 Winograd domain); errors are max |x - fp64|"))
+        if pg_info is not None:
+            out["process_group"] = pg_info
+        if f64w is not None:
+            f_ach = (FLOP_WINO88_GEMM_PER_BOARD * bpl / (f64w["conv_ms"] * 1e-3) / 1e12) if f64w["conv_ms"] > 0 \
+                else None
+            out["trained_weights_path"] = {
+                "note": "the same workload on the fp64 Winograd domain (KV_PREC_F64W): the path AUTO runs for weights "
+                        "at trained magnitudes, where no fp32 Winograd tower holds the 1e-4 logit tolerance (learn-"
+                        "loop weights after 20 iterations: F(8x8) fp32 1.0e-4 / value 3.4e-5; the stress set 3.8e-3; "
+                        "tests/test_nn_accuracy_gpu.py, profiles/r04_*accuracy*)",
+                "value": (f64w["sims"] if mcts else f64w["plies"]) / f64w["dt"], "unit": unit,
+                "steps": f64w["steps"], "warmup": f64w["warmup"], "ms_per_step": f64w["dt"] * 1e3 / f64w["steps"],
+                "dominant_kernel": gemm_label(3, G, 0)[0], "res_gemm_avg_launch_ms": f64w["conv_ms"],
+                "res_gemm_tflops": f_ach, "peak": FP64_MFMA_PEAK_TFLOPS,
+                "res_gemm_frac_fp64": (f_ach / FP64_MFMA_PEAK_TFLOPS) if f_ach else None}
         if alt_algo is not None:
             aa = alt_algo
-            per = {3: FLOP_WINO48_GEMM_PER_BOARD, 2: FLOP_WINO_GEMM_PER_BOARD}.get(aa["dom_algo"],
-                                                                                 FLOP_RES_CONV_PER_BOARD)
+            per = {1: FLOP_WINO48_GEMM_PER_BOARD, 2: FLOP_WINO88_GEMM_PER_BOARD}.get(aa["dom_path"],
+                                                                                    FLOP_RES_CONV_PER_BOARD)
             aa_ach = (per * bpl / (aa["conv_ms"] * 1e-3) / 1e12) if aa["conv_ms"] > 0 else None
             out["fp32_" + args.alt_algo] = {
                 "note": ("the same fp32 network with the Winograd F(4x8,3x3) tower (60 points, 2 tiles per board, "
-                         "KV_ALGO_WINOGRAD48): about half the logit error of the default F(8x8) (max |dlogit| vs "
-                         "float64 over 1,024 random boards on the peaked weights 2.3e-5 against 5.1e-5, "
-                         "profiles/r03_wino88_accuracy_speed.log) for 20 % more GEMM FLOPs and transform bytes"
-                         if aa["dom_algo"] == 3 else f"the same fp32 network with algo {args.alt_algo}"),
+                         "KV_ALGO_WINOGRAD48, AUTO's second candidate): about half the logit error of F(8x8) for "
+                         "20 % more GEMM FLOPs and transform bytes" if aa["dom_path"] == 1
+                         else f"the same fp32 network with algo {args.alt_algo}"),
                 "value": (aa["sims"] if mcts else aa["plies"]) / aa["dt"], "unit": unit,
                 "steps": aa["steps"], "warmup": aa["warmup"], "ms_per_step": aa["dt"] * 1e3 / aa["steps"],
                 "res_gemm_avg_launch_ms": aa["conv_ms"], "res_gemm_tflops": aa_ach,
@@ -550,16 +584,14 @@ def main():
         if alt is not None:
             # dominant launch of the alternate run (Winograd GEMM or direct residual conv), fp32-equivalent FLOPs
             a_ach = (alt["dom_flop"] / (alt["conv_ms"] * 1e-3) / 1e12) if alt["conv_ms"] > 0 else None
-            a_prod = {"bf16x6": 6, "bf16x3": 3, "f16x3": 3}.get(args.alt_precision)
+            a_prod = {"f16x3": 3}.get(args.alt_precision)
             notes = {
                 "f16x3": "fp32-accurate split: every fp32 operand scaled by an exact power of two (per layer for "
                          "the weights, per board for the activations) and split into 2 fp16 pieces (22 significant "
                          "bits), the 3 piece products of weight >= 2^-22 on f16 MFMA, fp32 accumulation, Winograd "
                          "F(4x8) tower; batch-invariant; logits within the fp32 tolerance (tests/test_nn_gpu.py); "
                          "narrower operands than the reference's fp32, so never the headline",
-                "bf16x6": "fp32-accurate split: every fp32 operand = 3 exact bf16 pieces, the 6 piece products of "
-                          "weight >= 2^-16 on bf16 MFMA, fp32 accumulation, Winograd tower",
-                "bf16x3": "convs 2-12 as bf16 hi/lo split, 3 bf16 MFMAs per product, fp32 accumulation, direct conv",
+                "f64w": "the fp64 Winograd domain (KV_PREC_F64W)",
                 "fp32": "exact f32 MFMA"}
             out["alt_precision"] = {
                 "precision": args.alt_precision, "note": notes.get(args.alt_precision, ""),
@@ -567,11 +599,7 @@ def main():
                 "steps": alt["steps"], "warmup": alt["warmup"],
                 "ms_per_step": alt["dt"] * 1e3 / alt["steps"], "plies_per_s": alt["plies"] / alt["dt"],
                 "nn_tflops_fp32_equiv": alt["nn_rows"] * FLOP_PER_EVAL / alt["dt"] / 1e12,
-                "dominant_kernel": ({"f16x3": "wino_gemm_h3_kernel<512,2,60,1>" if alt["dom_algo"] == 3
-                                     else "wino_gemm_h3_kernel<512,2,36,2>",
-                                     "bf16x6": "wino_gemm_bf6_kernel<512>"}
-                                    .get(args.alt_precision, "wino_gemm_kernel<512>") if alt["dom_algo"] in (2, 3)
-                                    else "conv3x3 (direct)"),
+                "dominant_kernel": gemm_label(alt["dom_path"], 2 * G, alt["dom_split"])[0],
                 "dominant_avg_launch_ms": alt["conv_ms"], "dominant_tflops_fp32_equiv": a_ach,
                 "dominant_bf16_mfma_frac": (a_ach * a_prod / BF16_MFMA_PEAK_TFLOPS) if (a_ach and a_prod) else None}
         if refsel is not None:

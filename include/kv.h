@@ -65,47 +65,66 @@ int kv_net_forward_boards_legal(kv_net* net, const int8_t* boards_dev, int B, co
 /* per-launch timing of the last forward (HIP events on `stream`): ms of the
  * residual conv launches summed, and count of those launches. */
 int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv);
-/* Arithmetic of the 3x3 convs with Cin 256/512 (the stem conv is always fp32):
- * KV_PREC_FP32   f32-input MFMA, exact fp32 products (default; the parity mode)
- * KV_PREC_BF16X3 each fp32 operand split into bf16 hi + lo, hi*hi + hi*lo +
- *                lo*hi on bf16 MFMA with fp32 accumulation (logits within
- *                1e-4 of the reference; not bit-exact to fp32) */
+/* Arithmetic of the 3x3 convs with Cin 256/512 (the stem conv, the heads and
+ * the activations between layers are fp32 in every mode):
+ * KV_PREC_FP32   fp32 (default; the parity mode). Under KV_ALGO_AUTO the net
+ *                picks its conv path per weight load by measuring the
+ *                candidates against an fp64 forward (kv_net_calibration).
+ * KV_PREC_F16X3  F(4x8) Winograd GEMMs on fp16 MFMA: both operands split into
+ *                two fp16 pieces (22 significant bits) after exact power-of-two
+ *                scaling (per layer for the weights, per board for the
+ *                activations), the three products of weight >= 2^-22 with fp32
+ *                accumulation (> 16 boards; fp32 direct below). Batch-invariant;
+ *                reported beside the fp32 headline, not a parity mode.
+ * KV_PREC_F64W   Winograd F(8x8) with every Winograd-domain quantity (U, V, M,
+ *                transforms) in fp64, on v_mfma_f64_16x16x4_f64, at every batch
+ *                size: logits within ~3e-6 of an fp64 forward on every weight set
+ *                measured (the fp32 AUTO fallback for trained weights).
+ * Values 1 and 2 (bf16x3 / bf16x6) were retired in round 4: KV_EINVAL. */
 #define KV_PREC_FP32 0
-#define KV_PREC_BF16X3 1
-/* KV_PREC_BF16X6 fp32-accurate: both operands split exactly into three bf16
- *                pieces, the six piece products of weight >= 2^-16 on bf16
- *                MFMA with fp32 accumulation (Winograd tower above 16 boards;
- *                fp32 direct below). Logit error at fp32's level. */
-#define KV_PREC_BF16X6 2
-/* KV_PREC_F16X3  fp32-accurate: both operands split into two fp16 pieces
- *                (22 significant bits) after exact power-of-two scaling (per
- *                layer for the weights, per board for the activations), the
- *                three products of weight >= 2^-22 on f16 MFMA with fp32
- *                accumulation (Winograd tower above 16 boards; fp32 direct
- *                below). Batch-invariant; logit error at fp32's level. */
 #define KV_PREC_F16X3 3
+#define KV_PREC_F64W 4
 int kv_net_set_precision(kv_net* net, int precision);
 /* Algorithm of the fp32 3x3 convs with Cin 256/512:
- * KV_ALGO_AUTO      Winograd for batches > 16 boards (F(8x8) in fp32, F(4x8)
- *                   for f16x3, F(4x4) for bf16x6), direct (split-K) below
+ * KV_ALGO_AUTO      per weight load, the fastest path whose logits / values are
+ *                   within 4e-5 / 4e-6 of an fp64 forward on 64 calibration
+ *                   boards: > 16 boards F(8x8) fp32, else F(4x8) fp32, else
+ *                   F(8x8) with the fp64 Winograd domain; <= 16 boards direct
+ *                   (split-K), else F(8x8) fp64 (kv_net_calibration reports it)
  * KV_ALGO_DIRECT    implicit GEMM over the 9 taps (exact fp32 products)
- * KV_ALGO_WINOGRAD  F(4x4,3x3): 36 GEMMs of 4 tiles x Cin x Cout per board, 4x
- *                   fewer FLOPs, fp32 transforms (logits within 1e-4)
  * KV_ALGO_WINOGRAD48 F(4x8,3x3): 60 GEMMs of 2 tiles x Cin x Cout per board,
- *                   4.8x fewer FLOPs than direct (fp32 and f16x3; bf16x6
- *                   runs F(4x4) under this setting); about half the logit
- *                   error of F(8x8) for 18 % more time at 2,048 boards
+ *                   4.8x fewer FLOPs than direct (fp32 and f16x3)
  * KV_ALGO_WINOGRAD88 F(8x8,3x3): 100 GEMMs of 1 tile x Cin x Cout per board,
- *                   5.76x fewer FLOPs than direct (fp32; the fp32 AUTO choice
- *                   above 16 boards; f16x3 runs F(4x8) under it, bf16x6
- *                   F(4x4))
+ *                   5.76x fewer FLOPs than direct (fp32; f16x3 runs F(4x8))
+ * Value 2 (F(4x4)) was retired in round 4: KV_EINVAL. Setting the precision or
+ * the algorithm of a loaded net re-prepares it (synchronous).
  * Results are batch-invariant inside a class (<= 16 boards, > 16 boards). */
 #define KV_ALGO_AUTO 0
 #define KV_ALGO_DIRECT 1
-#define KV_ALGO_WINOGRAD 2
 #define KV_ALGO_WINOGRAD48 3
 #define KV_ALGO_WINOGRAD88 4
 int kv_net_set_algo(kv_net* net, int algo);
+/* conv paths (what a forward runs) */
+#define KV_PATH_DIRECT 0
+#define KV_PATH_WINO48 1
+#define KV_PATH_WINO88 2
+#define KV_PATH_WINO88_F64 3
+#define KV_PATH_WINO48_F16X3 4
+#define KV_NPATH 5
+typedef struct {
+    int calibrated;      /* 1: the last load / setting ran the fp32 AUTO calibration */
+    int path_large;      /* KV_PATH_* of batches > 16 boards (also without calibration) */
+    int path_small;      /* KV_PATH_* of batches <= 16 boards */
+    int n_boards;        /* calibration boards */
+    double tol_logit;    /* budget: max |logit - fp64| */
+    double tol_value;    /* budget: max |value - fp64| */
+    double err_logit[KV_NPATH]; /* > 16-board candidates measured, per path (-1: not run) */
+    double err_value[KV_NPATH];
+    double err_small_logit;     /* the <= 16-board direct path on 16 of the boards */
+    double err_small_value;
+    double ms;                  /* wall time of the calibration */
+} kv_calib;
+int kv_net_calibration(kv_net* net, kv_calib* out);
 int kv_net_set_timing(kv_net* net, int enable);
 void kv_net_destroy(kv_net* net);
 
@@ -186,16 +205,22 @@ typedef struct {
     int64_t res_conv_launches;
     double step_ms;       /* wall time inside kv_run */
     double dom_flop;      /* MFMA FLOPs of one measured launch (padded rows included) */
-    int64_t dom_algo;     /* KV_ALGO_DIRECT, _WINOGRAD, _WINOGRAD48 or _WINOGRAD88 for those launches */
+    int64_t dom_algo;     /* KV_ALGO_DIRECT, _WINOGRAD48 or _WINOGRAD88 for those launches */
     int64_t tree_overflows; /* MCTS expansions dropped for a full edge pool (each also fails kv_run) */
     int64_t nn_rows_lazy;   /* KV_EVAL_LAZY above 16 slots: rows the compact batches sent through the
                                network (nn_rows counts the rows the reference's schedule evaluates) */
+    int64_t dom_path;       /* KV_PATH_* of those launches (F(8x8) fp32 or fp64 for KV_ALGO_WINOGRAD88) */
+    int64_t dom_split;      /* fp32 F(8x8): points of the GEMM layer run as 128x128 tiles in its first launch
+                               (the rest as 64x128 tiles in a second one; 100: one launch); 0 otherwise */
 } kv_stats;
 
 typedef struct kv_engine kv_engine;
 
 int kv_create(const kv_config* cfg, kv_engine** out);
+/* Loads the network weights; under fp32 + KV_ALGO_AUTO this runs the conv-path
+ * calibration (kv_net_calibration), reported by kv_engine_calibration. */
 int kv_load_weights(kv_engine* e, const float* packed, size_t n_floats);
+int kv_engine_calibration(kv_engine* e, kv_calib* out);
 /* Run ply-steps until every game is finished, or max_steps steps (>= 0), or
  * stop_after_games games have finished in total (>= 0), whichever is first. */
 int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games);

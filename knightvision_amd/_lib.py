@@ -38,7 +38,28 @@ class Stats(C.Structure):
     _fields_ = [("steps", C.c_int64), ("plies", C.c_int64), ("games_done", C.c_int64), ("nn_rows", C.c_int64),
                 ("sims", C.c_int64), ("records", C.c_int64), ("res_conv_ms", C.c_double),
                 ("res_conv_launches", C.c_int64), ("step_ms", C.c_double), ("dom_flop", C.c_double),
-                ("dom_algo", C.c_int64), ("tree_overflows", C.c_int64), ("nn_rows_lazy", C.c_int64)]
+                ("dom_algo", C.c_int64), ("tree_overflows", C.c_int64), ("nn_rows_lazy", C.c_int64),
+                ("dom_path", C.c_int64), ("dom_split", C.c_int64)]
+
+
+NPATH = 5  # KV_NPATH
+PATHS = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3"}  # KV_PATH_*
+
+
+class Calib(C.Structure):
+    _fields_ = [("calibrated", C.c_int), ("path_large", C.c_int), ("path_small", C.c_int), ("n_boards", C.c_int),
+                ("tol_logit", C.c_double), ("tol_value", C.c_double), ("err_logit", C.c_double * NPATH),
+                ("err_value", C.c_double * NPATH), ("err_small_logit", C.c_double),
+                ("err_small_value", C.c_double), ("ms", C.c_double)]
+
+
+def calib_dict(c: "Calib") -> dict:
+    """kv_calib as a plain dict (path names, candidate errors; -1 = candidate not run)."""
+    return {"calibrated": bool(c.calibrated), "path_large": PATHS[c.path_large], "path_small": PATHS[c.path_small],
+            "n_boards": c.n_boards, "tol_logit": c.tol_logit, "tol_value": c.tol_value,
+            "err_logit": {PATHS[p]: c.err_logit[p] for p in range(NPATH) if c.err_logit[p] >= 0},
+            "err_value": {PATHS[p]: c.err_value[p] for p in range(NPATH) if c.err_value[p] >= 0},
+            "err_small_logit": c.err_small_logit, "err_small_value": c.err_small_value, "ms": c.ms}
 
 
 class PgnRecord(C.Structure):
@@ -68,6 +89,8 @@ def _declare(L):
         "kv_net_destroy": ([vp], None),
         "kv_net_set_precision": ([vp, i], i),
         "kv_net_set_algo": ([vp, i], i),
+        "kv_net_calibration": ([vp, P(Calib)], i),
+        "kv_engine_calibration": ([vp, P(Calib)], i),
         "kv_create": ([P(Config), P(vp)], i),
         "kv_load_weights": ([vp, P(C.c_float), sz], i),
         "kv_run": ([vp, i64, i64], i),
@@ -119,6 +142,7 @@ def _declare(L):
 
 EXPORTED = ["kv_last_error", "kv_version", "kv_net_packed_size", "kv_net_create", "kv_net_load", "kv_net_forward",
             "kv_net_forward_boards", "kv_net_forward_boards_legal", "kv_net_set_timing", "kv_net_last_timing", "kv_net_destroy", "kv_net_set_precision", "kv_net_set_algo",
+            "kv_net_calibration", "kv_engine_calibration",
             "kv_create",
             "kv_load_weights", "kv_run", "kv_set_max_moves", "kv_records", "kv_games", "kv_stats_get", "kv_root_visits", "kv_root_visits_device", "kv_records_device", "kv_sync", "kv_reset_records", "kv_destroy",
             "kv_dev_valid_moves", "kv_dev_make_move", "kv_dev_attacks", "kv_dev_dirichlet", "kv_dev_py_random", "kv_host_libm",

@@ -448,6 +448,7 @@ struct kv_engine {
     double nn_res_ms = 0;
     long long nn_res_launches = 0;
     int dom_algo = KV_ALGO_DIRECT, dom_launches = 10;  // what each event pair brackets
+    int dom_path = KV_PATH_DIRECT, dom_split = 0;
     double dom_flop = 0;
     bool loaded = false;
     // MCTS (sims > 0)
@@ -676,9 +677,15 @@ int kv_create(const kv_config* cfg, kv_engine** out) {
 
 int kv_load_weights(kv_engine* e, const float* packed, size_t n_floats) {
     KV_REQUIRE(e, KV_EINVAL, "kv_load_weights: NULL engine");
+    KV_HIP(hipStreamSynchronize(e->st));  // the load (and its calibration) runs on the null stream
     int rc = kv_net_load(e->net, packed, n_floats);
     if (rc == KV_OK) e->loaded = true;
     return rc;
+}
+
+int kv_engine_calibration(kv_engine* e, kv_calib* out) {
+    KV_REQUIRE(e && out, KV_EINVAL, "kv_engine_calibration: NULL argument");
+    return kv_net_calibration(e->net, out);
 }
 
 int kv_set_max_moves(kv_engine* e, int max_moves) {
@@ -719,7 +726,7 @@ static int eng_eval(kv_engine* e, const int8_t* boards, int rows, bool leaf = fa
                                                                 values, st)
                         : kv::net_forward_boards_internal(net, boards, rows, logits, values, st);
     kv::net_set_res_events(net, nullptr, nullptr);
-    kv::net_dom_info(net, &e->dom_algo, &e->dom_launches, &e->dom_flop);
+    kv::net_dom_info(net, &e->dom_algo, &e->dom_launches, &e->dom_flop, &e->dom_path, &e->dom_split);
     return rc;
 }
 
@@ -898,6 +905,8 @@ int kv_stats_get(kv_engine* e, kv_stats* out) {
     out->step_ms = e->wall_ms;
     out->dom_flop = e->dom_flop;
     out->dom_algo = e->dom_algo;
+    out->dom_path = e->dom_path;
+    out->dom_split = e->dom_split;
     out->tree_overflows = (int64_t)e->ctr_host->tree_overflows;
     out->nn_rows_lazy = e->lazy_rows;
     return KV_OK;

@@ -18,18 +18,17 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <mutex>
 #include <set>
 #include <utility>
-
-#ifndef KV_STEM88
-#define KV_STEM88 4
-#endif
 
 #include "kv_common.h"
 #include "kv_wino.h"
 #include "kv_wino48.h"
 #include "kv_wino88.h"
+#include "kv_wino88d.h"
+#include "kv_ref64.h"
 
 namespace kv {
 
@@ -256,196 +255,6 @@ __global__ __launch_bounds__(512) void conv3x3_kernel(const float* __restrict__ 
     }
 }
 
-// ------------------------------------------------- bf16x3 conv kernel --
-// The same implicit GEMM with every fp32 operand split as x = hi + lo (two
-// bf16, hi = RNE(x), lo = RNE(x - hi)) and the product taken as
-// hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_bf16 with fp32 accumulation:
-// the dropped lo*lo term and the 16-bit mantissa of hi+lo keep the conv at
-// ~1e-5 relative error (logits within 3e-5 of the reference on the peaked
-// weight set; tolerance 1e-4). Three bf16 MFMAs cost 3/16 of one fp32 MFMA.
-// Workgroup: 4 boards x 128 output channels, 8 waves = 4 boards x 2 column
-// halves, 64x64 per wave (2x2 tiles). Weights are pre-split on the device at
-// load time ([Cout][9][Cin] bf16 hi and lo); activations stay fp32 in HBM and
-// are split while staging the halo into LDS. Strides (bytes): halo pixel 64,
-// halo row 656, weight row 80 -- conflict-free ds_read_b128 for every tap.
-
-__device__ inline void split2(float a, float b, unsigned& hi, unsigned& lo) {
-    const unsigned ha = bf16_rne(a), hb = bf16_rne(b);
-    const float ra = a - __uint_as_float(ha << 16), rb = b - __uint_as_float(hb << 16);
-    hi = ha | (hb << 16);
-    lo = bf16_rne(ra) | (bf16_rne(rb) << 16);
-}
-
-template <int CIN>
-struct Bf3Lds {
-    static constexpr int PSA = 64, RSA = 656, BOARDA = 10 * RSA;  // bytes
-    static constexpr int APART = 4 * BOARDA;                       // one of hi / lo
-    static constexpr int ABUF = 2 * APART;                         // hi + lo
-    static constexpr int PSB = 80, BPART = 128 * PSB, BBUF = 2 * BPART;
-    static constexpr int BYTES = 2 * ABUF + 2 * BBUF;
-};
-
-template <int CIN, bool RESID>
-__global__ __launch_bounds__(512) void conv3x3_bf16x3_kernel(const float* __restrict__ in,
-                                                             const uint16_t* __restrict__ whi,
-                                                             const uint16_t* __restrict__ wlo,
-                                                             const float* __restrict__ scale,
-                                                             const float* __restrict__ shift, const float* resid,
-                                                             float* out, int cout, int kt_per) {
-    using G = Bf3Lds<CIN>;
-    constexpr int PSA = G::PSA, RSA = G::RSA, BOARDA = G::BOARDA, APART = G::APART, ABUF = G::ABUF;
-    constexpr int PSB = G::PSB, BPART = G::BPART, BBUF = G::BBUF;
-    constexpr int CK = 32, NCH = CIN / CK, NK = 9 * NCH;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wb = wave >> 1;  // board inside the tile
-    const int wn = wave & 1;   // 64-column half
-    const int n_base = blockIdx.x * 128;
-    const int b0 = blockIdx.y * 4;
-    const int kt0 = kt_per > 0 ? (int)blockIdx.z * kt_per : 0;  // split-K, as in conv3x3_kernel
-    const int kt1 = kt_per > 0 ? min(NK, kt0 + kt_per) : NK;
-
-    for (int i = tid * 16; i < 2 * ABUF; i += 512 * 16) *(u32x4*)(lds + i) = u32x4{0u, 0u, 0u, 0u};
-
-    // staging: A = 4 boards x 64 px x 32 cin fp32 (4 float4 / thread), B = 128 n x 32 k (hi + lo 16 B / thread)
-    f32x4 ra[4];
-    u32x4 rbh, rbl;
-    auto loadA = [&](int ch) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int idx = tid + q * 512;  // 2048 float4
-            const int pix = idx >> 3, kq = idx & 7;
-            ra[q] = *(const f32x4*)(in + ((size_t)(b0 + (pix >> 6)) * 64 + (pix & 63)) * CIN + ch * CK + kq * 4);
-        }
-    };
-    auto storeA = [&](int buf) {
-        unsigned char* Ah = lds + buf * ABUF;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int idx = tid + q * 512;
-            const int pix = idx >> 3, kq = idx & 7;
-            const int p = pix & 63;
-            const int off = (pix >> 6) * BOARDA + ((p >> 3) + 1) * RSA + ((p & 7) + 1) * PSA + kq * 8;
-            unsigned h0, l0, h1, l1;
-            split2(ra[q][0], ra[q][1], h0, l0);
-            split2(ra[q][2], ra[q][3], h1, l1);
-            *(u32x2*)(Ah + off) = u32x2{h0, h1};
-            *(u32x2*)(Ah + APART + off) = u32x2{l0, l1};
-        }
-    };
-    auto loadB = [&](int kt) {
-        const int tap = kt % 9, ch = kt / 9;
-        const int n = tid >> 2, kq = tid & 3;
-        const size_t o = ((size_t)(n_base + n) * 9 + tap) * CIN + ch * CK + kq * 8;
-        rbh = *(const u32x4*)(whi + o);
-        rbl = *(const u32x4*)(wlo + o);
-    };
-    auto storeB = [&](int buf) {
-        unsigned char* Bh = lds + 2 * ABUF + buf * BBUF;
-        const int n = tid >> 2, kq = tid & 3;
-        *(u32x4*)(Bh + n * PSB + kq * 16) = rbh;
-        *(u32x4*)(Bh + BPART + n * PSB + kq * 16) = rbl;
-    };
-
-    const int h = lane >> 5, li = lane & 31;
-    int aoff[2], boff[2];
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-        const int p = mt * 32 + li;
-        aoff[mt] = wb * BOARDA + ((p >> 3) + 1) * RSA + ((p & 7) + 1) * PSA + 16 * h;
-    }
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) boff[nt] = (wn * 64 + nt * 32 + li) * PSB + 16 * h;
-
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    __syncthreads();
-    loadA(kt0 / 9);
-    loadB(kt0);
-    for (int kt = kt0; kt < kt1; ++kt) {  // one barrier per k-tile, as in conv3x3_kernel
-        const int tap = kt % 9, ch = kt / 9;
-        const bool chunk_start = tap == 0 || kt == kt0;
-        if (chunk_start) storeA(ch & 1);
-        storeB(kt & 1);
-        if (kt + 1 < kt1) loadB(kt + 1);
-        if (chunk_start && (ch + 1) * 9 < kt1) loadA(ch + 1);
-        __syncthreads();
-        const unsigned char* Ah = lds + (ch & 1) * ABUF;
-        const unsigned char* Bh = lds + 2 * ABUF + (kt & 1) * BBUF;
-        const int toff = (tap / 3 - 1) * RSA + (tap % 3 - 1) * PSA;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            bf16x8 ah[2], al[2], bh[2], bl[2];
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
-                ah[mt] = *(const bf16x8*)(Ah + aoff[mt] + toff + 32 * s);
-                al[mt] = *(const bf16x8*)(Ah + APART + aoff[mt] + toff + 32 * s);
-            }
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
-                bh[nt] = *(const bf16x8*)(Bh + boff[nt] + 32 * s);
-                bl[nt] = *(const bf16x8*)(Bh + BPART + boff[nt] + 32 * s);
-            }
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int nt = 0; nt < 2; ++nt) {
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[mt], bh[nt], acc[mt][nt], 0, 0, 0);
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mt], bl[nt], acc[mt][nt], 0, 0, 0);
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mt], bh[nt], acc[mt][nt], 0, 0, 0);
-                }
-        }
-    }
-
-    if (kt_per > 0) {
-        float* slab = out + (size_t)blockIdx.z * gridDim.y * 256 * cout;
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int pix = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    slab[((size_t)(b0 + wb) * 64 + pix) * cout + n_base + wn * 64 + nt * 32 + li] = acc[mt][nt][r];
-                }
-        return;
-    }
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-        const int n = n_base + wn * 64 + nt * 32 + li;
-        const float sc = scale[n], sh = shift[n];
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int pix = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const size_t idx = ((size_t)(b0 + wb) * 64 + pix) * cout + n;
-                float v = acc[mt][nt][r] * sc + sh;
-                if (RESID) v += resid[idx];
-                out[idx] = v > 0.f ? v : 0.f;
-            }
-        }
-    }
-}
-
-// fp32 weights -> bf16 hi / lo (RNE), elementwise
-__global__ void split_weights_kernel(const float* __restrict__ w, size_t n, uint16_t* __restrict__ hi,
-                                     uint16_t* __restrict__ lo) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const float x = w[i];
-    const unsigned hb = bf16_rne(x);
-    hi[i] = (uint16_t)hb;
-    lo[i] = (uint16_t)bf16_rne(x - __uint_as_float(hb << 16));
-}
-
 // split-K combine: fixed-order sum of the slabs + folded BN (+ residual) + ReLU.
 // The slab loads go out 16 at a time (a small batch has few outputs per split:
 // 64-thread blocks over every CU, and the 48 partials of an output are latency,
@@ -640,14 +449,11 @@ __global__ void encode_boards_kernel(const int8_t* __restrict__ boards, int nb, 
 // Block = two boards x 64 channels (grid 4 x nb_pad/2), 256 threads: the
 // 64-channel slice of conv1 ([tap][code][64], 30 KB, a zero row for empty) is
 // staged in LDS once for both boards; waves 2b, 2b+1 compute board b's pixels
-// 0..31 / 32..63. WINO: the activated 8x8 planes go through LDS to the tile
-// transforms -- wave w writes board w/2's tile w%2 (F(4x8)) or tiles 2(w%2),
-// 2(w%2)+1 (F(4x4)) of conv2's Winograd input V [points][rows][256]; else
-// NHWC T [board][64][256]. F(4x8) skips the plane (below). F(8x8): thread
-// (w % 2) of a (board, channel) plane stores rows 5(w % 2) .. 5(w % 2) + 4 of its
-// 10x10 transform (the column pass is done by both: same operations, same bits
-// as wino88_in_kernel over T).
-template <int WINO>  // 0: NHWC out, 1: F(4x4) V of conv2, 2: F(4x8) V of conv2, 3 / 4: F(8x8) V of conv2
+// 0..31 / 32..63 (WINO 0: NHWC T [board][64][256]). WINO 2: each wave
+// computes its own F(4x8) tile's 6x10 patch and writes that tile of conv2's
+// V [points][rows][256]. WINO 4: F(8x8) by lane swaps (below), the same bits
+// as wino88_in_kernel over T.
+template <int WINO>  // 0: NHWC out, 2: F(4x8) V of conv2, 4: F(8x8) V of conv2
 __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ boards, int nb,
                                                    const float* __restrict__ wT, const float* __restrict__ scale,
                                                    const float* __restrict__ shift, float* __restrict__ out,
@@ -738,7 +544,6 @@ __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ bo
             if (cl == 0) atomicMax(vmax + b, __float_as_uint(mx));
         }
     } else {
-    __shared__ float plane[2][64][64];  // [board][pixel][channel]
     // branch-free: an empty or off-board neighbour adds +0 (exact, acc starts at +0),
     // so every pixel issues its 9 independent LDS reads back to back
 #pragma unroll 4
@@ -748,53 +553,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ bo
 #pragma unroll
         for (int t = 0; t < 9; ++t) acc += wl[t * 13 + codes[bb][(py + t / 3) * 10 + px + t % 3]][cl];
         const float v = acc * sc + sh;
-        const float y = v > 0.f ? v : 0.f;
-        if (WINO)
-            plane[bb][p][cl] = y;
-        else
-            out[((size_t)b * 64 + p) * 256 + c] = y;
-    }
-    if (!WINO) return;
-    __syncthreads();
-    float mx = 0.f;
-    if constexpr (WINO == 3) {
-        const auto px = [&](int p) { return plane[bb][p][cl]; };
-        const size_t off = (size_t)b * 256 + c, xs = (size_t)rows * 256;
-        if (w & 1)
-            wino88_input_rows<5, 5>(px, out, off, xs);
-        else
-            wino88_input_rows<0, 5>(px, out, off, xs);
-        return;
-    } else if (WINO == 2) {
-        const int tile = w & 1;
-        float d48[60];
-#pragma unroll
-        for (int i = 0; i < 6; ++i)
-#pragma unroll
-            for (int j = 0; j < 10; ++j) {
-                const int yy = tile * 4 - 1 + i, xx = j - 1;
-                d48[i * 10 + j] = (yy >= 0 && yy < 8 && xx >= 0 && xx < 8) ? plane[bb][yy * 8 + xx][cl] : 0.f;
-            }
-        mx = wino48_input_tile(d48, out, ((size_t)b * 2 + tile) * 256 + c, (size_t)rows * 256);
-    } else {
-        for (int tt = 0; tt < 2; ++tt) {
-            const int tile = (w & 1) * 2 + tt;
-            const int y0 = (tile >> 1) * 4 - 1, x0 = (tile & 1) * 4 - 1;
-            float d[36];
-#pragma unroll
-            for (int i = 0; i < 6; ++i)
-#pragma unroll
-                for (int j = 0; j < 6; ++j) {
-                    const int yy = y0 + i, xx = x0 + j;
-                    d[i * 6 + j] = (yy >= 0 && yy < 8 && xx >= 0 && xx < 8) ? plane[bb][yy * 8 + xx][cl] : 0.f;
-                }
-            mx = fmaxf(mx, wino_input_tile(d, out, ((size_t)b * 4 + tile) * 256 + c, (size_t)rows * 256));
-        }
-    }
-    if (vmax) {  // KV_PREC_F16X3 operand scale of conv2: per-board max |V| (vmax zeroed per forward)
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-        if (cl == 0) atomicMax(vmax + b, __float_as_uint(mx));
+        out[((size_t)b * 64 + p) * 256 + c] = v > 0.f ? v : 0.f;
     }
     }
     }
@@ -836,12 +595,22 @@ __global__ void planes_to_nhwc16_kernel(const float* __restrict__ planes, int nb
 }  // namespace kv
 
 // ---------------------------------------------------------------- host --
+// Conv paths of the 11 3x3 convs with Cin 256 / 512 (the stem conv, the heads
+// and the activations between layers are fp32 on every path):
+//   KV_PATH_DIRECT     implicit GEMM over the 9 taps (split-K at <= 16 boards)
+//   KV_PATH_WINO48     fp32 Winograd F(4x8)
+//   KV_PATH_WINO88     fp32 Winograd F(8x8)
+//   KV_PATH_WINO88_F64 Winograd F(8x8) with an fp64 Winograd domain
+//   KV_PATH_WINO48_F16X3 F(4x8) with the f16x3 split GEMM
+// fp32 + KV_ALGO_AUTO picks its paths per weight load (kv_net_calibration).
+constexpr int kNPath = 5;
+
 struct kv_net {
     int device = 0;
     float* w = nullptr;  // packed weights on device
     kv::PackOffsets off;
     bool loaded = false;
-    int cap = 0;         // boards the workspace holds (even)
+    int cap = 0;         // boards the workspace holds
     float* x16 = nullptr;
     float* X = nullptr;
     float* T = nullptr;
@@ -850,28 +619,27 @@ struct kv_net {
     hipEvent_t ev[3];
     hipEvent_t res_a = nullptr, res_b = nullptr;  // engine hook: residual section
     int precision = KV_PREC_FP32;
-    uint16_t* whi = nullptr;  // bf16x3: split conv weights, layers 1..11, same offsets as w
-    uint16_t* wlo = nullptr;
-    float* slab = nullptr;  // split-K partial sums (small batches)
     int algo = KV_ALGO_AUTO;
-    float* U = nullptr;     // Winograd weights [36][Cout][Cin] of convs 1..11
-    float* U48 = nullptr;   // F(4x8) weights [60][Cout][Cin] of convs 1..11
+    float* slab = nullptr;  // split-K partial sums (small batches)
+    // Winograd weights of convs 1..11, built when a path needs them (ensure_path)
+    float* U48 = nullptr;   // F(4x8) [60][Cout][Cin]
     size_t uoff48[12] = {};
-    float* U88 = nullptr;   // F(8x8) weights [100][Cout][Cin] of convs 1..11 (KV_ALGO_WINOGRAD88)
-    size_t uoff88[12] = {};
-    uint16_t* Uf48[2] = {};  // fp16 pieces of U48 * 2^ut48[l] (KV_PREC_F16X3 on F(4x8))
+    uint16_t* Uf48[2] = {};  // fp16 pieces of U48 * 2^ut48[l] (KV_PREC_F16X3)
     int ut48[12] = {};
-    uint16_t* Up[3] = {};   // the same split into bf16 h / m / l (KV_PREC_BF16X6)
-    uint16_t* Uf[2] = {};   // fp16 pieces of U * 2^ut[l] (KV_PREC_F16X3)
-    int ut[12] = {};
+    float* U88 = nullptr;   // F(8x8) [100][Cout][Cin]
+    size_t uoff88[12] = {};
+    double* U88d = nullptr; // F(8x8), fp64 [100][Cout][Cin] (KV_PATH_WINO88_F64)
+    bool built[kNPath] = {};
     unsigned* vmax = nullptr;  // f16x3: per-board max |V| of each conv's input, [12][cap]
     float* stemT = nullptr; // conv1 as [tap][piece][cout] (stem_kernel)
     float* v1wT = nullptr;  // value_fc1 weight as [k][o] (heads_kernel)
-    size_t uoff[12] = {};
-    size_t utot = 0;
-    float* V = nullptr;     // Winograd workspaces [36][cap*4][512]
-    float* V256 = nullptr;  // conv2's input transform [36][cap*4][256]
-    float* Mw = nullptr;
+    // Winograd workspaces (bytes per board: kWsBoard / kWs256Board), shared by every path
+    void* V = nullptr;
+    void* V256 = nullptr;   // conv2's input transform
+    void* Mw = nullptr;
+    // fp32 + AUTO: the paths chosen by the last calibration (> 16 boards / <= 16)
+    int auto_large = KV_PATH_WINO88, auto_small = KV_PATH_DIRECT;
+    kv_calib calib = {};
     // kv_net_forward_boards_legal's request for the forward in flight (out == nullptr: full rows)
     struct {
         const uint16_t* moves = nullptr;
@@ -881,9 +649,15 @@ struct kv_net {
     } legal;
     // the dominant kernel bracketed by res_a/res_b in the last forward
     int dom_algo = KV_ALGO_DIRECT;
+    int dom_path = KV_PATH_DIRECT;
     int dom_launches = 10;
+    int dom_split = 0;  // F(8x8) fp32: points run as 128x128 tiles in the first launch (100: one launch)
     double dom_flop = 0;
 };
+
+// workspace bytes per board: the largest path's V / M (F(8x8) in fp64: 100 points x 512 doubles;
+// F(4x8): 120 rows x 512 floats; F(8x8) fp32: 100 x 512 floats)
+constexpr size_t kWsBoard = (size_t)100 * 512 * 8, kWs256Board = (size_t)100 * 256 * 8;
 
 // Small batches (<= 16 boards: the sequential reference path, batch-16
 // schedules) have far fewer output tiles than CUs: split K into groups of 3
@@ -892,6 +666,24 @@ struct kv_net {
 // for every batch inside a class (<= 16 boards, or > 16 boards).
 constexpr int kSplitMaxBoards = 16, kSplitKt = 3;
 static int split_kt(int nb_pad) { return nb_pad <= kSplitMaxBoards ? kSplitKt : 0; }
+
+// the conv path of a B-board forward
+static int path_for(const kv_net* net, int B) {
+    const bool small = B <= kSplitMaxBoards;
+    if (net->precision == KV_PREC_F64W) return KV_PATH_WINO88_F64;
+    if (net->precision == KV_PREC_F16X3) {
+        if (net->algo == KV_ALGO_DIRECT || (net->algo == KV_ALGO_AUTO && small)) return KV_PATH_DIRECT;
+        return KV_PATH_WINO48_F16X3;
+    }
+    switch (net->algo) {
+        case KV_ALGO_DIRECT: return KV_PATH_DIRECT;
+        case KV_ALGO_WINOGRAD48: return KV_PATH_WINO48;
+        case KV_ALGO_WINOGRAD88: return KV_PATH_WINO88;
+        default: return small ? net->auto_small : net->auto_large;
+    }
+}
+
+static bool path_is_wino(int path) { return path != KV_PATH_DIRECT; }
 
 static int launch_reduce(const float* slab, int splits, int rows, int cout, const float* sc, const float* sh,
                          const float* resid, float* out, hipStream_t st) {
@@ -919,27 +711,16 @@ static hipError_t lds_opt_in(const void* fn, int bytes) {
     return e;
 }
 
-template <int CIN, bool RESID>
-static int launch_conv_bf3(const float* in, const uint16_t* whi, const uint16_t* wlo, const float* sc,
-                           const float* sh, const float* resid, float* out, int cout, int nb_pad, float* slab,
-                           hipStream_t st) {
-    using G = kv::Bf3Lds<CIN>;
-    KV_HIP(lds_opt_in((const void*)kv::conv3x3_bf16x3_kernel<CIN, RESID>, (int)G::BYTES));
-    KV_HIP(lds_opt_in((const void*)kv::conv3x3_bf16x3_kernel<CIN, false>, (int)G::BYTES));
-    const int nk = 9 * (CIN / 32);
-    const int kt_per = slab ? split_kt(nb_pad) : 0;
-    if (kt_per) {
-        const int splits = (nk + kt_per - 1) / kt_per;
-        hipLaunchKernelGGL((kv::conv3x3_bf16x3_kernel<CIN, false>), dim3(cout / 128, nb_pad / 4, splits), dim3(512),
-                           G::BYTES, st, in, whi, wlo, sc, sh, nullptr, slab, cout, kt_per);
-        KV_HIP(hipGetLastError());
-        return launch_reduce(slab, splits, nb_pad * 64, cout, sc, sh, RESID ? resid : nullptr, out, st);
-    }
-    dim3 grid(cout / 128, nb_pad / 4);
-    hipLaunchKernelGGL((kv::conv3x3_bf16x3_kernel<CIN, RESID>), grid, dim3(512), G::BYTES, st, in, whi, wlo, sc, sh,
-                       resid, out, cout, 0);
-    KV_HIP(hipGetLastError());
-    return KV_OK;
+// CUs of the current device, cached per device (the F(8x8) point split reads it per launch)
+static int device_cus() {
+    static std::mutex mu;
+    static int cus[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    std::lock_guard<std::mutex> g(mu);
+    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus[dev] = 0;
+    return cus[dev];
 }
 
 template <int CIN, int CK, bool RESID>
@@ -964,36 +745,20 @@ static int launch_conv(const float* in, const float* w, const float* sc, const f
     return KV_OK;
 }
 
-// Winograd for the fp32 tower when the batch is past the split-K class
-static bool use_wino(const kv_net* net, int B) {
-    if (net->precision == KV_PREC_BF16X3) return false;
-    if (net->algo == KV_ALGO_WINOGRAD || net->algo == KV_ALGO_WINOGRAD48 || net->algo == KV_ALGO_WINOGRAD88)
-        return true;
-    return net->algo == KV_ALGO_AUTO && B > kSplitMaxBoards;
-}
-
-// the F(8x8) variant: fp32 under KV_ALGO_AUTO (the fp32 default above 16 boards) and WINOGRAD88
-static bool use_wino88(const kv_net* net, int B) {
-    return use_wino(net, B) && net->precision == KV_PREC_FP32 &&
-           (net->algo == KV_ALGO_WINOGRAD88 || net->algo == KV_ALGO_AUTO);
-}
-
-// the F(4x8) variant: fp32 under WINOGRAD48, f16x3 under AUTO / WINOGRAD48 / WINOGRAD88; bf16x6 keeps F(4x4)
-static bool use_wino48(const kv_net* net, int B) {
-    return use_wino(net, B) && (net->precision == KV_PREC_FP32 || net->precision == KV_PREC_F16X3) &&
-           net->algo != KV_ALGO_WINOGRAD && !use_wino88(net, B);
-}
-
-// padded batch: a multiple of 4 boards (direct tiles), 32 (128-row GEMM tiles of 2 rows per
-// board) or F(8x8)'s one row per board: 32 / 96 boards (32-row tiles: forward 0.556 -> 0.522 ms at
-// <= 32 boards, 0.895 -> 0.783 at 65-96) else a multiple of 64 (at 160 boards the 32-row tiles were
-// 1.26 -> 1.38 ms slower than padding to 192; profiles/r03_w88_rows32_ab.log)
+// padded batch: a multiple of 4 boards (direct tiles), 32 (F(4x8): 128-row GEMM tiles of 2 rows per
+// board; F(8x8) in fp64: 32 / 64 / 128-row tiles) or F(8x8)'s one row per board: 32 / 96 boards
+// (32-row tiles: forward 0.556 -> 0.522 ms at <= 32 boards, 0.895 -> 0.783 at 65-96) else a multiple of
+// 64 (at 160 boards the 32-row tiles were 1.26 -> 1.38 ms slower than padding to 192;
+// profiles/r03_w88_rows32_ab.log)
 static int net_pad(const kv_net* net, int B) {
-    if (use_wino88(net, B)) {  // 32 and 96 rows run 32-row GEMM tiles: faster there, slower at 160 (measured)
-        const int p32 = (B + 31) & ~31;
-        return (p32 == 32 || p32 == 96) ? p32 : (B + 63) & ~63;
+    switch (path_for(net, B)) {
+        case KV_PATH_WINO88: {
+            const int p32 = (B + 31) & ~31;
+            return (p32 == 32 || p32 == 96) ? p32 : (B + 63) & ~63;
+        }
+        case KV_PATH_DIRECT: return (B + 3) & ~3;
+        default: return (B + 31) & ~31;
     }
-    return use_wino(net, B) ? (B + 31) & ~31 : (B + 3) & ~3;
 }
 
 static int net_reserve(kv_net* net, int nb_pad) {
@@ -1001,16 +766,17 @@ static int net_reserve(kv_net* net, int nb_pad) {
     int cap = nb_pad < 64 ? 64 : nb_pad;
     (void)hipFree(net->x16); (void)hipFree(net->X); (void)hipFree(net->T); (void)hipFree(net->pfeat);
     (void)hipFree(net->V); (void)hipFree(net->Mw); (void)hipFree(net->V256); (void)hipFree(net->vmax);
-    net->x16 = net->X = net->T = net->pfeat = net->V = net->Mw = net->V256 = nullptr;
+    net->x16 = net->X = net->T = net->pfeat = nullptr;
+    net->V = net->Mw = net->V256 = nullptr;
     net->vmax = nullptr;
     net->cap = 0;
     KV_HIP(hipMalloc(&net->x16, (size_t)cap * 64 * 16 * 4));
     KV_HIP(hipMalloc(&net->X, (size_t)cap * 64 * 512 * 4));
     KV_HIP(hipMalloc(&net->T, (size_t)cap * 64 * 512 * 4));
     KV_HIP(hipMalloc(&net->pfeat, (size_t)cap * 128 * 4));
-    KV_HIP(hipMalloc(&net->V, (size_t)kv::WN_XI * cap * 4 * 512 * 4));
-    KV_HIP(hipMalloc(&net->Mw, (size_t)kv::WN_XI * cap * 4 * 512 * 4));
-    KV_HIP(hipMalloc(&net->V256, (size_t)kv::WN_XI * cap * 4 * 256 * 4));
+    KV_HIP(hipMalloc(&net->V, (size_t)cap * kWsBoard));
+    KV_HIP(hipMalloc(&net->Mw, (size_t)cap * kWsBoard));
+    KV_HIP(hipMalloc(&net->V256, (size_t)cap * kWs256Board));
     KV_HIP(hipMalloc(&net->vmax, (size_t)12 * cap * sizeof(unsigned)));
     if (!net->slab)  // 48 splits x 16 boards x 64 px x 512 channels
         KV_HIP(hipMalloc(&net->slab, (size_t)(144 / kSplitKt) * kSplitMaxBoards * 64 * 512 * 4));
@@ -1021,7 +787,7 @@ static int net_reserve(kv_net* net, int nb_pad) {
 static int net_heads(kv_net* net, int nb, float* policy, float* value, hipStream_t st);
 
 // LDS_PAD: dynamic LDS requested beyond the tiles' need, to cap workgroups per CU
-template <int K, int WR, int WC, int MT, int NT, int CK = 32, int LDS_PAD = 0, int XI = kv::WN_XI>
+template <int K, int WR, int WC, int MT, int NT, int CK, int LDS_PAD, int XI>
 static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st,
                               int xi0 = 0, int nxi = XI) {
     using T = kv::WinoTile<WR, WC, MT, NT, CK>;
@@ -1034,21 +800,6 @@ static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows
                        U, M, rows, 512, stride, xi0);
     KV_HIP(hipGetLastError());
     return KV_OK;
-}
-
-// Tile per batch size. 36 GEMMs x (rows/WM) x (512/WN) tiles over the CUs'
-// resident slots: at 1,024 rows (256 boards) 128x128 tiles give 1,152 tiles
-// for 512 slots (2 per CU: 2.25 rounds), 64x128 tiles with 3 workgroups per CU
-// give 2,304 for 768 slots -- exactly 3 rounds -- and run 3 % faster; above
-// that the 128x128 tile's operand reuse wins (measured: forward 2.10 vs 2.17
-// ms at 256 boards, 15.7 vs 15.1 ms at 2048). Both tiles accumulate each
-// output over k in the same MFMA order, so the choice does not change a bit
-// of the result (batch invariance holds across it).
-template <int K>
-static int launch_wino_gemm(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
-    if (rows <= 1024)  // 64 x 128, 4 waves of 32x64, k-tiles of 16, LDS padded to 48 KB -> 3 per CU
-        return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720>(V, U, M, rows, stride, st);
-    return launch_wino_gemm_t<K, 4, 2, 1, 2>(V, U, M, rows, stride, st);  // 128 x 128, 8 waves, 2 per CU
 }
 
 // F(4x8) GEMMs (60 points, rows = 2 per board): 128x128 tiles (8 waves, 2 per CU) when
@@ -1067,7 +818,7 @@ static int launch_wino48_gemm(const float* V, const float* U, float* M, int rows
     return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720, kv::W48_XI>(V, U, M, rows, stride, st);
 }
 
-template <int K, int TM, int XI = kv::WN_XI, int RSH = 2>
+template <int K, int TM, int XI, int RSH>
 static int launch_wino_gemm_h3_t(const float* V, const uint16_t* Uh, const uint16_t* Ul, const unsigned* vmax,
                                  float* M, int rows, int stride, hipStream_t st) {
     using T = kv::WinoH3<TM>;
@@ -1083,104 +834,41 @@ static int launch_wino_gemm_h3_t(const float* V, const uint16_t* Uh, const uint1
 // 128-row tiles (2 workgroups per CU) when the rows allow: at 1,024 rows 4 %
 // faster per forward than the 64-row tile's exact 3 rounds (operand traffic
 // into the CUs, not MFMA, bounds this kernel); same k order, same bits.
-template <int K, int XI = kv::WN_XI, int RSH = 2>
-static int launch_wino_gemm_h3(const float* V, const uint16_t* Uh, const uint16_t* Ul, const unsigned* vmax, float* M,
-                               int rows, int stride, hipStream_t st) {
-    if (rows % 128) return launch_wino_gemm_h3_t<K, 1, XI, RSH>(V, Uh, Ul, vmax, M, rows, stride, st);
-    return launch_wino_gemm_h3_t<K, 2, XI, RSH>(V, Uh, Ul, vmax, M, rows, stride, st);
-}
-
 template <int K>
-static int launch_wino_gemm_bf6(const float* V, const uint16_t* Uh, const uint16_t* Um, const uint16_t* Ul, float* M,
-                                int rows, int stride, hipStream_t st) {
-    using T = kv::WinoBf6;
-    KV_HIP(lds_opt_in((const void*)kv::wino_gemm_bf6_kernel<K>, (int)T::BYTES));
-    const int nwg = kv::WN_XI * (rows / T::WM) * (512 / T::WN);
-    KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0, KV_EINVAL, "wino gemm bf16x6: rows %d", rows);
-    hipLaunchKernelGGL((kv::wino_gemm_bf6_kernel<K>), dim3(nwg), dim3(256), T::BYTES, st, V, Uh, Um, Ul, M, rows, 512,
-                       stride);
-    KV_HIP(hipGetLastError());
-    return KV_OK;
+static int launch_wino48_gemm_h3(const float* V, const uint16_t* Uh, const uint16_t* Ul, const unsigned* vmax, float* M,
+                                 int rows, int stride, hipStream_t st) {
+    if (rows % 128) return launch_wino_gemm_h3_t<K, 1, kv::W48_XI, 1>(V, Uh, Ul, vmax, M, rows, stride, st);
+    return launch_wino_gemm_h3_t<K, 2, kv::W48_XI, 1>(V, Uh, Ul, vmax, M, rows, stride, st);
 }
 
 // f16x3: the per-board max |V| slot of conv layer l's input (nullptr otherwise)
-static unsigned* net_vmax(kv_net* net, int l) {
-    return net->precision == KV_PREC_F16X3 ? net->vmax + (size_t)l * net->cap : nullptr;
-}
-
-// the Winograd GEMMs of conv layer l in the net's precision
-template <int K>
-static int wino_gemm_layer(kv_net* net, int l, const float* V, float* M, int rows, int stride, hipStream_t st) {
-    if (net->precision == KV_PREC_BF16X6) {
-        const size_t o = net->uoff[l];
-        return launch_wino_gemm_bf6<K>(V, net->Up[0] + o, net->Up[1] + o, net->Up[2] + o, M, rows, stride, st);
-    }
-    if (net->precision == KV_PREC_F16X3) {
-        const size_t o = net->uoff[l];
-        return launch_wino_gemm_h3<K>(V, net->Uf[0] + o, net->Uf[1] + o, net_vmax(net, l), M, rows, stride, st);
-    }
-    return launch_wino_gemm<K>(V, net->U + net->uoff[l], M, rows, stride, st);
-}
-
-// output transform of conv layer l (its M) -> Y and / or the next conv's V
-template <bool RESID, bool WRITE_Y, bool NEXT_V>
-static int launch_wino_out(kv_net* net, int l, const float* M, int nb, int stride, const float* resid, float* Y,
-                           float* Vn, hipStream_t st) {
-    const float* W = net->w;
-    hipLaunchKernelGGL((kv::wino_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 64, nb), dim3(256), 0, st, M, stride,
-                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn, net_vmax(net, l), net->ut[l],
-                       NEXT_V ? net_vmax(net, l + 1) : nullptr);
-    KV_HIP(hipGetLastError());
-    return KV_OK;
-}
-
-// conv2 + the 5 residual blocks for boards [0, nb) on stream st
-static int wino_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
-    const int rows = nb * 4, stride = rows;
-    float* V = net->V;
-    float* M = net->Mw;
-    int rc;
-    if ((rc = wino_gemm_layer<256>(net, 1, net->V256, M, rows, stride, st))) return rc;
-    if ((rc = launch_wino_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st))) return rc;
-    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
-    for (int r = 0; r < 5; ++r) {
-        const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
-        const bool m = mark && r == 2;  // one representative residual GEMM for the engine's timing hook
-        if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-        if ((rc = wino_gemm_layer<512>(net, l1, V, M, rows, stride, st))) return rc;
-        if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
-        if ((rc = launch_wino_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st))) return rc;
-        if ((rc = wino_gemm_layer<512>(net, l2, V, M, rows, stride, st))) return rc;
-        rc = r < 4 ? launch_wino_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
-                   : launch_wino_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
-        if (rc) return rc;
-    }
-    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
-    return KV_OK;
+static unsigned* net_vmax(kv_net* net, int l, int path) {
+    return path == KV_PATH_WINO48_F16X3 ? net->vmax + (size_t)l * net->cap : nullptr;
 }
 
 template <bool RESID, bool WRITE_Y, bool NEXT_V>
-static int launch_wino48_out(kv_net* net, int l, const float* M, int nb, int stride, const float* resid, float* Y,
-                             float* Vn, hipStream_t st) {
+static int launch_wino48_out(kv_net* net, int l, int path, const float* M, int nb, int stride, const float* resid,
+                             float* Y, float* Vn, hipStream_t st) {
     const float* W = net->w;
     hipLaunchKernelGGL((kv::wino48_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 64, nb), dim3(128), 0, st, M,
-                       stride, W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn, net_vmax(net, l),
-                       net->ut48[l], NEXT_V ? net_vmax(net, l + 1) : nullptr);
+                       stride, W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn, net_vmax(net, l, path),
+                       net->ut48[l], NEXT_V ? net_vmax(net, l + 1, path) : nullptr);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
 
-// the F(4x8) GEMMs of conv layer l in the net's precision (fp32 or f16x3)
+// the F(4x8) GEMMs of conv layer l on the path (fp32 or f16x3)
 template <int K>
-static int wino48_gemm_layer(kv_net* net, int l, const float* V, float* M, int rows, int stride, hipStream_t st) {
+static int wino48_gemm_layer(kv_net* net, int l, int path, const float* V, float* M, int rows, int stride,
+                             hipStream_t st) {
     const size_t o = net->uoff48[l];
-    if (net->precision == KV_PREC_F16X3)
-        return launch_wino_gemm_h3<K, kv::W48_XI, 1>(V, net->Uf48[0] + o, net->Uf48[1] + o, net_vmax(net, l), M, rows,
-                                                      stride, st);
+    if (path == KV_PATH_WINO48_F16X3)
+        return launch_wino48_gemm_h3<K>(V, net->Uf48[0] + o, net->Uf48[1] + o, net_vmax(net, l, path), M, rows,
+                                        stride, st);
     return launch_wino48_gemm<K>(V, net->U48 + o, M, rows, stride, st);
 }
 
-// KV_DEBUG_SKIP_TRANSFORMS=1: the F(4x8) tower's output/input transform launches are skipped (timing
+// KV_DEBUG_SKIP_TRANSFORMS=1: the Winograd towers' output/input transform launches are skipped (timing
 // probe only: the GEMM-only forward bounds what fusing the transforms away could gain; outputs invalid)
 static bool debug_skip_transforms() {
     static const int v = [] {
@@ -1191,30 +879,32 @@ static bool debug_skip_transforms() {
 }
 
 // conv2 + the 5 residual blocks for boards [0, nb), F(4x8)
-static int wino48_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
+static int wino48_blocks(kv_net* net, int nb, int path, bool mark, hipStream_t st) {
     const int rows = nb * 2, stride = rows;
-    float* V = net->V;
-    float* M = net->Mw;
+    float* V = (float*)net->V;
+    float* M = (float*)net->Mw;
+    float* V256 = (float*)net->V256;
     int rc;
     if (debug_skip_transforms()) {
-        if ((rc = wino48_gemm_layer<256>(net, 1, net->V256, M, rows, stride, st))) return rc;
+        if ((rc = wino48_gemm_layer<256>(net, 1, path, V256, M, rows, stride, st))) return rc;
         for (int l = 2; l < 12; ++l)
-            if ((rc = wino48_gemm_layer<512>(net, l, V, M, rows, stride, st))) return rc;
+            if ((rc = wino48_gemm_layer<512>(net, l, path, V, M, rows, stride, st))) return rc;
         return KV_OK;
     }
-    if ((rc = wino48_gemm_layer<256>(net, 1, net->V256, M, rows, stride, st))) return rc;
-    if ((rc = launch_wino48_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st))) return rc;
+    if ((rc = wino48_gemm_layer<256>(net, 1, path, V256, M, rows, stride, st))) return rc;
+    if ((rc = launch_wino48_out<false, true, true>(net, 1, path, M, nb, stride, nullptr, net->X, V, st))) return rc;
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
     for (int r = 0; r < 5; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         const bool m = mark && r == 2;  // one representative residual GEMM for the engine's timing hook
         if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-        if ((rc = wino48_gemm_layer<512>(net, l1, V, M, rows, stride, st))) return rc;
+        if ((rc = wino48_gemm_layer<512>(net, l1, path, V, M, rows, stride, st))) return rc;
         if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
-        if ((rc = launch_wino48_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st))) return rc;
-        if ((rc = wino48_gemm_layer<512>(net, l2, V, M, rows, stride, st))) return rc;
-        rc = r < 4 ? launch_wino48_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
-                   : launch_wino48_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
+        if ((rc = launch_wino48_out<false, false, true>(net, l1, path, M, nb, stride, nullptr, nullptr, V, st)))
+            return rc;
+        if ((rc = wino48_gemm_layer<512>(net, l2, path, V, M, rows, stride, st))) return rc;
+        rc = r < 4 ? launch_wino48_out<true, true, true>(net, l2, path, M, nb, stride, net->X, net->X, V, st)
+                   : launch_wino48_out<true, true, false>(net, l2, path, M, nb, stride, net->X, net->X, nullptr, st);
         if (rc) return rc;
     }
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
@@ -1232,16 +922,14 @@ static int wino48_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 // -> 5.31 ms. At 2,048 boards the last round is one tile per CU, which the half tiles do
 // not beat (10.25 vs 10.32 ms), so it stays one launch; nor do 64x64 or 128x64 tiles for its last
 // 4 points (10.42-10.49 vs 10.39-10.42 ms, profiles/r03_w88_tail_ab.log). Same k order, same bits
-// (profiles/r03_w88split_ab.log). KV_W88_SPLIT=0 turns it off.
+// (profiles/r03_w88split_ab.log). KV_W88_SPLIT=0 turns it off. The split launch deals its grid in
+// XCD groups of 8, so both parts must be multiples of 8 workgroups; otherwise one launch.
 static int wino88_split_points(int rows) {
     static const int mode = [] {  // thread-safe one-time initialisation
         const char* e = getenv("KV_W88_SPLIT");
         return e ? atoi(e) : 1;
     }();
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 0;
+    const int cus = device_cus();
     if (!mode || cus <= 0) return kv::W88_XI;
     const int per_xi = (rows / 128) * 4, slots = 2 * cus;
     const int rem = (kv::W88_XI * per_xi) % slots;  // tiles of the last round
@@ -1249,7 +937,9 @@ static int wino88_split_points(int rows) {
     const int full = (kv::W88_XI * per_xi) / slots * slots;  // tiles in whole rounds
     int xa = full / per_xi;
     while (xa > 0 && (xa * per_xi) % slots) --xa;
-    return xa > 0 ? xa : kv::W88_XI;
+    // the second launch runs (100 - xa) points as 64x128 tiles: (rows / 64) * 4 per point
+    if (xa <= 0 || (xa * per_xi) % 8 || ((kv::W88_XI - xa) * (rows / 64) * 4) % 8) return kv::W88_XI;
+    return xa;
 }
 
 template <int K>
@@ -1283,16 +973,17 @@ static int launch_wino88_out(kv_net* net, int l, const float* M, int nb, int str
 // conv2 + the 5 residual blocks for boards [0, nb), F(8x8)
 static int wino88_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     const int rows = nb, stride = rows;
-    float* V = net->V;
-    float* M = net->Mw;
+    float* V = (float*)net->V;
+    float* M = (float*)net->Mw;
+    float* V256 = (float*)net->V256;
     int rc;
     if (debug_skip_transforms()) {
-        if ((rc = launch_wino88_gemm<256>(net->V256, net->U88 + net->uoff88[1], M, rows, stride, st))) return rc;
+        if ((rc = launch_wino88_gemm<256>(V256, net->U88 + net->uoff88[1], M, rows, stride, st))) return rc;
         for (int l = 2; l < 12; ++l)
             if ((rc = launch_wino88_gemm<512>(V, net->U88 + net->uoff88[l], M, rows, stride, st))) return rc;
         return KV_OK;
     }
-    if ((rc = launch_wino88_gemm<256>(net->V256, net->U88 + net->uoff88[1], M, rows, stride, st))) return rc;
+    if ((rc = launch_wino88_gemm<256>(V256, net->U88 + net->uoff88[1], M, rows, stride, st))) return rc;
     if ((rc = launch_wino88_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st))) return rc;
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
     for (int r = 0; r < 5; ++r) {
@@ -1311,45 +1002,97 @@ static int wino88_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     return KV_OK;
 }
 
-// Winograd tower: conv2 and the 5 residual blocks (conv1 output in net->T,
-// or conv2's input transform already in net->V256 when v256_ready)
-static int net_tower_wino(kv_net* net, int nb_pad, bool v256_ready, hipStream_t st) {
+// ---- F(8x8) with the fp64 Winograd domain (kv_wino88d.h) ----
+template <int K, int WR, int WC, int MT, int NT>
+static int launch_wino88d_gemm_t(const double* V, const double* U, double* M, int rows, int stride, hipStream_t st) {
+    using T = kv::Wino88dTile<WR, WC, MT, NT>;
+    KV_HIP(lds_opt_in((const void*)kv::wino88d_gemm_kernel<K, WR, WC, MT, NT>, (int)T::BYTES));
+    const int nwg = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
+    KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0, KV_EINVAL, "wino gemm f64: rows %d vs tile %d", rows, T::WM);
+    hipLaunchKernelGGL((kv::wino88d_gemm_kernel<K, WR, WC, MT, NT>), dim3(nwg), dim3(T::THREADS), T::BYTES, st, V, U,
+                       M, rows, 512, stride);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+// 128x128 tiles (8 waves of 64x32) when the rows allow, else 64x128 / 32x128 (4 waves); every
+// shape runs the same k-steps, so the same bits
+template <int K>
+static int launch_wino88d_gemm(const double* V, const double* U, double* M, int rows, int stride, hipStream_t st) {
+    if (rows % 128 == 0) return launch_wino88d_gemm_t<K, 2, 4, 4, 2>(V, U, M, rows, stride, st);
+    if (rows % 64 == 0) return launch_wino88d_gemm_t<K, 1, 4, 4, 2>(V, U, M, rows, stride, st);
+    return launch_wino88d_gemm_t<K, 1, 4, 2, 2>(V, U, M, rows, stride, st);
+}
+
+template <bool RESID, bool WRITE_Y, bool NEXT_V>
+static int launch_wino88d_out(kv_net* net, int l, const double* M, int nb, int stride, const float* resid, float* Y,
+                              double* Vn, hipStream_t st) {
+    const float* W = net->w;
+    hipLaunchKernelGGL((kv::wino88d_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 256, nb), dim3(256), 0, st, M,
+                       stride, W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+static int wino88d_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
+    const int rows = nb, stride = rows;
+    double* V = (double*)net->V;
+    double* M = (double*)net->Mw;
+    const double* U = net->U88d;
     int rc;
-    if (use_wino88(net, nb_pad)) {
+    if ((rc = launch_wino88d_gemm<256>((const double*)net->V256, U + net->uoff88[1], M, rows, stride, st)))
+        return rc;
+    if ((rc = launch_wino88d_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st))) return rc;
+    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
+    for (int r = 0; r < 5; ++r) {
+        const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
+        const bool m = mark && r == 2;
+        if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
+        if ((rc = launch_wino88d_gemm<512>(V, U + net->uoff88[l1], M, rows, stride, st))) return rc;
+        if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
+        if ((rc = launch_wino88d_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st))) return rc;
+        if ((rc = launch_wino88d_gemm<512>(V, U + net->uoff88[l2], M, rows, stride, st))) return rc;
+        rc = r < 4 ? launch_wino88d_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
+                   : launch_wino88d_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
+        if (rc) return rc;
+    }
+    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
+    return KV_OK;
+}
+
+// Winograd tower on `path`: conv2 and the 5 residual blocks (conv1 output in
+// net->T, or conv2's input transform already in net->V256 when v256_ready)
+static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hipStream_t st) {
+    int rc;
+    net->dom_path = path;
+    net->dom_launches = 1;
+    if (path == KV_PATH_WINO88 || path == KV_PATH_WINO88_F64) {
+        const bool f64 = path == KV_PATH_WINO88_F64;
         if (!v256_ready) {
-            hipLaunchKernelGGL(kv::wino88_in_kernel<256>, dim3(1, nb_pad), dim3(256), 0, st, net->T, nb_pad,
-                               net->V256);
+            if (f64)
+                hipLaunchKernelGGL(kv::wino88d_in_kernel<256>, dim3(1, nb_pad), dim3(256), 0, st, net->T, nb_pad,
+                                   (double*)net->V256);
+            else
+                hipLaunchKernelGGL(kv::wino88_in_kernel<256>, dim3(1, nb_pad), dim3(256), 0, st, net->T, nb_pad,
+                                   (float*)net->V256);
             KV_HIP(hipGetLastError());
         }
-        if ((rc = wino88_blocks(net, nb_pad, true, st))) return rc;
+        if ((rc = f64 ? wino88d_blocks(net, nb_pad, true, st) : wino88_blocks(net, nb_pad, true, st))) return rc;
         net->dom_flop = 2.0 * kv::W88_XI * nb_pad * 512.0 * 512.0;
         net->dom_algo = KV_ALGO_WINOGRAD88;
-        net->dom_launches = 1;
+        net->dom_split = f64 ? 0 : (nb_pad % 128 == 0 ? wino88_split_points(nb_pad) : kv::W88_XI);
         return KV_OK;
     }
-    if (use_wino48(net, nb_pad)) {
-        const int rows48 = nb_pad * 2;
-        if (!v256_ready) {
-            hipLaunchKernelGGL(kv::wino48_in_kernel<256>, dim3(256 / 64, nb_pad), dim3(128), 0, st, net->T, rows48,
-                               net->V256, net_vmax(net, 1));
-            KV_HIP(hipGetLastError());
-        }
-        if ((rc = wino48_blocks(net, nb_pad, true, st))) return rc;
-        net->dom_flop = 2.0 * kv::W48_XI * rows48 * 512.0 * 512.0;
-        net->dom_algo = KV_ALGO_WINOGRAD48;
-        net->dom_launches = 1;
-        return KV_OK;
-    }
-    const int rows = nb_pad * 4;
+    const int rows48 = nb_pad * 2;
     if (!v256_ready) {
-        hipLaunchKernelGGL(kv::wino_in_kernel<256>, dim3(256 / 64, nb_pad), dim3(256), 0, st, net->T, rows,
-                           net->V256, net_vmax(net, 1));
+        hipLaunchKernelGGL(kv::wino48_in_kernel<256>, dim3(256 / 64, nb_pad), dim3(128), 0, st, net->T, rows48,
+                           (float*)net->V256, net_vmax(net, 1, path));
         KV_HIP(hipGetLastError());
     }
-    if ((rc = wino_blocks(net, nb_pad, true, st))) return rc;
-    net->dom_flop = 2.0 * kv::WN_XI * rows * 512.0 * 512.0;
-    net->dom_algo = KV_ALGO_WINOGRAD;
-    net->dom_launches = 1;
+    if ((rc = wino48_blocks(net, nb_pad, path, true, st))) return rc;
+    net->dom_flop = 2.0 * kv::W48_XI * rows48 * 512.0 * 512.0;
+    net->dom_algo = KV_ALGO_WINOGRAD48;
+    net->dom_split = 0;
     return KV_OK;
 }
 
@@ -1361,55 +1104,41 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     const kv::PackOffsets& o = net->off;
     int rc;
     const bool tm = net->timing;
-    const bool wino = use_wino(net, nb);
+    const int path = path_for(net, nb);
+    KV_REQUIRE(net->built[path], KV_EINVAL, "kv_net: conv path %d has no weights (load the net after choosing it)",
+               path);
     if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
-    if (wino && net->precision == KV_PREC_F16X3)
+    if (path == KV_PATH_WINO48_F16X3)
         KV_HIP(hipMemsetAsync(net->vmax, 0, (size_t)12 * net->cap * sizeof(unsigned), st));
-    // F(8x8): the stem builds conv2's V itself (stem_kernel<KV_STEM88>: 4, the lane-swap form; 3, the LDS-plane form)
-    const bool w88 = wino && use_wino88(net, nb);
+    // fp32 F(8x8) and F(4x8): the stem builds conv2's V itself
+    bool v256_ready = false;
     if (boards) {
-        if (w88)
-            hipLaunchKernelGGL(kv::stem_kernel<KV_STEM88>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
-                               W + o.scale[0], W + o.shift[0], net->V256, nb_pad, nullptr);
-        else if (wino && use_wino48(net, nb))
+        if (path == KV_PATH_WINO88)
+            hipLaunchKernelGGL(kv::stem_kernel<4>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
+                               W + o.scale[0], W + o.shift[0], (float*)net->V256, nb_pad, nullptr);
+        else if (path == KV_PATH_WINO48 || path == KV_PATH_WINO48_F16X3)
             hipLaunchKernelGGL(kv::stem_kernel<2>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
-                               W + o.scale[0], W + o.shift[0], net->V256, nb_pad * 2, net_vmax(net, 1));
-        else if (wino)
-            hipLaunchKernelGGL(kv::stem_kernel<1>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
-                               W + o.scale[0], W + o.shift[0], net->V256, nb_pad * 4, net_vmax(net, 1));
+                               W + o.scale[0], W + o.shift[0], (float*)net->V256, nb_pad * 2,
+                               net_vmax(net, 1, path));
         else
             hipLaunchKernelGGL(kv::stem_kernel<0>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], net->T, nb_pad * 4, nullptr);
         KV_HIP(hipGetLastError());
+        v256_ready = path != KV_PATH_DIRECT && path != KV_PATH_WINO88_F64;
     } else if ((rc = launch_conv<16, 16, false>(net->x16, W + o.w[0], W + o.scale[0], W + o.shift[0], nullptr,
                                                 net->T, 256, nb_pad, nullptr, st))) {
         return rc;
     }
-    if (wino) {
-        if ((rc = net_tower_wino(net, nb_pad, boards != nullptr, st))) return rc;
+    if (path_is_wino(path)) {
+        if ((rc = net_tower_wino(net, nb_pad, path, v256_ready, st))) return rc;
         return net_heads(net, nb, policy, value, st);
     }
-    const bool bf3 = net->precision == KV_PREC_BF16X3;
-    if (bf3) {
-        if ((rc = launch_conv_bf3<256, false>(net->T, net->whi + o.w[1], net->wlo + o.w[1], W + o.scale[1],
-                                              W + o.shift[1], nullptr, net->X, 512, nb_pad, net->slab, st)))
-            return rc;
-    } else if ((rc = launch_conv<256, 32, false>(net->T, W + o.w[1], W + o.scale[1], W + o.shift[1], nullptr, net->X,
-                                                 512, nb_pad, net->slab, st))) {
+    if ((rc = launch_conv<256, 32, false>(net->T, W + o.w[1], W + o.scale[1], W + o.shift[1], nullptr, net->X, 512,
+                                          nb_pad, net->slab, st)))
         return rc;
-    }
     if (tm) KV_HIP(hipEventRecord(net->ev[1], st));
     if (net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-    for (int r = 0; r < 5 && bf3; ++r) {
-        const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
-        if ((rc = launch_conv_bf3<512, false>(net->X, net->whi + o.w[l1], net->wlo + o.w[l1], W + o.scale[l1],
-                                              W + o.shift[l1], nullptr, net->T, 512, nb_pad, net->slab, st)))
-            return rc;
-        if ((rc = launch_conv_bf3<512, true>(net->T, net->whi + o.w[l2], net->wlo + o.w[l2], W + o.scale[l2],
-                                             W + o.shift[l2], net->X, net->X, 512, nb_pad, net->slab, st)))
-            return rc;
-    }
-    for (int r = 0; r < 5 && !bf3; ++r) {
+    for (int r = 0; r < 5; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         if ((rc = launch_conv<512, 32, false>(net->X, W + o.w[l1], W + o.scale[l1], W + o.shift[l1], nullptr, net->T,
                                               512, nb_pad, net->slab, st)))
@@ -1421,6 +1150,8 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     if (tm) KV_HIP(hipEventRecord(net->ev[2], st));
     if (net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
     net->dom_algo = KV_ALGO_DIRECT;
+    net->dom_path = KV_PATH_DIRECT;
+    net->dom_split = 0;
     net->dom_launches = 10;
     net->dom_flop = (double)nb_pad * 64 * 512 * 4608 * 2;
     return net_heads(net, nb, policy, value, st);
@@ -1443,6 +1174,7 @@ static int net_heads(kv_net* net, int nb, float* policy, float* value, hipStream
     return KV_OK;
 }
 
+// ------------------------------------------------ path weights (lazy) --
 // f16x3 weights of one Winograd set: per-layer scale 2^ut putting max |U| in
 // [2^14, 2^15), then the two fp16 pieces in the GEMM's B-image layout
 static int split_f16_set(const float* U, const size_t* uoff, int nxi, uint16_t* const* Uf, int* ut) {
@@ -1472,10 +1204,269 @@ static int split_f16_set(const float* U, const size_t* uoff, int nxi, uint16_t* 
     return KV_OK;
 }
 
+static size_t wino_offsets(size_t* uoff, int nxi) {
+    size_t tot = 0;
+    for (int l = 1; l < 12; ++l) {
+        uoff[l] = tot;
+        tot += (size_t)nxi * kv::kConv[l].cout * kv::kConv[l].cin;
+    }
+    return tot;
+}
+
+// the Winograd weights `path` reads, transformed from the loaded packed weights
+// (once per load; a path not used is never allocated)
+static int ensure_path(kv_net* net, int path) {
+    if (net->built[path]) return KV_OK;
+    const auto each_conv = [&](auto&& launch) {
+        for (int l = 1; l < 12; ++l) {
+            const size_t n = (size_t)kv::kConv[l].cout * kv::kConv[l].cin;
+            launch(l, dim3((unsigned)((n + 255) / 256)));
+        }
+    };
+    int rc;
+    switch (path) {
+        case KV_PATH_DIRECT: break;
+        case KV_PATH_WINO48:
+        case KV_PATH_WINO48_F16X3: {
+            if (!net->built[KV_PATH_WINO48]) {
+                const size_t tot = wino_offsets(net->uoff48, kv::W48_XI);
+                if (!net->U48) KV_HIP(hipMalloc(&net->U48, tot * sizeof(float)));
+                each_conv([&](int l, dim3 g) {
+                    hipLaunchKernelGGL(kv::wino48_weights_kernel, g, dim3(256), 0, 0, net->w + net->off.w[l],
+                                       kv::kConv[l].cout, kv::kConv[l].cin, net->U48 + net->uoff48[l]);
+                });
+                KV_HIP(hipGetLastError());
+                net->built[KV_PATH_WINO48] = true;
+            }
+            if (path == KV_PATH_WINO48_F16X3) {
+                const size_t tot = wino_offsets(net->uoff48, kv::W48_XI);
+                for (int p = 0; p < 2; ++p)
+                    if (!net->Uf48[p]) KV_HIP(hipMalloc(&net->Uf48[p], tot * sizeof(uint16_t)));
+                if ((rc = split_f16_set(net->U48, net->uoff48, kv::W48_XI, net->Uf48, net->ut48))) return rc;
+            }
+            break;
+        }
+        case KV_PATH_WINO88: {
+            const size_t tot = wino_offsets(net->uoff88, kv::W88_XI);
+            if (!net->U88) KV_HIP(hipMalloc(&net->U88, tot * sizeof(float)));
+            each_conv([&](int l, dim3 g) {
+                hipLaunchKernelGGL(kv::wino88_weights_kernel, g, dim3(256), 0, 0, net->w + net->off.w[l],
+                                   kv::kConv[l].cout, kv::kConv[l].cin, net->U88 + net->uoff88[l]);
+            });
+            KV_HIP(hipGetLastError());
+            break;
+        }
+        case KV_PATH_WINO88_F64: {
+            const size_t tot = wino_offsets(net->uoff88, kv::W88_XI);
+            if (!net->U88d) KV_HIP(hipMalloc(&net->U88d, tot * sizeof(double)));
+            each_conv([&](int l, dim3 g) {
+                hipLaunchKernelGGL(kv::wino88d_weights_kernel, g, dim3(256), 0, 0, net->w + net->off.w[l],
+                                   kv::kConv[l].cout, kv::kConv[l].cin, net->U88d + net->uoff88[l]);
+            });
+            KV_HIP(hipGetLastError());
+            break;
+        }
+        default: KV_REQUIRE(false, KV_EINVAL, "kv_net: unknown conv path %d", path);
+    }
+    KV_HIP(hipDeviceSynchronize());
+    net->built[path] = true;
+    return KV_OK;
+}
+
+// free the Winograd weights no configured path reads (after a calibration chose)
+static void release_unused(kv_net* net) {
+    bool keep[kNPath] = {};
+    keep[path_for(net, 1)] = keep[path_for(net, 1024)] = true;
+    if (!keep[KV_PATH_WINO48] && !keep[KV_PATH_WINO48_F16X3]) {
+        (void)hipFree(net->U48);
+        net->U48 = nullptr;
+        net->built[KV_PATH_WINO48] = false;
+    }
+    if (!keep[KV_PATH_WINO48_F16X3]) {
+        for (int p = 0; p < 2; ++p) {
+            (void)hipFree(net->Uf48[p]);
+            net->Uf48[p] = nullptr;
+        }
+        net->built[KV_PATH_WINO48_F16X3] = false;
+    }
+    if (!keep[KV_PATH_WINO88]) {
+        (void)hipFree(net->U88);
+        net->U88 = nullptr;
+        net->built[KV_PATH_WINO88] = false;
+    }
+    if (!keep[KV_PATH_WINO88_F64]) {
+        (void)hipFree(net->U88d);
+        net->U88d = nullptr;
+        net->built[KV_PATH_WINO88_F64] = false;
+    }
+}
+
+// ------------------------------------------------------- calibration --
+// fp32 + KV_ALGO_AUTO: after each weight load the net measures its candidate
+// paths against the fp64 direct forward (kv_ref64.h) on kCalibBoards seeded
+// boards and keeps, per size class, the fastest one within the budget:
+//   > 16 boards: F(8x8) fp32, then F(4x8) fp32, else F(8x8) with the fp64
+//                Winograd domain (always accepted: its error is the fp32
+//                activations' own, ~1e-6 on every weight set measured);
+//   <= 16:       direct fp32 (split-K), else F(8x8) fp64.
+// Budget: max |dlogit| <= 4e-5 and max |dvalue| <= 4e-6 against fp64 -- the
+// tolerance (1e-4 / 1e-5 against the reference's own fp32 forward, which is
+// itself up to ~3e-5 from fp64 on trained-magnitude weights) less that and a
+// margin for boards outside the calibration set.
+constexpr int kCalibBoards = 64;
+constexpr double kCalibTolLogit = 4e-5, kCalibTolValue = 4e-6;
+
+// the calibration boards: seeded random positions, 40 % of squares occupied by
+// any of the 12 pieces (the parity tests' board distribution), board 0 the
+// initial position
+static void calib_boards(int8_t* b) {
+    uint64_t s = 0x4b56414d44ull;
+    auto next = [&]() {  // splitmix64
+        uint64_t z = (s += 0x9e3779b97f4a7c15ull);
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        return z ^ (z >> 31);
+    };
+    for (int i = 0; i < kCalibBoards * 64; ++i) {
+        const uint64_t r = next();
+        b[i] = (int8_t)(((r >> 8) % 1000) < 400 ? 1 + (r % 12) : 0);
+    }
+    static const int8_t start[64] = {9, 11, 10, 8, 7, 10, 11, 9, 12, 12, 12, 12, 12, 12, 12, 12,
+                                     0, 0,  0,  0, 0, 0,  0,  0, 0,  0,  0,  0,  0,  0,  0,  0,
+                                     0, 0,  0,  0, 0, 0,  0,  0, 0,  0,  0,  0,  0,  0,  0,  0,
+                                     6, 6,  6,  6, 6, 6,  6,  6, 3,  5,  4,  2,  1,  4,  5,  3};
+    memcpy(b, start, 64);
+}
+
+struct Ref64Bufs {
+    double *x0 = nullptr, *xa = nullptr, *xb = nullptr, *pol = nullptr, *val = nullptr;
+    ~Ref64Bufs() {
+        (void)hipFree(x0); (void)hipFree(xa); (void)hipFree(xb); (void)hipFree(pol); (void)hipFree(val);
+    }
+};
+
+// the fp64 forward of nb boards (codes on the device) into r.pol [nb][4096], r.val [nb]
+static int ref64_forward(kv_net* net, const int8_t* boards, int nb, Ref64Bufs& r) {
+    const float* W = net->w;
+    const kv::PackOffsets& o = net->off;
+    KV_HIP(hipMalloc(&r.x0, (size_t)nb * 64 * 16 * sizeof(double)));
+    KV_HIP(hipMalloc(&r.xa, (size_t)nb * 64 * 512 * sizeof(double)));
+    KV_HIP(hipMalloc(&r.xb, (size_t)nb * 64 * 512 * sizeof(double)));
+    KV_HIP(hipMalloc(&r.pol, (size_t)nb * 4096 * sizeof(double)));
+    KV_HIP(hipMalloc(&r.val, (size_t)nb * sizeof(double)));
+    hipLaunchKernelGGL(kv::ref64_encode_kernel, dim3((nb * 64 + 255) / 256), dim3(256), 0, 0, boards, nb, r.x0);
+    hipLaunchKernelGGL(kv::ref64_conv_kernel<16>, dim3(256 / 64, nb), dim3(256), 0, 0, r.x0, W + o.w[0],
+                       W + o.scale[0], W + o.shift[0], nullptr, r.xb, 256);
+    hipLaunchKernelGGL(kv::ref64_conv_kernel<256>, dim3(512 / 64, nb), dim3(256), 0, 0, r.xb, W + o.w[1],
+                       W + o.scale[1], W + o.shift[1], nullptr, r.xa, 512);
+    for (int k = 0; k < 5; ++k) {
+        const int l1 = 2 + 2 * k, l2 = 3 + 2 * k;
+        hipLaunchKernelGGL(kv::ref64_conv_kernel<512>, dim3(512 / 64, nb), dim3(256), 0, 0, r.xa, W + o.w[l1],
+                           W + o.scale[l1], W + o.shift[l1], nullptr, r.xb, 512);
+        hipLaunchKernelGGL(kv::ref64_conv_kernel<512>, dim3(512 / 64, nb), dim3(256), 0, 0, r.xb, W + o.w[l2],
+                           W + o.scale[l2], W + o.shift[l2], r.xa, r.xa, 512);
+    }
+    hipLaunchKernelGGL(kv::ref64_heads_kernel, dim3(nb), dim3(256), 0, 0, r.xa, W + o.head_w, W + o.head_scale,
+                       W + o.head_shift, W + o.pfc_w, W + o.pfc_b, W + o.vfc1_w, W + o.vfc1_b, W + o.vfc2_w,
+                       W + o.vfc2_b, r.pol, r.val);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+// max |candidate - fp64| of nb boards' logits and values
+static int calib_errors(const float* pol, const float* val, const Ref64Bufs& r, int nb, unsigned long long* dmax,
+                        double* e_logit, double* e_value) {
+    KV_HIP(hipMemset(dmax, 0, 2 * sizeof(unsigned long long)));
+    hipLaunchKernelGGL(kv::ref64_maxdiff_kernel, dim3(64), dim3(256), 0, 0, pol, r.pol, (size_t)nb * 4096, dmax);
+    hipLaunchKernelGGL(kv::ref64_maxdiff_kernel, dim3(1), dim3(256), 0, 0, val, r.val, (size_t)nb, dmax + 1);
+    KV_HIP(hipGetLastError());
+    unsigned long long h[2];
+    KV_HIP(hipMemcpy(h, dmax, sizeof h, hipMemcpyDeviceToHost));
+    memcpy(e_logit, &h[0], sizeof(double));
+    memcpy(e_value, &h[1], sizeof(double));
+    return KV_OK;
+}
+
+static int net_calibrate(kv_net* net) {
+    const auto t0 = std::chrono::steady_clock::now();
+    kv_calib& c = net->calib;
+    c = kv_calib{};
+    c.n_boards = kCalibBoards;
+    c.tol_logit = kCalibTolLogit;
+    c.tol_value = kCalibTolValue;
+    for (int p = 0; p < KV_NPATH; ++p) c.err_logit[p] = c.err_value[p] = -1.0;
+    c.err_small_logit = c.err_small_value = -1.0;
+    int8_t hb[kCalibBoards * 64];
+    calib_boards(hb);
+    int8_t* boards = nullptr;
+    float *pol = nullptr, *val = nullptr;
+    unsigned long long* dmax = nullptr;
+    Ref64Bufs r;
+    int rc = KV_OK;
+    auto fail = [&](int code) {
+        (void)hipFree(boards); (void)hipFree(pol); (void)hipFree(val); (void)hipFree(dmax);
+        return code;
+    };
+    if (hipMalloc(&boards, sizeof hb) != hipSuccess || hipMalloc(&pol, (size_t)kCalibBoards * 4096 * 4) ||
+        hipMalloc(&val, kCalibBoards * 4) || hipMalloc(&dmax, 2 * sizeof(unsigned long long)) ||
+        hipMemcpy(boards, hb, sizeof hb, hipMemcpyHostToDevice)) {
+        kv::set_error("kv_net calibration: device allocation failed");
+        return fail(KV_EHIP);
+    }
+    if ((rc = ref64_forward(net, boards, kCalibBoards, r)) || (rc = net_reserve(net, kCalibBoards))) return fail(rc);
+    const auto within = [&](double el, double ev) { return el <= kCalibTolLogit && ev <= kCalibTolValue; };
+    // > 16 boards
+    const int cands[3] = {KV_PATH_WINO88, KV_PATH_WINO48, KV_PATH_WINO88_F64};
+    net->auto_small = KV_PATH_DIRECT;
+    for (int i = 0; i < 3; ++i) {
+        const int p = cands[i];
+        if ((rc = ensure_path(net, p))) return fail(rc);
+        net->auto_large = p;
+        const int nb_pad = net_pad(net, kCalibBoards);
+        if ((rc = net_reserve(net, nb_pad)) ||
+            (rc = net_tower(net, kCalibBoards, nb_pad, boards, pol, val, (hipStream_t)0)) ||
+            (rc = calib_errors(pol, val, r, kCalibBoards, dmax, &c.err_logit[p], &c.err_value[p])))
+            return fail(rc);
+        if (p == KV_PATH_WINO88_F64 || within(c.err_logit[p], c.err_value[p])) break;
+    }
+    // <= 16 boards: the direct split-K class on the first 16 boards
+    const int ns = kSplitMaxBoards;
+    if ((rc = net_tower(net, ns, net_pad(net, ns), boards, pol, val, (hipStream_t)0)) ||
+        (rc = calib_errors(pol, val, r, ns, dmax, &c.err_small_logit, &c.err_small_value)))
+        return fail(rc);
+    if (!within(c.err_small_logit, c.err_small_value)) {
+        if ((rc = ensure_path(net, KV_PATH_WINO88_F64))) return fail(rc);
+        net->auto_small = KV_PATH_WINO88_F64;
+    }
+    c.calibrated = 1;
+    c.path_large = net->auto_large;
+    c.path_small = net->auto_small;
+    release_unused(net);
+    c.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return fail(KV_OK);
+}
+
+// choose (calibrate) and build the paths of the net's precision / algo for the loaded weights
+static int net_prepare(kv_net* net) {
+    if (!net->loaded) return KV_OK;
+    KV_HIP(hipSetDevice(net->device));
+    if (net->precision == KV_PREC_FP32 && net->algo == KV_ALGO_AUTO) {
+        const char* e = getenv("KV_CALIBRATE");  // "0": skip, AUTO keeps F(8x8) / direct (timing probes only)
+        if (!(e && e[0] == '0')) return net_calibrate(net);
+        net->calib = kv_calib{};
+        net->auto_large = KV_PATH_WINO88;
+        net->auto_small = KV_PATH_DIRECT;
+    }
+    int rc;
+    if ((rc = ensure_path(net, path_for(net, 1))) || (rc = ensure_path(net, path_for(net, 1024)))) return rc;
+    release_unused(net);
+    return KV_OK;
+}
+
 extern "C" {
 
 const char* kv_last_error(void) { return kv::g_err; }
-int kv_version(void) { return 1; }
+int kv_version(void) { return 2; }
 
 size_t kv_net_packed_size(void) { return kv::pack_offsets().total; }
 
@@ -1502,68 +1493,8 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
                n_floats);
     KV_HIP(hipSetDevice(net->device));
     KV_HIP(hipMemcpy(net->w, packed, n_floats * sizeof(float), hipMemcpyHostToDevice));
-    if (!net->whi) {
-        KV_HIP(hipMalloc(&net->whi, net->off.total * sizeof(uint16_t)));
-        KV_HIP(hipMalloc(&net->wlo, net->off.total * sizeof(uint16_t)));
-    }
-    for (int l = 1; l < 12; ++l) {  // the 11 convs with Cin 256 / 512
-        const size_t n = (size_t)kv::kConv[l].cout * 9 * kv::kConv[l].cin_pad;
-        hipLaunchKernelGGL(kv::split_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0,
-                           net->w + net->off.w[l], n, net->whi + net->off.w[l], net->wlo + net->off.w[l]);
-        KV_HIP(hipGetLastError());
-    }
-    if (!net->U) {
-        size_t tot = 0;
-        for (int l = 1; l < 12; ++l) {
-            net->uoff[l] = tot;
-            tot += (size_t)kv::WN_XI * kv::kConv[l].cout * kv::kConv[l].cin;
-        }
-        KV_HIP(hipMalloc(&net->U, tot * sizeof(float)));
-        for (int p = 0; p < 3; ++p) KV_HIP(hipMalloc(&net->Up[p], tot * sizeof(uint16_t)));
-        for (int p = 0; p < 2; ++p) KV_HIP(hipMalloc(&net->Uf[p], tot * sizeof(uint16_t)));
-        net->utot = tot;
-    }
-    for (int l = 1; l < 12; ++l) {
-        const size_t n = (size_t)kv::kConv[l].cout * kv::kConv[l].cin;
-        hipLaunchKernelGGL(kv::wino_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0,
-                           net->w + net->off.w[l], kv::kConv[l].cout, kv::kConv[l].cin, net->U + net->uoff[l]);
-        KV_HIP(hipGetLastError());
-    }
-    if (!net->U48) {
-        size_t tot = 0;
-        for (int l = 1; l < 12; ++l) {
-            net->uoff48[l] = tot;
-            tot += (size_t)kv::W48_XI * kv::kConv[l].cout * kv::kConv[l].cin;
-        }
-        KV_HIP(hipMalloc(&net->U48, tot * sizeof(float)));
-        for (int p = 0; p < 2; ++p) KV_HIP(hipMalloc(&net->Uf48[p], tot * sizeof(uint16_t)));
-    }
-    for (int l = 1; l < 12; ++l) {
-        const size_t n = (size_t)kv::kConv[l].cout * kv::kConv[l].cin;
-        hipLaunchKernelGGL(kv::wino48_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0,
-                           net->w + net->off.w[l], kv::kConv[l].cout, kv::kConv[l].cin, net->U48 + net->uoff48[l]);
-        KV_HIP(hipGetLastError());
-    }
-    hipLaunchKernelGGL(kv::split3_kernel, dim3((unsigned)((net->utot + 255) / 256)), dim3(256), 0, 0, net->U,
-                       net->utot, net->Up[0], net->Up[1], net->Up[2]);
-    KV_HIP(hipGetLastError());
-    int rc;
-    if (!net->U88) {
-        size_t tot = 0;
-        for (int l = 1; l < 12; ++l) {
-            net->uoff88[l] = tot;
-            tot += (size_t)kv::W88_XI * kv::kConv[l].cout * kv::kConv[l].cin;
-        }
-        KV_HIP(hipMalloc(&net->U88, tot * sizeof(float)));
-    }
-    for (int l = 1; l < 12; ++l) {
-        const size_t n = (size_t)kv::kConv[l].cout * kv::kConv[l].cin;
-        hipLaunchKernelGGL(kv::wino88_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0,
-                           net->w + net->off.w[l], kv::kConv[l].cout, kv::kConv[l].cin, net->U88 + net->uoff88[l]);
-        KV_HIP(hipGetLastError());
-    }
-    if ((rc = split_f16_set(net->U, net->uoff, kv::WN_XI, net->Uf, net->ut))) return rc;
-    if ((rc = split_f16_set(net->U48, net->uoff48, kv::W48_XI, net->Uf48, net->ut48))) return rc;
+    for (int p = 0; p < kNPath; ++p) net->built[p] = false;
+    net->built[KV_PATH_DIRECT] = true;
     if (!net->stemT) KV_HIP(hipMalloc(&net->stemT, 9 * 12 * 256 * sizeof(float)));
     hipLaunchKernelGGL(kv::stem_weights_kernel, dim3(9 * 12), dim3(256), 0, 0, net->w + net->off.w[0], net->stemT);
     if (!net->v1wT) KV_HIP(hipMalloc(&net->v1wT, 64 * 512 * sizeof(float)));
@@ -1572,26 +1503,38 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
     KV_HIP(hipGetLastError());
     KV_HIP(hipDeviceSynchronize());
     net->loaded = true;
-    return KV_OK;
+    return net_prepare(net);
 }
 
 int kv_net_set_algo(kv_net* net, int algo) {
     KV_REQUIRE(net, KV_EINVAL, "kv_net_set_algo: NULL");
-    KV_REQUIRE(algo == KV_ALGO_AUTO || algo == KV_ALGO_DIRECT || algo == KV_ALGO_WINOGRAD ||
-                   algo == KV_ALGO_WINOGRAD48 || algo == KV_ALGO_WINOGRAD88,
-               KV_EINVAL,
-               "kv_net_set_algo: unknown algo %d", algo);
+    KV_REQUIRE(algo != 2, KV_EINVAL, "kv_net_set_algo: KV_ALGO 2 (Winograd F(4x4)) was retired; use "
+                                     "KV_ALGO_WINOGRAD48 or KV_ALGO_WINOGRAD88");
+    KV_REQUIRE(algo == KV_ALGO_AUTO || algo == KV_ALGO_DIRECT || algo == KV_ALGO_WINOGRAD48 ||
+                   algo == KV_ALGO_WINOGRAD88,
+               KV_EINVAL, "kv_net_set_algo: unknown algo %d", algo);
+    if (net->algo == algo) return KV_OK;
     net->algo = algo;
-    return KV_OK;
+    return net_prepare(net);
 }
 
 int kv_net_set_precision(kv_net* net, int precision) {
     KV_REQUIRE(net, KV_EINVAL, "kv_net_set_precision: NULL");
-    KV_REQUIRE(precision == KV_PREC_FP32 || precision == KV_PREC_BF16X3 || precision == KV_PREC_BF16X6 ||
-                   precision == KV_PREC_F16X3,
-               KV_EINVAL,
+    KV_REQUIRE(precision != 1 && precision != 2, KV_EINVAL,
+               "kv_net_set_precision: precision %d (bf16x3 / bf16x6) was retired; use KV_PREC_FP32, KV_PREC_F16X3 "
+               "or KV_PREC_F64W", precision);
+    KV_REQUIRE(precision == KV_PREC_FP32 || precision == KV_PREC_F16X3 || precision == KV_PREC_F64W, KV_EINVAL,
                "kv_net_set_precision: unknown precision %d", precision);
+    if (net->precision == precision) return KV_OK;
     net->precision = precision;
+    return net_prepare(net);
+}
+
+int kv_net_calibration(kv_net* net, kv_calib* out) {
+    KV_REQUIRE(net && out, KV_EINVAL, "kv_net_calibration: NULL argument");
+    *out = net->calib;
+    out->path_large = path_for(net, 1024);
+    out->path_small = path_for(net, 1);
     return KV_OK;
 }
 
@@ -1657,20 +1600,16 @@ void kv_net_destroy(kv_net* net) {
     if (!net) return;
     (void)hipSetDevice(net->device);
     (void)hipFree(net->w);
-    (void)hipFree(net->whi);
-    (void)hipFree(net->wlo);
     (void)hipFree(net->slab);
     (void)hipFree(net->x16);
     (void)hipFree(net->X);
     (void)hipFree(net->T);
     (void)hipFree(net->pfeat);
-    (void)hipFree(net->U);
     (void)hipFree(net->U48);
     (void)hipFree(net->U88);
+    (void)hipFree(net->U88d);
     (void)hipFree(net->stemT);
     (void)hipFree(net->v1wT);
-    for (int p = 0; p < 3; ++p) (void)hipFree(net->Up[p]);
-    for (int p = 0; p < 2; ++p) (void)hipFree(net->Uf[p]);
     for (int p = 0; p < 2; ++p) (void)hipFree(net->Uf48[p]);
     (void)hipFree(net->vmax);
     (void)hipFree(net->V);
@@ -1697,10 +1636,11 @@ int net_set_res_events(kv_net* net, hipEvent_t a, hipEvent_t b) {
     net->res_b = b;
     return KV_OK;
 }
-void net_dom_info(const kv_net* net, int* algo, int* launches, double* flop) {
+void net_dom_info(const kv_net* net, int* algo, int* launches, double* flop, int* path, int* split) {
+    *split = net->dom_split;
     *algo = net->dom_algo;
     *launches = net->dom_launches;
     *flop = net->dom_flop;
+    *path = net->dom_path;
 }
-int net_set_algo_internal(kv_net* net, int algo) { return kv_net_set_algo(net, algo); }
 }  // namespace kv

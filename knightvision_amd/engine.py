@@ -31,7 +31,7 @@ def packed_from(weights) -> np.ndarray:
     return pack_weights(state_dict_to_numpy(weights))[0]
 
 
-ALGOS = {"auto": 0, "direct": 1, "winograd": 2, "winograd48": 3, "winograd88": 4}
+from .model import ALGOS, PRECISIONS  # noqa: E402
 
 
 class SelfPlayEngine:
@@ -50,7 +50,7 @@ class SelfPlayEngine:
                           game_id_stride=game_id_stride, seed=seed, seed_mode=seed_mode,
                           max_moves=max_moves if max_moves else 0, batch=batch, eps=eps, alpha=alpha, sims=sims,
                           c_puct=c_puct, eval_mode=eval_mode, record_cap=record_cap, recycle=1 if recycle else 0,
-                          precision={"fp32": 0, "bf16x3": 1, "bf16x6": 2, "f16x3": 3}[precision], algo=ALGOS[algo],
+                          precision=PRECISIONS[precision], algo=ALGOS[algo],
                           tree_edge_cap=int(tree_edge_cap), keep_root_visits=1 if keep_root_visits else 0)
         h = C.c_void_p()
         _lib.check(L.kv_create(C.byref(cfg), C.byref(h)), "kv_create")
@@ -134,6 +134,12 @@ class SelfPlayEngine:
             _lib.check(L.kv_games(self.h, out.ctypes.data_as(C.POINTER(_lib.Game)), n.value, C.byref(n)),
                        "kv_games")
         return out
+
+    def calibration(self) -> dict:
+        """The network's conv paths and load-time calibration (kv_engine_calibration)."""
+        c = _lib.Calib()
+        _lib.check(_lib.lib().kv_engine_calibration(self.h, C.byref(c)), "kv_engine_calibration")
+        return _lib.calib_dict(c)
 
     def stats(self) -> dict:
         st = _lib.Stats()

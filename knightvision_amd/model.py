@@ -27,8 +27,10 @@ from . import _lib
 from .weights import pack_weights, state_dict_to_numpy
 
 
-PRECISIONS = {"fp32": 0, "bf16x3": 1, "bf16x6": 2, "f16x3": 3}
-ALGOS = {"auto": 0, "direct": 1, "winograd": 2, "winograd48": 3, "winograd88": 4}
+# KV_PREC_* / KV_ALGO_* (include/kv.h). fp32 + auto: the conv path is chosen per weight load by the
+# library's calibration against an fp64 forward (KVNet.calibration()); f64w: the fp64 Winograd domain.
+PRECISIONS = {"fp32": 0, "f16x3": 3, "f64w": 4}
+ALGOS = {"auto": 0, "direct": 1, "winograd48": 3, "winograd88": 4}
 
 
 def batch_norm_rows(bn: nn.BatchNorm2d, x, n_real=None, explicit: bool = False):
@@ -117,6 +119,13 @@ class KVNet:
         _lib.check(L.kv_net_set_algo(self.h, ALGOS[algo]), "kv_net_set_algo")
         p = np.ascontiguousarray(packed, dtype=np.float32)
         _lib.check(L.kv_net_load(self.h, p.ctypes.data_as(C.POINTER(C.c_float)), p.size), "kv_net_load")
+
+    def calibration(self) -> dict:
+        """The conv paths this net runs (> 16 / <= 16 boards) and, for fp32 + auto, the load-time
+        calibration's measured errors against the fp64 forward (kv_net_calibration)."""
+        c = _lib.Calib()
+        _lib.check(_lib.lib().kv_net_calibration(self.h, C.byref(c)), "kv_net_calibration")
+        return _lib.calib_dict(c)
 
     def forward_planes(self, x: torch.Tensor):
         """x: CUDA fp32 [B,12,8,8] -> (policy [B,4096], value [B,1])."""

@@ -14,6 +14,8 @@ The packed layout (one contiguous fp32 blob, offsets in ``PACK_LAYOUT``) is what
 from __future__ import annotations
 
 import collections
+import functools
+
 import numpy as np
 
 BN_EPS = 1e-5
@@ -54,7 +56,10 @@ def synthetic_state_dict(seed: int = 42, variant: str = "init") -> "collections.
                   BN at its init state (gamma 1, beta 0, mean 0, var 1).
       "bn"     -- same convs/FCs, BN affine + running stats randomised.
       "peaked" -- "bn" with policy_fc x30 so move choice depends on the network.
+      "stress" -- trained-network magnitudes (see stress_state_dict).
     """
+    if variant == "stress":
+        return stress_state_dict(seed)
     if variant not in ("init", "bn", "peaked"):
         raise ValueError(f"unknown weight variant {variant!r}")
     rng = np.random.default_rng(seed)
@@ -89,6 +94,71 @@ def synthetic_state_dict(seed: int = 42, variant: str = "init") -> "collections.
             val = val * 30.0
         out[name] = val.astype(np.float32)
     return out
+
+
+STRESS_LOGIT_STD = 4.0
+STRESS_VALUE_STD = 1.0
+STRESS_CAL_BOARDS = 16
+
+
+def _stress_calibration_codes(seed: int) -> np.ndarray:
+    rng = np.random.default_rng(seed + 1000)
+    codes = rng.integers(1, 13, size=(STRESS_CAL_BOARDS, 64)) * (rng.random((STRESS_CAL_BOARDS, 64)) < 0.4)
+    return codes.astype(np.int64)
+
+
+@functools.lru_cache(maxsize=2)
+def _stress_cached(seed: int):
+    import torch
+    import torch.nn.functional as F
+    sd = synthetic_state_dict(seed, "bn")
+    t = {k: torch.from_numpy(np.asarray(v, dtype=np.float64)) for k, v in sd.items()
+         if not k.endswith("num_batches_tracked")}
+    codes = torch.from_numpy(_stress_calibration_codes(seed))
+    x = F.one_hot(codes, 13)[..., 1:].permute(0, 2, 1).reshape(-1, 12, 8, 8).to(torch.float64)
+
+    def cal(h, conv, bn, pad, relu=True):
+        z = F.conv2d(h, t[conv + ".weight"], t[conv + ".bias"], padding=pad)
+        mu = z.mean(dim=(0, 2, 3))
+        var = z.var(dim=(0, 2, 3), unbiased=False)
+        t[bn + ".running_mean"], t[bn + ".running_var"] = mu, var
+        y = (z - mu[None, :, None, None]) / torch.sqrt(var + BN_EPS)[None, :, None, None]
+        y = y * t[bn + ".weight"][None, :, None, None] + t[bn + ".bias"][None, :, None, None]
+        return F.relu(y) if relu else y
+
+    with torch.no_grad():
+        x = cal(x, "conv1", "bn1", 1)
+        x = cal(x, "conv2", "bn2", 1)
+        for i in range(N_RES):
+            p = f"res_blocks.{i}"
+            y = cal(cal(x, p + ".conv1", p + ".bn1", 1), p + ".conv2", p + ".bn2", 1, relu=False)
+            x = F.relu(y + x)
+        pol = torch.flatten(cal(x, "policy_conv", "policy_bn", 0), 1)
+        logits = F.linear(pol, t["policy_fc.weight"], t["policy_fc.bias"])
+        t["policy_fc.weight"] = t["policy_fc.weight"] * (STRESS_LOGIT_STD / float(logits.std()))
+        val = torch.flatten(cal(x, "value_conv", "value_bn", 0), 1)
+        h = F.relu(F.linear(val, t["value_fc1.weight"], t["value_fc1.bias"]))
+        pre = F.linear(h, t["value_fc2.weight"], t["value_fc2.bias"])
+        t["value_fc2.weight"] = t["value_fc2.weight"] * (STRESS_VALUE_STD / float(pre.std()))
+    out = collections.OrderedDict()
+    for k, v in sd.items():
+        out[k] = v if k.endswith("num_batches_tracked") else t[k].numpy().astype(np.float32)
+    return out
+
+
+def stress_state_dict(seed: int = 42) -> "collections.OrderedDict[str, np.ndarray]":
+    """Weights at trained-network magnitudes: the "bn" convolutions and BN affine
+    parameters, with every BatchNorm's running mean / variance set to the batch
+    statistics of its convolution's output over 16 seeded random boards (float64
+    forward), as training leaves them -- so each BN output is O(1) and the
+    residual stream grows through the tower as in a trained ChessNet, instead
+    of shrinking by ~sqrt(3) per default-init convolution -- and policy_fc /
+    value_fc2 scaled so that the logits have standard deviation 4 (max |logit|
+    about 10-15 over 4,096 moves) and the value head's pre-tanh output has
+    standard deviation 1 on those boards. This is the weight set that stresses
+    the fp32 Winograd towers' rounding (error grows with the activations and
+    the head gain; ai/model.py:51-77)."""
+    return collections.OrderedDict((k, v.copy()) for k, v in _stress_cached(seed).items())
 
 
 def _fold(sd, conv, bn):

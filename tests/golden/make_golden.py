@@ -239,7 +239,7 @@ def gen_nn(ref_model, ref_ai, mg, torch):
     idx = np.linspace(0, len(mg["states"]) - 1, 12).astype(int)
     planes = np.stack([planes_from_state(ref_ai, mg["states"][i]) for i in idx])
     out = {"planes": planes}
-    for variant in ("init", "bn", "peaked"):
+    for variant in ("init", "bn", "peaked", "stress"):
         sd = synthetic_state_dict(42, variant)
         net = ref_model.ChessNet()
         net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
@@ -367,18 +367,25 @@ def gen_unittests(ce):
 
 
 def main():
-    ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    nn_only = "--nn-only" in sys.argv  # regenerate nn.npz from the committed movegen.npz positions
+    ref = args[0] if args else "/root/reference"
     sp, ce, ref_model, ref_ai = import_reference(ref)
     import torch
     torch.set_num_threads(8)
 
-    mg = gen_movegen(ce)
-    np.savez_compressed(os.path.join(HERE, "movegen.npz"), **mg)
-    print("movegen positions", len(mg["states"]), "moves", len(mg["moves"]))
+    if nn_only:
+        mg = dict(np.load(os.path.join(HERE, "movegen.npz")))
+    else:
+        mg = gen_movegen(ce)
+        np.savez_compressed(os.path.join(HERE, "movegen.npz"), **mg)
+        print("movegen positions", len(mg["states"]), "moves", len(mg["moves"]))
 
     nn = gen_nn(ref_model, ref_ai, mg, torch)
     np.savez_compressed(os.path.join(HERE, "nn.npz"), **nn)
     print("nn boards", nn["planes"].shape)
+    if nn_only:
+        return
 
     groups = {
         "pg_init_mm80": run_games(sp, ref_model, torch, "init", list(range(42, 42 + 32)), 80, 16, False),

@@ -37,17 +37,18 @@ def test_gemm_traffic_summary_present():
     assert t is not None and 0.94e9 <= t < 1.2e9
 
 
-@pytest.mark.parametrize("rows,cus,xa", [(2048, 256, 100), (1024, 256, 96), (512, 256, 96), (256, 256, 64),
-                                         (384, 256, 100), (128, 256, 100), (64, 256, 100), (2048, 304, 95)])
-def test_w88_split_rule(monkeypatch, rows, cus, xa):
-    """bench.py's label of the F(8x8) GEMM layer mirrors kv_nn.hip wino88_split_points: the points whose
-    128x128 tiles fill whole rounds of 2 workgroups per CU, unless the last round of the one-launch grid is
-    empty or puts exactly one tile on every CU (then one launch)."""
-    monkeypatch.delenv("KV_W88_SPLIT", raising=False)
-    got = bench._w88_split_points(rows, cus)
-    assert got == xa
-    if got < 100:
-        assert (got * (rows // 128) * 4) % (2 * cus) == 0
+@pytest.mark.parametrize("path,rows,split,name", [
+    (2, 2048, 100, "wino_gemm_kernel<512,4,2,1,2,32,100>"), (2, 256, 64, "wino_gemm_kernel<512,4,2,1,2,32,100>"),
+    (2, 320, 100, "wino_gemm_kernel<512,2,2,1,2,16,100>"), (2, 32, 100, "wino_gemm_kernel<512,1,2,1,2,32,100>"),
+    (2, 96, 100, "wino_gemm_kernel<512,1,2,1,2,16,100>"), (3, 2048, 0, "wino88d_gemm_kernel<512,2,4,4,2>"),
+    (3, 64, 0, "wino88d_gemm_kernel<512,1,4,4,2>"), (3, 32, 0, "wino88d_gemm_kernel<512,1,4,2,2>"),
+    (1, 4096, 0, "wino_gemm_kernel<512,4,2,1,2,32,60>"), (0, 2048, 0, "conv3x3_kernel<512,32>")])
+def test_gemm_label(path, rows, split, name):
+    """bench.py names the dominant GEMM launch as kv_nn.hip picks it (rows per point; the F(8x8) point split
+    is the one the library reports in kv_stats.dom_split, not re-derived)."""
+    got, desc = bench.gemm_label(path, rows, split)
+    assert got == name
+    assert (f"points 0-{split - 1}" in desc) == (path == 2 and split < 100)
 
 
 @pytest.mark.parametrize("sims", [0, 8])

@@ -13,10 +13,13 @@ pytestmark = pytest.mark.gpu
 TOL_P, TOL_V = 1e-4, 1e-5
 
 
-# (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x4,3x3) / fp32 Winograd F(4x8,3x3) / fp32
-# Winograd F(8x8,3x3) (the fp32 default above 16 boards) / f16x3 Winograd F(4x4) and F(4x8) (its default) / bf16x6 Winograd F(4x4) / bf16x3 direct
-MODES = [("fp32", "direct"), ("fp32", "winograd"), ("fp32", "winograd48"), ("fp32", "winograd88"),
-         ("f16x3", "winograd"), ("f16x3", "winograd48"), ("bf16x6", "winograd"), ("bf16x3", "auto")]
+# (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x8,3x3) / fp32 Winograd F(8x8,3x3) / fp32 auto
+# (the calibrated choice every product caller runs) / f16x3 Winograd F(4x8) / F(8x8) with the fp64 Winograd domain
+MODES = [("fp32", "direct"), ("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "auto"),
+         ("f16x3", "winograd48"), ("f64w", "auto")]
+# the explicit fp32 / f16x3 Winograd towers are outside the tolerance at trained magnitudes ("stress": 1.2e-3 to
+# 3.6e-3); AUTO measures that at load time and runs the fp64 Winograd domain instead (test_nn_accuracy_gpu.py)
+UNGUARDED = {("fp32", "winograd48"), ("fp32", "winograd88"), ("f16x3", "winograd48")}
 
 
 def _net(variant, precision="fp32", algo="auto"):
@@ -28,8 +31,10 @@ def _net(variant, precision="fp32", algo="auto"):
 
 
 @pytest.mark.parametrize("precision,algo", MODES)
-@pytest.mark.parametrize("variant", ["init", "bn", "peaked"])
+@pytest.mark.parametrize("variant", ["init", "bn", "peaked", "stress"])
 def test_forward_matches_reference_golden(golden_dir, variant, precision, algo):
+    if variant == "stress" and (precision, algo) in UNGUARDED:
+        pytest.skip("explicit Winograd fp32 / f16x3: outside the tolerance at trained magnitudes by design")
     g = np.load(os.path.join(golden_dir, "nn.npz"))
     m = _net(variant, precision, algo)
     p, v = m(torch.from_numpy(g["planes"]).cuda())
@@ -61,7 +66,7 @@ def test_forward_batch_sizes_vs_torch(B, precision, algo):
     assert np.abs(vb.cpu().numpy() - v.cpu().numpy()).max() == 0.0
 
 
-@pytest.mark.parametrize("precision", ["fp32", "f16x3", "bf16x6", "bf16x3"])
+@pytest.mark.parametrize("precision", ["fp32", "f16x3", "f64w"])
 def test_batch_invariance(precision):
     """A board's outputs do not depend on the batch it is evaluated in, within a
     batch-size class (<= 16 boards: split-K direct kernels; > 16: whole-K
@@ -75,7 +80,7 @@ def test_batch_invariance(precision):
     p_all, v_all = m(planes)  # 40 boards: whole-K class
     p_20, v_20 = m(planes[20:])
     assert torch.equal(p_20, p_all[20:]) and torch.equal(v_20, v_all[20:])
-    if precision in ("fp32", "f16x3"):  # f16x3 (F(4x8)): 300 boards run the 128-row GEMM tile, 40 the 64-row one
+    if precision in ("fp32", "f16x3", "f64w"):  # 300 boards run the 128-row GEMM tiles, 40 the 64-row ones
         codes_l = rng.integers(0, 13, size=(300, 64)) * (rng.random((300, 64)) < 0.4)
         codes_l[:40] = codes
         p_l, v_l = m(torch.from_numpy(codes_to_planes(codes_l)).cuda())
@@ -87,18 +92,21 @@ def test_batch_invariance(precision):
     assert float((p_16 - p_all[:16]).abs().max()) < 1e-4
 
 
-def test_wino88_batch_invariance():
+@pytest.mark.parametrize("precision", ["fp32", "f64w"])
+def test_wino88_batch_invariance(precision):
     """F(8x8) (one row per board): a board's outputs are the same bits at 20
     boards (padded to 32: 32-row GEMM tiles, k-tiles of 32), 80 / 96 (padded to
     96: 32-row tiles, k-tiles of 16), 40 / 300 (padded to 64 / 320: 64x128
-    tiles) and 512 boards (128x128 tiles for points 0-95, 64x128 for 96-99)."""
+    tiles) and 512 boards (128x128 tiles for points 0-95, 64x128 for 96-99).
+    f64w (the fp64 Winograd domain, every batch size): 32 / 64 / 128-row tiles,
+    the same k-steps."""
     from knightvision_amd.ai import codes_to_planes
     rng = np.random.default_rng(88)
     codes = rng.integers(0, 13, size=(512, 64)) * (rng.random((512, 64)) < 0.4)
     planes = torch.from_numpy(codes_to_planes(codes)).cuda()
-    m = _net("peaked", "fp32", "winograd88")
+    m = _net("peaked", "fp32", "winograd88") if precision == "fp32" else _net("peaked", "f64w", "auto")
     p_l, v_l = m(planes)
-    for lo, hi in ((0, 40), (20, 40), (0, 300), (0, 96), (16, 96)):
+    for lo, hi in ((0, 40), (20, 40), (0, 300), (0, 96), (16, 96)) + (((0, 1), (5, 8)) if precision == "f64w" else ()):
         p, v = m(planes[lo:hi])
         assert torch.equal(p, p_l[lo:hi]) and torch.equal(v, v_l[lo:hi]), (lo, hi)
 
