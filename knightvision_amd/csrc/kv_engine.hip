@@ -358,7 +358,7 @@ __global__ __launch_bounds__(1024) void k_compact(DevCfg cfg, const Slot* slots,
 // class, so every active slot's leaf row equals its row in the full batch and
 // the searches are unchanged (tests/test_mcts_gpu.py).
 __global__ __launch_bounds__(1024) void k_compact_active(DevCfg cfg, const Slot* slots, int rows, int* slot_of,
-                                                         int* row_of) {
+                                                         int* row_of, Ctr* ctr) {
     __shared__ int wsum[16];
     __shared__ int base;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -381,6 +381,8 @@ __global__ __launch_bounds__(1024) void k_compact_active(DevCfg cfg, const Slot*
         __syncthreads();
     }
     const int cnt = base < rows ? base : rows;
+    // more active slots than the host sized the batch for: some slot would search on stale leaf rows
+    if (tid == 0 && base > rows) atomicOr(&ctr->error, 16);
     __syncthreads();
     const int first = cnt > 0 ? slot_of[0] : 0;
     for (int r = cnt + tid; r < rows; r += 1024) slot_of[r] = first;  // padding rows
@@ -481,9 +483,13 @@ static int eng_wait_copies(kv_engine* e) {
     return KV_OK;
 }
 
+// The engine stream waits for the copy right away (whatever stream the caller used), so two copies on
+// two caller streams are both ordered before the next write to e->rec / root_visits; the event is
+// kept for kv_destroy, which waits for the last copy before freeing the buffers.
 static int eng_note_copy(kv_engine* e, hipStream_t caller) {
     if (!e->copy_done) KV_HIP(hipEventCreateWithFlags(&e->copy_done, hipEventDisableTiming));
     KV_HIP(hipEventRecord(e->copy_done, caller));
+    KV_HIP(hipStreamWaitEvent(e->st, e->copy_done, 0));
     e->copy_pending = true;
     return KV_OK;
 }
@@ -498,9 +504,10 @@ static int eng_counters(kv_engine* e, bool check_error = true) {
         kv::set_error("engine device error flags 0x%x (1: move list overflow, 2: record buffer full, "
                       "4: MCTS tree pool full, %llu expansions dropped -- raise kv_config.tree_edge_cap; "
                       "8: move weights not finite -- every Dirichlet gamma draw of a ply was 0, where the "
-                      "reference's random.choices raises ValueError)",
+                      "reference's random.choices raises ValueError; 16: more active MCTS slots than the compact "
+                      "leaf batch holds -- a host / device count mismatch)",
                       e->ctr_host->error, (unsigned long long)e->ctr_host->tree_overflows);
-        return (e->ctr_host->error & 8) ? KV_EINVAL : KV_EOVERFLOW;
+        return (e->ctr_host->error & (8 | 16)) ? KV_EINVAL : KV_EOVERFLOW;
     }
     return KV_OK;
 }
@@ -786,7 +793,7 @@ int kv_run(kv_engine* e, int64_t max_steps, int64_t stop_after_games) {
             const int R = comp ? (S > 16 ? std::max(act, 17) : act) : S;
             if (comp) {
                 hipLaunchKernelGGL(kv::k_compact_active, dim3(1), dim3(1024), 0, e->st, e->dc, e->slots, R,
-                                   e->mc_slot_of, e->mc_row_of);
+                                   e->mc_slot_of, e->mc_row_of, e->ctr);
                 KV_HIP(hipGetLastError());
             }
             if ((rc = kv::mcts_root(e->dc, t, e->slots, e->moves, e->logits, e->values, e->probs, e->np_mt, e->ctr, e->st)))

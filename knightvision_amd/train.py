@@ -126,12 +126,13 @@ def batch_loss(model, b: Batch, entropy_coef: float = ENTROPY_COEF, amp: bool = 
     return loss, loss_policy, loss_value, entropy, pol
 
 
-def _finite_on_all_ranks(loss: torch.Tensor) -> bool:
+def _finite_on_all_ranks(loss: torch.Tensor, force: bool = False) -> bool:
     """isfinite(loss), agreed over the ranks of an initialised process group
-    (MIN all-reduce of the flag: one rank's NaN skips the batch everywhere)."""
+    (MIN all-reduce of the flag: one rank's NaN skips the batch everywhere).
+    force: run the all-reduce even at world size 1 (tests of the RCCL path)."""
     ok = torch.isfinite(loss.detach()).all()
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or force):
         dev = loss.device if dist.get_backend() == "nccl" else torch.device("cpu")
         flag = ok.to(device=dev, dtype=torch.int32).reshape(1)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
@@ -144,10 +145,11 @@ def make_scaler(device) -> torch.amp.GradScaler:
 
 
 def train_one_epoch(model, data, optimizer, scaler, accumulate_steps: int = ACCUM_STEPS,
-                    entropy_coef: float = ENTROPY_COEF, amp: bool = True) -> dict:
+                    entropy_coef: float = ENTROPY_COEF, amp: bool = True, force_collective: bool = False) -> dict:
     """_train_one_epoch (train.py:126-196) over an iterable of Batch. `model` may be
     a DistributedDataParallel wrapper: gradients are averaged over the ranks by
-    RCCL all-reduce during backward (bucketed, overlapped with the backward)."""
+    RCCL all-reduce during backward (bucketed, overlapped with the backward).
+    force_collective: the rank-agreed NaN skip all-reduces even at world size 1."""
     data = list(data)
     n = len(data)
     model.train()
@@ -155,7 +157,7 @@ def train_one_epoch(model, data, optimizer, scaler, accumulate_steps: int = ACCU
     total, skipped, correct, seen, steps = 0.0, 0, 0, 0, 0
     for i, b in enumerate(data):
         loss, lp, lv, ent, pol = batch_loss(model, b, entropy_coef, amp)
-        if not _finite_on_all_ranks(loss):
+        if not _finite_on_all_ranks(loss, force_collective):
             # the reference skips a non-finite batch (train.py:178-180); under DDP every
             # rank skips together, or the gradient all-reduces of backward would pair up
             # different batches across ranks (or hang)
@@ -194,11 +196,12 @@ def evaluate(model, data) -> float:
     return tot / cnt if cnt else math.inf
 
 
-def wrap_ddp(model, device):
+def wrap_ddp(model, device, force: bool = False):
     """DistributedDataParallel over the default process group (RCCL on GPUs, gloo on
-    CPU) when one is initialised with more than one rank; else the model itself."""
+    CPU) when one is initialised with more than one rank (or with one, when
+    `force`: the RCCL path exercised on a 1-GPU box); else the model itself."""
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or force):
         dev = torch.device(device)
         ids = [dev.index if dev.index is not None else 0] if dev.type == "cuda" else None
         return torch.nn.parallel.DistributedDataParallel(model, device_ids=ids, bucket_cap_mb=64)

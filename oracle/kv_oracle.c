@@ -857,14 +857,6 @@ static void hash_eval_board(const int8_t* b, float* logits, float* value) {
     *value = (float)((int)(h % 129u) - 64) / 64.0f;
 }
 
-static void eval_one(kvo_eval_fn cb, void* ctx, const GS* g, float* logits, float* value) {
-    if (!cb) { hash_eval_board(g->b, logits, value); return; }
-    int8_t vec[80];
-    float planes[768];
-    gs_to_vec(g, vec);
-    kvo_encode_board(vec, planes);
-    cb(ctx, planes, 1, logits, value);
-}
 
 static float puct_score(float c_puct, float P, float sq, int N, float W) {
     const float u = c_puct * P * sq / (float)(1 + N);
@@ -883,147 +875,281 @@ static int choose_weighted_c(MT* py, const double* w, int n) {
     return k;
 }
 
+/* One game's search state (the lock-step batch below plays G of them; the
+ * single game is the batch of one, so both give the same bits per game). */
+typedef struct {
+    const kvo_mcts_cfg* cfg;
+    MT *np_mt, *py_mt;
+    int S, ncap, ecap, overflow;
+    float* sqt;
+    Mv* e_mv;
+    float *e_P, *e_W;
+    int *e_N, *e_child, *n_first, *n_cnt, *n_N, *path;
+    float *logits, *probs, *lterm;
+    double *noise, *w;
+    int* lidx;
+    ML *ml, *lm;
+    GS g, b;
+    int move_count, outcome, reason, maxed, resigned, evals, done;
+    float root_value, v;
+    int root_wtm, node_count, edge_count, depth, leaf;
+    uint16_t* rec_moves;
+    int cap;
+    int32_t* visits;
+    int maxm;
+} MG;
+
+static void mg_init(MG* m, const kvo_mcts_cfg* cfg, MT* np_mt, MT* py_mt, uint16_t* rec_moves, int cap,
+                    int32_t* visits, int maxm) {
+    memset(m, 0, sizeof *m);
+    m->cfg = cfg; m->np_mt = np_mt; m->py_mt = py_mt;
+    m->S = cfg->sims; m->ncap = m->S + 2;
+    const int full = KVO_MAXM * (m->S + 1);
+    m->ecap = cfg->edge_cap > 0 && cfg->edge_cap < full ? cfg->edge_cap : full;
+    m->sqt = (float*)malloc(sizeof(float) * (size_t)(m->ncap + 2));
+    for (int k = 0; k < m->ncap + 2; ++k) m->sqt[k] = (float)sqrt((double)k);
+    m->e_mv = (Mv*)malloc(sizeof(Mv) * (size_t)m->ecap);
+    m->e_P = (float*)malloc(sizeof(float) * (size_t)m->ecap);
+    m->e_N = (int*)malloc(sizeof(int) * (size_t)m->ecap);
+    m->e_W = (float*)malloc(sizeof(float) * (size_t)m->ecap);
+    m->e_child = (int*)malloc(sizeof(int) * (size_t)m->ecap);
+    m->n_first = (int*)malloc(sizeof(int) * (size_t)m->ncap);
+    m->n_cnt = (int*)malloc(sizeof(int) * (size_t)m->ncap);
+    m->n_N = (int*)malloc(sizeof(int) * (size_t)m->ncap);
+    m->path = (int*)malloc(sizeof(int) * (size_t)m->ncap);
+    m->logits = (float*)malloc(sizeof(float) * 4096);
+    m->probs = (float*)malloc(sizeof(float) * 4096);
+    m->noise = (double*)malloc(sizeof(double) * 4096);
+    m->w = (double*)malloc(sizeof(double) * MAXMV);
+    m->lidx = (int*)malloc(sizeof(int) * MAXMV);
+    m->lterm = (float*)malloc(sizeof(float) * MAXMV);
+    m->ml = (ML*)malloc(sizeof(ML));
+    m->lm = (ML*)malloc(sizeof(ML));
+    m->reason = -1;
+    m->rec_moves = rec_moves; m->cap = cap; m->visits = visits; m->maxm = maxm;
+    gs_init(&m->g);
+}
+
+static void mg_free(MG* m) {
+    free(m->sqt); free(m->e_mv); free(m->e_P); free(m->e_N); free(m->e_W); free(m->e_child); free(m->n_first);
+    free(m->n_cnt); free(m->n_N); free(m->path); free(m->logits); free(m->probs); free(m->noise); free(m->w);
+    free(m->lidx); free(m->lterm); free(m->ml); free(m->lm);
+}
+
+/* start of a move: 1 = the root position needs a network row, 0 = the game is over (no legal move) */
+static int mg_move_start(MG* m) {
+    valid_moves(&m->g, m->ml);
+    if (m->ml->n == 0) { m->done = 1; return 0; }
+    return 1;
+}
+
+/* the root's network row (logits in m->logits, value) -> priors and a fresh tree */
+static void mg_root(MG* m, float root_value) {
+    const kvo_mcts_cfg* cfg = m->cfg;
+    const ML* ml = m->ml;
+    m->root_value = root_value;
+    m->evals++;
+    kvo_softmax_det_4096(m->logits, m->probs);
+    kvo_dirichlet(m->np_mt, cfg->alpha, 4096, m->noise);
+    const float keep = (float)(1.0 - cfg->eps);
+    double total = 0.0;
+    for (int i = 0; i < ml->n; i++) {
+        int idx = (ml->m[i].fr * 8 + ml->m[i].fc) * 64 + ml->m[i].tr * 8 + ml->m[i].tc;
+        float p32 = keep * m->probs[idx];
+        m->w[i] = (double)p32 + cfg->eps * m->noise[idx];
+        total = total + m->w[i];
+    }
+    m->root_wtm = m->g.wtm;
+    m->node_count = 1;
+    m->edge_count = ml->n;
+    m->n_first[0] = 0; m->n_cnt[0] = ml->n; m->n_N[0] = 1;
+    for (int i = 0; i < ml->n; i++) {
+        m->e_mv[i] = ml->m[i];
+        m->e_P[i] = total == 0.0 ? 1.0f / (float)ml->n : (float)(m->w[i] / total);
+        m->e_N[i] = 0; m->e_W[i] = 0.f; m->e_child[i] = -1;
+    }
+}
+
+/* one simulation's descent: 1 = the leaf position (m->b) needs a network row,
+ * 0 = its value is known (draw, mate, stalemate; m->v) */
+static int mg_descend(MG* m) {
+    m->b = m->g;
+    int node = 0;
+    m->depth = 0;
+    m->leaf = -1;
+    for (;;) {
+        const int first = m->n_first[node], cnt = m->n_cnt[node];
+        const float sq = m->sqt[m->n_N[node]];
+        float best = -INFINITY;
+        int bi = 0;
+        for (int j = 0; j < cnt; ++j) {
+            const float sc = puct_score(m->cfg->c_puct, m->e_P[first + j], sq, m->e_N[first + j], m->e_W[first + j]);
+            if (sc > best) { best = sc; bi = j; }
+        }
+        const int e = first + bi;
+        m->path[m->depth++] = e;
+        make_move(&m->b, &m->e_mv[e]);
+        const int child = m->e_child[e];
+        if (child < 0 || m->depth >= m->ncap) { m->leaf = e; break; }
+        node = child;
+    }
+    m->v = 0.f;
+    if (is_draw(&m->b)) return 0;
+    valid_moves(&m->b, m->lm);
+    if (m->lm->n == 0) {
+        m->v = in_check(&m->b) ? (m->b.wtm ? -1.f : 1.f) : 0.f;
+        return 0;
+    }
+    return 1;
+}
+
+/* the leaf's network row (m->logits, value) -> expansion */
+static void mg_expand(MG* m, float value) {
+    const ML* lm = m->lm;
+    m->v = value;
+    m->evals++;
+    for (int j = 0; j < lm->n; ++j)
+        m->lidx[j] = (lm->m[j].fr * 8 + lm->m[j].fc) * 64 + lm->m[j].tr * 8 + lm->m[j].tc;
+    const float sum = legal_softmax_terms(m->logits, m->lidx, lm->n, m->lterm);
+    if (m->edge_count + lm->n <= m->ecap && m->node_count < m->ncap) {
+        const int id = m->node_count++;
+        m->n_first[id] = m->edge_count; m->n_cnt[id] = lm->n; m->n_N[id] = 0;
+        for (int j = 0; j < lm->n; ++j) {
+            const int e = m->edge_count + j;
+            m->e_mv[e] = lm->m[j];
+            m->e_P[e] = sum > 0.f ? m->lterm[j] / sum : 1.0f / (float)lm->n;
+            m->e_N[e] = 0; m->e_W[e] = 0.f; m->e_child[e] = -1;
+        }
+        m->edge_count += lm->n;
+        m->e_child[m->leaf] = id;
+    } else {
+        m->overflow++;
+    }
+}
+
+static void mg_backup(MG* m) {
+    m->n_N[0] += 1;
+    for (int d = 0; d < m->depth; ++d) {
+        const int e = m->path[d];
+        const int white_moved = ((m->root_wtm != 0) ^ (d & 1)) != 0;
+        m->e_N[e] += 1;
+        m->e_W[e] = m->e_W[e] + (white_moved ? m->v : -m->v);
+        const int nd = m->e_child[e];
+        if (nd >= 0) m->n_N[nd] += 1;
+    }
+}
+
+/* the move: random.choices over the root visit counts, then the reference's termination checks */
+static void mg_commit(MG* m) {
+    const ML* ml = m->ml;
+    for (int i = 0; i < ml->n; ++i) m->w[i] = (double)m->e_N[i];
+    if (m->visits && m->move_count < m->cap)
+        for (int j = 0; j < m->maxm; ++j)
+            m->visits[(size_t)m->move_count * m->maxm + j] = j < ml->n ? m->e_N[j] : -1;
+    const int pick = choose_weighted_c(m->py_mt, m->w, ml->n);
+    const Mv mv = ml->m[pick];
+    if (m->move_count < m->cap) m->rec_moves[m->move_count] = (uint16_t)((mv.fr * 8 + mv.fc) * 64 + mv.tr * 8 + mv.tc);
+    make_move(&m->g, &mv);
+    m->move_count++;
+    if (is_draw(&m->g)) { m->done = 1; return; }
+    if (m->move_count > 15 && (double)m->root_value < -0.7) {
+        m->outcome = m->g.wtm ? -1 : 1; m->reason = 1; m->resigned = 1; m->done = 1; return;
+    }
+    if (m->cfg->max_moves > 0 && m->move_count >= m->cfg->max_moves) { m->maxed = 1; m->done = 1; }
+}
+
+static void mg_result(MG* m, kvo_game_result* res) {
+    GS* g = &m->g;
+    if (m->maxed) { m->outcome = 0; m->reason = 0; }
+    else if (!m->resigned) {
+        int chk = in_check(g);
+        int mate = 0;
+        if (chk) { valid_moves(g, m->ml); mate = m->ml->n == 0; }
+        if (mate) { m->outcome = g->wtm ? -1 : 1; m->reason = 2; }
+        else {
+            valid_moves(g, m->ml);
+            if (m->ml->n == 0) { m->outcome = 0; m->reason = 3; }
+            else { m->outcome = 0; m->reason = is_draw(g) ? 4 : 5; }
+        }
+    }
+    res->plies = m->move_count;
+    res->outcome = m->outcome;
+    res->reward = m->outcome == 1 ? 1.0f : (m->outcome == 0 ? 0.2f : -1.0f);
+    res->reason = m->reason;
+    res->n_evals = m->evals;
+}
+
+/* network rows of the games in want[] (positions gs[k]): one callback over all of them (the
+ * leaf batch), or the hash test evaluator per game; results into each game's m->logits, val[k] */
+static void mg_eval(MG* const* want, const GS* const* pos, int n, kvo_eval_fn cb, void* ctx, float* planes,
+                    float* lg, float* val) {
+    if (!cb) {
+        for (int k = 0; k < n; ++k) hash_eval_board(pos[k]->b, want[k]->logits, &val[k]);
+        return;
+    }
+    int8_t vec[80];
+    for (int k = 0; k < n; ++k) {
+        gs_to_vec(pos[k], vec);
+        kvo_encode_board(vec, planes + (size_t)k * 768);
+    }
+    cb(ctx, planes, n, lg, val);
+    for (int k = 0; k < n; ++k) memcpy(want[k]->logits, lg + (size_t)k * 4096, sizeof(float) * 4096);
+}
+
+/* G games in lock-step (the device's batch shape: every game runs the same
+ * simulation index, the leaves that need the network go out as one batch of
+ * up to G rows). Game k uses np_mts[k] / py_mts[k], records rec_moves + k*cap
+ * and (visits != NULL) visits + k*cap*maxm, and res[k]. Each game's search is
+ * the single-game one exactly (the batch only groups the network calls).
+ * Returns 0, or -1 when some expansion did not fit its edge pool. */
+int kvo_mcts_play_batch(const kvo_mcts_cfg* cfg, int G, MT** np_mts, MT** py_mts, kvo_eval_fn cb, void* ctx,
+                        uint16_t* rec_moves, int cap, int32_t* visits, int maxm, kvo_game_result* res) {
+    MG* gm = (MG*)malloc(sizeof(MG) * (size_t)G);
+    MG** want = (MG**)malloc(sizeof(MG*) * (size_t)G);
+    const GS** pos = (const GS**)malloc(sizeof(GS*) * (size_t)G);
+    float* planes = (float*)malloc(sizeof(float) * 768 * (size_t)G);
+    float* lg = (float*)malloc(sizeof(float) * 4096 * (size_t)G);
+    float* val = (float*)malloc(sizeof(float) * (size_t)G);
+    for (int k = 0; k < G; ++k)
+        mg_init(&gm[k], cfg, np_mts[k], py_mts[k], rec_moves + (size_t)k * cap, cap,
+                visits ? visits + (size_t)k * cap * maxm : NULL, maxm);
+    for (;;) {
+        int n = 0;
+        for (int k = 0; k < G; ++k)
+            if (!gm[k].done && mg_move_start(&gm[k])) { want[n] = &gm[k]; pos[n] = &gm[k].g; n++; }
+        if (n == 0) break;
+        mg_eval(want, pos, n, cb, ctx, planes, lg, val);
+        for (int k = 0; k < n; ++k) mg_root(want[k], val[k]);
+        MG** act = (MG**)malloc(sizeof(MG*) * (size_t)n);
+        const int na = n;
+        memcpy(act, want, sizeof(MG*) * (size_t)na);
+        for (int s = 0; s < cfg->sims; ++s) {
+            n = 0;
+            for (int k = 0; k < na; ++k)
+                if (mg_descend(act[k])) { want[n] = act[k]; pos[n] = &act[k]->b; n++; }
+            if (n) mg_eval(want, pos, n, cb, ctx, planes, lg, val);
+            for (int k = 0; k < n; ++k) mg_expand(want[k], val[k]);
+            for (int k = 0; k < na; ++k) mg_backup(act[k]);
+        }
+        for (int k = 0; k < na; ++k) mg_commit(act[k]);
+        free(act);
+    }
+    int overflow = 0;
+    for (int k = 0; k < G; ++k) {
+        mg_result(&gm[k], &res[k]);
+        overflow |= gm[k].overflow != 0;
+        mg_free(&gm[k]);
+    }
+    free(gm); free(want); free(pos); free(planes); free(lg); free(val);
+    return overflow ? -1 : 0;
+}
+
 /* plays one game; rec_moves[ply], visits[ply * maxm + j] = root visit counts
  * in root move-list order (maxm entries per ply, -1 padded). Returns the
  * number of plies, or -1 when an expansion did not fit the edge pool (the
  * device raises KV_EOVERFLOW there). */
 int kvo_mcts_play_game(const kvo_mcts_cfg* cfg, MT* np_mt, MT* py_mt, kvo_eval_fn cb, void* ctx,
                        uint16_t* rec_moves, int cap, int32_t* visits, int maxm, kvo_game_result* res) {
-    const int S = cfg->sims, ncap = S + 2;
-    const int full = KVO_MAXM * (S + 1);
-    const int ecap = cfg->edge_cap > 0 && cfg->edge_cap < full ? cfg->edge_cap : full;
-    int overflow = 0;
-    int lidx[MAXMV];
-    float lterm[MAXMV];
-    float* sqt = (float*)malloc(sizeof(float) * (size_t)(ncap + 2));
-    for (int k = 0; k < ncap + 2; ++k) sqt[k] = (float)sqrt((double)k);
-    Mv* e_mv = (Mv*)malloc(sizeof(Mv) * (size_t)ecap);
-    float* e_P = (float*)malloc(sizeof(float) * (size_t)ecap);
-    int* e_N = (int*)malloc(sizeof(int) * (size_t)ecap);
-    float* e_W = (float*)malloc(sizeof(float) * (size_t)ecap);
-    int* e_child = (int*)malloc(sizeof(int) * (size_t)ecap);
-    int* n_first = (int*)malloc(sizeof(int) * (size_t)ncap);
-    int* n_cnt = (int*)malloc(sizeof(int) * (size_t)ncap);
-    int* n_N = (int*)malloc(sizeof(int) * (size_t)ncap);
-    int* path = (int*)malloc(sizeof(int) * (size_t)ncap);
-    float* logits = (float*)malloc(sizeof(float) * 4096);
-    float* probs = (float*)malloc(sizeof(float) * 4096);
-    double* noise = (double*)malloc(sizeof(double) * 4096);
-    double* w = (double*)malloc(sizeof(double) * MAXMV);
-    static ML ml, lm;
-    GS g;
-    gs_init(&g);
-    int move_count = 0, outcome = 0, reason = -1, maxed = 0, resigned = 0, evals = 0;
-    for (;;) {
-        valid_moves(&g, &ml);
-        if (ml.n == 0) break;
-        float root_value;
-        eval_one(cb, ctx, &g, logits, &root_value);
-        evals++;
-        kvo_softmax_det_4096(logits, probs);
-        kvo_dirichlet(np_mt, cfg->alpha, 4096, noise);
-        const float keep = (float)(1.0 - cfg->eps);
-        double total = 0.0;
-        for (int i = 0; i < ml.n; i++) {
-            int idx = (ml.m[i].fr * 8 + ml.m[i].fc) * 64 + ml.m[i].tr * 8 + ml.m[i].tc;
-            float p32 = keep * probs[idx];
-            w[i] = (double)p32 + cfg->eps * noise[idx];
-            total = total + w[i];
-        }
-        const int root_wtm = g.wtm;
-        int node_count = 1, edge_count = ml.n;
-        n_first[0] = 0; n_cnt[0] = ml.n; n_N[0] = 1;
-        for (int i = 0; i < ml.n; i++) {
-            e_mv[i] = ml.m[i];
-            e_P[i] = total == 0.0 ? 1.0f / (float)ml.n : (float)(w[i] / total);
-            e_N[i] = 0; e_W[i] = 0.f; e_child[i] = -1;
-        }
-        for (int s = 0; s < S; ++s) {
-            GS b = g;
-            int node = 0, depth = 0, leaf = -1;
-            for (;;) {
-                const int first = n_first[node], cnt = n_cnt[node];
-                const float sq = sqt[n_N[node]];
-                float best = -INFINITY;
-                int bi = 0;
-                for (int j = 0; j < cnt; ++j) {
-                    const float sc = puct_score(cfg->c_puct, e_P[first + j], sq, e_N[first + j], e_W[first + j]);
-                    if (sc > best) { best = sc; bi = j; }
-                }
-                const int e = first + bi;
-                path[depth++] = e;
-                make_move(&b, &e_mv[e]);
-                const int child = e_child[e];
-                if (child < 0 || depth >= ncap) { leaf = e; break; }
-                node = child;
-            }
-            float v = 0.f;
-            if (!is_draw(&b)) {
-                valid_moves(&b, &lm);
-                if (lm.n == 0) {
-                    v = in_check(&b) ? (b.wtm ? -1.f : 1.f) : 0.f;
-                } else {
-                    eval_one(cb, ctx, &b, logits, &v);
-                    evals++;
-                    for (int j = 0; j < lm.n; ++j)
-                        lidx[j] = (lm.m[j].fr * 8 + lm.m[j].fc) * 64 + lm.m[j].tr * 8 + lm.m[j].tc;
-                    const float sum = legal_softmax_terms(logits, lidx, lm.n, lterm);
-                    if (edge_count + lm.n <= ecap && node_count < ncap) {
-                        const int id = node_count++;
-                        n_first[id] = edge_count; n_cnt[id] = lm.n; n_N[id] = 0;
-                        for (int j = 0; j < lm.n; ++j) {
-                            const int e = edge_count + j;
-                            e_mv[e] = lm.m[j];
-                            e_P[e] = sum > 0.f ? lterm[j] / sum : 1.0f / (float)lm.n;
-                            e_N[e] = 0; e_W[e] = 0.f; e_child[e] = -1;
-                        }
-                        edge_count += lm.n;
-                        e_child[leaf] = id;
-                    } else {
-                        overflow++;
-                    }
-                }
-            }
-            n_N[0] += 1;
-            for (int d = 0; d < depth; ++d) {
-                const int e = path[d];
-                const int white_moved = ((root_wtm != 0) ^ (d & 1)) != 0;
-                e_N[e] += 1;
-                e_W[e] = e_W[e] + (white_moved ? v : -v);
-                const int nd = e_child[e];
-                if (nd >= 0) n_N[nd] += 1;
-            }
-        }
-        for (int i = 0; i < ml.n; ++i) w[i] = (double)e_N[i];
-        if (visits && move_count < cap)
-            for (int j = 0; j < maxm; ++j) visits[(size_t)move_count * maxm + j] = j < ml.n ? e_N[j] : -1;
-        const int pick = choose_weighted_c(py_mt, w, ml.n);
-        const Mv m = ml.m[pick];
-        if (move_count < cap) rec_moves[move_count] = (uint16_t)((m.fr * 8 + m.fc) * 64 + m.tr * 8 + m.tc);
-        make_move(&g, &m);
-        move_count++;
-        if (is_draw(&g)) break;
-        if (move_count > 15 && (double)root_value < -0.7) { outcome = g.wtm ? -1 : 1; reason = 1; resigned = 1; break; }
-        if (cfg->max_moves > 0 && move_count >= cfg->max_moves) { maxed = 1; break; }
-    }
-    if (maxed) { outcome = 0; reason = 0; }
-    else if (!resigned) {
-        int chk = in_check(&g);
-        int mate = 0;
-        if (chk) { valid_moves(&g, &ml); mate = ml.n == 0; }
-        if (mate) { outcome = g.wtm ? -1 : 1; reason = 2; }
-        else {
-            valid_moves(&g, &ml);
-            if (ml.n == 0) { outcome = 0; reason = 3; }
-            else { outcome = 0; reason = is_draw(&g) ? 4 : 5; }
-        }
-    }
-    res->plies = move_count;
-    res->outcome = outcome;
-    res->reward = outcome == 1 ? 1.0f : (outcome == 0 ? 0.2f : -1.0f);
-    res->reason = reason;
-    res->n_evals = evals;
-    free(sqt); free(e_mv); free(e_P); free(e_N); free(e_W); free(e_child); free(n_first); free(n_cnt); free(n_N);
-    free(path); free(logits); free(probs); free(noise); free(w);
-    return overflow ? -1 : move_count;
+    const int rc = kvo_mcts_play_batch(cfg, 1, &np_mt, &py_mt, cb, ctx, rec_moves, cap, visits, maxm, res);
+    return rc < 0 ? -1 : res->plies;
 }

@@ -228,3 +228,45 @@ def mcts_play_game(sims, np_mt: MT, py_mt: MT, eval_fn=None, max_moves=None, c_p
         raise TreeOverflow(f"edge pool of {edge_cap} edges overflowed")
     return dict(moves=moves[:n].copy(), visits=visits[:n].copy(), plies=res.plies, outcome=res.outcome,
                 reward=float(res.reward), reason=res.reason, n_evals=res.n_evals)
+
+
+def mcts_play_batch(sims, seeds, eval_fn=None, max_moves=None, c_puct=1.5, eps=0.25, alpha=0.3, edge_cap=0,
+                    cap=2048, maxm=320, keep_visits=False):
+    """G restated PUCT games in lock-step (kvo_mcts_play_batch): game k seeded seeds[k] (both streams),
+    every simulation's leaves that need the network evaluated as ONE eval_fn batch -- the device's batch
+    shape. Each game equals mcts_play_game on its own seed. Returns a list of per-game dicts."""
+    L = lib()
+    if not hasattr(L.kvo_mcts_play_batch, "_sig"):
+        L.kvo_mcts_play_batch.argtypes = [C.POINTER(MctsCfg), C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                          C.c_void_p, C.c_void_p, C.POINTER(C.c_uint16), C.c_int,
+                                          C.POINTER(C.c_int32), C.c_int, C.POINTER(GameResult)]
+        L.kvo_mcts_play_batch._sig = True
+    G = len(seeds)
+    nps = [MT(int(s), "numpy") for s in seeds]
+    pys = [MT(int(s), "python") for s in seeds]
+    np_arr = (C.c_void_p * G)(*[C.cast(m.buf, C.c_void_p) for m in nps])
+    py_arr = (C.c_void_p * G)(*[C.cast(m.buf, C.c_void_p) for m in pys])
+    cb = None
+    if eval_fn is not None:
+        def _cb(ctx, planes, n, logits, values):
+            x = np.ctypeslib.as_array(planes, shape=(n, 12, 8, 8)).copy()
+            lg, vl = eval_fn(x)
+            np.ctypeslib.as_array(logits, shape=(n, 4096))[:] = lg
+            np.ctypeslib.as_array(values, shape=(n,))[:] = np.asarray(vl).reshape(n)
+        cb = EVAL_FN(_cb)
+    cfg = MctsCfg(sims, c_puct, max_moves if max_moves else 0, eps, alpha, int(edge_cap))
+    moves = np.zeros((G, cap), dtype=np.uint16)
+    visits = np.full((G, cap, maxm), -1, dtype=np.int32) if keep_visits else None
+    res = (GameResult * G)()
+    rc = L.kvo_mcts_play_batch(C.byref(cfg), G, np_arr, py_arr, C.cast(cb, C.c_void_p) if cb else None, None,
+                               _p(moves, C.c_uint16), cap, _p(visits, C.c_int32) if keep_visits else None, maxm,
+                               res)
+    if rc < 0:
+        raise TreeOverflow(f"edge pool of {edge_cap} edges overflowed")
+    out = []
+    for k in range(G):
+        n = res[k].plies
+        out.append(dict(moves=moves[k, :n].copy(), visits=visits[k, :n].copy() if keep_visits else None,
+                        plies=n, outcome=res[k].outcome, reward=float(res[k].reward), reason=res[k].reason,
+                        n_evals=res[k].n_evals))
+    return out

@@ -51,11 +51,12 @@ def test_gemm_label(path, rows, split, name):
     assert (f"points 0-{split - 1}" in desc) == (path == 2 and split < 100)
 
 
-@pytest.mark.parametrize("sims", [0, 8])
-def test_cpu_baseline_pool(monkeypatch, sims):
+@pytest.mark.parametrize("sims,batch", [(0, 1), (8, 1), (8, 4)])
+def test_cpu_baseline_pool(monkeypatch, sims, batch):
     monkeypatch.setenv("KV_CPU_WORKERS", "2")
-    r = bench.cpu_baseline(2.0, sims)
+    r = bench.cpu_baseline(2.0, sims, batch=batch)
     assert r["kind"] == "port" and r["workers"] == 2 and r["cores"] == 2 and r["threads_per_worker"] == 1
+    assert r["leaf_batch"] == batch
     assert r["value"] > 0 and r["unit"] == ("sims/s" if sims else "plies/s")
     assert r["whole_host_extrapolated"] >= r["value"]
     json.dumps(r)
