@@ -924,6 +924,12 @@ static int wino48_blocks(kv_net* net, int nb, int path, bool mark, hipStream_t s
 // 4 points (10.42-10.49 vs 10.39-10.42 ms, profiles/r03_w88_tail_ab.log). Same k order, same bits
 // (profiles/r03_w88split_ab.log). KV_W88_SPLIT=0 turns it off. The split launch deals its grid in
 // XCD groups of 8, so both parts must be multiples of 8 workgroups; otherwise one launch.
+// (Measured and dropped, round 4: the 256-board layer as 96 points of 128x128 tiles with k-tiles of 16 at
+// 3 workgroups per CU -- exactly one round -- plus the last 4 points as 32x128 or 32x64 tiles: 112.7 +
+// 19.8 us against 76.0 + 55.5 us for the split below, forward 1.568 vs 1.562 ms, bit-identical;
+// profiles/r04_w88c2_ab.log. A single round of 128x128 tiles runs at ~113 TFLOP/s whatever the count per
+// CU -- every workgroup's first k-tile load and its M epilogue are exposed -- against ~134 in the 12.5
+// rounds of C3.)
 static int wino88_split_points(int rows) {
     static const int mode = [] {  // thread-safe one-time initialisation
         const char* e = getenv("KV_W88_SPLIT");
@@ -937,7 +943,7 @@ static int wino88_split_points(int rows) {
     const int full = (kv::W88_XI * per_xi) / slots * slots;  // tiles in whole rounds
     int xa = full / per_xi;
     while (xa > 0 && (xa * per_xi) % slots) --xa;
-    // the second launch runs (100 - xa) points as 64x128 tiles: (rows / 64) * 4 per point
+    // the second launch runs (100 - xa) points as 64x128 tiles: both grids are dealt in XCD groups of 8
     if (xa <= 0 || (xa * per_xi) % 8 || ((kv::W88_XI - xa) * (rows / 64) * 4) % 8) return kv::W88_XI;
     return xa;
 }

@@ -21,12 +21,13 @@ def test_game_length_summary_is_complete_and_tight():
 
 
 def test_tree_summary_is_at_c3_sims():
+    """The tree-kernel HBM figure the bench line carries is measured at C3 itself (800 sims, round 4); it
+    agrees with round 3's derived estimate (300-sim network run x the hash evaluator's growth)."""
     tj, f = bench._tree_pmc(2048)
+    assert f.startswith("r04_") and tj["measured_directly"]
     assert tj["sims_per_move"] == 800 and tj["per_sim"]["bytes_per_sim"] > 0
-    m = tj["measured"]
-    assert m["hash_evaluator_800_sims"]["launches"] == 799
-    est = m["network_300_sims"]["bytes_per_sim"] * m["growth_300_to_800"]
-    assert abs(est - tj["per_sim"]["bytes_per_sim"]) < 1e-6 * est
+    old = json.load(open(os.path.join(os.path.dirname(bench.__file__), "profiles", "r03_pmc_tree_c3_2048.json")))
+    assert abs(old["per_sim"]["bytes_per_sim"] / tj["per_sim"]["bytes_per_sim"] - 1) < 0.02
 
 
 def test_gemm_traffic_summary_present():

@@ -138,7 +138,7 @@ def test_calibration_choice_is_consistent(variant):
     ok = {k: c["err_logit"][k] <= c["tol_logit"] and c["err_value"][k] <= c["tol_value"] for k in c["err_logit"]}
     first = next(k for k in order if k == "winograd88_f64" or ok.get(k))
     assert c["path_large"] == first, c
-    assert list(c["err_logit"]) == order[:order.index(first) + 1]
+    assert sorted(c["err_logit"]) == sorted(order[:order.index(first) + 1])  # each candidate up to the choice
     assert c["err_logit"].get("winograd88_f64", 0.0) < 1e-5
     small_ok = c["err_small_logit"] <= c["tol_logit"] and c["err_small_value"] <= c["tol_value"]
     assert c["path_small"] == ("direct" if small_ok else "winograd88_f64")
