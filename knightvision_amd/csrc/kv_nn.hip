@@ -452,8 +452,9 @@ __global__ void encode_boards_kernel(const int8_t* __restrict__ boards, int nb, 
 // 0..31 / 32..63 (WINO 0: NHWC T [board][64][256]). WINO 2: each wave
 // computes its own F(4x8) tile's 6x10 patch and writes that tile of conv2's
 // V [points][rows][256]. WINO 4: F(8x8) by lane swaps (below), the same bits
-// as wino88_in_kernel over T.
-template <int WINO>  // 0: NHWC out, 2: F(4x8) V of conv2, 4: F(8x8) V of conv2
+// as wino88_in_kernel over T; WINO 5 the same into the fp64 V64
+// (wino88d_in_kernel's bits).
+template <int WINO>  // 0: NHWC out, 2: F(4x8) V of conv2, 4: F(8x8) V of conv2, 5: its fp64 V64
 __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ boards, int nb,
                                                    const float* __restrict__ wT, const float* __restrict__ scale,
                                                    const float* __restrict__ shift, float* __restrict__ out,
@@ -479,7 +480,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ bo
     for (int it = 0; it < 30; ++it)
         if (w + 4 * it < 9 * 13) wl[w + 4 * it][cl] = wv[it];
     __syncthreads();
-    if constexpr (WINO == 4) {
+    if constexpr (WINO == 4 || WINO == 5) {
         // F(8x8) without the plane exchange: a wave holds 32 channels of one board, lane half h the
         // plane rows 4h .. 4h+3 of its channel (the same sums as below), and the two halves finish the
         // transform by lane swaps (wino88_input_half): no 32 KB plane in LDS, so more workgroups per CU
@@ -498,7 +499,10 @@ __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ bo
                 const float v = acc * sc4 + sh4;
                 x2[ii][px] = v > 0.f ? v : 0.f;
             }
-        wino88_input_half(x2, h, out, (size_t)b4 * 256 + c4, (size_t)rows * 256);
+        if constexpr (WINO == 4)
+            wino88_input_half(x2, h, out, (size_t)b4 * 256 + c4, (size_t)rows * 256);
+        else  // the fp64 Winograd domain: V64 (out is double storage)
+            wino88d_input_half(x2, h, reinterpret_cast<double*>(out), (size_t)b4 * 256 + c4, (size_t)rows * 256);
     } else {
     const float sc = scale[c], sh = shift[c];
     const int bb = w >> 1, b = b0 + bb;
@@ -1034,8 +1038,16 @@ template <bool RESID, bool WRITE_Y, bool NEXT_V>
 static int launch_wino88d_out(kv_net* net, int l, const double* M, int nb, int stride, const float* resid, float* Y,
                               double* Vn, hipStream_t st) {
     const float* W = net->w;
-    hipLaunchKernelGGL((kv::wino88d_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 256, nb), dim3(256), 0, st, M,
-                       stride, W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn);
+    static const bool half = [] {  // KV_W88D_OUT=1: the one-lane-per-plane form (A/B only)
+        const char* e = getenv("KV_W88D_OUT");
+        return !(e && e[0] == '1');
+    }();
+    if (half)
+        hipLaunchKernelGGL((kv::wino88d_out_half_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 128, nb), dim3(256), 0,
+                           st, M, stride, W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn);
+    else
+        hipLaunchKernelGGL((kv::wino88d_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 256, nb), dim3(256), 0, st,
+                           M, stride, W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -1116,11 +1128,14 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
     if (path == KV_PATH_WINO48_F16X3)
         KV_HIP(hipMemsetAsync(net->vmax, 0, (size_t)12 * net->cap * sizeof(unsigned), st));
-    // fp32 F(8x8) and F(4x8): the stem builds conv2's V itself
+    // Winograd paths: the stem builds conv2's V itself
     bool v256_ready = false;
     if (boards) {
         if (path == KV_PATH_WINO88)
             hipLaunchKernelGGL(kv::stem_kernel<4>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
+                               W + o.scale[0], W + o.shift[0], (float*)net->V256, nb_pad, nullptr);
+        else if (path == KV_PATH_WINO88_F64)
+            hipLaunchKernelGGL(kv::stem_kernel<5>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], (float*)net->V256, nb_pad, nullptr);
         else if (path == KV_PATH_WINO48 || path == KV_PATH_WINO48_F16X3)
             hipLaunchKernelGGL(kv::stem_kernel<2>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
@@ -1130,7 +1145,7 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
             hipLaunchKernelGGL(kv::stem_kernel<0>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], net->T, nb_pad * 4, nullptr);
         KV_HIP(hipGetLastError());
-        v256_ready = path != KV_PATH_DIRECT && path != KV_PATH_WINO88_F64;
+        v256_ready = path != KV_PATH_DIRECT;
     } else if ((rc = launch_conv<16, 16, false>(net->x16, W + o.w[0], W + o.scale[0], W + o.shift[0], nullptr,
                                                 net->T, 256, nb_pad, nullptr, st))) {
         return rc;

@@ -2,6 +2,7 @@
 seeded boards, and the outputs saved for a bit-for-bit comparison of builds.
 
     KV_LIB_PATH=knightvision_amd/libkv_b.so python tools/ab_forward.py TAG 2048 256
+    (KV_PREC=f64w: the fp64 Winograd domain)
 """
 import os
 import sys
@@ -14,7 +15,7 @@ from knightvision_amd.model import ChessNet  # noqa: E402
 from knightvision_amd.weights import synthetic_state_dict  # noqa: E402
 
 tag = sys.argv[1]
-m = ChessNet()
+m = ChessNet(precision=os.environ.get("KV_PREC", "fp32"))
 m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(42, "bn").items()})
 m.eval()
 net = m.kv_net(0)
