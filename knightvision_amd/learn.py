@@ -73,6 +73,7 @@ def selfplay_shard(model, n_games: int, iteration: int, device, *, sims=0, max_m
                         game_id_base=base, game_id_stride=world, device=dev.index or 0,
                         precision=precision, eval_mode=batched_eval_mode() if sims == 0 else 0) as eng:
         eng.run()
+        selfplay_shard.last_calibration = eng.calibration()  # the conv paths these weights ran on
         return eng.records(), eng.games()
 
 
@@ -230,6 +231,9 @@ def reinforcement_loop(model, iterations: int, games_per_iter: int, device, *, e
         t0 = time.perf_counter()
         recs, games = selfplay_shard(model, games_per_iter, it, dev, sims=sims, max_moves=max_moves, slots=slots)
         st["selfplay_s"] = time.perf_counter() - t0
+        cal = getattr(selfplay_shard, "last_calibration", None)
+        if cal is not None:  # fp32 AUTO: the self-play network's conv path for this iteration's weights
+            st["nn_path"] = cal["path_large"]
         model.train()
         data = extend_dataset(data, recs, games, dev)
         st.update(records=int(data[0].shape[0]) if data is not None else 0,

@@ -63,6 +63,7 @@ def main():
                           "sims": a.sims, "selfplay_s": sp_s, "train_s": tr_s,
                           "train_samples_per_s": cnt.item() / tr_s if tr_s else None,
                           "val_loss": last.get("val_loss"), "records": last["records"], "wall_s": wall,
+                          "nn_path_per_iteration": [st.get("nn_path") for st in stats],
                           "data": "synthetic"}), flush=True)
     if world > 1:
         dist.barrier()
