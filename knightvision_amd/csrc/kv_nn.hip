@@ -1026,7 +1026,8 @@ static int launch_wino88d_gemm_t(const double* V, const double* U, double* M, in
 }
 
 // 128x128 tiles (8 waves of 64x32) when the rows allow, else 64x128 / 32x128 (4 waves); every
-// shape runs the same k-steps, so the same bits
+// shape runs the same k-steps, so the same bits. (128x128 as 4 waves of 64x64: forward 27.8 vs 20.3 ms at
+// 2,048 boards, bit-identical; profiles/r04_w88d_out_ab.log)
 template <int K>
 static int launch_wino88d_gemm(const double* V, const double* U, double* M, int rows, int stride, hipStream_t st) {
     if (rows % 128 == 0) return launch_wino88d_gemm_t<K, 2, 4, 4, 2>(V, U, M, rows, stride, st);
@@ -1038,16 +1039,8 @@ template <bool RESID, bool WRITE_Y, bool NEXT_V>
 static int launch_wino88d_out(kv_net* net, int l, const double* M, int nb, int stride, const float* resid, float* Y,
                               double* Vn, hipStream_t st) {
     const float* W = net->w;
-    static const bool half = [] {  // KV_W88D_OUT=1: the one-lane-per-plane form (A/B only)
-        const char* e = getenv("KV_W88D_OUT");
-        return !(e && e[0] == '1');
-    }();
-    if (half)
-        hipLaunchKernelGGL((kv::wino88d_out_half_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 128, nb), dim3(256), 0,
-                           st, M, stride, W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn);
-    else
-        hipLaunchKernelGGL((kv::wino88d_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 256, nb), dim3(256), 0, st,
-                           M, stride, W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn);
+    hipLaunchKernelGGL((kv::wino88d_out_half_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 128, nb), dim3(256), 0, st,
+                       M, stride, W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
