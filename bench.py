@@ -48,8 +48,11 @@ FLOP_WINO88_GEMM_PER_BOARD = 52428800  # the fp32 default, F(8x8,3x3) GEMMs: 2 *
 FP32_MFMA_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md, f32-input MFMA (dense)
 FP64_MFMA_PEAK_TFLOPS = 78.6          # AMD's MI355X FP64 matrix figure (the guides give no f64 row; measured in
                                       # profiles/r04_f64_mfma_peak.log)
-PATH_NAMES = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3"}  # KV_PATH_*
+PATH_NAMES = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3",
+              5: "winograd88_i8"}  # KV_PATH_*
 BF16_MFMA_PEAK_TFLOPS = 2500.0        # dense bf16 MFMA
+I8_MFMA_PEAK_TOPS = 5000.0            # dense int8 MFMA: 2x the bf16 rate (cdna_hip_programming.md, MFMA rate per dtype)
+I8_DIGIT_PRODUCTS = 15                # KV_PREC_I8X5: int8 GEMMs per Winograd GEMM (digit pairs i + j < 5)
 
 
 def parse():
@@ -60,15 +63,19 @@ def parse():
     ap.add_argument("--mode", choices=["mcts", "ref"], default=os.environ.get("KV_BENCH_MODE", "mcts"))
     ap.add_argument("--slots", type=int, default=2048)
     ap.add_argument("--sims", type=int, default=800)
-    ap.add_argument("--precision", choices=["fp32", "f16x3", "f64w"], default="fp32")
+    ap.add_argument("--precision", choices=["fp32", "f16x3", "f64w", "i8x5"], default="fp32")
     ap.add_argument("--algo", choices=["auto", "direct", "winograd48", "winograd88"], default="auto",
                     help="conv algorithm of the fp32 tower (auto: the library's calibrated choice per weight load -- "
                          "Winograd F(8x8,3x3) fp32 for the random-init weights)")
     ap.add_argument("--compare-direct", type=int, default=0,
                     help="also measure the fp32 direct implicit-GEMM tower ('fp32_direct'; ~40 s per step at C3)")
-    ap.add_argument("--f64w-steps", type=int, default=2,
-                    help="fp32 headline: also time this many moves with the fp64 Winograd domain (KV_PREC_F64W, the "
-                         "AUTO path for trained-magnitude weights), reported under 'trained_weights_path'; 0 to skip")
+    ap.add_argument("--trained-steps", type=int, default=2,
+                    help="fp32 headline: also time this many moves with the fp64 Winograd domain on int8 digits "
+                         "(KV_PREC_I8X5, the AUTO path for trained-magnitude weights), reported under "
+                         "'trained_weights_path'; 0 to skip")
+    ap.add_argument("--f64w-steps", type=int, default=0,
+                    help="also time this many moves with the fp64 Winograd domain on fp64 MFMA (KV_PREC_F64W), "
+                         "reported under 'f64w_path'")
     ap.add_argument("--alt-precision", default="f16x3",
                     help="also measure this network precision (reported under 'alt_precision'; '' to skip)")
     ap.add_argument("--alt-algo", default="winograd48",
@@ -300,6 +307,10 @@ def gemm_label(path: int, rows: int, split: int):
             desc = (f" points 0-{split - 1} + wino_gemm_kernel<512,2,2,1,2,16,100> points {split}-99 (residual-tower "
                     "Winograd F(8x8,3x3) GEMM layer: two launches, both inside the timed events)")
         return name, desc
+    if path == 5:
+        name = "wino88i_gemm_kernel<512,5,2,4,1,1>" if rows % 64 == 0 else "wino88i_gemm_kernel<512,5,1,4,1,1>"
+        return name, (" (residual-tower Winograd F(8x8,3x3) GEMMs in the fp64 domain from 5 int8 digits per value: "
+                      "15 v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation)")
     if path == 3:
         name = ("wino88d_gemm_kernel<512,2,4,4,2>" if rows % 128 == 0 else
                 "wino88d_gemm_kernel<512,1,4,4,2>" if rows % 64 == 0 else "wino88d_gemm_kernel<512,1,4,2,2>")
@@ -473,6 +484,9 @@ def main():
     direct = None
     if args.compare_direct and args.precision == "fp32" and m["dom_path"] != 0:
         direct = measure("fp32", "direct", steps=1, warmup=1, tag="direct")
+    trained = None
+    if args.trained_steps > 0 and args.precision == "fp32" and m["dom_path"] != 5:
+        trained = measure("i8x5", steps=args.trained_steps, warmup=args.alt_warmup, tag="i8x5")
     f64w = None
     if args.f64w_steps > 0 and args.precision == "fp32" and m["dom_path"] != 3:
         f64w = measure("f64w", steps=args.f64w_steps, warmup=args.alt_warmup, tag="f64w")
@@ -482,13 +496,17 @@ def main():
     # the direct algorithm, the residual convs
     path = m["dom_path"]  # KV_PATH_*: 0 direct, 1 F(4x8), 2 F(8x8) fp32 (the fp32 default), 3 F(8x8) fp64, 4 f16x3
     per_board = {1: FLOP_WINO48_GEMM_PER_BOARD, 2: FLOP_WINO88_GEMM_PER_BOARD, 3: FLOP_WINO88_GEMM_PER_BOARD,
-                 4: FLOP_WINO48_GEMM_PER_BOARD}.get(path, FLOP_RES_CONV_PER_BOARD)
+                 4: FLOP_WINO48_GEMM_PER_BOARD, 5: FLOP_WINO88_GEMM_PER_BOARD}.get(path, FLOP_RES_CONV_PER_BOARD)
     bpl = min(G, int(round(m["dom_flop"] / per_board))) if m["dom_flop"] else G
     flop_alg = per_board * bpl
     achieved = flop_alg / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
-    rows = int(round(m["dom_flop"] / (2 * 512 * 512 * (100 if path in (2, 3) else 60)))) if path else bpl
+    rows = int(round(m["dom_flop"] / (2 * 512 * 512 * (100 if path in (2, 3, 5) else 60)))) if path else bpl
     kname, kdesc = gemm_label(path, rows, m["dom_split"])
     peak = FP64_MFMA_PEAK_TFLOPS if path == 3 else FP32_MFMA_PEAK_TFLOPS
+    if path == 5:  # int8 operations of the digit products against the int8 peak
+        achieved = achieved * I8_DIGIT_PRODUCTS if achieved else None
+        flop_alg *= I8_DIGIT_PRODUCTS
+        peak = I8_MFMA_PEAK_TOPS
     traffic, traffic_src = _pmc_traffic(kname, bpl)
 
     # HBM side of the search (north_star: tree kernels as a fraction of the HBM roofline), from the
@@ -584,17 +602,31 @@ def main():
         out["calibration"] = dict(m["calibration"], note=(
             "the network's conv paths for these weights: fp32 + AUTO measures its candidates at load time against an "
             "fp64 forward on 64 seeded boards and keeps the fastest within max |dlogit| 4e-5 / |dvalue| 4e-6 "
-            "(F(8x8) fp32, then F(4x8) fp32, else F(8x8) with the fp64 Winograd domain); errors are max |x - fp64|"))
+            "(F(8x8) fp32, then F(4x8) fp32, then F(8x8) with the fp64 Winograd domain on int8 digits, else on fp64 "
+            "MFMA); errors are max |x - fp64|"))
         if pg_info is not None:
             out["process_group"] = pg_info
+        if trained is not None:
+            t_ach = (FLOP_WINO88_GEMM_PER_BOARD * bpl / (trained["conv_ms"] * 1e-3) / 1e12) \
+                if trained["conv_ms"] > 0 else None
+            out["trained_weights_path"] = {
+                "note": "the same workload on the fp64 Winograd domain with the GEMMs on int8 digits (KV_PREC_I8X5): "
+                        "the path AUTO runs for weights at trained magnitudes, where no fp32 Winograd tower holds the "
+                        "1e-4 logit tolerance (learn-loop weights after 20 iterations: F(8x8) fp32 1.0e-4 / value "
+                        "3.4e-5; the stress set 3.8e-3; tests/test_nn_accuracy_gpu.py, profiles/r04_*accuracy*)",
+                "value": (trained["sims"] if mcts else trained["plies"]) / trained["dt"], "unit": unit,
+                "steps": trained["steps"], "warmup": trained["warmup"],
+                "ms_per_step": trained["dt"] * 1e3 / trained["steps"],
+                "dominant_kernel": gemm_label(5, G, 0)[0], "res_gemm_avg_launch_ms": trained["conv_ms"],
+                "res_gemm_fp64_equiv_tflops": t_ach,
+                "res_gemm_i8_tops": (t_ach * I8_DIGIT_PRODUCTS) if t_ach else None, "peak_i8_tops": I8_MFMA_PEAK_TOPS,
+                "res_gemm_frac_i8": (t_ach * I8_DIGIT_PRODUCTS / I8_MFMA_PEAK_TOPS) if t_ach else None,
+                "res_gemm_over_fp64_mfma_peak": (t_ach / FP64_MFMA_PEAK_TFLOPS) if t_ach else None}
         if f64w is not None:
             f_ach = (FLOP_WINO88_GEMM_PER_BOARD * bpl / (f64w["conv_ms"] * 1e-3) / 1e12) if f64w["conv_ms"] > 0 \
                 else None
-            out["trained_weights_path"] = {
-                "note": "the same workload on the fp64 Winograd domain (KV_PREC_F64W): the path AUTO runs for weights "
-                        "at trained magnitudes, where no fp32 Winograd tower holds the 1e-4 logit tolerance (learn-"
-                        "loop weights after 20 iterations: F(8x8) fp32 1.0e-4 / value 3.4e-5; the stress set 3.8e-3; "
-                        "tests/test_nn_accuracy_gpu.py, profiles/r04_*accuracy*)",
+            out["f64w_path"] = {
+                "note": "the fp64 Winograd domain on v_mfma_f64 (KV_PREC_F64W)",
                 "value": (f64w["sims"] if mcts else f64w["plies"]) / f64w["dt"], "unit": unit,
                 "steps": f64w["steps"], "warmup": f64w["warmup"], "ms_per_step": f64w["dt"] * 1e3 / f64w["steps"],
                 "dominant_kernel": gemm_label(3, G, 0)[0], "res_gemm_avg_launch_ms": f64w["conv_ms"],

@@ -79,18 +79,27 @@ int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv);
  * KV_PREC_F64W   Winograd F(8x8) with every Winograd-domain quantity (U, V, M,
  *                transforms) in fp64, on v_mfma_f64_16x16x4_f64, at every batch
  *                size: logits within ~3e-6 of an fp64 forward on every weight set
- *                measured (the fp32 AUTO fallback for trained weights).
+ *                measured.
+ * KV_PREC_I8X5   the same fp64 Winograd domain with the GEMMs on the int8
+ *                matrix cores: every V / U row scaled by a power of two and
+ *                split into 5 int8 digits, the 15 digit products of weight
+ *                >= 2^-28 accumulated exactly in int32 and combined in fp64
+ *                (the exact dot product of the 35-bit truncated rows); logits
+ *                as close to fp64 as KV_PREC_F64W's, at every batch size (the
+ *                fp32 AUTO fallback for trained weights before F64W).
  * Values 1 and 2 (bf16x3 / bf16x6) were retired in round 4: KV_EINVAL. */
 #define KV_PREC_FP32 0
 #define KV_PREC_F16X3 3
 #define KV_PREC_F64W 4
+#define KV_PREC_I8X5 5
 int kv_net_set_precision(kv_net* net, int precision);
 /* Algorithm of the fp32 3x3 convs with Cin 256/512:
  * KV_ALGO_AUTO      per weight load, the fastest path whose logits / values are
  *                   within 4e-5 / 4e-6 of an fp64 forward on 64 calibration
  *                   boards: > 16 boards F(8x8) fp32, else F(4x8) fp32, else
- *                   F(8x8) with the fp64 Winograd domain; <= 16 boards direct
- *                   (split-K), else F(8x8) fp64 (kv_net_calibration reports it)
+ *                   F(8x8) on int8 digits (KV_PREC_I8X5), else F(8x8) with the
+ *                   fp64 Winograd domain; <= 16 boards direct (split-K), else
+ *                   F(8x8) fp64 (kv_net_calibration reports it)
  * KV_ALGO_DIRECT    implicit GEMM over the 9 taps (exact fp32 products)
  * KV_ALGO_WINOGRAD48 F(4x8,3x3): 60 GEMMs of 2 tiles x Cin x Cout per board,
  *                   4.8x fewer FLOPs than direct (fp32 and f16x3)
@@ -110,7 +119,8 @@ int kv_net_set_algo(kv_net* net, int algo);
 #define KV_PATH_WINO88 2
 #define KV_PATH_WINO88_F64 3
 #define KV_PATH_WINO48_F16X3 4
-#define KV_NPATH 5
+#define KV_PATH_WINO88_I8 5
+#define KV_NPATH 6
 typedef struct {
     int calibrated;      /* 1: the last load / setting ran the fp32 AUTO calibration */
     int path_large;      /* KV_PATH_* of batches > 16 boards (also without calibration) */
@@ -279,6 +289,13 @@ int kv_dev_dirichlet(int device, const uint64_t* seeds, int n, double alpha, int
 int kv_host_libm(int op, const double* x, const double* y, int n, double* out);
 /* CPython random.Random(seed[i]): count random() values -> out [n][count]. */
 int kv_dev_py_random(int device, const uint64_t* seeds, int n, int count, double* out);
+/* KV_PREC_I8X5's Winograd GEMM of one conv layer (csrc/kv_wino88i.h): V [100][rows][K]
+ * and U [100][512][K] fp64 (K 256 or 512, rows a multiple of 32) are split into
+ * int8 digits by the product's slice kernel and multiplied by its GEMM kernel:
+ * M [100][rows][512] fp64; v_digits [100][rows][K/32][5][32] and v_exp
+ * [100][rows] (either may be NULL) return V's digits and row exponents. */
+int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, double* M, int8_t* v_digits,
+                   int* v_exp);
 
 /* ------------------------------------------------------- data pipeline ---
  * Full-rules chess (python-chess 1.999 semantics, csrc/kv_chess.cpp) for the

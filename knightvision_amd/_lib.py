@@ -42,8 +42,9 @@ class Stats(C.Structure):
                 ("dom_path", C.c_int64), ("dom_split", C.c_int64)]
 
 
-NPATH = 5  # KV_NPATH
-PATHS = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3"}  # KV_PATH_*
+NPATH = 6  # KV_NPATH
+PATHS = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3",
+         5: "winograd88_i8"}  # KV_PATH_*
 
 
 class Calib(C.Structure):
@@ -110,6 +111,7 @@ def _declare(L):
         "kv_dev_dirichlet": ([i, P(C.c_uint64), i, C.c_double, i, i, P(C.c_double), P(i64), P(C.c_double)], i),
         "kv_dev_py_random": ([i, P(C.c_uint64), i, i, P(C.c_double)], i),
         "kv_host_libm": ([i, P(C.c_double), P(C.c_double), i, P(C.c_double)], i),
+        "kv_dev_wino88i": ([i, P(C.c_double), i, P(C.c_double), i, P(C.c_double), P(C.c_int8), P(i)], i),
         "kv_pgn_extract": ([C.c_char_p, sz, P(PgnRecord), sz, P(sz), P(sz), P(i64)], i),
         "kv_fen_codes": ([C.c_char_p, sz, i, P(C.c_int8)], i),
         "kv_san_move_index": ([C.c_char_p, sz, C.c_char_p, sz, i, P(C.c_int32)], i),
@@ -146,6 +148,7 @@ EXPORTED = ["kv_last_error", "kv_version", "kv_net_packed_size", "kv_net_create"
             "kv_create",
             "kv_load_weights", "kv_run", "kv_set_max_moves", "kv_records", "kv_games", "kv_stats_get", "kv_root_visits", "kv_root_visits_device", "kv_records_device", "kv_sync", "kv_reset_records", "kv_destroy",
             "kv_dev_valid_moves", "kv_dev_make_move", "kv_dev_attacks", "kv_dev_dirichlet", "kv_dev_py_random", "kv_host_libm",
+            "kv_dev_wino88i",
             "kv_pgn_extract", "kv_fen_codes", "kv_san_move_index", "kv_chess_perft", "kv_chess_san", "kv_chess_fen",
             "kv_tr_conv3x3_f16", "kv_tr_conv3x3_add_f16", "kv_tr_conv_weights_f16", "kv_tr_wgrad_workspace", "kv_tr_conv3x3_wgrad_f16",
             "kv_tr_bn_workspace", "kv_tr_bn_stats_f16", "kv_tr_bn_apply_f16", "kv_tr_bn_backward_f16",

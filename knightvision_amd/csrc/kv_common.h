@@ -10,6 +10,16 @@ namespace kv {
 
 void set_error(const char* fmt, ...);
 
+// a device buffer freed with its scope (the device-test entry points)
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t alloc(size_t n) { return hipMalloc(&p, n * sizeof(T) + 16); }
+};
+
 }  // namespace kv
 
 #define KV_HIP(call)                                                                                  \

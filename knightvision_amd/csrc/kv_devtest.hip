@@ -119,15 +119,6 @@ __global__ void k_dev_py_random(const unsigned long long* seeds, int n, int coun
     for (int j = 0; j < count; ++j) out[(size_t)i * count + j] = mt_random_serial(g);
 }
 
-template <class T>
-struct DevBuf {
-    T* p = nullptr;
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
-    }
-    hipError_t alloc(size_t n) { return hipMalloc(&p, n * sizeof(T) + 16); }
-};
-
 }  // namespace kv
 
 extern "C" {

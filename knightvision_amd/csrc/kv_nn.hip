@@ -28,6 +28,7 @@
 #include "kv_wino48.h"
 #include "kv_wino88.h"
 #include "kv_wino88d.h"
+#include "kv_wino88i.h"
 #include "kv_ref64.h"
 
 namespace kv {
@@ -606,8 +607,9 @@ __global__ void planes_to_nhwc16_kernel(const float* __restrict__ planes, int nb
 //   KV_PATH_WINO88     fp32 Winograd F(8x8)
 //   KV_PATH_WINO88_F64 Winograd F(8x8) with an fp64 Winograd domain
 //   KV_PATH_WINO48_F16X3 F(4x8) with the f16x3 split GEMM
+//   KV_PATH_WINO88_I8  F(8x8), fp64 Winograd domain, GEMMs on int8 digits (kv_wino88i.h)
 // fp32 + KV_ALGO_AUTO picks its paths per weight load (kv_net_calibration).
-constexpr int kNPath = 5;
+constexpr int kNPath = KV_NPATH;
 
 struct kv_net {
     int device = 0;
@@ -633,6 +635,9 @@ struct kv_net {
     float* U88 = nullptr;   // F(8x8) [100][Cout][Cin]
     size_t uoff88[12] = {};
     double* U88d = nullptr; // F(8x8), fp64 [100][Cout][Cin] (KV_PATH_WINO88_F64)
+    int8_t* U88i = nullptr; // F(8x8) int8 digits [100][Cout][Cin/32][5][32] (KV_PATH_WINO88_I8)
+    int* eu88i = nullptr;   // their row exponents [100][Cout]
+    size_t euoff[12] = {};
     bool built[kNPath] = {};
     unsigned* vmax = nullptr;  // f16x3: per-board max |V| of each conv's input, [12][cap]
     float* stemT = nullptr; // conv1 as [tap][piece][cout] (stem_kernel)
@@ -641,6 +646,8 @@ struct kv_net {
     void* V = nullptr;
     void* V256 = nullptr;   // conv2's input transform
     void* Mw = nullptr;
+    int8_t* V8 = nullptr;   // KV_PATH_WINO88_I8: V's digits [100][board][512/32][5][32] and exponents [100][board]
+    int* ev8 = nullptr;
     // fp32 + AUTO: the paths chosen by the last calibration (> 16 boards / <= 16)
     int auto_large = KV_PATH_WINO88, auto_small = KV_PATH_DIRECT;
     kv_calib calib = {};
@@ -675,6 +682,7 @@ static int split_kt(int nb_pad) { return nb_pad <= kSplitMaxBoards ? kSplitKt : 
 static int path_for(const kv_net* net, int B) {
     const bool small = B <= kSplitMaxBoards;
     if (net->precision == KV_PREC_F64W) return KV_PATH_WINO88_F64;
+    if (net->precision == KV_PREC_I8X5) return KV_PATH_WINO88_I8;
     if (net->precision == KV_PREC_F16X3) {
         if (net->algo == KV_ALGO_DIRECT || (net->algo == KV_ALGO_AUTO && small)) return KV_PATH_DIRECT;
         return KV_PATH_WINO48_F16X3;
@@ -770,8 +778,11 @@ static int net_reserve(kv_net* net, int nb_pad) {
     int cap = nb_pad < 64 ? 64 : nb_pad;
     (void)hipFree(net->x16); (void)hipFree(net->X); (void)hipFree(net->T); (void)hipFree(net->pfeat);
     (void)hipFree(net->V); (void)hipFree(net->Mw); (void)hipFree(net->V256); (void)hipFree(net->vmax);
+    (void)hipFree(net->V8); (void)hipFree(net->ev8);
     net->x16 = net->X = net->T = net->pfeat = nullptr;
     net->V = net->Mw = net->V256 = nullptr;
+    net->V8 = nullptr;
+    net->ev8 = nullptr;
     net->vmax = nullptr;
     net->cap = 0;
     KV_HIP(hipMalloc(&net->x16, (size_t)cap * 64 * 16 * 4));
@@ -782,6 +793,8 @@ static int net_reserve(kv_net* net, int nb_pad) {
     KV_HIP(hipMalloc(&net->Mw, (size_t)cap * kWsBoard));
     KV_HIP(hipMalloc(&net->V256, (size_t)cap * kWs256Board));
     KV_HIP(hipMalloc(&net->vmax, (size_t)12 * cap * sizeof(unsigned)));
+    KV_HIP(hipMalloc(&net->V8, (size_t)cap * kv::W88_XI * 512 / 32 * kv::kI8Chunk));
+    KV_HIP(hipMalloc(&net->ev8, (size_t)cap * kv::W88_XI * sizeof(int)));
     if (!net->slab)  // 48 splits x 16 boards x 64 px x 512 channels
         KV_HIP(hipMalloc(&net->slab, (size_t)(144 / kSplitKt) * kSplitMaxBoards * 64 * 512 * 4));
     net->cap = cap;
@@ -1071,14 +1084,96 @@ static int wino88d_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     return KV_OK;
 }
 
+// ---- F(8x8) on int8 digits (kv_wino88i.h): the fp64 tower's transforms, V64 sliced into digits
+// before each GEMM ----
+template <int K>
+static int launch_wino88i_slice(const double* src, int n, int slab_rows, int nslab, int8_t* dst, int* ex,
+                                hipStream_t st) {
+    const int waves = n * nslab;
+    hipLaunchKernelGGL(kv::wino88i_slice_kernel<K>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, src, n,
+                       slab_rows, nslab, dst, ex);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+template <int K, int WR, int WC, int MT, int NT>
+static int launch_wino88i_gemm_t(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, double* M,
+                                 int rows, int stride, hipStream_t st) {
+    using T = kv::Wino88iTile<kv::kI8Levels, WR, WC, MT, NT>;
+    KV_HIP(lds_opt_in((const void*)kv::wino88i_gemm_kernel<K, kv::kI8Levels, WR, WC, MT, NT>, (int)T::BYTES));
+    const int nwg = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
+    KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0, KV_EINVAL, "wino gemm i8: rows %d vs tile %d", rows, T::WM);
+    hipLaunchKernelGGL((kv::wino88i_gemm_kernel<K, kv::kI8Levels, WR, WC, MT, NT>), dim3(nwg), dim3(T::THREADS),
+                       T::BYTES, st, V8, ev, U8, eu, M, rows, 512, stride);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+// KV_I8_TILE (timing probes): 0 = 64x128 as 8 waves of 32x32 (default), 1 = 128x64 the same way,
+// 2 = 64x128 as 4 waves of 32x64; rows not a multiple of 64 run 32x128 as 4 waves of 32x32
+static int i8_tile_mode() {
+    static const int v = [] {
+        const char* e = getenv("KV_I8_TILE");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
+template <int K>
+static int launch_wino88i_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, double* M, int rows,
+                               int stride, hipStream_t st) {
+    if (rows % 64) return launch_wino88i_gemm_t<K, 1, 4, 1, 1>(V8, ev, U8, eu, M, rows, stride, st);
+    switch (i8_tile_mode()) {
+        case 1: return launch_wino88i_gemm_t<K, 4, 2, 1, 1>(V8, ev, U8, eu, M, rows, stride, st);
+        case 2: return launch_wino88i_gemm_t<K, 2, 2, 1, 2>(V8, ev, U8, eu, M, rows, stride, st);
+        default: return launch_wino88i_gemm_t<K, 2, 4, 1, 1>(V8, ev, U8, eu, M, rows, stride, st);
+    }
+}
+
+// conv layer l's GEMMs from V64 (K channels, rows boards per point)
+template <int K>
+static int wino88i_layer(kv_net* net, int l, const double* V64, double* M, int rows, int stride, hipStream_t st) {
+    int rc;
+    if ((rc = launch_wino88i_slice<K>(V64, rows, stride, kv::W88_XI, net->V8, net->ev8, st))) return rc;
+    return launch_wino88i_gemm<K>(net->V8, net->ev8, net->U88i + net->uoff88[l] * kv::kI8Digits,
+                                  net->eu88i + net->euoff[l], M, rows, stride, st);
+}
+
+static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
+    const int rows = nb, stride = rows;
+    double* V = (double*)net->V;
+    double* M = (double*)net->Mw;
+    int rc;
+    if ((rc = wino88i_layer<256>(net, 1, (const double*)net->V256, M, rows, stride, st))) return rc;
+    if ((rc = launch_wino88d_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st))) return rc;
+    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
+    for (int r = 0; r < 5; ++r) {
+        const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
+        const bool m = mark && r == 2;
+        if ((rc = launch_wino88i_slice<512>(V, rows, stride, kv::W88_XI, net->V8, net->ev8, st))) return rc;
+        if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
+        if ((rc = launch_wino88i_gemm<512>(net->V8, net->ev8, net->U88i + net->uoff88[l1] * kv::kI8Digits,
+                                           net->eu88i + net->euoff[l1], M, rows, stride, st)))
+            return rc;
+        if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
+        if ((rc = launch_wino88d_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st))) return rc;
+        if ((rc = wino88i_layer<512>(net, l2, V, M, rows, stride, st))) return rc;
+        rc = r < 4 ? launch_wino88d_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
+                   : launch_wino88d_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
+        if (rc) return rc;
+    }
+    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
+    return KV_OK;
+}
+
 // Winograd tower on `path`: conv2 and the 5 residual blocks (conv1 output in
 // net->T, or conv2's input transform already in net->V256 when v256_ready)
 static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hipStream_t st) {
     int rc;
     net->dom_path = path;
     net->dom_launches = 1;
-    if (path == KV_PATH_WINO88 || path == KV_PATH_WINO88_F64) {
-        const bool f64 = path == KV_PATH_WINO88_F64;
+    if (path == KV_PATH_WINO88 || path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8) {
+        const bool f64 = path != KV_PATH_WINO88;
         if (!v256_ready) {
             if (f64)
                 hipLaunchKernelGGL(kv::wino88d_in_kernel<256>, dim3(1, nb_pad), dim3(256), 0, st, net->T, nb_pad,
@@ -1088,7 +1183,10 @@ static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hi
                                    (float*)net->V256);
             KV_HIP(hipGetLastError());
         }
-        if ((rc = f64 ? wino88d_blocks(net, nb_pad, true, st) : wino88_blocks(net, nb_pad, true, st))) return rc;
+        if ((rc = path == KV_PATH_WINO88_I8  ? wino88i_blocks(net, nb_pad, true, st)
+                  : path == KV_PATH_WINO88_F64 ? wino88d_blocks(net, nb_pad, true, st)
+                                               : wino88_blocks(net, nb_pad, true, st)))
+            return rc;
         net->dom_flop = 2.0 * kv::W88_XI * nb_pad * 512.0 * 512.0;
         net->dom_algo = KV_ALGO_WINOGRAD88;
         net->dom_split = f64 ? 0 : (nb_pad % 128 == 0 ? wino88_split_points(nb_pad) : kv::W88_XI);
@@ -1127,7 +1225,7 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
         if (path == KV_PATH_WINO88)
             hipLaunchKernelGGL(kv::stem_kernel<4>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], (float*)net->V256, nb_pad, nullptr);
-        else if (path == KV_PATH_WINO88_F64)
+        else if (path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8)
             hipLaunchKernelGGL(kv::stem_kernel<5>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], (float*)net->V256, nb_pad, nullptr);
         else if (path == KV_PATH_WINO48 || path == KV_PATH_WINO48_F16X3)
@@ -1237,7 +1335,7 @@ static int ensure_path(kv_net* net, int path) {
             launch(l, dim3((unsigned)((n + 255) / 256)));
         }
     };
-    int rc;
+    int rc = KV_OK;
     switch (path) {
         case KV_PATH_DIRECT: break;
         case KV_PATH_WINO48:
@@ -1280,6 +1378,37 @@ static int ensure_path(kv_net* net, int path) {
             KV_HIP(hipGetLastError());
             break;
         }
+        case KV_PATH_WINO88_I8: {
+            // U64 per layer (from the fp64 set when it is built, else into a one-layer scratch), then its digits
+            const size_t tot = wino_offsets(net->uoff88, kv::W88_XI);
+            size_t tot_co = 0;
+            for (int l = 1; l < 12; ++l) {
+                net->euoff[l] = tot_co;
+                tot_co += (size_t)kv::W88_XI * kv::kConv[l].cout;
+            }
+            if (!net->U88i) KV_HIP(hipMalloc(&net->U88i, tot * kv::kI8Digits));
+            if (!net->eu88i) KV_HIP(hipMalloc(&net->eu88i, tot_co * sizeof(int)));
+            double* scratch = nullptr;
+            if (!net->built[KV_PATH_WINO88_F64])
+                KV_HIP(hipMalloc(&scratch, (size_t)kv::W88_XI * 512 * 512 * sizeof(double)));
+            for (int l = 1; l < 12 && rc == KV_OK; ++l) {
+                const int co = kv::kConv[l].cout, ci = kv::kConv[l].cin;
+                const double* U64 = scratch ? scratch : net->U88d + net->uoff88[l];
+                if (scratch) {
+                    hipLaunchKernelGGL(kv::wino88d_weights_kernel, dim3((unsigned)(((size_t)co * ci + 255) / 256)),
+                                       dim3(256), 0, 0, net->w + net->off.w[l], co, ci, scratch);
+                }
+                int8_t* dst = net->U88i + net->uoff88[l] * kv::kI8Digits;
+                int* ex = net->eu88i + net->euoff[l];
+                rc = ci == 256 ? launch_wino88i_slice<256>(U64, co, co, kv::W88_XI, dst, ex, 0)
+                               : launch_wino88i_slice<512>(U64, co, co, kv::W88_XI, dst, ex, 0);
+            }
+            const hipError_t e = hipDeviceSynchronize();
+            (void)hipFree(scratch);
+            if (rc) return rc;
+            KV_HIP(e);
+            break;
+        }
         default: KV_REQUIRE(false, KV_EINVAL, "kv_net: unknown conv path %d", path);
     }
     KV_HIP(hipDeviceSynchronize());
@@ -1312,6 +1441,13 @@ static void release_unused(kv_net* net) {
         (void)hipFree(net->U88d);
         net->U88d = nullptr;
         net->built[KV_PATH_WINO88_F64] = false;
+    }
+    if (!keep[KV_PATH_WINO88_I8]) {
+        (void)hipFree(net->U88i);
+        (void)hipFree(net->eu88i);
+        net->U88i = nullptr;
+        net->eu88i = nullptr;
+        net->built[KV_PATH_WINO88_I8] = false;
     }
 }
 
@@ -1430,9 +1566,9 @@ static int net_calibrate(kv_net* net) {
     if ((rc = ref64_forward(net, boards, kCalibBoards, r)) || (rc = net_reserve(net, kCalibBoards))) return fail(rc);
     const auto within = [&](double el, double ev) { return el <= kCalibTolLogit && ev <= kCalibTolValue; };
     // > 16 boards
-    const int cands[3] = {KV_PATH_WINO88, KV_PATH_WINO48, KV_PATH_WINO88_F64};
+    const int cands[4] = {KV_PATH_WINO88, KV_PATH_WINO48, KV_PATH_WINO88_I8, KV_PATH_WINO88_F64};
     net->auto_small = KV_PATH_DIRECT;
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < 4; ++i) {
         const int p = cands[i];
         if ((rc = ensure_path(net, p))) return fail(rc);
         net->auto_large = p;
@@ -1537,7 +1673,9 @@ int kv_net_set_precision(kv_net* net, int precision) {
     KV_REQUIRE(precision != 1 && precision != 2, KV_EINVAL,
                "kv_net_set_precision: precision %d (bf16x3 / bf16x6) was retired; use KV_PREC_FP32, KV_PREC_F16X3 "
                "or KV_PREC_F64W", precision);
-    KV_REQUIRE(precision == KV_PREC_FP32 || precision == KV_PREC_F16X3 || precision == KV_PREC_F64W, KV_EINVAL,
+    KV_REQUIRE(precision == KV_PREC_FP32 || precision == KV_PREC_F16X3 || precision == KV_PREC_F64W ||
+                   precision == KV_PREC_I8X5,
+               KV_EINVAL,
                "kv_net_set_precision: unknown precision %d", precision);
     if (net->precision == precision) return KV_OK;
     net->precision = precision;
@@ -1594,6 +1732,41 @@ int kv_net_forward_boards_legal(kv_net* net, const int8_t* boards_dev, int B, co
     return rc;
 }
 
+int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, double* M, int8_t* v_digits,
+                   int* v_exp) {
+    KV_REQUIRE(V && U && M && rows > 0 && rows % 32 == 0 && (K == 256 || K == 512), KV_EINVAL,
+               "kv_dev_wino88i: bad arguments (rows %d must be a multiple of 32, K %d 256 or 512)", rows, K);
+    KV_HIP(hipSetDevice(device));
+    const size_t nv = (size_t)kv::W88_XI * rows * K, nu = (size_t)kv::W88_XI * 512 * K;
+    const size_t nm = (size_t)kv::W88_XI * rows * 512;
+    kv::DevBuf<double> dv, du, dm;
+    kv::DevBuf<int8_t> v8, u8;
+    kv::DevBuf<int> ev, eu;
+    KV_HIP(dv.alloc(nv));
+    KV_HIP(du.alloc(nu));
+    KV_HIP(dm.alloc(nm));
+    KV_HIP(v8.alloc(nv * kv::kI8Digits));
+    KV_HIP(u8.alloc(nu * kv::kI8Digits));
+    KV_HIP(ev.alloc((size_t)kv::W88_XI * rows));
+    KV_HIP(eu.alloc((size_t)kv::W88_XI * 512));
+    KV_HIP(hipMemcpy(dv.p, V, nv * sizeof(double), hipMemcpyHostToDevice));
+    KV_HIP(hipMemcpy(du.p, U, nu * sizeof(double), hipMemcpyHostToDevice));
+    int rc = K == 256 ? launch_wino88i_slice<256>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0)
+                      : launch_wino88i_slice<512>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0);
+    if (rc) return rc;
+    rc = K == 256 ? launch_wino88i_slice<256>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0)
+                  : launch_wino88i_slice<512>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
+    if (rc) return rc;
+    rc = K == 256 ? launch_wino88i_gemm<256>(v8.p, ev.p, u8.p, eu.p, dm.p, rows, rows, 0)
+                  : launch_wino88i_gemm<512>(v8.p, ev.p, u8.p, eu.p, dm.p, rows, rows, 0);
+    if (rc) return rc;
+    KV_HIP(hipDeviceSynchronize());
+    KV_HIP(hipMemcpy(M, dm.p, nm * sizeof(double), hipMemcpyDeviceToHost));
+    if (v_digits) KV_HIP(hipMemcpy(v_digits, v8.p, nv * kv::kI8Digits, hipMemcpyDeviceToHost));
+    if (v_exp) KV_HIP(hipMemcpy(v_exp, ev.p, (size_t)kv::W88_XI * rows * sizeof(int), hipMemcpyDeviceToHost));
+    return KV_OK;
+}
+
 int kv_net_set_timing(kv_net* net, int enable) {
     KV_REQUIRE(net, KV_EINVAL, "kv_net_set_timing: NULL");
     net->timing = enable != 0;
@@ -1622,6 +1795,10 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->U48);
     (void)hipFree(net->U88);
     (void)hipFree(net->U88d);
+    (void)hipFree(net->U88i);
+    (void)hipFree(net->eu88i);
+    (void)hipFree(net->V8);
+    (void)hipFree(net->ev8);
     (void)hipFree(net->stemT);
     (void)hipFree(net->v1wT);
     for (int p = 0; p < 2; ++p) (void)hipFree(net->Uf48[p]);

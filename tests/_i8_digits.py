@@ -1,0 +1,51 @@
+"""numpy restatement of KV_PREC_I8X5's digit split and integer GEMM
+(knightvision_amd/csrc/kv_wino88i.h) for the tests: the same fp64 operations
+in the same order, so digits, exponents and M compare bit for bit."""
+import numpy as np
+
+DIGITS = 5
+LEVELS = 5
+
+
+def row_exponents(a):
+    """a [..., K] fp64 -> e [...] int: the row max's biased exponent - 1022 (0 for an all-zero row)."""
+    hi = (a.view(np.uint64) >> np.uint64(32)).astype(np.uint32) & np.uint32(0x7FFFFFFF)
+    m = hi.max(axis=-1)
+    return np.where(m > 0, (m >> np.uint32(20)).astype(np.int64) - 1022, 0)
+
+
+def split(a, e):
+    """a [..., K], e [...] -> digits [DIGITS][..., K] int8 (t *= 128; q = clamp(rint(t)); t -= q)."""
+    t = np.ldexp(a, -e[..., None].astype(np.int32))
+    out = []
+    for _ in range(DIGITS):
+        t = t * 128.0
+        q = np.clip(np.rint(t), -127.0, 127.0)
+        t = t - q
+        out.append(q.astype(np.int8))
+    return np.stack(out)
+
+
+def pack(d):
+    """digits [DIGITS][rows..., K] -> the product layout [rows..., K/32][DIGITS][32] int8."""
+    K = d.shape[-1]
+    x = d.reshape(d.shape[:-1] + (K // 32, 32))
+    return np.moveaxis(x, 0, -2).copy()
+
+
+def gemm(V, U):
+    """V [X][R][K], U [X][C][K] fp64 -> (M [X][R][C], V digits [DIGITS][X][R][K], V exponents [X][R])."""
+    ev, eu = row_exponents(V), row_exponents(U)
+    dv, du = split(V, ev), split(U, eu)
+    fv, fu = dv.astype(np.float64), du.astype(np.float64)
+    lev = []
+    for l in range(LEVELS):  # exact: every partial sum is an integer below 2^31
+        acc = np.zeros((V.shape[0], V.shape[1], U.shape[1]))
+        for i in range(l + 1):
+            acc += np.matmul(fv[i], np.swapaxes(fu[l - i], 1, 2))
+        lev.append(acc)
+    m = lev[LEVELS - 1]
+    for l in range(LEVELS - 2, -1, -1):
+        m = m * 0.0078125 + lev[l]  # exact, as the kernel's fma
+    M = np.ldexp(m, (ev[:, :, None] + eu[:, None, :] - 14).astype(np.int32))
+    return M, dv, ev

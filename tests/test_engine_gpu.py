@@ -139,7 +139,7 @@ GROUPS = {"pg_init_mm80": ("init", 80, 16), "pg_peaked_mm80": ("peaked", 80, 16)
           "pg_init_b1_mm60": ("init", 60, 1), "pg_init_full": ("init", None, 16)}
 
 
-@pytest.mark.parametrize("precision,algo", [("fp32", "auto"), ("f16x3", "auto"), ("f64w", "auto"),
+@pytest.mark.parametrize("precision,algo", [("fp32", "auto"), ("f16x3", "auto"), ("f64w", "auto"), ("i8x5", "auto"),
                                             ("fp32", "winograd48"), ("fp32", "winograd88")])
 @pytest.mark.parametrize("group", list(GROUPS))
 def test_engine_games_match_reference(golden_dir, group, precision, algo):
@@ -147,7 +147,8 @@ def test_engine_games_match_reference(golden_dir, group, precision, algo):
     the network in the <= 16-board class; ("fp32", "winograd48") forces the
     F(4x8) Winograd tower and ("fp32", "winograd88") the F(8x8) one (the
     > 16-board class of C2 / C3) on the same games; ("f64w", "auto") the fp64
-    Winograd domain (AUTO's fallback for trained weights)."""
+    Winograd domain and ("i8x5", "auto") the same domain on int8 digits (AUTO's
+    fallback for trained weights)."""
     from knightvision_amd.engine import SelfPlayEngine, records_by_game
     variant, mm, batch = GROUPS[group]
     gold = _golden_games(golden_dir, group)
@@ -172,7 +173,7 @@ def test_engine_games_match_reference(golden_dir, group, precision, algo):
     # fp32 towers: every golden game identical (0 near-tie divergences measured on every run, the kernels are
     # deterministic and the fixtures fixed); the split precisions keep the near-tie allowance (a divergence
     # only where the reference's own decision margin is < MARGIN_TOL, see _compare)
-    assert len(ties) <= (0 if precision in ("fp32", "f64w") else max(1, n // 8))
+    assert len(ties) <= (0 if precision in ("fp32", "f64w", "i8x5") else max(1, n // 8))
 
 
 def test_sequential_self_play_api_matches_reference(golden_dir):

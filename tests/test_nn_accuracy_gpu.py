@@ -27,7 +27,7 @@ def _planes(n, seed=5):
 
 def _net(sd, algo):
     from knightvision_amd.model import ChessNet
-    m = ChessNet(precision="f64w") if algo == "f64w" else ChessNet(algo=algo)
+    m = ChessNet(precision=algo) if algo in ("f64w", "i8x5") else ChessNet(algo=algo)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
     return m.eval()
 
@@ -39,7 +39,7 @@ def _f64(sd, planes):
     return p.numpy(), v.numpy()
 
 
-def accuracy_table(sd, planes, algos=("direct", "winograd48", "winograd88", "f64w", "auto")):
+def accuracy_table(sd, planes, algos=("direct", "winograd48", "winograd88", "i8x5", "f64w", "auto")):
     """{name: (max |dlogit|, max |dvalue|) vs float64} for the reference's fp32
     forward ("ref32") and each HIP algorithm, plus each algorithm against ref32."""
     from oracle import torch_ref
@@ -79,13 +79,13 @@ def test_auto_within_tolerance_of_reference(variant):
     planes = _planes(N_BOARDS)
     tab, pmax, calib = accuracy_table(sd, planes)
     _report(variant, tab, pmax, N_BOARDS, calib)
-    for k in ("auto", "auto<=16", "f64w"):
+    for k in ("auto", "auto<=16", "f64w", "i8x5"):
         _, _, dpr, dvr = tab[k]
         assert dpr <= TOL_P and dvr <= TOL_V, (k, dpr, dvr)
     if variant in ("bn",):  # random-init magnitudes: the fp32 F(8x8) tower passes and is chosen
         assert calib["path_large"] == "winograd88" and calib["path_small"] == "direct"
-    if variant == "stress":  # trained magnitudes: no fp32 Winograd tower passes
-        assert calib["path_large"] == "winograd88_f64"
+    if variant == "stress":  # trained magnitudes: no fp32 Winograd tower passes; the int8-digit one does
+        assert calib["path_large"] == "winograd88_i8"
 
 
 def _bn_summary(sd):
@@ -120,7 +120,7 @@ def test_trained_weights_table():
     nb = int(os.environ.get("KV_TRAINED_BOARDS", str(N_BOARDS)))
     tab, pmax, calib = accuracy_table(sd, _planes(nb))
     _report(f"trained-{iters}x{games}", tab, pmax, nb, calib)
-    for k in ("auto", "auto<=16", "f64w"):
+    for k in ("auto", "auto<=16", "f64w", "i8x5"):
         _, _, dpr, dvr = tab[k]
         assert dpr <= TOL_P and dvr <= TOL_V, (k, dpr, dvr)
 
@@ -128,18 +128,18 @@ def test_trained_weights_table():
 @pytest.mark.parametrize("variant", ["init", "peaked", "stress"])
 def test_calibration_choice_is_consistent(variant):
     """kv_net_calibration: each candidate run was measured, the chosen path is the
-    first in F(8x8) -> F(4x8) -> F(8x8) fp64 order within the budget, and the
+    first in F(8x8) -> F(4x8) -> F(8x8) int8 digits -> F(8x8) fp64 order within the budget, and the
     engine reports the same choice for the same weights."""
     from knightvision_amd.engine import SelfPlayEngine
     sd = synthetic_state_dict(42, variant)
     c = _net(sd, "auto").kv_net(0).calibration()
     assert c["calibrated"] and c["n_boards"] == 64
-    order = ["winograd88", "winograd48", "winograd88_f64"]
+    order = ["winograd88", "winograd48", "winograd88_i8", "winograd88_f64"]
     ok = {k: c["err_logit"][k] <= c["tol_logit"] and c["err_value"][k] <= c["tol_value"] for k in c["err_logit"]}
     first = next(k for k in order if k == "winograd88_f64" or ok.get(k))
     assert c["path_large"] == first, c
     assert sorted(c["err_logit"]) == sorted(order[:order.index(first) + 1])  # each candidate up to the choice
-    assert c["err_logit"].get("winograd88_f64", 0.0) < 1e-5
+    assert c["err_logit"].get("winograd88_f64", 0.0) < 1e-5 and c["err_logit"].get("winograd88_i8", 0.0) < 1e-5
     small_ok = c["err_small_logit"] <= c["tol_logit"] and c["err_small_value"] <= c["tol_value"]
     assert c["path_small"] == ("direct" if small_ok else "winograd88_f64")
     with SelfPlayEngine(sd, slots=4, n_games=4, max_moves=2) as eng:

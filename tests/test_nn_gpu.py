@@ -15,8 +15,9 @@ TOL_P, TOL_V = 1e-4, 1e-5
 
 # (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x8,3x3) / fp32 Winograd F(8x8,3x3) / fp32 auto
 # (the calibrated choice every product caller runs) / f16x3 Winograd F(4x8) / F(8x8) with the fp64 Winograd domain
+# on fp64 MFMA / the same domain with the GEMMs on int8 digits
 MODES = [("fp32", "direct"), ("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "auto"),
-         ("f16x3", "winograd48"), ("f64w", "auto")]
+         ("f16x3", "winograd48"), ("f64w", "auto"), ("i8x5", "auto")]
 # the explicit fp32 / f16x3 Winograd towers are outside the tolerance at trained magnitudes ("stress": 1.2e-3 to
 # 3.6e-3); AUTO measures that at load time and runs the fp64 Winograd domain instead (test_nn_accuracy_gpu.py)
 UNGUARDED = {("fp32", "winograd48"), ("fp32", "winograd88"), ("f16x3", "winograd48")}
@@ -66,7 +67,7 @@ def test_forward_batch_sizes_vs_torch(B, precision, algo):
     assert np.abs(vb.cpu().numpy() - v.cpu().numpy()).max() == 0.0
 
 
-@pytest.mark.parametrize("precision", ["fp32", "f16x3", "f64w"])
+@pytest.mark.parametrize("precision", ["fp32", "f16x3", "f64w", "i8x5"])
 def test_batch_invariance(precision):
     """A board's outputs do not depend on the batch it is evaluated in, within a
     batch-size class (<= 16 boards: split-K direct kernels; > 16: whole-K
@@ -80,7 +81,7 @@ def test_batch_invariance(precision):
     p_all, v_all = m(planes)  # 40 boards: whole-K class
     p_20, v_20 = m(planes[20:])
     assert torch.equal(p_20, p_all[20:]) and torch.equal(v_20, v_all[20:])
-    if precision in ("fp32", "f16x3", "f64w"):  # 300 boards run the 128-row GEMM tiles, 40 the 64-row ones
+    if precision in ("fp32", "f16x3", "f64w", "i8x5"):  # 300 boards run the 128-row GEMM tiles, 40 the 64-row ones
         codes_l = rng.integers(0, 13, size=(300, 64)) * (rng.random((300, 64)) < 0.4)
         codes_l[:40] = codes
         p_l, v_l = m(torch.from_numpy(codes_to_planes(codes_l)).cuda())
@@ -92,23 +93,44 @@ def test_batch_invariance(precision):
     assert float((p_16 - p_all[:16]).abs().max()) < 1e-4
 
 
-@pytest.mark.parametrize("precision", ["fp32", "f64w"])
+@pytest.mark.parametrize("precision", ["fp32", "f64w", "i8x5"])
 def test_wino88_batch_invariance(precision):
     """F(8x8) (one row per board): a board's outputs are the same bits at 20
     boards (padded to 32: 32-row GEMM tiles, k-tiles of 32), 80 / 96 (padded to
     96: 32-row tiles, k-tiles of 16), 40 / 300 (padded to 64 / 320: 64x128
     tiles) and 512 boards (128x128 tiles for points 0-95, 64x128 for 96-99).
     f64w (the fp64 Winograd domain, every batch size): 32 / 64 / 128-row tiles,
-    the same k-steps."""
+    the same k-steps. i8x5: 32 / 64-row tiles of an exact integer GEMM."""
     from knightvision_amd.ai import codes_to_planes
     rng = np.random.default_rng(88)
     codes = rng.integers(0, 13, size=(512, 64)) * (rng.random((512, 64)) < 0.4)
     planes = torch.from_numpy(codes_to_planes(codes)).cuda()
-    m = _net("peaked", "fp32", "winograd88") if precision == "fp32" else _net("peaked", "f64w", "auto")
+    m = _net("peaked", "fp32", "winograd88") if precision == "fp32" else _net("peaked", precision, "auto")
     p_l, v_l = m(planes)
-    for lo, hi in ((0, 40), (20, 40), (0, 300), (0, 96), (16, 96)) + (((0, 1), (5, 8)) if precision == "f64w" else ()):
+    for lo, hi in ((0, 40), (20, 40), (0, 300), (0, 96), (16, 96)) + (((0, 1), (5, 8)) if precision != "fp32" else ()):
         p, v = m(planes[lo:hi])
         assert torch.equal(p, p_l[lo:hi]) and torch.equal(v, v_l[lo:hi]), (lo, hi)
+
+
+@pytest.mark.parametrize("variant", ["peaked", "stress"])
+def test_i8_digits_track_fp64_domain(variant):
+    """The int8-digit GEMMs (KV_PREC_I8X5) compute the exact dot products of
+    35-bit truncated rows, so the tower lands on the fp64-MFMA tower's outputs to
+    within the truncation (~2^-35 of each row's magnitude) and the fp32 rounding
+    of the activations between layers it can flip: logits within 1e-5 (a few
+    fp32 ulps of the peaked set's logits, which reach ~30) of KV_PREC_F64W's at
+    1 / 31 / 300 boards (measured: 2.4e-6 at one board, peaked)."""
+    from knightvision_amd.ai import codes_to_planes
+    rng = np.random.default_rng(55)
+    codes = rng.integers(0, 13, size=(300, 64)) * (rng.random((300, 64)) < 0.4)
+    planes = torch.from_numpy(codes_to_planes(codes)).cuda()
+    mi, md = _net(variant, "i8x5"), _net(variant, "f64w")
+    for n in (1, 31, 300):
+        pi, vi = mi(planes[:n])
+        pd, vd = md(planes[:n])
+        dp, dv = float((pi - pd).abs().max()), float((vi - vd).abs().max())
+        print(variant, n, "i8x5 vs f64w: max |dlogit|", dp, "|dvalue|", dv)
+        assert dp < 1e-5 and dv < 1e-6, (n, dp, dv)
 
 
 @pytest.mark.parametrize("B", [17, 300, 2048])

@@ -1,0 +1,43 @@
+"""KV_PREC_I8X5's slice and GEMM kernels (csrc/kv_wino88i.h) through
+kv_dev_wino88i, bit for bit against the numpy restatement (tests/_i8_digits.py):
+the digits and row exponents of V, and M -- the exact dot products of the
+digit-truncated rows, so any lane-mapping or accumulation slip shows as a
+differing bit."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from tests import _i8_digits as D
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(V, U):
+    from knightvision_amd import _lib
+    L = _lib.lib()
+    X, R, K = V.shape
+    M = np.zeros((X, R, 512))
+    dg = np.zeros((X, R, K // 32, D.DIGITS, 32), dtype=np.int8)
+    ex = np.zeros((X, R), dtype=np.int32)
+    P = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
+    _lib.check(L.kv_dev_wino88i(0, P(np.ascontiguousarray(V), C.c_double), R, P(np.ascontiguousarray(U), C.c_double),
+                                K, P(M, C.c_double), P(dg, C.c_int8), P(ex, C.c_int32)), "kv_dev_wino88i")
+    return M, dg, ex
+
+
+@pytest.mark.parametrize("K,rows", [(256, 32), (512, 64), (512, 96)])
+def test_i8_gemm_bit_exact(K, rows):
+    rng = np.random.default_rng(K + rows)
+    V = rng.standard_normal((100, rows, K)) * np.exp2(rng.integers(-20, 20, size=(100, rows, 1)))
+    V[0, 0] = 0.0                                 # all-zero row
+    V[1, 1] = np.nextafter(np.exp2(3.0), 0.0)     # first digit clamps and carries
+    V[2, 2, ::3] = 1e-310                         # subnormals beside normals
+    V[3, 3] = np.where(rng.random(K) < 0.5, -1.0, 1.0) * np.exp2(-40.0)
+    U = rng.standard_normal((100, 512, K)) * 0.05
+    U[5, 7] = 0.0
+    M, dg, ex = _run(V, U)
+    Mr, dv, evr = D.gemm(V, U)
+    assert np.array_equal(ex, evr.astype(np.int32))
+    assert np.array_equal(dg, D.pack(dv))
+    assert np.array_equal(M.view(np.uint64), Mr.view(np.uint64)), float(np.abs(M - Mr).max())
