@@ -308,9 +308,9 @@ def gemm_label(path: int, rows: int, split: int):
                     "Winograd F(8x8,3x3) GEMM layer: two launches, both inside the timed events)")
         return name, desc
     if path == 5:
-        name = "wino88i_gemm_kernel<512,5,2,4,1,1>" if rows % 64 == 0 else "wino88i_gemm_kernel<512,5,1,4,1,1>"
-        return name, (" (residual-tower Winograd F(8x8,3x3) GEMMs in the fp64 domain from 5 int8 digits per value: "
-                      "15 v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation)")
+        return "wino88i_gemm_kernel<512,5>", (
+            " (residual-tower Winograd F(8x8,3x3) GEMMs in the fp64 domain from 5 int8 digits per value: 15 "
+            "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, 128x128 tiles)")
     if path == 3:
         name = ("wino88d_gemm_kernel<512,2,4,4,2>" if rows % 128 == 0 else
                 "wino88d_gemm_kernel<512,1,4,4,2>" if rows % 64 == 0 else "wino88d_gemm_kernel<512,1,4,2,2>")

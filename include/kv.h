@@ -290,10 +290,10 @@ int kv_host_libm(int op, const double* x, const double* y, int n, double* out);
 /* CPython random.Random(seed[i]): count random() values -> out [n][count]. */
 int kv_dev_py_random(int device, const uint64_t* seeds, int n, int count, double* out);
 /* KV_PREC_I8X5's Winograd GEMM of one conv layer (csrc/kv_wino88i.h): V [100][rows][K]
- * and U [100][512][K] fp64 (K 256 or 512, rows a multiple of 32) are split into
+ * and U [100][512][K] fp64 (K 256 or 512, rows a multiple of 128) are split into
  * int8 digits by the product's slice kernel and multiplied by its GEMM kernel:
- * M [100][rows][512] fp64; v_digits [100][rows][K/32][5][32] and v_exp
- * [100][rows] (either may be NULL) return V's digits and row exponents. */
+ * M [100][rows][512] fp64; v_digits (digit planes [100][K/32][5][rows][32]) and
+ * v_exp [100][rows] (either may be NULL) return V's digits and row exponents. */
 int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, double* M, int8_t* v_digits,
                    int* v_exp);
 

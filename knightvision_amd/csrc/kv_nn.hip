@@ -635,7 +635,7 @@ struct kv_net {
     float* U88 = nullptr;   // F(8x8) [100][Cout][Cin]
     size_t uoff88[12] = {};
     double* U88d = nullptr; // F(8x8), fp64 [100][Cout][Cin] (KV_PATH_WINO88_F64)
-    int8_t* U88i = nullptr; // F(8x8) int8 digits [100][Cout][Cin/32][5][32] (KV_PATH_WINO88_I8)
+    int8_t* U88i = nullptr; // F(8x8) int8 digit planes [100][Cin/32][5][Cout][32] (KV_PATH_WINO88_I8)
     int* eu88i = nullptr;   // their row exponents [100][Cout]
     size_t euoff[12] = {};
     bool built[kNPath] = {};
@@ -646,7 +646,7 @@ struct kv_net {
     void* V = nullptr;
     void* V256 = nullptr;   // conv2's input transform
     void* Mw = nullptr;
-    int8_t* V8 = nullptr;   // KV_PATH_WINO88_I8: V's digits [100][board][512/32][5][32] and exponents [100][board]
+    int8_t* V8 = nullptr;   // KV_PATH_WINO88_I8: V's digit planes [100][512/32][5][board][32], exponents [100][board]
     int* ev8 = nullptr;
     // fp32 + AUTO: the paths chosen by the last calibration (> 16 boards / <= 16)
     int auto_large = KV_PATH_WINO88, auto_small = KV_PATH_DIRECT;
@@ -769,6 +769,7 @@ static int net_pad(const kv_net* net, int B) {
             return (p32 == 32 || p32 == 96) ? p32 : (B + 63) & ~63;
         }
         case KV_PATH_DIRECT: return (B + 3) & ~3;
+        case KV_PATH_WINO88_I8: return (B + 127) & ~127;  // the int8 GEMM's 128-row tiles
         default: return (B + 31) & ~31;
     }
 }
@@ -793,7 +794,7 @@ static int net_reserve(kv_net* net, int nb_pad) {
     KV_HIP(hipMalloc(&net->Mw, (size_t)cap * kWsBoard));
     KV_HIP(hipMalloc(&net->V256, (size_t)cap * kWs256Board));
     KV_HIP(hipMalloc(&net->vmax, (size_t)12 * cap * sizeof(unsigned)));
-    KV_HIP(hipMalloc(&net->V8, (size_t)cap * kv::W88_XI * 512 / 32 * kv::kI8Chunk));
+    KV_HIP(hipMalloc(&net->V8, (size_t)cap * kv::W88_XI * 512 * kv::kI8Digits));
     KV_HIP(hipMalloc(&net->ev8, (size_t)cap * kv::W88_XI * sizeof(int)));
     if (!net->slab)  // 48 splits x 16 boards x 64 px x 512 channels
         KV_HIP(hipMalloc(&net->slab, (size_t)(144 / kSplitKt) * kSplitMaxBoards * 64 * 512 * 4));
@@ -1096,69 +1097,59 @@ static int launch_wino88i_slice(const double* src, int n, int slab_rows, int nsl
     return KV_OK;
 }
 
-template <int K, int WR, int WC, int MT, int NT>
-static int launch_wino88i_gemm_t(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, double* M,
-                                 int rows, int stride, hipStream_t st) {
-    using T = kv::Wino88iTile<kv::kI8Levels, WR, WC, MT, NT>;
-    KV_HIP(lds_opt_in((const void*)kv::wino88i_gemm_kernel<K, kv::kI8Levels, WR, WC, MT, NT>, (int)T::BYTES));
+// 128 x 128 tiles only (net_pad rounds this path's batch up to 128 boards)
+template <int K>
+static int launch_wino88i_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, double* M, int rows,
+                               int stride, hipStream_t st) {
+    using T = kv::Wino88iTile;
+    constexpr auto kern = kv::wino88i_gemm_kernel<K, kv::kI8Levels>;
+    KV_HIP(lds_opt_in((const void*)kern, (int)T::BYTES));
     const int nwg = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
-    KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0, KV_EINVAL, "wino gemm i8: rows %d vs tile %d", rows, T::WM);
-    hipLaunchKernelGGL((kv::wino88i_gemm_kernel<K, kv::kI8Levels, WR, WC, MT, NT>), dim3(nwg), dim3(T::THREADS),
-                       T::BYTES, st, V8, ev, U8, eu, M, rows, 512, stride);
+    KV_REQUIRE(rows % T::WM == 0 && stride % T::WM == 0 && nwg % 8 == 0, KV_EINVAL,
+               "wino gemm i8: rows %d / stride %d vs tile %d", rows, stride, T::WM);
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(T::THREADS), T::BYTES, st, V8, ev, U8, eu, M, rows, 512, stride);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
 
-// KV_I8_TILE (timing probes): 0 = 64x128 as 8 waves of 32x32 (default), 1 = 128x64 the same way,
-// 2 = 64x128 as 4 waves of 32x64; rows not a multiple of 64 run 32x128 as 4 waves of 32x32
-static int i8_tile_mode() {
-    static const int v = [] {
-        const char* e = getenv("KV_I8_TILE");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-
-template <int K>
-static int launch_wino88i_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, double* M, int rows,
-                               int stride, hipStream_t st) {
-    if (rows % 64) return launch_wino88i_gemm_t<K, 1, 4, 1, 1>(V8, ev, U8, eu, M, rows, stride, st);
-    switch (i8_tile_mode()) {
-        case 1: return launch_wino88i_gemm_t<K, 4, 2, 1, 1>(V8, ev, U8, eu, M, rows, stride, st);
-        case 2: return launch_wino88i_gemm_t<K, 2, 2, 1, 2>(V8, ev, U8, eu, M, rows, stride, st);
-        default: return launch_wino88i_gemm_t<K, 2, 4, 1, 1>(V8, ev, U8, eu, M, rows, stride, st);
-    }
-}
-
-// conv layer l's GEMMs from V64 (K channels, rows boards per point)
-template <int K>
-static int wino88i_layer(kv_net* net, int l, const double* V64, double* M, int rows, int stride, hipStream_t st) {
-    int rc;
-    if ((rc = launch_wino88i_slice<K>(V64, rows, stride, kv::W88_XI, net->V8, net->ev8, st))) return rc;
-    return launch_wino88i_gemm<K>(net->V8, net->ev8, net->U88i + net->uoff88[l] * kv::kI8Digits,
-                                  net->eu88i + net->euoff[l], M, rows, stride, st);
+template <bool RESID, bool WRITE_Y>
+static int launch_wino88i_out(kv_net* net, int l, const double* M, int nb, int stride, const float* resid, float* Y,
+                              hipStream_t st) {
+    const float* W = net->w;
+    constexpr size_t bytes = kv::Wino88iOutLds::BYTES;
+    KV_HIP(lds_opt_in((const void*)kv::wino88i_out_kernel<RESID, WRITE_Y>, (int)bytes));
+    hipLaunchKernelGGL((kv::wino88i_out_kernel<RESID, WRITE_Y>), dim3(nb), dim3(1024), bytes, st, M, stride,
+                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, net->V8, net->ev8);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
 }
 
 static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     const int rows = nb, stride = rows;
-    double* V = (double*)net->V;
     double* M = (double*)net->Mw;
+    const int8_t* U = net->U88i;
     int rc;
-    if ((rc = wino88i_layer<256>(net, 1, (const double*)net->V256, M, rows, stride, st))) return rc;
-    if ((rc = launch_wino88d_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st))) return rc;
+    // conv2: the stem wrote V64 (256 channels); its digits by the slice kernel
+    if ((rc = launch_wino88i_slice<256>((const double*)net->V256, rows, stride, kv::W88_XI, net->V8, net->ev8, st)))
+        return rc;
+    if ((rc = launch_wino88i_gemm<256>(net->V8, net->ev8, U + net->uoff88[1] * kv::kI8Digits,
+                                       net->eu88i + net->euoff[1], M, rows, stride, st)))
+        return rc;
+    if ((rc = launch_wino88i_out<false, true>(net, 1, M, nb, stride, nullptr, net->X, st))) return rc;
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
     for (int r = 0; r < 5; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         const bool m = mark && r == 2;
-        if ((rc = launch_wino88i_slice<512>(V, rows, stride, kv::W88_XI, net->V8, net->ev8, st))) return rc;
         if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-        if ((rc = launch_wino88i_gemm<512>(net->V8, net->ev8, net->U88i + net->uoff88[l1] * kv::kI8Digits,
+        if ((rc = launch_wino88i_gemm<512>(net->V8, net->ev8, U + net->uoff88[l1] * kv::kI8Digits,
                                            net->eu88i + net->euoff[l1], M, rows, stride, st)))
             return rc;
         if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
-        if ((rc = launch_wino88d_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st))) return rc;
-        if ((rc = wino88i_layer<512>(net, l2, V, M, rows, stride, st))) return rc;
-        rc = r < 4 ? launch_wino88d_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
+        if ((rc = launch_wino88i_out<false, false>(net, l1, M, nb, stride, nullptr, nullptr, st))) return rc;
+        if ((rc = launch_wino88i_gemm<512>(net->V8, net->ev8, U + net->uoff88[l2] * kv::kI8Digits,
+                                           net->eu88i + net->euoff[l2], M, rows, stride, st)))
+            return rc;
+        rc = r < 4 ? launch_wino88i_out<true, true>(net, l2, M, nb, stride, net->X, net->X, st)
                    : launch_wino88d_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
         if (rc) return rc;
     }
@@ -1734,8 +1725,8 @@ int kv_net_forward_boards_legal(kv_net* net, const int8_t* boards_dev, int B, co
 
 int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, double* M, int8_t* v_digits,
                    int* v_exp) {
-    KV_REQUIRE(V && U && M && rows > 0 && rows % 32 == 0 && (K == 256 || K == 512), KV_EINVAL,
-               "kv_dev_wino88i: bad arguments (rows %d must be a multiple of 32, K %d 256 or 512)", rows, K);
+    KV_REQUIRE(V && U && M && rows > 0 && rows % 128 == 0 && (K == 256 || K == 512), KV_EINVAL,
+               "kv_dev_wino88i: bad arguments (rows %d must be a multiple of 128, K %d 256 or 512)", rows, K);
     KV_HIP(hipSetDevice(device));
     const size_t nv = (size_t)kv::W88_XI * rows * K, nu = (size_t)kv::W88_XI * 512 * K;
     const size_t nm = (size_t)kv::W88_XI * rows * 512;

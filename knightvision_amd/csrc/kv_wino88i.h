@@ -20,8 +20,9 @@
 // GEMM it replaces, at the same accuracy (host emulation on the stress weights:
 // max |dlogit| 2.4e-6 against fp64's 2.9e-6, profiles/r04_ozaki_emulation.log).
 //
-// Layouts: digits [slab xi][row][K / 32][5][32] int8 (one 160-B chunk per 32 k:
-// the five digits' 32 bytes each), exponents [xi][row] int32.
+// Layouts: digit planes [slab xi][K / 32][digit 5][row][32] int8 (plane (xi, kc,
+// d): digit d of channels 32 kc .. 32 kc + 31 of every row), exponents
+// [xi][row] int32.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -31,16 +32,17 @@
 namespace kv {
 
 constexpr int kI8Digits = 5;                  // digits stored per value
-constexpr int kI8Chunk = kI8Digits * 32;      // bytes of one row's 32-k chunk
 constexpr int kI8Levels = 5;                  // S: the GEMM keeps digit pairs i + j < S
 
 typedef int i8x16_t __attribute__((ext_vector_type(4)));   // 16 int8 in 4 dwords (MFMA A / B)
 typedef int i32x16_t __attribute__((ext_vector_type(16)));  // 32x32 int32 accumulator block
 
 // The digits and exponent of `nslab` slabs of n rows of K fp64 values: row r of
-// slab x is src[(x * slab_rows + r) * K ...]; digits go to dst at the same row
-// index (K * 5 bytes per row), the exponent to ex[x * slab_rows + r]. One wave
-// per row; lane l holds channels [l * K/64, (l + 1) * K/64).
+// slab x is src[(x * slab_rows + r) * K ...]; digit d of its channels
+// [32 kc, 32 kc + 32) goes to plane (x, kc, d) of dst -- 32 bytes at
+// (((x * K/32 + kc) * 5 + d) * slab_rows + r) * 32 -- and the exponent to
+// ex[x * slab_rows + r]. One wave per row; lane l holds channels
+// [l * K/64, (l + 1) * K/64).
 template <int K>
 __global__ __launch_bounds__(256) void wino88i_slice_kernel(const double* __restrict__ src, int n, int slab_rows,
                                                             int nslab, int8_t* __restrict__ dst,
@@ -50,7 +52,8 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const double* __rest
     const int lane = threadIdx.x & 63;
     const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (gw >= n * nslab) return;  // whole waves
-    const size_t row = (size_t)(gw / n) * slab_rows + gw % n;
+    const int x = gw / n, r = gw % n;
+    const size_t row = (size_t)x * slab_rows + r;
     const double* s = src + row * K + lane * CPL;
     double v[CPL];
 #pragma unroll
@@ -87,140 +90,270 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const double* __rest
             pk[d] |= (unsigned long long)(unsigned char)(signed char)(int)q << (8 * i);
         }
     }
-    const int c = lane * CPL;
-    int8_t* o = dst + row * (size_t)(K / 32) * kI8Chunk + (c / 32) * kI8Chunk + (c % 32);
+    const int c = lane * CPL, kc = c / 32;
+    int8_t* o = dst + ((((size_t)x * (K / 32) + kc) * kI8Digits) * slab_rows + r) * 32 + (c % 32);
 #pragma unroll
     for (int d = 0; d < kI8Digits; ++d) {
+        int8_t* od = o + (size_t)d * slab_rows * 32;
         if constexpr (CPL == 8)
-            *(unsigned long long*)(o + d * 32) = pk[d];
+            *(unsigned long long*)od = pk[d];
         else
-            *(unsigned*)(o + d * 32) = (unsigned)pk[d];
+            *(unsigned*)od = (unsigned)pk[d];
     }
 }
 
-// Workgroup tile: WM rows x WN output channels of one point, WR x WC waves of
-// (MT x 32) x (NT x 32). Each 32-k stage stages S digits' 32 bytes per row in
-// LDS rows of S * 32 + 16 bytes (the pad makes the 16 rows of a ds_read_b128
-// lane group hit 16 distinct 4-bank groups), double-buffered.
-template <int S, int WR, int WC, int MT, int NT>
+// The GEMM: a workgroup computes 128 rows x 128 output channels of one point
+// with 8 waves of 32 x 64 (1 x 2 accumulator blocks per digit level). K
+// streams in 32-k stages; a stage is the 5 digit planes of the tile's rows
+// (5 x 128 x 32 B of V, the same of U), copied global -> LDS by
+// global_load_lds (1 KiB = 32 rows per wave-instruction, 5 per wave per
+// stage) into a ring of 3 LDS buffers: the copies of stage kt + 2 run during
+// stage kt's MFMAs, retired by a counted s_waitcnt vmcnt and a raw barrier.
+// The LDS image is linear; the two 16-byte halves of a row are swapped when
+// bit 3 of the row is set (on the global source address), so each ds_read_b128
+// lane group reads 16 distinct 4-bank groups.
 struct Wino88iTile {
+    static constexpr int WR = 4, WC = 2, MT = 1, NT = 2;
     static constexpr int THREADS = WR * WC * 64;
-    static constexpr int WM = WR * MT * 32, WN = WC * NT * 32;
-    static constexpr int RB = S * 32, RS = RB + 16;
-    static constexpr size_t STAGE = (size_t)(WM + WN) * RS;
-    static constexpr size_t BYTES = 2 * STAGE;
+    static constexpr int WM = WR * MT * 32, WN = WC * NT * 32;  // 128 x 128
+    static constexpr int PLANE = 128 * 32;                      // bytes of one digit plane of a tile
+    static constexpr int STAGE = 2 * kI8Digits * PLANE;         // A planes then B planes: 40 KiB
+    static constexpr int NBUF = 3;
+    static constexpr size_t BYTES = (size_t)NBUF * STAGE;
+    static constexpr int GL = STAGE / 1024 / (THREADS / 64);    // global_load_lds per wave and stage
 };
 
+__device__ inline int i8_lds_half(int row, int h) { return 16 * (h ^ ((row >> 3) & 1)); }
+
 // M[xi] (fp64 [xi][stride rows][cout]) = V[xi] x U[xi]^T from the digits (see the header comment).
-// XCD-aware tile order as kv_wino.h's wino_gemm_kernel.
-template <int K, int S, int WR, int WC, int MT, int NT>
-__global__ __launch_bounds__(WR * WC * 64) void wino88i_gemm_kernel(const int8_t* __restrict__ V8,
-                                                                      const int* __restrict__ ev,
-                                                                      const int8_t* __restrict__ U8,
-                                                                      const int* __restrict__ eu,
-                                                                      double* __restrict__ M, int rows, int cout,
-                                                                      int stride) {
-    using T = Wino88iTile<S, WR, WC, MT, NT>;
-    constexpr int WM = T::WM, WN = T::WN, TH = T::THREADS, RS = T::RS;
+// V8: planes [xi][K/32][5][stride][32], U8: [xi][K/32][5][cout][32]. XCD-aware tile order as kv_wino.h's
+// wino_gemm_kernel.
+template <int K, int S>
+__global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restrict__ V8,
+                                                            const int* __restrict__ ev,
+                                                            const int8_t* __restrict__ U8,
+                                                            const int* __restrict__ eu,
+                                                            double* __restrict__ M, int rows, int cout,
+                                                            int stride) {
+    using T = Wino88iTile;
+    constexpr int MT = T::MT, NT = T::NT, WM = T::WM, WN = T::WN, GL = T::GL;
     constexpr int NK = K / 32;
-    constexpr int CH = T::RB / 16;                 // 16-byte pieces per row and stage
-    constexpr int TOT = (WM + WN) * CH;
-    constexpr int NQ = (TOT + TH - 1) / TH;
-    constexpr size_t ROWB = (size_t)(K / 32) * kI8Chunk;  // bytes of one digit row
-    static_assert(S >= 1 && S <= kI8Digits, "digit levels");
+    static_assert(S >= 1 && S <= kI8Digits && GL * (T::THREADS / 64) * 1024 == T::STAGE, "stage split");
 
     extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8[];
     char* const L0 = (char*)lds_i8;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
-    const int wm = wave / WC, wn = wave % WC;
+    const int wm = wave / T::WC, wn = wave % T::WC;
     const int CT = cout / WN, RT = rows / WM;
     const int nwg = (int)gridDim.x;  // a multiple of 8
     const int idx = (int)(blockIdx.x & 7) * (nwg >> 3) + (int)(blockIdx.x >> 3);
     const int xi = idx / (CT * RT);
     const int n_base = (idx % CT) * WN;
     const int r_base = ((idx / CT) % RT) * WM;
-    const int8_t* Va = V8 + ((size_t)xi * stride + r_base) * ROWB;
-    const int8_t* Ub = U8 + ((size_t)xi * cout + n_base) * ROWB;
 
-    i8x16_t rg[NQ];
-    auto load = [&](int kt) {
+    // the GL pieces per stage of this wave: piece q = wave * GL + g covers operand q / 20 (V, U: the
+    // same for all of a wave's pieces), digit (q % 20) / 4, rows 32 (q % 4) .. +31 of the tile; lane l
+    // fills LDS row 32 (q % 4) + l / 2, half l & 1 (bit 3 of that row is bit 4 of l). Everything but the
+    // lane's offset is wave-uniform.
+    const int op = (wave * GL) / 20;
+    const size_t rstride = op ? (size_t)cout : (size_t)stride;
+    const int8_t* gbase = op ? U8 + (((size_t)xi * NK) * kI8Digits * cout + n_base) * 32
+                             : V8 + (((size_t)xi * NK) * kI8Digits * stride + r_base) * 32;
+    const size_t sstep = (size_t)kI8Digits * rstride * 32;  // the next 32-k chunk
+    const int lane_off = (lane >> 1) * 32 + 16 * ((lane & 1) ^ ((lane >> 4) & 1));
+    auto issue = [&](int kt, int buf) {
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int i = tid + q * TH;
-            if (TOT % TH == 0 || i < TOT) {
-                const int r = i / CH, c = i % CH;
-                const int8_t* p = (r < WM ? Va + (size_t)r * ROWB : Ub + (size_t)(r - WM) * ROWB) + kt * kI8Chunk;
-                rg[q] = *(const i8x16_t*)(p + c * 16);
-            }
+        for (int g = 0; g < GL; ++g) {
+            const int q = wave * GL + g, d = (q % 20) / 4, rg = q % 4;
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(gbase + kt * sstep + ((size_t)d * rstride + rg * 32) * 32 + lane_off),
+                (__attribute__((address_space(3))) void*)(L0 + buf * T::STAGE + op * kI8Digits * T::PLANE +
+                                                          d * T::PLANE + rg * 1024),
+                16, 0, 0);
         }
     };
-    auto store = [&](char* buf) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int i = tid + q * TH;
-            if (TOT % TH == 0 || i < TOT) *(i8x16_t*)(buf + (i / CH) * RS + (i % CH) * 16) = rg[q];
-        }
-    };
 
-    // A: lane l holds A[row l & 31][k = 16 (l >> 5) + j], B: B[k = 16 (l >> 5) + j][col l & 31]
+    // fragments: A digit d of row r: plane d, row wm * 32 + (lane & 31), half lane >> 5 (swapped as stored)
     const int lr = lane & 31, lh = lane >> 5;
-    int aoff[MT], boff[NT];
+    const int arow = wm * 32 + lr;
+    const int aoff = arow * 32 + i8_lds_half(arow, lh);
+    int boff[NT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) aoff[mt] = (wm * MT * 32 + mt * 32 + lr) * RS + lh * 16;
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) boff[nt] = (WM + wn * NT * 32 + nt * 32 + lr) * RS + lh * 16;
+    for (int nt = 0; nt < NT; ++nt) {
+        const int bcol = wn * NT * 32 + nt * 32 + lr;
+        boff[nt] = kI8Digits * T::PLANE + bcol * 32 + i8_lds_half(bcol, lh);
+    }
 
     i32x16_t acc[S][MT][NT];
 #pragma unroll
     for (int l = 0; l < S; ++l)
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-            for (int j = 0; j < NT; ++j) acc[l][i][j] = i32x16_t{};
+        for (int nt = 0; nt < NT; ++nt) acc[l][0][nt] = i32x16_t{};
 
-    load(0);
+    issue(0, 0);
+    issue(1, 1);
     for (int kt = 0; kt < NK; ++kt) {
-        char* buf = L0 + (kt & 1) * T::STAGE;
-        store(buf);
-        if (kt + 1 < NK) load(kt + 1);
-        __syncthreads();
-        i8x16_t a[S][MT], b[S][NT];
+        // this wave's copies of stage kt have landed (stage kt + 1's may still be in flight), then
+        // every wave's have, and every wave is done reading the buffer stage kt + 2 goes into
+        if (kt + 1 < NK)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + 2 < NK) issue(kt + 2, (kt + 2) % 3);
+        const char* buf = L0 + (kt % 3) * T::STAGE;
+        // the A digits (one 32-row block) stay live; B digit j (two 32-column blocks) dies after its
+        // S - j products, pairs i + j < S
+        i8x16_t a[S];
 #pragma unroll
-        for (int d = 0; d < S; ++d) {
+        for (int i = 0; i < S; ++i) a[i] = *(const i8x16_t*)(buf + aoff + i * T::PLANE);
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt) a[d][mt] = *(const i8x16_t*)(buf + aoff[mt] + d * 32);
+        for (int j = 0; j < S; ++j) {
+            i8x16_t b[NT];
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt) b[d][nt] = *(const i8x16_t*)(buf + boff[nt] + d * 32);
+            for (int nt = 0; nt < NT; ++nt) b[nt] = *(const i8x16_t*)(buf + boff[nt] + j * T::PLANE);
+#pragma unroll
+            for (int i = 0; i + j < S; ++i)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    acc[i + j][0][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[nt], acc[i + j][0][nt], 0, 0, 0);
         }
-#pragma unroll
-        for (int l = 0; l < S; ++l)
-#pragma unroll
-            for (int i = 0; i <= l; ++i)
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-                    for (int nt = 0; nt < NT; ++nt)
-                        acc[l][mt][nt] =
-                            __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i][mt], b[l - i][nt], acc[l][mt][nt], 0, 0, 0);
     }
 
     // D: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) inside the 32 x 32 block
-    const int* evx = ev + (size_t)xi * stride + r_base + wm * MT * 32;
+    const int* evx = ev + (size_t)xi * stride + r_base + wm * 32;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
         const int col = n_base + wn * NT * 32 + nt * 32 + lr;
         const int ec = eu[(size_t)xi * cout + col] - 14;
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+            double m = (double)acc[S - 1][0][nt][r];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                double m = (double)acc[S - 1][mt][nt][r];
+            for (int l = S - 2; l >= 0; --l) m = __builtin_fma(m, 0.0078125, (double)acc[l][0][nt][r]);  // exact
+            M[((size_t)xi * stride + r_base + wm * 32 + row) * cout + col] = ldexp(m, evx[row] + ec);
+        }
+    }
+}
+
+// Output transform of a residual-tower conv (as kv_wino88d.h's out kernel: fp64,
+// folded BN, residual, ReLU -> fp32 Y) fused with the next conv's input
+// transform straight into digit planes: one workgroup per board, 16 waves = its
+// 512 channels, each plane split over lanes l and l ^ 32. Pass 1 stores the fp32
+// activation plane in LDS, computes the next V64 rows and reduces each point's
+// largest magnitude over the 512 channels (within a half-wave by shuffles,
+// across waves in LDS): the row exponent. Pass 2 recomputes the same rows from
+// the stored plane (the same fma chains, the same bits) and writes their 5
+// digits -- what wino88i_slice_kernel makes of the V64 the fp64 out kernel
+// writes, without V64's round trip through HBM. (The plane is re-read from LDS
+// rather than kept in registers: at 1,024 threads a lane has 128 VGPRs.)
+struct Wino88iOutLds {
+    static constexpr int PS = 68;  // floats per channel plane row in LDS (64 + 4: 16 consecutive channels
+                                   // of a ds_write_b128 / ds_read_b128 lane group on distinct banks)
+    static constexpr size_t PLANES = (size_t)512 * PS * 4;
+    static constexpr size_t RED = (size_t)16 * 2 * 5 * 16 * 4;
+    static constexpr size_t BYTES = PLANES + RED + 100 * 4;
+};
+
+template <bool RESID, bool WRITE_Y>
+__global__ __launch_bounds__(1024) void wino88i_out_kernel(const double* __restrict__ M, int rows,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift, const float* resid,
+                                                           float* Y, int8_t* __restrict__ V8n, int* __restrict__ evn) {
+    constexpr int C = 512, PS = Wino88iOutLds::PS;
+    extern __shared__ __attribute__((aligned(16))) float lds_out[];
+    float* const planes = lds_out;  // [channel][PS]
+    unsigned* const red = (unsigned*)(lds_out + C * PS);  // [wave 16][half 2][aa 5][16]
+    int* const exs = (int*)(red + 16 * 2 * 5 * 16);       // [100]
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+    const int c = w * 32 + (lane & 31), b = blockIdx.x;
+    float* const pl = planes + c * PS + 32 * h;  // this half's rows 4h .. 4h+3
+    // pass 1: the activation plane, then the max |V| of each point over the board's channels
+    {
+        float x2[4][8];
+        wino88d_out_plane<RESID, WRITE_Y>(M, rows, b, c, h, (double)scale[c], (double)shift[c], resid, Y, x2);
 #pragma unroll
-                for (int l = S - 2; l >= 0; --l) m = __builtin_fma(m, 0.0078125, (double)acc[l][mt][nt][r]);  // exact
-                M[((size_t)xi * stride + r_base + wm * MT * 32 + row) * cout + col] = ldexp(m, evx[row] + ec);
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                *(f32x4*)(pl + ii * 8 + 4 * q) =
+                    f32x4{x2[ii][4 * q], x2[ii][4 * q + 1], x2[ii][4 * q + 2], x2[ii][4 * q + 3]};
+        double t2[10][4];
+        wino88d_input_cols(x2, h, t2);
+#pragma unroll
+        for (int aa = 0; aa < 5; ++aa) {
+            double o[10];
+            wino88d_input_row(t2, h, aa, o);
+            unsigned v[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                v[j] = j < 10 ? (unsigned)(__double_as_longlong(o[j]) >> 32) & 0x7fffffffu : 0u;
+            // halving over the lanes of this half (offsets 8, 4, 2, 1): lane keeps index lane & 15
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const int off = 8 >> st;
+                const bool up = (lane & off) != 0;
+#pragma unroll
+                for (int i = 0; i < off; ++i) {
+                    const unsigned mine = up ? v[off + i] : v[i];
+                    const unsigned other = (unsigned)__shfl_xor((int)(up ? v[i] : v[off + i]), off, 64);
+                    v[i] = mine > other ? mine : other;
+                }
+            }
+            const unsigned o16 = (unsigned)__shfl_xor((int)v[0], 16, 64);
+            const unsigned m = v[0] > o16 ? v[0] : o16;
+            if ((lane & 16) == 0 && (lane & 15) < 10) red[((w * 2 + h) * 5 + aa) * 16 + (lane & 15)] = m;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 100) {
+        const int xi = threadIdx.x, a = xi / 10, bb = xi % 10, hh = a / 5, aa = a % 5;
+        unsigned m = 0;
+#pragma unroll
+        for (int ww = 0; ww < 16; ++ww) {
+            const unsigned r = red[((ww * 2 + hh) * 5 + aa) * 16 + bb];
+            m = r > m ? r : m;
+        }
+        const int e = m ? (int)(m >> 20) - 1022 : 0;
+        exs[xi] = e;
+        evn[(size_t)xi * rows + b] = e;
+    }
+    __syncthreads();
+    // pass 2: digits of the same values (plane (xi, kc = w, d), row b, byte lane & 31)
+    float x2[4][8];
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const f32x4 p = *(const f32x4*)(pl + ii * 8 + 4 * q);
+            x2[ii][4 * q] = p[0];
+            x2[ii][4 * q + 1] = p[1];
+            x2[ii][4 * q + 2] = p[2];
+            x2[ii][4 * q + 3] = p[3];
+        }
+    double t2[10][4];
+    wino88d_input_cols(x2, h, t2);
+#pragma unroll
+    for (int aa = 0; aa < 5; ++aa) {
+        double o[10];
+        wino88d_input_row(t2, h, aa, o);
+        const int a = 5 * h + aa;
+#pragma unroll
+        for (int bb = 0; bb < 10; ++bb) {
+            const int xi = a * 10 + bb;
+            double t = ldexp(o[bb], -exs[xi]);
+            int8_t* dst = V8n + ((((size_t)xi * (C / 32) + w) * kI8Digits) * rows + b) * 32 + (lane & 31);
+#pragma unroll
+            for (int d = 0; d < kI8Digits; ++d) {
+                t *= 128.0;
+                double q = rint(t);
+                q = q > 127.0 ? 127.0 : (q < -127.0 ? -127.0 : q);
+                t -= q;
+                dst[(size_t)d * rows * 32] = (int8_t)(int)q;
             }
         }
     }

@@ -27,10 +27,9 @@ def split(a, e):
 
 
 def pack(d):
-    """digits [DIGITS][rows..., K] -> the product layout [rows..., K/32][DIGITS][32] int8."""
-    K = d.shape[-1]
-    x = d.reshape(d.shape[:-1] + (K // 32, 32))
-    return np.moveaxis(x, 0, -2).copy()
+    """digits [DIGITS][X][R][K] -> the product's digit planes [X][K/32][DIGITS][R][32] int8."""
+    D, X, R, K = d.shape
+    return d.reshape(D, X, R, K // 32, 32).transpose(1, 3, 0, 2, 4).copy()
 
 
 def gemm(V, U):

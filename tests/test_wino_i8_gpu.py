@@ -18,7 +18,7 @@ def _run(V, U):
     L = _lib.lib()
     X, R, K = V.shape
     M = np.zeros((X, R, 512))
-    dg = np.zeros((X, R, K // 32, D.DIGITS, 32), dtype=np.int8)
+    dg = np.zeros((X, K // 32, D.DIGITS, R, 32), dtype=np.int8)
     ex = np.zeros((X, R), dtype=np.int32)
     P = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
     _lib.check(L.kv_dev_wino88i(0, P(np.ascontiguousarray(V), C.c_double), R, P(np.ascontiguousarray(U), C.c_double),
@@ -26,7 +26,7 @@ def _run(V, U):
     return M, dg, ex
 
 
-@pytest.mark.parametrize("K,rows", [(256, 32), (512, 64), (512, 96)])
+@pytest.mark.parametrize("K,rows", [(256, 128), (512, 128), (512, 256)])
 def test_i8_gemm_bit_exact(K, rows):
     rng = np.random.default_rng(K + rows)
     V = rng.standard_normal((100, rows, K)) * np.exp2(rng.integers(-20, 20, size=(100, rows, 1)))
