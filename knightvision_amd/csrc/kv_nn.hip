@@ -648,6 +648,7 @@ struct kv_net {
     void* Mw = nullptr;
     int8_t* V8 = nullptr;   // KV_PATH_WINO88_I8: V's digit planes [100][512/32][5][board][32], exponents [100][board]
     int* ev8 = nullptr;
+    unsigned* evmax8 = nullptr;  // the next V's per-row max |V| (high words), [100][board]
     // fp32 + AUTO: the paths chosen by the last calibration (> 16 boards / <= 16)
     int auto_large = KV_PATH_WINO88, auto_small = KV_PATH_DIRECT;
     kv_calib calib = {};
@@ -779,11 +780,12 @@ static int net_reserve(kv_net* net, int nb_pad) {
     int cap = nb_pad < 64 ? 64 : nb_pad;
     (void)hipFree(net->x16); (void)hipFree(net->X); (void)hipFree(net->T); (void)hipFree(net->pfeat);
     (void)hipFree(net->V); (void)hipFree(net->Mw); (void)hipFree(net->V256); (void)hipFree(net->vmax);
-    (void)hipFree(net->V8); (void)hipFree(net->ev8);
+    (void)hipFree(net->V8); (void)hipFree(net->ev8); (void)hipFree(net->evmax8);
     net->x16 = net->X = net->T = net->pfeat = nullptr;
     net->V = net->Mw = net->V256 = nullptr;
     net->V8 = nullptr;
     net->ev8 = nullptr;
+    net->evmax8 = nullptr;
     net->vmax = nullptr;
     net->cap = 0;
     KV_HIP(hipMalloc(&net->x16, (size_t)cap * 64 * 16 * 4));
@@ -796,6 +798,7 @@ static int net_reserve(kv_net* net, int nb_pad) {
     KV_HIP(hipMalloc(&net->vmax, (size_t)12 * cap * sizeof(unsigned)));
     KV_HIP(hipMalloc(&net->V8, (size_t)cap * kv::W88_XI * 512 * kv::kI8Digits));
     KV_HIP(hipMalloc(&net->ev8, (size_t)cap * kv::W88_XI * sizeof(int)));
+    KV_HIP(hipMalloc(&net->evmax8, (size_t)cap * kv::W88_XI * sizeof(unsigned)));
     if (!net->slab)  // 48 splits x 16 boards x 64 px x 512 channels
         KV_HIP(hipMalloc(&net->slab, (size_t)(144 / kSplitKt) * kSplitMaxBoards * 64 * 512 * 4));
     net->cap = cap;
@@ -1112,14 +1115,18 @@ static int launch_wino88i_gemm(const int8_t* V8, const int* ev, const int8_t* U8
     return KV_OK;
 }
 
-template <bool RESID, bool WRITE_Y>
+// conv l's output transform into Y (fp32), then the next conv's digit planes from Y (kv_wino88i.h)
+template <bool RESID>
 static int launch_wino88i_out(kv_net* net, int l, const double* M, int nb, int stride, const float* resid, float* Y,
                               hipStream_t st) {
     const float* W = net->w;
-    constexpr size_t bytes = kv::Wino88iOutLds::BYTES;
-    KV_HIP(lds_opt_in((const void*)kv::wino88i_out_kernel<RESID, WRITE_Y>, (int)bytes));
-    hipLaunchKernelGGL((kv::wino88i_out_kernel<RESID, WRITE_Y>), dim3(nb), dim3(1024), bytes, st, M, stride,
-                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, net->V8, net->ev8);
+    unsigned* evmax = (unsigned*)net->evmax8;
+    KV_HIP(hipMemsetAsync(evmax, 0, (size_t)kv::W88_XI * stride * sizeof(unsigned), st));
+    hipLaunchKernelGGL((kv::wino88i_outmax_kernel<RESID>), dim3(512 / 128, nb), dim3(256), 0, st, M, stride,
+                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, evmax);
+    KV_REQUIRE(nb % 4 == 0, KV_EINVAL, "wino88i: %d boards (a multiple of 4)", nb);
+    hipLaunchKernelGGL(kv::wino88i_in_kernel, dim3(512 / 32, nb / 4), dim3(256), 0, st, Y, stride,
+                       (const unsigned*)evmax, net->V8, net->ev8);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -1135,7 +1142,7 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     if ((rc = launch_wino88i_gemm<256>(net->V8, net->ev8, U + net->uoff88[1] * kv::kI8Digits,
                                        net->eu88i + net->euoff[1], M, rows, stride, st)))
         return rc;
-    if ((rc = launch_wino88i_out<false, true>(net, 1, M, nb, stride, nullptr, net->X, st))) return rc;
+    if ((rc = launch_wino88i_out<false>(net, 1, M, nb, stride, nullptr, net->X, st))) return rc;
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
     for (int r = 0; r < 5; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
@@ -1145,11 +1152,11 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
                                            net->eu88i + net->euoff[l1], M, rows, stride, st)))
             return rc;
         if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
-        if ((rc = launch_wino88i_out<false, false>(net, l1, M, nb, stride, nullptr, nullptr, st))) return rc;
+        if ((rc = launch_wino88i_out<false>(net, l1, M, nb, stride, nullptr, net->T, st))) return rc;
         if ((rc = launch_wino88i_gemm<512>(net->V8, net->ev8, U + net->uoff88[l2] * kv::kI8Digits,
                                            net->eu88i + net->euoff[l2], M, rows, stride, st)))
             return rc;
-        rc = r < 4 ? launch_wino88i_out<true, true>(net, l2, M, nb, stride, net->X, net->X, st)
+        rc = r < 4 ? launch_wino88i_out<true>(net, l2, M, nb, stride, net->X, net->X, st)
                    : launch_wino88d_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
         if (rc) return rc;
     }
@@ -1790,6 +1797,7 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->eu88i);
     (void)hipFree(net->V8);
     (void)hipFree(net->ev8);
+    (void)hipFree(net->evmax8);
     (void)hipFree(net->stemT);
     (void)hipFree(net->v1wT);
     for (int p = 0; p < 2; ++p) (void)hipFree(net->Uf48[p]);

@@ -240,103 +240,100 @@ __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restr
     }
 }
 
-// Output transform of a residual-tower conv (as kv_wino88d.h's out kernel: fp64,
-// folded BN, residual, ReLU -> fp32 Y) fused with the next conv's input
-// transform straight into digit planes: one workgroup per board, 16 waves = its
-// 512 channels, each plane split over lanes l and l ^ 32. Pass 1 stores the fp32
-// activation plane in LDS, computes the next V64 rows and reduces each point's
-// largest magnitude over the 512 channels (within a half-wave by shuffles,
-// across waves in LDS): the row exponent. Pass 2 recomputes the same rows from
-// the stored plane (the same fma chains, the same bits) and writes their 5
-// digits -- what wino88i_slice_kernel makes of the V64 the fp64 out kernel
-// writes, without V64's round trip through HBM. (The plane is re-read from LDS
-// rather than kept in registers: at 1,024 threads a lane has 128 VGPRs.)
-struct Wino88iOutLds {
-    static constexpr int PS = 68;  // floats per channel plane row in LDS (64 + 4: 16 consecutive channels
-                                   // of a ds_write_b128 / ds_read_b128 lane group on distinct banks)
-    static constexpr size_t PLANES = (size_t)512 * PS * 4;
-    static constexpr size_t RED = (size_t)16 * 2 * 5 * 16 * 4;
-    static constexpr size_t BYTES = PLANES + RED + 100 * 4;
-};
+// The next conv's digits come from two kernels, each at the occupancy of the
+// fp64 out kernel (one workgroup = 128 channels of one board): the exponent of
+// a V row needs the largest magnitude over all 512 channels, i.e. over 4
+// workgroups. (One 1,024-thread workgroup per board computing both in one
+// kernel was measured and dropped: 540-665 us per layer at 2,048 boards, its
+// two passes serialised at one workgroup per CU, against 300-420 us for the
+// fp64 out kernel; profiles/r04_i8_fused_out.log.)
+//   wino88i_outmax_kernel: output transform + BN (+ residual) + ReLU -> fp32 Y
+//     (as wino88d_out_half_kernel), the next V64 rows computed and reduced to
+//     each point's max |V| over the workgroup's channels, folded into
+//     evmax[xi][board] (high words of the doubles, atomicMax; zeroed before);
+//   wino88i_in_kernel: the input transform of Y again (the same fma chains on
+//     the same fp32 inputs: the same bits) and its 5 digits under the row
+//     exponents -- what wino88i_slice_kernel makes of that V64.
 
-template <bool RESID, bool WRITE_Y>
-__global__ __launch_bounds__(1024) void wino88i_out_kernel(const double* __restrict__ M, int rows,
-                                                           const float* __restrict__ scale,
-                                                           const float* __restrict__ shift, const float* resid,
-                                                           float* Y, int8_t* __restrict__ V8n, int* __restrict__ evn) {
-    constexpr int C = 512, PS = Wino88iOutLds::PS;
-    extern __shared__ __attribute__((aligned(16))) float lds_out[];
-    float* const planes = lds_out;  // [channel][PS]
-    unsigned* const red = (unsigned*)(lds_out + C * PS);  // [wave 16][half 2][aa 5][16]
-    int* const exs = (int*)(red + 16 * 2 * 5 * 16);       // [100]
+// max over the 32 lanes of this half of v[0..9] (16 shuffles): lanes with (lane & 16) == 0 and
+// (lane & 15) < 10 return the max of index lane & 15
+__device__ inline unsigned i8_half_max10(const double (&o)[10], int lane) {
+    unsigned v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = j < 10 ? (unsigned)(__double_as_longlong(o[j]) >> 32) & 0x7fffffffu : 0u;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {  // halving over offsets 8, 4, 2, 1: lane keeps index lane & 15
+        const int off = 8 >> st;
+        const bool up = (lane & off) != 0;
+#pragma unroll
+        for (int i = 0; i < off; ++i) {
+            const unsigned mine = up ? v[off + i] : v[i];
+            const unsigned other = (unsigned)__shfl_xor((int)(up ? v[i] : v[off + i]), off, 64);
+            v[i] = mine > other ? mine : other;
+        }
+    }
+    const unsigned o16 = (unsigned)__shfl_xor((int)v[0], 16, 64);
+    return v[0] > o16 ? v[0] : o16;
+}
+
+template <bool RESID>
+__global__ __launch_bounds__(256) void wino88i_outmax_kernel(const double* __restrict__ M, int rows,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift, const float* resid,
+                                                             float* Y, unsigned* __restrict__ evmax) {
+    __shared__ unsigned red[4][2][5][16];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
-    const int c = w * 32 + (lane & 31), b = blockIdx.x;
-    float* const pl = planes + c * PS + 32 * h;  // this half's rows 4h .. 4h+3
-    // pass 1: the activation plane, then the max |V| of each point over the board's channels
+    const int c = blockIdx.x * 128 + w * 32 + (lane & 31), b = blockIdx.y;
+    double t2[10][4];
     {
         float x2[4][8];
-        wino88d_out_plane<RESID, WRITE_Y>(M, rows, b, c, h, (double)scale[c], (double)shift[c], resid, Y, x2);
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-                *(f32x4*)(pl + ii * 8 + 4 * q) =
-                    f32x4{x2[ii][4 * q], x2[ii][4 * q + 1], x2[ii][4 * q + 2], x2[ii][4 * q + 3]};
-        double t2[10][4];
+        wino88d_out_plane<RESID, true>(M, rows, b, c, h, (double)scale[c], (double)shift[c], resid, Y, x2);
         wino88d_input_cols(x2, h, t2);
+    }
 #pragma unroll
-        for (int aa = 0; aa < 5; ++aa) {
-            double o[10];
-            wino88d_input_row(t2, h, aa, o);
-            unsigned v[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                v[j] = j < 10 ? (unsigned)(__double_as_longlong(o[j]) >> 32) & 0x7fffffffu : 0u;
-            // halving over the lanes of this half (offsets 8, 4, 2, 1): lane keeps index lane & 15
-#pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                const int off = 8 >> st;
-                const bool up = (lane & off) != 0;
-#pragma unroll
-                for (int i = 0; i < off; ++i) {
-                    const unsigned mine = up ? v[off + i] : v[i];
-                    const unsigned other = (unsigned)__shfl_xor((int)(up ? v[i] : v[off + i]), off, 64);
-                    v[i] = mine > other ? mine : other;
-                }
-            }
-            const unsigned o16 = (unsigned)__shfl_xor((int)v[0], 16, 64);
-            const unsigned m = v[0] > o16 ? v[0] : o16;
-            if ((lane & 16) == 0 && (lane & 15) < 10) red[((w * 2 + h) * 5 + aa) * 16 + (lane & 15)] = m;
-        }
+    for (int aa = 0; aa < 5; ++aa) {
+        double o[10];
+        wino88d_input_row(t2, h, aa, o);
+        const unsigned m = i8_half_max10(o, lane);
+        if ((lane & 16) == 0 && (lane & 15) < 10) red[w][h][aa][lane & 15] = m;
     }
     __syncthreads();
     if (threadIdx.x < 100) {
         const int xi = threadIdx.x, a = xi / 10, bb = xi % 10, hh = a / 5, aa = a % 5;
         unsigned m = 0;
 #pragma unroll
-        for (int ww = 0; ww < 16; ++ww) {
-            const unsigned r = red[((ww * 2 + hh) * 5 + aa) * 16 + bb];
-            m = r > m ? r : m;
-        }
-        const int e = m ? (int)(m >> 20) - 1022 : 0;
-        exs[xi] = e;
-        evn[(size_t)xi * rows + b] = e;
+        for (int ww = 0; ww < 4; ++ww) m = red[ww][hh][aa][bb] > m ? red[ww][hh][aa][bb] : m;
+        if (m) atomicMax(evmax + (size_t)xi * rows + b, m);
     }
-    __syncthreads();
-    // pass 2: digits of the same values (plane (xi, kc = w, d), row b, byte lane & 31)
+}
+
+// grid (512 / 32, boards / 4) x 256: wave w = board 4 blockIdx.y + w, lanes = the 32 channels of chunk
+// kc = blockIdx.x (plane split over lanes l, l ^ 32), so the 4 waves write 4 consecutive rows -- one
+// whole 128-byte line -- of each digit plane (xi, kc, d): 32-byte pieces from different workgroups made
+// the plane writes 2.8x slower (421 us per layer at 2,048 boards, profiles/r04_i8_fused_out.log).
+// X the fp32 activation [board][64][512]; writes the row exponents ex[xi][board] (from evmax) too.
+__global__ __launch_bounds__(256) void wino88i_in_kernel(const float* __restrict__ X, int rows,
+                                                         const unsigned* __restrict__ evmax,
+                                                         int8_t* __restrict__ V8n, int* __restrict__ ex) {
+    constexpr int C = 512;
+    __shared__ int exs[4][100];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+    const int kc = blockIdx.x, c = kc * 32 + (lane & 31), b = blockIdx.y * 4 + w;
+    for (int i = threadIdx.x; i < 400; i += 256) {
+        const int bw = i / 100, xi = i % 100, bb = blockIdx.y * 4 + bw;
+        const unsigned m = evmax[(size_t)xi * rows + bb];
+        const int e = m ? (int)(m >> 20) - 1022 : 0;
+        exs[bw][xi] = e;
+        if (kc == 0) ex[(size_t)xi * rows + bb] = e;
+    }
     float x2[4][8];
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const f32x4 p = *(const f32x4*)(pl + ii * 8 + 4 * q);
-            x2[ii][4 * q] = p[0];
-            x2[ii][4 * q + 1] = p[1];
-            x2[ii][4 * q + 2] = p[2];
-            x2[ii][4 * q + 3] = p[3];
-        }
+        for (int j = 0; j < 8; ++j) x2[ii][j] = X[((size_t)b * 64 + (4 * h + ii) * 8 + j) * C + c];
     double t2[10][4];
     wino88d_input_cols(x2, h, t2);
+    __syncthreads();
 #pragma unroll
     for (int aa = 0; aa < 5; ++aa) {
         double o[10];
@@ -345,8 +342,8 @@ __global__ __launch_bounds__(1024) void wino88i_out_kernel(const double* __restr
 #pragma unroll
         for (int bb = 0; bb < 10; ++bb) {
             const int xi = a * 10 + bb;
-            double t = ldexp(o[bb], -exs[xi]);
-            int8_t* dst = V8n + ((((size_t)xi * (C / 32) + w) * kI8Digits) * rows + b) * 32 + (lane & 31);
+            double t = ldexp(o[bb], -exs[w][xi]);
+            int8_t* dst = V8n + ((((size_t)xi * (C / 32) + kc) * kI8Digits) * rows + b) * 32 + (lane & 31);
 #pragma unroll
             for (int d = 0; d < kI8Digits; ++d) {
                 t *= 128.0;
