@@ -18,7 +18,7 @@
 // 15 int8 products at 32x the fp32 MFMA rate (the int8 rate is 2x bf16's)
 // against v_mfma_f64 at half the fp32 rate: a ~4x higher ceiling than the fp64
 // GEMM it replaces, at the same accuracy (host emulation on the stress weights:
-// max |dlogit| 2.4e-6 against fp64's 2.9e-6, profiles/r04_ozaki_emulation.log).
+// max |dlogit| 3.0e-6 against the fp64 path's 2.9e-6, profiles/r04_ozaki_emulation.log).
 //
 // Layouts: digit planes [slab xi][K / 32][digit 5][row][32] int8 (plane (xi, kc,
 // d): digit d of channels 32 kc .. 32 kc + 31 of every row), exponents
