@@ -1102,11 +1102,21 @@ static int launch_wino88i_slice(const double* src, int n, int slab_rows, int nsl
 }
 
 // 128 x 128 tiles only (net_pad rounds this path's batch up to 128 boards)
+// KV_I8_SPREAD=0 (timing probe): a stage's copies issued together after the barrier
+static bool i8_spread() {
+    static const bool v = [] {
+        const char* e = getenv("KV_I8_SPREAD");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 template <int K>
 static int launch_wino88i_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, double* M, int rows,
                                int stride, hipStream_t st) {
     using T = kv::Wino88iTile;
-    constexpr auto kern = kv::wino88i_gemm_kernel<K, kv::kI8Levels>;
+    auto kern = i8_spread() ? kv::wino88i_gemm_kernel<K, kv::kI8Levels, true>
+                            : kv::wino88i_gemm_kernel<K, kv::kI8Levels, false>;
     KV_HIP(lds_opt_in((const void*)kern, (int)T::BYTES));
     const int nwg = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
     KV_REQUIRE(rows % T::WM == 0 && stride % T::WM == 0 && nwg % 8 == 0, KV_EINVAL,

@@ -128,7 +128,7 @@ __device__ inline int i8_lds_half(int row, int h) { return 16 * (h ^ ((row >> 3)
 // M[xi] (fp64 [xi][stride rows][cout]) = V[xi] x U[xi]^T from the digits (see the header comment).
 // V8: planes [xi][K/32][5][stride][32], U8: [xi][K/32][5][cout][32]. XCD-aware tile order as kv_wino.h's
 // wino_gemm_kernel.
-template <int K, int S>
+template <int K, int S, bool SPREAD = true>
 __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restrict__ V8,
                                                             const int* __restrict__ ev,
                                                             const int8_t* __restrict__ U8,
@@ -163,16 +163,17 @@ __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restr
                              : V8 + (((size_t)xi * NK) * kI8Digits * stride + r_base) * 32;
     const size_t sstep = (size_t)kI8Digits * rstride * 32;  // the next 32-k chunk
     const int lane_off = (lane >> 1) * 32 + 16 * ((lane & 1) ^ ((lane >> 4) & 1));
+    auto issue1 = [&](int g, int kt, int buf) {  // this wave's piece g of stage kt
+        const int q = wave * GL + g, d = (q % 20) / 4, rg = q % 4;
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(gbase + kt * sstep + ((size_t)d * rstride + rg * 32) * 32 + lane_off),
+            (__attribute__((address_space(3))) void*)(L0 + buf * T::STAGE + op * kI8Digits * T::PLANE +
+                                                      d * T::PLANE + rg * 1024),
+            16, 0, 0);
+    };
     auto issue = [&](int kt, int buf) {
 #pragma unroll
-        for (int g = 0; g < GL; ++g) {
-            const int q = wave * GL + g, d = (q % 20) / 4, rg = q % 4;
-            __builtin_amdgcn_global_load_lds(
-                (const void*)(gbase + kt * sstep + ((size_t)d * rstride + rg * 32) * 32 + lane_off),
-                (__attribute__((address_space(3))) void*)(L0 + buf * T::STAGE + op * kI8Digits * T::PLANE +
-                                                          d * T::PLANE + rg * 1024),
-                16, 0, 0);
-        }
+        for (int g = 0; g < GL; ++g) issue1(g, kt, buf);
     };
 
     // fragments: A digit d of row r: plane d, row wm * 32 + (lane & 31), half lane >> 5 (swapped as stored)
@@ -203,10 +204,11 @@ __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restr
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (kt + 2 < NK) issue(kt + 2, (kt + 2) % 3);
         const char* buf = L0 + (kt % 3) * T::STAGE;
         // the A digits (one 32-row block) stay live; B digit j (two 32-column blocks) dies after its
-        // S - j products, pairs i + j < S
+        // S - j products, pairs i + j < S. Stage kt + 2's copies go out one per B digit, between the
+        // MFMA groups (issued back to back after the barrier they delayed every wave's first MFMA:
+        // profiles/r04_i8_glds_spread_ab.log)
         i8x16_t a[S];
 #pragma unroll
         for (int i = 0; i < S; ++i) a[i] = *(const i8x16_t*)(buf + aoff + i * T::PLANE);
@@ -220,7 +222,12 @@ __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restr
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt)
                     acc[i + j][0][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[nt], acc[i + j][0][nt], 0, 0, 0);
+            if (SPREAD && kt + 2 < NK) {
+#pragma unroll
+                for (int g = j * GL / S; g < (j + 1) * GL / S; ++g) issue1(g, kt + 2, (kt + 2) % 3);
+            }
         }
+        if (!SPREAD && kt + 2 < NK) issue(kt + 2, (kt + 2) % 3);
     }
 
     // D: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) inside the 32 x 32 block
