@@ -4,9 +4,10 @@
 // int8 digits instead of v_mfma_f64.
 //
 // Every row of V (point xi, board) and of U (xi, output channel) -- K input
-// channels -- is scaled by a power of two 2^-e to |a| < 1 (e from the row's
-// largest magnitude) and split into 5 signed int8 digits,
-//     a * 2^-e = sum_i d_i * 2^(-7(i+1)) + rest,  |d_i| <= 127,  |rest| <= 2^-35,
+// channels -- is scaled by a power of two 2^-e to |a| < 255/256 (e from the
+// row's largest magnitude, i8_row_exponent) and split into 5 signed int8 digits,
+//     a * 2^-e = sum_i d_i * 2^(-7(i+1)) + rest,  |d_0| <= 127, |d_i| <= 64,
+//     |rest| <= 2^-36,
 // d_i = rint(t_i), t_{i+1} = 128 (t_i - d_i), t_0 = 128 a 2^-e (each step exact
 // in fp64). The product keeps the digit pairs with i + j <= S - 1, S = 5:
 //     M = 2^(e_v + e_u - 14) * sum_{l < S} 2^(-7l) * sum_{i+j=l} (D_i . E_j)
@@ -36,6 +37,27 @@ constexpr int kI8Levels = 5;                  // S: the GEMM keeps digit pairs i
 
 typedef int i8x16_t __attribute__((ext_vector_type(4)));   // 16 int8 in 4 dwords (MFMA A / B)
 typedef int i32x16_t __attribute__((ext_vector_type(16)));  // 32x32 int32 accumulator block
+
+// Row exponent from the high word m of the row's largest |value| (biased exponent E in bits 20-30):
+// 2^(e-1) <= max < 2^e, e = E - 1022, plus one when the max's top 7 fraction bits are all ones (max >=
+// 255/256 * 2^e): then every t = a 2^-e < 255/256, so the first digit rint(128 t) <= 127 and every later
+// remainder is within 1/2 -- no digit needs a clamp (35 bits kept on all but ~0.8 % of rows, 34 on
+// those). An all-zero row gets e = 0 (digits 0).
+__device__ inline int i8_row_exponent(unsigned m) {
+    if (!m) return 0;
+    return (int)(m >> 20) - 1022 + ((m & 0xFE000u) == 0xFE000u ? 1 : 0);
+}
+
+// 5 digits of v under exponent e: t = 128 v 2^-e, d = rint(t), t = 128 (t - d), each step exact
+__device__ inline void i8_digits(double v, int e, int (&d)[kI8Digits]) {
+    double t = ldexp(v, 7 - e);
+#pragma unroll
+    for (int i = 0; i < kI8Digits; ++i) {
+        const double q = rint(t);
+        d[i] = (int)q;
+        t = (t - q) * 128.0;
+    }
+}
 
 // The digits and exponent of `nslab` slabs of n rows of K fp64 values: row r of
 // slab x is src[(x * slab_rows + r) * K ...]; digit d of its channels
@@ -75,20 +97,15 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const double* __rest
         const unsigned t = (unsigned)__shfl_xor((int)m, o, 64);
         m = t > m ? t : m;
     }
-    const int e = m ? (int)(m >> 20) - 1022 : 0;  // an all-zero row: digits 0
+    const int e = i8_row_exponent(m);
     if (lane == 0) ex[row] = e;
     unsigned long long pk[kI8Digits] = {};
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
-        double t = ldexp(v[i], -e);  // |t| < 1, exact
+        int dg[kI8Digits];
+        i8_digits(v[i], e, dg);
 #pragma unroll
-        for (int d = 0; d < kI8Digits; ++d) {
-            t *= 128.0;
-            double q = rint(t);
-            q = q > 127.0 ? 127.0 : (q < -127.0 ? -127.0 : q);  // a clamped digit carries into the next
-            t -= q;
-            pk[d] |= (unsigned long long)(unsigned char)(signed char)(int)q << (8 * i);
-        }
+        for (int d = 0; d < kI8Digits; ++d) pk[d] |= (unsigned long long)(unsigned char)(signed char)dg[d] << (8 * i);
     }
     const int c = lane * CPL, kc = c / 32;
     int8_t* o = dst + ((((size_t)x * (K / 32) + kc) * kI8Digits) * slab_rows + r) * 32 + (c % 32);
@@ -328,8 +345,7 @@ __global__ __launch_bounds__(256) void wino88i_in_kernel(const float* __restrict
     const int kc = blockIdx.x, c = kc * 32 + (lane & 31), b = blockIdx.y * 4 + w;
     for (int i = threadIdx.x; i < 400; i += 256) {
         const int bw = i / 100, xi = i % 100, bb = blockIdx.y * 4 + bw;
-        const unsigned m = evmax[(size_t)xi * rows + bb];
-        const int e = m ? (int)(m >> 20) - 1022 : 0;
+        const int e = i8_row_exponent(evmax[(size_t)xi * rows + bb]);
         exs[bw][xi] = e;
         if (kc == 0) ex[(size_t)xi * rows + bb] = e;
     }
@@ -349,16 +365,11 @@ __global__ __launch_bounds__(256) void wino88i_in_kernel(const float* __restrict
 #pragma unroll
         for (int bb = 0; bb < 10; ++bb) {
             const int xi = a * 10 + bb;
-            double t = ldexp(o[bb], -exs[w][xi]);
+            int dg[kI8Digits];
+            i8_digits(o[bb], exs[w][xi], dg);
             int8_t* dst = V8n + ((((size_t)xi * (C / 32) + kc) * kI8Digits) * rows + b) * 32 + (lane & 31);
 #pragma unroll
-            for (int d = 0; d < kI8Digits; ++d) {
-                t *= 128.0;
-                double q = rint(t);
-                q = q > 127.0 ? 127.0 : (q < -127.0 ? -127.0 : q);
-                t -= q;
-                dst[(size_t)d * rows * 32] = (int8_t)(int)q;
-            }
+            for (int d = 0; d < kI8Digits; ++d) dst[(size_t)d * rows * 32] = (int8_t)dg[d];
         }
     }
 }

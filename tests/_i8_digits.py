@@ -8,21 +8,22 @@ LEVELS = 5
 
 
 def row_exponents(a):
-    """a [..., K] fp64 -> e [...] int: the row max's biased exponent - 1022 (0 for an all-zero row)."""
+    """a [..., K] fp64 -> e [...] int (i8_row_exponent): the row max's biased exponent - 1022, plus one when
+    its top 7 fraction bits are all ones; 0 for an all-zero row."""
     hi = (a.view(np.uint64) >> np.uint64(32)).astype(np.uint32) & np.uint32(0x7FFFFFFF)
     m = hi.max(axis=-1)
-    return np.where(m > 0, (m >> np.uint32(20)).astype(np.int64) - 1022, 0)
+    bump = ((m & np.uint32(0xFE000)) == np.uint32(0xFE000)).astype(np.int64)
+    return np.where(m > 0, (m >> np.uint32(20)).astype(np.int64) - 1022 + bump, 0)
 
 
 def split(a, e):
-    """a [..., K], e [...] -> digits [DIGITS][..., K] int8 (t *= 128; q = clamp(rint(t)); t -= q)."""
-    t = np.ldexp(a, -e[..., None].astype(np.int32))
+    """a [..., K], e [...] -> digits [DIGITS][..., K] int8 (t = 128 a 2^-e; q = rint(t); t = 128 (t - q))."""
+    t = np.ldexp(a, (7 - e[..., None]).astype(np.int32))
     out = []
     for _ in range(DIGITS):
-        t = t * 128.0
-        q = np.clip(np.rint(t), -127.0, 127.0)
-        t = t - q
+        q = np.rint(t)
         out.append(q.astype(np.int8))
+        t = (t - q) * 128.0
     return np.stack(out)
 
 

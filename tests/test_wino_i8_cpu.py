@@ -9,7 +9,7 @@ from tests import _i8_digits as D
 def _rows(rng, n, K):
     a = rng.standard_normal((n, K)) * np.exp2(rng.integers(-30, 30, size=(n, 1)))
     a[0] = 0.0                                   # an all-zero row
-    a[1] = np.nextafter(np.exp2(5.0), 0.0)       # |t0| just below 128: the first digit clamps and carries
+    a[1] = np.nextafter(np.exp2(5.0), 0.0)       # max just below 2^5: the exponent steps up (no clamp needed)
     a[2, ::2] = -a[2, ::2]
     a[3] = 5e-320                                # subnormals
     a[4, :] = 0.0
@@ -23,18 +23,20 @@ def test_digits_reconstruct_to_2_pow_minus_35_of_row_max():
         a = _rows(rng, 64, K)
         e = D.row_exponents(a)
         d = D.split(a, e)
-        assert d.dtype == np.int8 and np.abs(d.astype(int)).max() <= 127
+        di = d.astype(int)
+        assert d.dtype == np.int8 and np.abs(di[0]).max() <= 127 and np.abs(di[1:]).max() <= 64  # no clamp needed
         rec = sum(d[i].astype(np.float64) * 2.0 ** (-7 * (i + 1)) for i in range(D.DIGITS))
         err = np.abs(np.ldexp(rec, e[:, None].astype(np.int32)) - a)
-        bound = np.ldexp(np.ones_like(e, dtype=np.float64), (e - 35).astype(np.int32))
+        bound = np.ldexp(np.ones_like(e, dtype=np.float64), (e - 36).astype(np.int32))
         assert (err <= bound[:, None]).all()
-        nz = np.abs(a).max(axis=1) > 1e-300  # 2^(e-1) <= max |row| < 2^e (rows of tiny subnormals: e = 0, digits 0)
+        nz = np.abs(a).max(axis=1) > 1e-300  # max |row| < 255/256 2^e, and >= 2^(e-2) (rows of tiny subnormals: e = 0)
         mx = np.abs(a).max(axis=1)[nz]
-        assert (mx < np.exp2(e[nz].astype(float))).all() and (mx >= np.exp2(e[nz] - 1.0)).all()
+        assert (mx < np.exp2(e[nz].astype(float)) * 255 / 256).all() and (mx >= np.exp2(e[nz] - 2.0)).all()
+        assert (e[1] == 6)  # row 1: max = 2^5 - ulp, top fraction bits all ones -> bumped from 5 to 6
 
 
 def test_level_sums_fit_int32_and_combine_exactly():
-    # worst case: every digit at the clamp, K = 512: level l sums (l + 1) products of 512 terms
+    # worst case (bound of any digit 127), K = 512: level l sums (l + 1) products of 512 terms
     worst = max((l + 1) * 512 * 127 * 127 for l in range(D.LEVELS))
     assert worst < 2 ** 31
     # combining the five levels spans <= 23 + 28 bits: exact in fp64

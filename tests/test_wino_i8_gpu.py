@@ -31,7 +31,7 @@ def test_i8_gemm_bit_exact(K, rows):
     rng = np.random.default_rng(K + rows)
     V = rng.standard_normal((100, rows, K)) * np.exp2(rng.integers(-20, 20, size=(100, rows, 1)))
     V[0, 0] = 0.0                                 # all-zero row
-    V[1, 1] = np.nextafter(np.exp2(3.0), 0.0)     # first digit clamps and carries
+    V[1, 1] = np.nextafter(np.exp2(3.0), 0.0)     # max just under a power of two: the exponent steps up
     V[2, 2, ::3] = 1e-310                         # subnormals beside normals
     V[3, 3] = np.where(rng.random(K) < 0.5, -1.0, 1.0) * np.exp2(-40.0)
     U = rng.standard_normal((100, 512, K)) * 0.05

@@ -37,9 +37,12 @@ P88 = [Fr(0), Fr(2, 5), Fr(-2, 5), Fr(4, 5), Fr(-4, 5), Fr(5, 4), Fr(-5, 4), Fr(
 AT, G, BT = toom_cook(P88, 8)
 
 
+HEADROOM = 0  # 1: scale rows to |a| < 1/2 (no digit can exceed 64: no clamp needed)
+
+
 def split(a, e, s):
     """a [..., K] fp64, e [..., 1] exponents with |a| * 2^-e < 1 -> s int digit arrays (as fp64)."""
-    r = a * np.exp2(-e)
+    r = a * np.exp2(-e - HEADROOM)
     out = []
     for i in range(s):
         d = np.rint(r * 2.0 ** (7 * (i + 1)))
@@ -79,7 +82,7 @@ def ozaki_gemm(V, U, s, mode, gain, ymax):
         for i in range(lev + 1):
             acc += np.einsum("bxk,xok->bxo", dv[i], du[lev - i])  # exact: |acc| < 2^53
         M += acc * 2.0 ** (-7 * (lev + 2))
-    return M * np.exp2(ev) * np.exp2(eu[..., 0])[None]
+    return M * np.exp2(ev + HEADROOM) * np.exp2(eu[..., 0] + HEADROOM)[None]
 
 
 def conv(x, w, s, mode):
@@ -128,6 +131,8 @@ def fwd(sd, planes, s, mode):
 if __name__ == "__main__":
     variant = sys.argv[1]
     nb = int(sys.argv[2])
+    if os.environ.get("HEADROOM"):
+        HEADROOM = int(os.environ["HEADROOM"])
     cases = sys.argv[3:] or ["f64:0", "row:3", "row:4", "row:5", "row:6", "group128:5", "bound:5", "bound:6"]
     sd = synthetic_state_dict(42, variant)
     rng = np.random.default_rng(5)
