@@ -49,10 +49,11 @@ FP32_MFMA_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md, f32-input MFMA (den
 FP64_MFMA_PEAK_TFLOPS = 78.6          # AMD's MI355X FP64 matrix figure (the guides give no f64 row; measured in
                                       # profiles/r04_f64_mfma_peak.log)
 PATH_NAMES = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3",
-              5: "winograd88_i8"}  # KV_PATH_*
+              5: "winograd88_i8", 6: "winograd88_i8f32"}  # KV_PATH_*
 BF16_MFMA_PEAK_TFLOPS = 2500.0        # dense bf16 MFMA
 I8_MFMA_PEAK_TOPS = 5000.0            # dense int8 MFMA: 2x the bf16 rate (cdna_hip_programming.md, MFMA rate per dtype)
-I8_DIGIT_PRODUCTS = 15                # KV_PREC_I8X5: int8 GEMMs per Winograd GEMM (digit pairs i + j < 5)
+I8_DIGIT_PRODUCTS = {5: 15, 6: 10}    # int8 GEMMs per Winograd GEMM: digit pairs i + j < 5 (KV_PREC_I8X5, fp64
+                                      # domain) / < 4 (KV_ALGO_WINOGRAD88_I8, fp32 domain)
 
 
 def parse():
@@ -64,7 +65,7 @@ def parse():
     ap.add_argument("--slots", type=int, default=2048)
     ap.add_argument("--sims", type=int, default=800)
     ap.add_argument("--precision", choices=["fp32", "f16x3", "f64w", "i8x5"], default="fp32")
-    ap.add_argument("--algo", choices=["auto", "direct", "winograd48", "winograd88"], default="auto",
+    ap.add_argument("--algo", choices=["auto", "direct", "winograd48", "winograd88", "winograd88i8"], default="auto",
                     help="conv algorithm of the fp32 tower (auto: the library's calibrated choice per weight load -- "
                          "Winograd F(8x8,3x3) fp32 for the random-init weights)")
     ap.add_argument("--compare-direct", type=int, default=0,
@@ -78,9 +79,9 @@ def parse():
                          "reported under 'f64w_path'")
     ap.add_argument("--alt-precision", default="f16x3",
                     help="also measure this network precision (reported under 'alt_precision'; '' to skip)")
-    ap.add_argument("--alt-algo", default="winograd48",
-                    help="fp32 only: also time this conv algorithm for --alt-steps moves when the headline runs "
-                         "F(8x8) (the fp32 default); '' to skip")
+    ap.add_argument("--alt-algo", default="winograd88",
+                    help="fp32 only: also time this conv algorithm for --alt-steps moves beside the headline's own "
+                         "(the fp32 MFMA F(8x8) tower beside the int8-digit one AUTO chooses); '' to skip")
     ap.add_argument("--alt-steps", type=int, default=2)
     ap.add_argument("--alt-warmup", type=int, default=1)
     ap.add_argument("--ref-block", type=int, default=1,
@@ -307,8 +308,12 @@ def gemm_label(path: int, rows: int, split: int):
             desc = (f" points 0-{split - 1} + wino_gemm_kernel<512,2,2,1,2,16,100> points {split}-99 (residual-tower "
                     "Winograd F(8x8,3x3) GEMM layer: two launches, both inside the timed events)")
         return name, desc
+    if path == 6:
+        return "wino88i_gemm_kernel<512,4,true,float>", (
+            " (residual-tower Winograd F(8x8,3x3) GEMMs of the fp32 tower from 4 int8 digits per value: 10 "
+            "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 tiles)")
     if path == 5:
-        return "wino88i_gemm_kernel<512,5>", (
+        return "wino88i_gemm_kernel<512,5,true,double>", (
             " (residual-tower Winograd F(8x8,3x3) GEMMs in the fp64 domain from 5 int8 digits per value: 15 "
             "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, 128x128 tiles)")
     if path == 3:
@@ -468,7 +473,9 @@ def main():
     if args.alt_precision and args.alt_precision != args.precision:
         alt = measure(args.alt_precision, steps=args.alt_steps, warmup=args.alt_warmup, tag="alt " + args.alt_precision)
     alt_algo = None
-    if args.alt_algo and args.precision == "fp32" and m["dom_path"] == 2:
+    if args.alt_algo and args.precision == "fp32" and PATH_NAMES.get(m["dom_path"]) != {
+            "winograd88": "winograd88", "winograd48": "winograd48", "direct": "direct",
+            "winograd88i8": "winograd88_i8f32"}.get(args.alt_algo):
         alt_algo = measure("fp32", args.alt_algo, steps=args.alt_steps, warmup=args.alt_warmup,
                            tag="alt " + args.alt_algo)
     refsel = reflazy = None
@@ -496,16 +503,17 @@ def main():
     # the direct algorithm, the residual convs
     path = m["dom_path"]  # KV_PATH_*: 0 direct, 1 F(4x8), 2 F(8x8) fp32 (the fp32 default), 3 F(8x8) fp64, 4 f16x3
     per_board = {1: FLOP_WINO48_GEMM_PER_BOARD, 2: FLOP_WINO88_GEMM_PER_BOARD, 3: FLOP_WINO88_GEMM_PER_BOARD,
-                 4: FLOP_WINO48_GEMM_PER_BOARD, 5: FLOP_WINO88_GEMM_PER_BOARD}.get(path, FLOP_RES_CONV_PER_BOARD)
+                 4: FLOP_WINO48_GEMM_PER_BOARD, 5: FLOP_WINO88_GEMM_PER_BOARD,
+                 6: FLOP_WINO88_GEMM_PER_BOARD}.get(path, FLOP_RES_CONV_PER_BOARD)
     bpl = min(G, int(round(m["dom_flop"] / per_board))) if m["dom_flop"] else G
     flop_alg = per_board * bpl
     achieved = flop_alg / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
-    rows = int(round(m["dom_flop"] / (2 * 512 * 512 * (100 if path in (2, 3, 5) else 60)))) if path else bpl
+    rows = int(round(m["dom_flop"] / (2 * 512 * 512 * (100 if path in (2, 3, 5, 6) else 60)))) if path else bpl
     kname, kdesc = gemm_label(path, rows, m["dom_split"])
     peak = FP64_MFMA_PEAK_TFLOPS if path == 3 else FP32_MFMA_PEAK_TFLOPS
-    if path == 5:  # int8 operations of the digit products against the int8 peak
-        achieved = achieved * I8_DIGIT_PRODUCTS if achieved else None
-        flop_alg *= I8_DIGIT_PRODUCTS
+    if path in I8_DIGIT_PRODUCTS:  # int8 operations of the digit products against the int8 peak
+        achieved = achieved * I8_DIGIT_PRODUCTS[path] if achieved else None
+        flop_alg *= I8_DIGIT_PRODUCTS[path]
         peak = I8_MFMA_PEAK_TOPS
     traffic, traffic_src = _pmc_traffic(kname, bpl)
 
@@ -602,8 +610,20 @@ def main():
         out["calibration"] = dict(m["calibration"], note=(
             "the network's conv paths for these weights: fp32 + AUTO measures its candidates at load time against an "
             "fp64 forward on 64 seeded boards and keeps the fastest within max |dlogit| 4e-5 / |dvalue| 4e-6 "
-            "(F(8x8) fp32, then F(4x8) fp32, then F(8x8) with the fp64 Winograd domain on int8 digits, else on fp64 "
-            "MFMA); errors are max |x - fp64|"))
+            "(F(8x8) fp32 with int8-digit GEMMs, F(8x8) fp32, F(4x8) fp32, the fp64 Winograd domain on int8 digits, "
+            "else on fp64 MFMA); errors are max |x - fp64|"))
+        out["conv_path"] = PATH_NAMES.get(path)
+        out["conv_arithmetic"] = {
+            6: "fp32 network (fp32 activations, fp32 Winograd transforms, U, V and M); each Winograd GEMM the exact "
+               "product of the fp32 operands' 28-bit truncations (4 int8 digits per value per row exponent, 10 "
+               "v_mfma_i32_32x32x32_i8 chains, int32 accumulation without rounding, fp64 combine), rounded to fp32 "
+               "once -- closer to the fp64 result than fp32 MFMA accumulation (calibration errors above; "
+               "fp32_winograd88 is the fp32 MFMA tower)",
+            2: "fp32 network, Winograd GEMMs on v_mfma_f32_32x32x2_f32",
+            1: "fp32 network, Winograd F(4x8) GEMMs on v_mfma_f32_32x32x2_f32",
+            5: "fp32 activations, fp64 Winograd domain, GEMMs from 5 int8 digits per value",
+            3: "fp32 activations, fp64 Winograd domain on v_mfma_f64",
+            0: "fp32 direct implicit-GEMM convs"}.get(path)
         if pg_info is not None:
             out["process_group"] = pg_info
         if trained is not None:
@@ -619,8 +639,8 @@ def main():
                 "ms_per_step": trained["dt"] * 1e3 / trained["steps"],
                 "dominant_kernel": gemm_label(5, G, 0)[0], "res_gemm_avg_launch_ms": trained["conv_ms"],
                 "res_gemm_fp64_equiv_tflops": t_ach,
-                "res_gemm_i8_tops": (t_ach * I8_DIGIT_PRODUCTS) if t_ach else None, "peak_i8_tops": I8_MFMA_PEAK_TOPS,
-                "res_gemm_frac_i8": (t_ach * I8_DIGIT_PRODUCTS / I8_MFMA_PEAK_TOPS) if t_ach else None,
+                "res_gemm_i8_tops": (t_ach * I8_DIGIT_PRODUCTS[5]) if t_ach else None, "peak_i8_tops": I8_MFMA_PEAK_TOPS,
+                "res_gemm_frac_i8": (t_ach * I8_DIGIT_PRODUCTS[5] / I8_MFMA_PEAK_TOPS) if t_ach else None,
                 "res_gemm_over_fp64_mfma_peak": (t_ach / FP64_MFMA_PEAK_TFLOPS) if t_ach else None}
         if f64w is not None:
             f_ach = (FLOP_WINO88_GEMM_PER_BOARD * bpl / (f64w["conv_ms"] * 1e-3) / 1e12) if f64w["conv_ms"] > 0 \
@@ -639,8 +659,10 @@ def main():
             aa_ach = (per * bpl / (aa["conv_ms"] * 1e-3) / 1e12) if aa["conv_ms"] > 0 else None
             out["fp32_" + args.alt_algo] = {
                 "note": ("the same fp32 network with the Winograd F(4x8,3x3) tower (60 points, 2 tiles per board, "
-                         "KV_ALGO_WINOGRAD48, AUTO's second candidate): about half the logit error of F(8x8) for "
-                         "20 % more GEMM FLOPs and transform bytes" if aa["dom_path"] == 1
+                         "KV_ALGO_WINOGRAD48): about half the logit error of F(8x8) for 20 % more GEMM FLOPs and "
+                         "transform bytes" if aa["dom_path"] == 1 else
+                         "the same fp32 F(8x8) tower with its GEMMs on v_mfma_f32_32x32x2_f32 (fp32 products, "
+                         "fp32 accumulation after every product; KV_ALGO_WINOGRAD88)" if aa["dom_path"] == 2
                          else f"the same fp32 network with algo {args.alt_algo}"),
                 "value": (aa["sims"] if mcts else aa["plies"]) / aa["dt"], "unit": unit,
                 "steps": aa["steps"], "warmup": aa["warmup"], "ms_per_step": aa["dt"] * 1e3 / aa["steps"],

@@ -96,15 +96,20 @@ int kv_net_set_precision(kv_net* net, int precision);
 /* Algorithm of the fp32 3x3 convs with Cin 256/512:
  * KV_ALGO_AUTO      per weight load, the fastest path whose logits / values are
  *                   within 4e-5 / 4e-6 of an fp64 forward on 64 calibration
- *                   boards: > 16 boards F(8x8) fp32, else F(4x8) fp32, else
- *                   F(8x8) on int8 digits (KV_PREC_I8X5), else F(8x8) with the
- *                   fp64 Winograd domain; <= 16 boards direct (split-K), else
- *                   F(8x8) fp64 (kv_net_calibration reports it)
+ *                   boards: > 16 boards F(8x8) fp32 with int8-digit GEMMs
+ *                   (KV_ALGO_WINOGRAD88_I8), else F(8x8) fp32, else F(4x8)
+ *                   fp32, else the fp64 Winograd domain on int8 digits
+ *                   (KV_PREC_I8X5), else on fp64 MFMA; <= 16 boards direct
+ *                   (split-K), else F(8x8) fp64 (kv_net_calibration reports it)
  * KV_ALGO_DIRECT    implicit GEMM over the 9 taps (exact fp32 products)
  * KV_ALGO_WINOGRAD48 F(4x8,3x3): 60 GEMMs of 2 tiles x Cin x Cout per board,
  *                   4.8x fewer FLOPs than direct (fp32 and f16x3)
  * KV_ALGO_WINOGRAD88 F(8x8,3x3): 100 GEMMs of 1 tile x Cin x Cout per board,
  *                   5.76x fewer FLOPs than direct (fp32; f16x3 runs F(4x8))
+ * KV_ALGO_WINOGRAD88_I8 the F(8x8) fp32 tower (fp32 U, V, M, transforms) with
+ *                   each GEMM the exact product of 4 int8 digits per value
+ *                   (28-bit rows, int32 levels, fp64 combine, one rounding to
+ *                   fp32) on v_mfma_i32_32x32x32_i8
  * Value 2 (F(4x4)) was retired in round 4: KV_EINVAL. Setting the precision or
  * the algorithm of a loaded net re-prepares it (synchronous).
  * Results are batch-invariant inside a class (<= 16 boards, > 16 boards). */
@@ -112,6 +117,7 @@ int kv_net_set_precision(kv_net* net, int precision);
 #define KV_ALGO_DIRECT 1
 #define KV_ALGO_WINOGRAD48 3
 #define KV_ALGO_WINOGRAD88 4
+#define KV_ALGO_WINOGRAD88_I8 5
 int kv_net_set_algo(kv_net* net, int algo);
 /* conv paths (what a forward runs) */
 #define KV_PATH_DIRECT 0
@@ -120,7 +126,8 @@ int kv_net_set_algo(kv_net* net, int algo);
 #define KV_PATH_WINO88_F64 3
 #define KV_PATH_WINO48_F16X3 4
 #define KV_PATH_WINO88_I8 5
-#define KV_NPATH 6
+#define KV_PATH_WINO88_I8F32 6
+#define KV_NPATH 7
 typedef struct {
     int calibrated;      /* 1: the last load / setting ran the fp32 AUTO calibration */
     int path_large;      /* KV_PATH_* of batches > 16 boards (also without calibration) */
@@ -289,13 +296,15 @@ int kv_dev_dirichlet(int device, const uint64_t* seeds, int n, double alpha, int
 int kv_host_libm(int op, const double* x, const double* y, int n, double* out);
 /* CPython random.Random(seed[i]): count random() values -> out [n][count]. */
 int kv_dev_py_random(int device, const uint64_t* seeds, int n, int count, double* out);
-/* KV_PREC_I8X5's Winograd GEMM of one conv layer (csrc/kv_wino88i.h): V [100][rows][K]
+/* The int8-digit Winograd GEMM of one conv layer (csrc/kv_wino88i.h): V [100][rows][K]
  * and U [100][512][K] fp64 (K 256 or 512, rows a multiple of 128) are split into
- * int8 digits by the product's slice kernel and multiplied by its GEMM kernel:
- * M [100][rows][512] fp64; v_digits (digit planes [100][K/32][5][rows][32]) and
- * v_exp [100][rows] (either may be NULL) return V's digits and row exponents. */
-int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, double* M, int8_t* v_digits,
-                   int* v_exp);
+ * `digits` int8 digits by the product's slice kernel and multiplied by its GEMM
+ * kernel: M [100][rows][512] (digits 5: KV_PREC_I8X5's fp64 M; 4: the fp32
+ * domain's (KV_ALGO_WINOGRAD88_I8) fp32 M, widened); v_digits (digit planes
+ * [100][K/32][digits][rows][32]) and v_exp [100][rows] (either may be NULL)
+ * return V's digits and row exponents. */
+int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, int digits, double* M,
+                   int8_t* v_digits, int* v_exp);
 
 /* ------------------------------------------------------- data pipeline ---
  * Full-rules chess (python-chess 1.999 semantics, csrc/kv_chess.cpp) for the

@@ -42,9 +42,9 @@ class Stats(C.Structure):
                 ("dom_path", C.c_int64), ("dom_split", C.c_int64)]
 
 
-NPATH = 6  # KV_NPATH
+NPATH = 7  # KV_NPATH
 PATHS = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3",
-         5: "winograd88_i8"}  # KV_PATH_*
+         5: "winograd88_i8", 6: "winograd88_i8f32"}  # KV_PATH_*
 
 
 class Calib(C.Structure):
@@ -111,7 +111,7 @@ def _declare(L):
         "kv_dev_dirichlet": ([i, P(C.c_uint64), i, C.c_double, i, i, P(C.c_double), P(i64), P(C.c_double)], i),
         "kv_dev_py_random": ([i, P(C.c_uint64), i, i, P(C.c_double)], i),
         "kv_host_libm": ([i, P(C.c_double), P(C.c_double), i, P(C.c_double)], i),
-        "kv_dev_wino88i": ([i, P(C.c_double), i, P(C.c_double), i, P(C.c_double), P(C.c_int8), P(i)], i),
+        "kv_dev_wino88i": ([i, P(C.c_double), i, P(C.c_double), i, i, P(C.c_double), P(C.c_int8), P(i)], i),
         "kv_pgn_extract": ([C.c_char_p, sz, P(PgnRecord), sz, P(sz), P(sz), P(i64)], i),
         "kv_fen_codes": ([C.c_char_p, sz, i, P(C.c_int8)], i),
         "kv_san_move_index": ([C.c_char_p, sz, C.c_char_p, sz, i, P(C.c_int32)], i),

@@ -23,6 +23,7 @@
 #include <mutex>
 #include <set>
 #include <utility>
+#include <vector>
 
 #include "kv_common.h"
 #include "kv_wino.h"
@@ -609,6 +610,7 @@ __global__ void planes_to_nhwc16_kernel(const float* __restrict__ planes, int nb
 //   KV_PATH_WINO88_F64 Winograd F(8x8) with an fp64 Winograd domain
 //   KV_PATH_WINO48_F16X3 F(4x8) with the f16x3 split GEMM
 //   KV_PATH_WINO88_I8  F(8x8), fp64 Winograd domain, GEMMs on int8 digits (kv_wino88i.h)
+//   KV_PATH_WINO88_I8F32 F(8x8), fp32 Winograd domain, GEMMs on int8 digits (kv_wino88i.h)
 // fp32 + KV_ALGO_AUTO picks its paths per weight load (kv_net_calibration).
 constexpr int kNPath = KV_NPATH;
 
@@ -638,6 +640,8 @@ struct kv_net {
     double* U88d = nullptr; // F(8x8), fp64 [100][Cout][Cin] (KV_PATH_WINO88_F64)
     int8_t* U88i = nullptr; // F(8x8) int8 digit planes [100][Cin/32][5][Cout][32] (KV_PATH_WINO88_I8)
     int* eu88i = nullptr;   // their row exponents [100][Cout]
+    int8_t* U88i32 = nullptr;  // the same with 4 digits (KV_PATH_WINO88_I8F32)
+    int* eu88i32 = nullptr;
     size_t euoff[12] = {};
     bool built[kNPath] = {};
     unsigned* vmax = nullptr;  // f16x3: per-board max |V| of each conv's input, [12][cap]
@@ -685,6 +689,7 @@ static int path_for(const kv_net* net, int B) {
     const bool small = B <= kSplitMaxBoards;
     if (net->precision == KV_PREC_F64W) return KV_PATH_WINO88_F64;
     if (net->precision == KV_PREC_I8X5) return KV_PATH_WINO88_I8;
+    if (net->precision == KV_PREC_FP32 && net->algo == KV_ALGO_WINOGRAD88_I8) return KV_PATH_WINO88_I8F32;
     if (net->precision == KV_PREC_F16X3) {
         if (net->algo == KV_ALGO_DIRECT || (net->algo == KV_ALGO_AUTO && small)) return KV_PATH_DIRECT;
         return KV_PATH_WINO48_F16X3;
@@ -771,7 +776,8 @@ static int net_pad(const kv_net* net, int B) {
             return (p32 == 32 || p32 == 96) ? p32 : (B + 63) & ~63;
         }
         case KV_PATH_DIRECT: return (B + 3) & ~3;
-        case KV_PATH_WINO88_I8: return (B + 127) & ~127;  // the int8 GEMM's 128-row tiles
+        case KV_PATH_WINO88_I8:
+        case KV_PATH_WINO88_I8F32: return (B + 127) & ~127;  // the int8 GEMM's 128-row tiles
         default: return (B + 31) & ~31;
     }
 }
@@ -1091,12 +1097,12 @@ static int wino88d_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 
 // ---- F(8x8) on int8 digits (kv_wino88i.h): the fp64 tower's transforms, V64 sliced into digits
 // before each GEMM ----
-template <int K>
-static int launch_wino88i_slice(const double* src, int n, int slab_rows, int nslab, int8_t* dst, int* ex,
+template <int K, int D = kv::kI8Digits, class T>
+static int launch_wino88i_slice(const T* src, int n, int slab_rows, int nslab, int8_t* dst, int* ex,
                                 hipStream_t st) {
     const int waves = n * nslab;
-    hipLaunchKernelGGL(kv::wino88i_slice_kernel<K>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, src, n,
-                       slab_rows, nslab, dst, ex);
+    hipLaunchKernelGGL((kv::wino88i_slice_kernel<K, T, D>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st,
+                       src, n, slab_rows, nslab, dst, ex);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -1111,12 +1117,11 @@ static bool i8_spread() {
     return v;
 }
 
-template <int K>
-static int launch_wino88i_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, double* M, int rows,
+template <int K, int D = kv::kI8Digits, class OutT = double>
+static int launch_wino88i_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, OutT* M, int rows,
                                int stride, hipStream_t st) {
-    using T = kv::Wino88iTile;
-    auto kern = i8_spread() ? kv::wino88i_gemm_kernel<K, kv::kI8Levels, true>
-                            : kv::wino88i_gemm_kernel<K, kv::kI8Levels, false>;
+    using T = kv::Wino88iTile<D>;
+    auto kern = i8_spread() ? kv::wino88i_gemm_kernel<K, D, true, OutT> : kv::wino88i_gemm_kernel<K, D, false, OutT>;
     KV_HIP(lds_opt_in((const void*)kern, (int)T::BYTES));
     const int nwg = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
     KV_REQUIRE(rows % T::WM == 0 && stride % T::WM == 0 && nwg % 8 == 0, KV_EINVAL,
@@ -1175,14 +1180,65 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     return KV_OK;
 }
 
+// ---- the fp32 domain on int8 digits (KV_PATH_WINO88_I8F32): the fp32 F(8x8) transforms, 4 digits ----
+template <bool RESID>
+static int launch_wino88i32_out(kv_net* net, int l, const float* M, int nb, int stride, const float* resid, float* Y,
+                                hipStream_t st) {
+    const float* W = net->w;
+    unsigned* evmax = (unsigned*)net->evmax8;
+    KV_REQUIRE(nb % 4 == 0, KV_EINVAL, "wino88i32: %d boards (a multiple of 4)", nb);
+    KV_HIP(hipMemsetAsync(evmax, 0, (size_t)kv::W88_XI * stride * sizeof(unsigned), st));
+    hipLaunchKernelGGL((kv::wino88i_outmax32_kernel<RESID>), dim3(512 / 128, nb), dim3(256), 0, st, M, stride,
+                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, evmax);
+    hipLaunchKernelGGL(kv::wino88i_in32_kernel, dim3(512 / 32, nb / 4), dim3(256), 0, st, Y, stride,
+                       (const unsigned*)evmax, net->V8, net->ev8);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+static int wino88i32_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
+    constexpr int D = kv::kI8DigitsF32;
+    const int rows = nb, stride = rows;
+    float* M = (float*)net->Mw;
+    const int8_t* U = net->U88i32;
+    int rc;
+    // conv2: the stem wrote the fp32 V (256 channels); its digits by the slice kernel
+    if ((rc = launch_wino88i_slice<256, D>((const float*)net->V256, rows, stride, kv::W88_XI, net->V8, net->ev8, st)))
+        return rc;
+    if ((rc = launch_wino88i_gemm<256, D>(net->V8, net->ev8, U + net->uoff88[1] * D, net->eu88i32 + net->euoff[1], M,
+                                          rows, stride, st)))
+        return rc;
+    if ((rc = launch_wino88i32_out<false>(net, 1, M, nb, stride, nullptr, net->X, st))) return rc;
+    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
+    for (int r = 0; r < 5; ++r) {
+        const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
+        const bool m = mark && r == 2;
+        if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
+        if ((rc = launch_wino88i_gemm<512, D>(net->V8, net->ev8, U + net->uoff88[l1] * D,
+                                              net->eu88i32 + net->euoff[l1], M, rows, stride, st)))
+            return rc;
+        if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
+        if ((rc = launch_wino88i32_out<false>(net, l1, M, nb, stride, nullptr, net->T, st))) return rc;
+        if ((rc = launch_wino88i_gemm<512, D>(net->V8, net->ev8, U + net->uoff88[l2] * D,
+                                              net->eu88i32 + net->euoff[l2], M, rows, stride, st)))
+            return rc;
+        rc = r < 4 ? launch_wino88i32_out<true>(net, l2, M, nb, stride, net->X, net->X, st)
+                   : launch_wino88_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
+        if (rc) return rc;
+    }
+    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
+    return KV_OK;
+}
+
 // Winograd tower on `path`: conv2 and the 5 residual blocks (conv1 output in
 // net->T, or conv2's input transform already in net->V256 when v256_ready)
 static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hipStream_t st) {
     int rc;
     net->dom_path = path;
     net->dom_launches = 1;
-    if (path == KV_PATH_WINO88 || path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8) {
-        const bool f64 = path != KV_PATH_WINO88;
+    if (path == KV_PATH_WINO88 || path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8 ||
+        path == KV_PATH_WINO88_I8F32) {
+        const bool f64 = path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8;
         if (!v256_ready) {
             if (f64)
                 hipLaunchKernelGGL(kv::wino88d_in_kernel<256>, dim3(1, nb_pad), dim3(256), 0, st, net->T, nb_pad,
@@ -1192,13 +1248,14 @@ static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hi
                                    (float*)net->V256);
             KV_HIP(hipGetLastError());
         }
-        if ((rc = path == KV_PATH_WINO88_I8  ? wino88i_blocks(net, nb_pad, true, st)
+        if ((rc = path == KV_PATH_WINO88_I8F32 ? wino88i32_blocks(net, nb_pad, true, st)
+                  : path == KV_PATH_WINO88_I8  ? wino88i_blocks(net, nb_pad, true, st)
                   : path == KV_PATH_WINO88_F64 ? wino88d_blocks(net, nb_pad, true, st)
                                                : wino88_blocks(net, nb_pad, true, st)))
             return rc;
         net->dom_flop = 2.0 * kv::W88_XI * nb_pad * 512.0 * 512.0;
         net->dom_algo = KV_ALGO_WINOGRAD88;
-        net->dom_split = f64 ? 0 : (nb_pad % 128 == 0 ? wino88_split_points(nb_pad) : kv::W88_XI);
+        net->dom_split = path != KV_PATH_WINO88 ? 0 : (nb_pad % 128 == 0 ? wino88_split_points(nb_pad) : kv::W88_XI);
         return KV_OK;
     }
     const int rows48 = nb_pad * 2;
@@ -1231,7 +1288,7 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     // Winograd paths: the stem builds conv2's V itself
     bool v256_ready = false;
     if (boards) {
-        if (path == KV_PATH_WINO88)
+        if (path == KV_PATH_WINO88 || path == KV_PATH_WINO88_I8F32)
             hipLaunchKernelGGL(kv::stem_kernel<4>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], (float*)net->V256, nb_pad, nullptr);
         else if (path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8)
@@ -1387,16 +1444,22 @@ static int ensure_path(kv_net* net, int path) {
             KV_HIP(hipGetLastError());
             break;
         }
-        case KV_PATH_WINO88_I8: {
+        case KV_PATH_WINO88_I8:
+        case KV_PATH_WINO88_I8F32: {
             // U64 per layer (from the fp64 set when it is built, else into a one-layer scratch), then its digits
+            // (5 for the fp64 domain, 4 for the fp32 one)
+            const bool f32 = path == KV_PATH_WINO88_I8F32;
+            const int D = f32 ? kv::kI8DigitsF32 : kv::kI8Digits;
+            int8_t*& Ud = f32 ? net->U88i32 : net->U88i;
+            int*& Ue = f32 ? net->eu88i32 : net->eu88i;
             const size_t tot = wino_offsets(net->uoff88, kv::W88_XI);
             size_t tot_co = 0;
             for (int l = 1; l < 12; ++l) {
                 net->euoff[l] = tot_co;
                 tot_co += (size_t)kv::W88_XI * kv::kConv[l].cout;
             }
-            if (!net->U88i) KV_HIP(hipMalloc(&net->U88i, tot * kv::kI8Digits));
-            if (!net->eu88i) KV_HIP(hipMalloc(&net->eu88i, tot_co * sizeof(int)));
+            if (!Ud) KV_HIP(hipMalloc(&Ud, tot * D));
+            if (!Ue) KV_HIP(hipMalloc(&Ue, tot_co * sizeof(int)));
             double* scratch = nullptr;
             if (!net->built[KV_PATH_WINO88_F64])
                 KV_HIP(hipMalloc(&scratch, (size_t)kv::W88_XI * 512 * 512 * sizeof(double)));
@@ -1407,10 +1470,14 @@ static int ensure_path(kv_net* net, int path) {
                     hipLaunchKernelGGL(kv::wino88d_weights_kernel, dim3((unsigned)(((size_t)co * ci + 255) / 256)),
                                        dim3(256), 0, 0, net->w + net->off.w[l], co, ci, scratch);
                 }
-                int8_t* dst = net->U88i + net->uoff88[l] * kv::kI8Digits;
-                int* ex = net->eu88i + net->euoff[l];
-                rc = ci == 256 ? launch_wino88i_slice<256>(U64, co, co, kv::W88_XI, dst, ex, 0)
-                               : launch_wino88i_slice<512>(U64, co, co, kv::W88_XI, dst, ex, 0);
+                int8_t* dst = Ud + net->uoff88[l] * D;
+                int* ex = Ue + net->euoff[l];
+                if (f32)
+                    rc = ci == 256 ? launch_wino88i_slice<256, kv::kI8DigitsF32>(U64, co, co, kv::W88_XI, dst, ex, 0)
+                                   : launch_wino88i_slice<512, kv::kI8DigitsF32>(U64, co, co, kv::W88_XI, dst, ex, 0);
+                else
+                    rc = ci == 256 ? launch_wino88i_slice<256>(U64, co, co, kv::W88_XI, dst, ex, 0)
+                                   : launch_wino88i_slice<512>(U64, co, co, kv::W88_XI, dst, ex, 0);
             }
             const hipError_t e = hipDeviceSynchronize();
             (void)hipFree(scratch);
@@ -1457,6 +1524,13 @@ static void release_unused(kv_net* net) {
         net->U88i = nullptr;
         net->eu88i = nullptr;
         net->built[KV_PATH_WINO88_I8] = false;
+    }
+    if (!keep[KV_PATH_WINO88_I8F32]) {
+        (void)hipFree(net->U88i32);
+        (void)hipFree(net->eu88i32);
+        net->U88i32 = nullptr;
+        net->eu88i32 = nullptr;
+        net->built[KV_PATH_WINO88_I8F32] = false;
     }
 }
 
@@ -1575,9 +1649,10 @@ static int net_calibrate(kv_net* net) {
     if ((rc = ref64_forward(net, boards, kCalibBoards, r)) || (rc = net_reserve(net, kCalibBoards))) return fail(rc);
     const auto within = [&](double el, double ev) { return el <= kCalibTolLogit && ev <= kCalibTolValue; };
     // > 16 boards
-    const int cands[4] = {KV_PATH_WINO88, KV_PATH_WINO48, KV_PATH_WINO88_I8, KV_PATH_WINO88_F64};
+    const int cands[5] = {KV_PATH_WINO88_I8F32, KV_PATH_WINO88, KV_PATH_WINO48, KV_PATH_WINO88_I8,
+                          KV_PATH_WINO88_F64};
     net->auto_small = KV_PATH_DIRECT;
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 5; ++i) {
         const int p = cands[i];
         if ((rc = ensure_path(net, p))) return fail(rc);
         net->auto_large = p;
@@ -1670,7 +1745,7 @@ int kv_net_set_algo(kv_net* net, int algo) {
     KV_REQUIRE(algo != 2, KV_EINVAL, "kv_net_set_algo: KV_ALGO 2 (Winograd F(4x4)) was retired; use "
                                      "KV_ALGO_WINOGRAD48 or KV_ALGO_WINOGRAD88");
     KV_REQUIRE(algo == KV_ALGO_AUTO || algo == KV_ALGO_DIRECT || algo == KV_ALGO_WINOGRAD48 ||
-                   algo == KV_ALGO_WINOGRAD88,
+                   algo == KV_ALGO_WINOGRAD88 || algo == KV_ALGO_WINOGRAD88_I8,
                KV_EINVAL, "kv_net_set_algo: unknown algo %d", algo);
     if (net->algo == algo) return KV_OK;
     net->algo = algo;
@@ -1741,37 +1816,59 @@ int kv_net_forward_boards_legal(kv_net* net, const int8_t* boards_dev, int B, co
     return rc;
 }
 
-int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, double* M, int8_t* v_digits,
-                   int* v_exp) {
-    KV_REQUIRE(V && U && M && rows > 0 && rows % 128 == 0 && (K == 256 || K == 512), KV_EINVAL,
-               "kv_dev_wino88i: bad arguments (rows %d must be a multiple of 128, K %d 256 or 512)", rows, K);
+int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, int digits, double* M,
+                   int8_t* v_digits, int* v_exp) {
+    KV_REQUIRE(V && U && M && rows > 0 && rows % 128 == 0 && (K == 256 || K == 512) && (digits == 4 || digits == 5),
+               KV_EINVAL, "kv_dev_wino88i: bad arguments (rows %d must be a multiple of 128, K %d 256 or 512, "
+               "digits %d 4 or 5)", rows, K, digits);
     KV_HIP(hipSetDevice(device));
     const size_t nv = (size_t)kv::W88_XI * rows * K, nu = (size_t)kv::W88_XI * 512 * K;
     const size_t nm = (size_t)kv::W88_XI * rows * 512;
     kv::DevBuf<double> dv, du, dm;
+    kv::DevBuf<float> dmf;
     kv::DevBuf<int8_t> v8, u8;
     kv::DevBuf<int> ev, eu;
     KV_HIP(dv.alloc(nv));
     KV_HIP(du.alloc(nu));
     KV_HIP(dm.alloc(nm));
-    KV_HIP(v8.alloc(nv * kv::kI8Digits));
-    KV_HIP(u8.alloc(nu * kv::kI8Digits));
+    KV_HIP(dmf.alloc(nm));
+    KV_HIP(v8.alloc(nv * digits));
+    KV_HIP(u8.alloc(nu * digits));
     KV_HIP(ev.alloc((size_t)kv::W88_XI * rows));
     KV_HIP(eu.alloc((size_t)kv::W88_XI * 512));
     KV_HIP(hipMemcpy(dv.p, V, nv * sizeof(double), hipMemcpyHostToDevice));
     KV_HIP(hipMemcpy(du.p, U, nu * sizeof(double), hipMemcpyHostToDevice));
-    int rc = K == 256 ? launch_wino88i_slice<256>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0)
+    int rc;
+    if (digits == 5) {  // the fp64 domain: fp64 M
+        rc = K == 256 ? launch_wino88i_slice<256>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0)
                       : launch_wino88i_slice<512>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0);
-    if (rc) return rc;
-    rc = K == 256 ? launch_wino88i_slice<256>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0)
-                  : launch_wino88i_slice<512>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
-    if (rc) return rc;
-    rc = K == 256 ? launch_wino88i_gemm<256>(v8.p, ev.p, u8.p, eu.p, dm.p, rows, rows, 0)
-                  : launch_wino88i_gemm<512>(v8.p, ev.p, u8.p, eu.p, dm.p, rows, rows, 0);
+        if (!rc)
+            rc = K == 256 ? launch_wino88i_slice<256>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0)
+                          : launch_wino88i_slice<512>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
+        if (!rc)
+            rc = K == 256 ? launch_wino88i_gemm<256>(v8.p, ev.p, u8.p, eu.p, dm.p, rows, rows, 0)
+                          : launch_wino88i_gemm<512>(v8.p, ev.p, u8.p, eu.p, dm.p, rows, rows, 0);
+    } else {  // the fp32 domain: 4 digits, M rounded to fp32 (returned widened)
+        constexpr int D = kv::kI8DigitsF32;
+        rc = K == 256 ? launch_wino88i_slice<256, D>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0)
+                      : launch_wino88i_slice<512, D>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0);
+        if (!rc)
+            rc = K == 256 ? launch_wino88i_slice<256, D>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0)
+                          : launch_wino88i_slice<512, D>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
+        if (!rc)
+            rc = K == 256 ? launch_wino88i_gemm<256, D>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, 0)
+                          : launch_wino88i_gemm<512, D>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, 0);
+    }
     if (rc) return rc;
     KV_HIP(hipDeviceSynchronize());
-    KV_HIP(hipMemcpy(M, dm.p, nm * sizeof(double), hipMemcpyDeviceToHost));
-    if (v_digits) KV_HIP(hipMemcpy(v_digits, v8.p, nv * kv::kI8Digits, hipMemcpyDeviceToHost));
+    if (digits == 5) {
+        KV_HIP(hipMemcpy(M, dm.p, nm * sizeof(double), hipMemcpyDeviceToHost));
+    } else {
+        std::vector<float> mf(nm);
+        KV_HIP(hipMemcpy(mf.data(), dmf.p, nm * sizeof(float), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < nm; ++i) M[i] = mf[i];
+    }
+    if (v_digits) KV_HIP(hipMemcpy(v_digits, v8.p, nv * digits, hipMemcpyDeviceToHost));
     if (v_exp) KV_HIP(hipMemcpy(v_exp, ev.p, (size_t)kv::W88_XI * rows * sizeof(int), hipMemcpyDeviceToHost));
     return KV_OK;
 }
@@ -1806,6 +1903,8 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->U88d);
     (void)hipFree(net->U88i);
     (void)hipFree(net->eu88i);
+    (void)hipFree(net->U88i32);
+    (void)hipFree(net->eu88i32);
     (void)hipFree(net->V8);
     (void)hipFree(net->ev8);
     (void)hipFree(net->evmax8);

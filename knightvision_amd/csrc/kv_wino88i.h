@@ -32,8 +32,10 @@
 
 namespace kv {
 
-constexpr int kI8Digits = 5;                  // digits stored per value
-constexpr int kI8Levels = 5;                  // S: the GEMM keeps digit pairs i + j < S
+constexpr int kI8Digits = 5;    // digits per value in the fp64 domain (KV_PATH_WINO88_I8); the GEMM keeps
+                                // the digit pairs i + j < digits
+constexpr int kI8DigitsF32 = 4; // in the fp32 domain (KV_PATH_WINO88_I8F32): 28 bits, an fp32 value exactly
+                                // when it is within 2^-4 of its row's max
 
 typedef int i8x16_t __attribute__((ext_vector_type(4)));   // 16 int8 in 4 dwords (MFMA A / B)
 typedef int i32x16_t __attribute__((ext_vector_type(16)));  // 32x32 int32 accumulator block
@@ -48,14 +50,22 @@ __device__ inline int i8_row_exponent(unsigned m) {
     return (int)(m >> 20) - 1022 + ((m & 0xFE000u) == 0xFE000u ? 1 : 0);
 }
 
-// 5 digits of v under exponent e: t = 128 v 2^-e, d = rint(t), t = 128 (t - d), each step exact
-__device__ inline void i8_digits(double v, int e, int (&d)[kI8Digits]) {
-    double t = ldexp(v, 7 - e);
+// fp32 form: m = the bits of the row's largest |float| (exponent in bits 23-30, top 7 fraction bits 16-22)
+__device__ inline int i8_row_exponent_f32(unsigned m) {
+    if (!m) return 0;
+    return (int)(m >> 23) - 126 + ((m & 0x7F0000u) == 0x7F0000u ? 1 : 0);
+}
+
+// D digits of v under exponent e: t = 128 v 2^-e, d = rint(t), t = 128 (t - d), each step exact (in fp32
+// too: t never has more significant bits than v)
+template <int D, class T>
+__device__ inline void i8_digits(T v, int e, int (&d)[D]) {
+    T t = ldexp(v, 7 - e);
 #pragma unroll
-    for (int i = 0; i < kI8Digits; ++i) {
-        const double q = rint(t);
+    for (int i = 0; i < D; ++i) {
+        const T q = rint(t);
         d[i] = (int)q;
-        t = (t - q) * 128.0;
+        t = (t - q) * (T)128;
     }
 }
 
@@ -65,8 +75,8 @@ __device__ inline void i8_digits(double v, int e, int (&d)[kI8Digits]) {
 // (((x * K/32 + kc) * 5 + d) * slab_rows + r) * 32 -- and the exponent to
 // ex[x * slab_rows + r]. One wave per row; lane l holds channels
 // [l * K/64, (l + 1) * K/64).
-template <int K>
-__global__ __launch_bounds__(256) void wino88i_slice_kernel(const double* __restrict__ src, int n, int slab_rows,
+template <int K, class T, int D>
+__global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict__ src, int n, int slab_rows,
                                                             int nslab, int8_t* __restrict__ dst,
                                                             int* __restrict__ ex) {
     static_assert(K == 256 || K == 512, "rows of 256 or 512 channels");
@@ -76,20 +86,19 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const double* __rest
     if (gw >= n * nslab) return;  // whole waves
     const int x = gw / n, r = gw % n;
     const size_t row = (size_t)x * slab_rows + r;
-    const double* s = src + row * K + lane * CPL;
-    double v[CPL];
+    const T* s = src + row * K + lane * CPL;
+    T v[CPL];
 #pragma unroll
-    for (int i = 0; i < CPL; i += 2) {
-        const f64x2 p = *(const f64x2*)(s + i);
-        v[i] = p[0];
-        v[i + 1] = p[1];
-    }
-    // the high words of |v| order like |v|: their max carries the row's largest biased exponent E,
-    // and every |v| < 2^(E - 1022)
+    for (int i = 0; i < CPL; ++i) v[i] = s[i];
+    // the (high) words of |v| order like |v|: their max carries the row's largest exponent
     unsigned m = 0;
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
-        const unsigned hw = (unsigned)(__double_as_longlong(v[i]) >> 32) & 0x7fffffffu;
+        unsigned hw;
+        if constexpr (sizeof(T) == 8)
+            hw = (unsigned)(__double_as_longlong(v[i]) >> 32) & 0x7fffffffu;
+        else
+            hw = __float_as_uint(v[i]) & 0x7fffffffu;
         m = hw > m ? hw : m;
     }
 #pragma unroll
@@ -97,20 +106,20 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const double* __rest
         const unsigned t = (unsigned)__shfl_xor((int)m, o, 64);
         m = t > m ? t : m;
     }
-    const int e = i8_row_exponent(m);
+    const int e = sizeof(T) == 8 ? i8_row_exponent(m) : i8_row_exponent_f32(m);
     if (lane == 0) ex[row] = e;
-    unsigned long long pk[kI8Digits] = {};
+    unsigned long long pk[D] = {};
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
-        int dg[kI8Digits];
-        i8_digits(v[i], e, dg);
+        int dg[D];
+        i8_digits<D>(v[i], e, dg);
 #pragma unroll
-        for (int d = 0; d < kI8Digits; ++d) pk[d] |= (unsigned long long)(unsigned char)(signed char)dg[d] << (8 * i);
+        for (int d = 0; d < D; ++d) pk[d] |= (unsigned long long)(unsigned char)(signed char)dg[d] << (8 * i);
     }
     const int c = lane * CPL, kc = c / 32;
-    int8_t* o = dst + ((((size_t)x * (K / 32) + kc) * kI8Digits) * slab_rows + r) * 32 + (c % 32);
+    int8_t* o = dst + ((((size_t)x * (K / 32) + kc) * D) * slab_rows + r) * 32 + (c % 32);
 #pragma unroll
-    for (int d = 0; d < kI8Digits; ++d) {
+    for (int d = 0; d < D; ++d) {
         int8_t* od = o + (size_t)d * slab_rows * 32;
         if constexpr (CPL == 8)
             *(unsigned long long*)od = pk[d];
@@ -129,15 +138,16 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const double* __rest
 // The LDS image is linear; the two 16-byte halves of a row are swapped when
 // bit 3 of the row is set (on the global source address), so each ds_read_b128
 // lane group reads 16 distinct 4-bank groups.
+template <int D>
 struct Wino88iTile {
     static constexpr int WR = 4, WC = 2, MT = 1, NT = 2;
     static constexpr int THREADS = WR * WC * 64;
     static constexpr int WM = WR * MT * 32, WN = WC * NT * 32;  // 128 x 128
     static constexpr int PLANE = 128 * 32;                      // bytes of one digit plane of a tile
-    static constexpr int STAGE = 2 * kI8Digits * PLANE;         // A planes then B planes: 40 KiB
+    static constexpr int STAGE = 2 * D * PLANE;                 // A planes then B planes: 8 D KiB
     static constexpr int NBUF = 3;
     static constexpr size_t BYTES = (size_t)NBUF * STAGE;
-    static constexpr int GL = STAGE / 1024 / (THREADS / 64);    // global_load_lds per wave and stage
+    static constexpr int GL = STAGE / 1024 / (THREADS / 64);    // global_load_lds per wave and stage (= D)
 };
 
 __device__ inline int i8_lds_half(int row, int h) { return 16 * (h ^ ((row >> 3) & 1)); }
@@ -145,17 +155,18 @@ __device__ inline int i8_lds_half(int row, int h) { return 16 * (h ^ ((row >> 3)
 // M[xi] (fp64 [xi][stride rows][cout]) = V[xi] x U[xi]^T from the digits (see the header comment).
 // V8: planes [xi][K/32][5][stride][32], U8: [xi][K/32][5][cout][32]. XCD-aware tile order as kv_wino.h's
 // wino_gemm_kernel.
-template <int K, int S, bool SPREAD = true>
+template <int K, int S, bool SPREAD = true, class OutT = double>
 __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restrict__ V8,
                                                             const int* __restrict__ ev,
                                                             const int8_t* __restrict__ U8,
                                                             const int* __restrict__ eu,
-                                                            double* __restrict__ M, int rows, int cout,
+                                                            OutT* __restrict__ M, int rows, int cout,
                                                             int stride) {
-    using T = Wino88iTile;
+    constexpr int kI8Digits = S;  // digit planes per chunk = the levels kept
+    using T = Wino88iTile<S>;
     constexpr int MT = T::MT, NT = T::NT, WM = T::WM, WN = T::WN, GL = T::GL;
     constexpr int NK = K / 32;
-    static_assert(S >= 1 && S <= kI8Digits && GL * (T::THREADS / 64) * 1024 == T::STAGE, "stage split");
+    static_assert(GL == S && GL * (T::THREADS / 64) * 1024 == T::STAGE, "stage split");
 
     extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8[];
     char* const L0 = (char*)lds_i8;
@@ -170,18 +181,18 @@ __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restr
     const int n_base = (idx % CT) * WN;
     const int r_base = ((idx / CT) % RT) * WM;
 
-    // the GL pieces per stage of this wave: piece q = wave * GL + g covers operand q / 20 (V, U: the
-    // same for all of a wave's pieces), digit (q % 20) / 4, rows 32 (q % 4) .. +31 of the tile; lane l
+    // the GL pieces per stage of this wave: piece q = wave * GL + g covers operand q / 4S (V, U: the
+    // same for all of a wave's pieces), digit (q % 4S) / 4, rows 32 (q % 4) .. +31 of the tile; lane l
     // fills LDS row 32 (q % 4) + l / 2, half l & 1 (bit 3 of that row is bit 4 of l). Everything but the
     // lane's offset is wave-uniform.
-    const int op = (wave * GL) / 20;
+    const int op = (wave * GL) / (4 * S);
     const size_t rstride = op ? (size_t)cout : (size_t)stride;
     const int8_t* gbase = op ? U8 + (((size_t)xi * NK) * kI8Digits * cout + n_base) * 32
                              : V8 + (((size_t)xi * NK) * kI8Digits * stride + r_base) * 32;
     const size_t sstep = (size_t)kI8Digits * rstride * 32;  // the next 32-k chunk
     const int lane_off = (lane >> 1) * 32 + 16 * ((lane & 1) ^ ((lane >> 4) & 1));
     auto issue1 = [&](int g, int kt, int buf) {  // this wave's piece g of stage kt
-        const int q = wave * GL + g, d = (q % 20) / 4, rg = q % 4;
+        const int q = wave * GL + g, d = (q % (4 * S)) / 4, rg = q % 4;
         __builtin_amdgcn_global_load_lds(
             (const void*)(gbase + kt * sstep + ((size_t)d * rstride + rg * 32) * 32 + lane_off),
             (__attribute__((address_space(3))) void*)(L0 + buf * T::STAGE + op * kI8Digits * T::PLANE +
@@ -259,7 +270,7 @@ __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restr
             double m = (double)acc[S - 1][0][nt][r];
 #pragma unroll
             for (int l = S - 2; l >= 0; --l) m = __builtin_fma(m, 0.0078125, (double)acc[l][0][nt][r]);  // exact
-            M[((size_t)xi * stride + r_base + wm * 32 + row) * cout + col] = ldexp(m, evx[row] + ec);
+            M[((size_t)xi * stride + r_base + wm * 32 + row) * cout + col] = (OutT)ldexp(m, evx[row] + ec);
         }
     }
 }
@@ -366,10 +377,104 @@ __global__ __launch_bounds__(256) void wino88i_in_kernel(const float* __restrict
         for (int bb = 0; bb < 10; ++bb) {
             const int xi = a * 10 + bb;
             int dg[kI8Digits];
-            i8_digits(o[bb], exs[w][xi], dg);
+            i8_digits<kI8Digits>(o[bb], exs[w][xi], dg);
             int8_t* dst = V8n + ((((size_t)xi * (C / 32) + kc) * kI8Digits) * rows + b) * 32 + (lane & 31);
 #pragma unroll
             for (int d = 0; d < kI8Digits; ++d) dst[(size_t)d * rows * 32] = (int8_t)dg[d];
+        }
+    }
+}
+
+// ---- the fp32 Winograd domain with int8-digit GEMMs (KV_PATH_WINO88_I8F32) ----
+// The fp32 F(8x8) tower's arithmetic (kv_wino88.h: fp32 U rounded once from fp64, fp32 transforms,
+// fp32 M and activations) with each GEMM taken from 4 int8 digits per value: the product of the
+// 28-bit truncated rows is exact (int32 levels, fp64 combine) and rounded to fp32 once, where the
+// fp32 MFMA GEMM rounds after every product. 10 int8 MFMAs per point product against one fp32 one at
+// 1/32 the rate. The kernels mirror the fp64-domain pair above.
+
+// output transform (fp32) + BN (+ residual) + ReLU -> Y, the next V rows reduced to each point's
+// max |V| over the workgroup's 128 channels -> atomicMax into evmax[xi][board] (float bits)
+template <bool RESID>
+__global__ __launch_bounds__(256) void wino88i_outmax32_kernel(const float* __restrict__ M, int rows,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ shift, const float* resid,
+                                                               float* Y, unsigned* __restrict__ evmax) {
+    __shared__ unsigned red[4][2][5][16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+    const int c = blockIdx.x * 128 + w * 32 + (lane & 31), b = blockIdx.y;
+    float t2[10][4];
+    {
+        float x2[4][8];
+        wino88_out_plane_half<RESID, true>(M, rows, b, c, h, scale[c], shift[c], resid, Y, x2);
+        wino88_input_cols(x2, h, t2);
+    }
+#pragma unroll
+    for (int aa = 0; aa < 5; ++aa) {
+        float o[10];
+        wino88_input_row(t2, h, aa, o);
+        unsigned v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = j < 10 ? __float_as_uint(o[j]) & 0x7fffffffu : 0u;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {  // halving over offsets 8, 4, 2, 1: lane keeps index lane & 15
+            const int off = 8 >> st;
+            const bool up = (lane & off) != 0;
+#pragma unroll
+            for (int i = 0; i < off; ++i) {
+                const unsigned mine = up ? v[off + i] : v[i];
+                const unsigned other = (unsigned)__shfl_xor((int)(up ? v[i] : v[off + i]), off, 64);
+                v[i] = mine > other ? mine : other;
+            }
+        }
+        const unsigned o16 = (unsigned)__shfl_xor((int)v[0], 16, 64);
+        const unsigned m = v[0] > o16 ? v[0] : o16;
+        if ((lane & 16) == 0 && (lane & 15) < 10) red[w][h][aa][lane & 15] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x < 100) {
+        const int xi = threadIdx.x, a = xi / 10, bb = xi % 10, hh = a / 5, aa = a % 5;
+        unsigned m = 0;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) m = red[ww][hh][aa][bb] > m ? red[ww][hh][aa][bb] : m;
+        if (m) atomicMax(evmax + (size_t)xi * rows + b, m);
+    }
+}
+
+// the input transform (fp32) of Y and its 4 digits (layout and workgroup shape of wino88i_in_kernel)
+__global__ __launch_bounds__(256) void wino88i_in32_kernel(const float* __restrict__ X, int rows,
+                                                           const unsigned* __restrict__ evmax,
+                                                           int8_t* __restrict__ V8n, int* __restrict__ ex) {
+    constexpr int C = 512, D = kI8DigitsF32;
+    __shared__ int exs[4][100];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+    const int kc = blockIdx.x, c = kc * 32 + (lane & 31), b = blockIdx.y * 4 + w;
+    for (int i = threadIdx.x; i < 400; i += 256) {
+        const int bw = i / 100, xi = i % 100, bb = blockIdx.y * 4 + bw;
+        const int e = i8_row_exponent_f32(evmax[(size_t)xi * rows + bb]);
+        exs[bw][xi] = e;
+        if (kc == 0) ex[(size_t)xi * rows + bb] = e;
+    }
+    float x2[4][8];
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x2[ii][j] = X[((size_t)b * 64 + (4 * h + ii) * 8 + j) * C + c];
+    float t2[10][4];
+    wino88_input_cols(x2, h, t2);
+    __syncthreads();
+#pragma unroll
+    for (int aa = 0; aa < 5; ++aa) {
+        float o[10];
+        wino88_input_row(t2, h, aa, o);
+        const int a = 5 * h + aa;
+#pragma unroll
+        for (int bb = 0; bb < 10; ++bb) {
+            const int xi = a * 10 + bb;
+            int dg[D];
+            i8_digits<D>(o[bb], exs[w][xi], dg);
+            int8_t* dst = V8n + ((((size_t)xi * (C / 32) + kc) * D) * rows + b) * 32 + (lane & 31);
+#pragma unroll
+            for (int d = 0; d < D; ++d) dst[(size_t)d * rows * 32] = (int8_t)dg[d];
         }
     }
 }

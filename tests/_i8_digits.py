@@ -16,11 +16,11 @@ def row_exponents(a):
     return np.where(m > 0, (m >> np.uint32(20)).astype(np.int64) - 1022 + bump, 0)
 
 
-def split(a, e):
-    """a [..., K], e [...] -> digits [DIGITS][..., K] int8 (t = 128 a 2^-e; q = rint(t); t = 128 (t - q))."""
+def split(a, e, digits=DIGITS):
+    """a [..., K], e [...] -> digits [digits][..., K] int8 (t = 128 a 2^-e; q = rint(t); t = 128 (t - q))."""
     t = np.ldexp(a, (7 - e[..., None]).astype(np.int32))
     out = []
-    for _ in range(DIGITS):
+    for _ in range(digits):
         q = np.rint(t)
         out.append(q.astype(np.int8))
         t = (t - q) * 128.0
@@ -33,19 +33,22 @@ def pack(d):
     return d.reshape(D, X, R, K // 32, 32).transpose(1, 3, 0, 2, 4).copy()
 
 
-def gemm(V, U):
-    """V [X][R][K], U [X][C][K] fp64 -> (M [X][R][C], V digits [DIGITS][X][R][K], V exponents [X][R])."""
+def gemm(V, U, digits=DIGITS):
+    """V [X][R][K], U [X][C][K] fp64 -> (M [X][R][C], V digits [digits][X][R][K], V exponents [X][R]).
+    digits 5: fp64 M (KV_PREC_I8X5); 4: M rounded to fp32 once (KV_ALGO_WINOGRAD88_I8), returned widened."""
     ev, eu = row_exponents(V), row_exponents(U)
-    dv, du = split(V, ev), split(U, eu)
+    dv, du = split(V, ev, digits), split(U, eu, digits)
     fv, fu = dv.astype(np.float64), du.astype(np.float64)
     lev = []
-    for l in range(LEVELS):  # exact: every partial sum is an integer below 2^31
+    for l in range(digits):  # exact: every partial sum is an integer below 2^31
         acc = np.zeros((V.shape[0], V.shape[1], U.shape[1]))
         for i in range(l + 1):
             acc += np.matmul(fv[i], np.swapaxes(fu[l - i], 1, 2))
         lev.append(acc)
-    m = lev[LEVELS - 1]
-    for l in range(LEVELS - 2, -1, -1):
+    m = lev[digits - 1]
+    for l in range(digits - 2, -1, -1):
         m = m * 0.0078125 + lev[l]  # exact, as the kernel's fma
     M = np.ldexp(m, (ev[:, :, None] + eu[:, None, :] - 14).astype(np.int32))
+    if digits == 4:
+        M = M.astype(np.float32).astype(np.float64)
     return M, dv, ev

@@ -39,7 +39,7 @@ def _f64(sd, planes):
     return p.numpy(), v.numpy()
 
 
-def accuracy_table(sd, planes, algos=("direct", "winograd48", "winograd88", "i8x5", "f64w", "auto")):
+def accuracy_table(sd, planes, algos=("direct", "winograd48", "winograd88", "winograd88i8", "i8x5", "f64w", "auto")):
     """{name: (max |dlogit|, max |dvalue|) vs float64} for the reference's fp32
     forward ("ref32") and each HIP algorithm, plus each algorithm against ref32."""
     from oracle import torch_ref
@@ -82,8 +82,8 @@ def test_auto_within_tolerance_of_reference(variant):
     for k in ("auto", "auto<=16", "f64w", "i8x5"):
         _, _, dpr, dvr = tab[k]
         assert dpr <= TOL_P and dvr <= TOL_V, (k, dpr, dvr)
-    if variant in ("bn",):  # random-init magnitudes: the fp32 F(8x8) tower passes and is chosen
-        assert calib["path_large"] == "winograd88" and calib["path_small"] == "direct"
+    if variant in ("bn",):  # random-init magnitudes: the fp32 F(8x8) tower on int8 digits passes and is chosen
+        assert calib["path_large"] == "winograd88_i8f32" and calib["path_small"] == "direct"
     if variant == "stress":  # trained magnitudes: no fp32 Winograd tower passes; the int8-digit one does
         assert calib["path_large"] == "winograd88_i8"
 
@@ -128,13 +128,14 @@ def test_trained_weights_table():
 @pytest.mark.parametrize("variant", ["init", "peaked", "stress"])
 def test_calibration_choice_is_consistent(variant):
     """kv_net_calibration: each candidate run was measured, the chosen path is the
-    first in F(8x8) -> F(4x8) -> F(8x8) int8 digits -> F(8x8) fp64 order within the budget, and the
+    first in F(8x8) fp32 on int8 digits -> F(8x8) -> F(4x8) -> F(8x8) fp64 domain on int8 digits -> F(8x8)
+    fp64 order within the budget, and the
     engine reports the same choice for the same weights."""
     from knightvision_amd.engine import SelfPlayEngine
     sd = synthetic_state_dict(42, variant)
     c = _net(sd, "auto").kv_net(0).calibration()
     assert c["calibrated"] and c["n_boards"] == 64
-    order = ["winograd88", "winograd48", "winograd88_i8", "winograd88_f64"]
+    order = ["winograd88_i8f32", "winograd88", "winograd48", "winograd88_i8", "winograd88_f64"]
     ok = {k: c["err_logit"][k] <= c["tol_logit"] and c["err_value"][k] <= c["tol_value"] for k in c["err_logit"]}
     first = next(k for k in order if k == "winograd88_f64" or ok.get(k))
     assert c["path_large"] == first, c

@@ -15,12 +15,13 @@ TOL_P, TOL_V = 1e-4, 1e-5
 
 # (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x8,3x3) / fp32 Winograd F(8x8,3x3) / fp32 auto
 # (the calibrated choice every product caller runs) / f16x3 Winograd F(4x8) / F(8x8) with the fp64 Winograd domain
-# on fp64 MFMA / the same domain with the GEMMs on int8 digits
-MODES = [("fp32", "direct"), ("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "auto"),
-         ("f16x3", "winograd48"), ("f64w", "auto"), ("i8x5", "auto")]
+# on fp64 MFMA / the same domain with the GEMMs on int8 digits; ("fp32", "winograd88i8") the fp32 F(8x8) tower with
+# its GEMMs on int8 digits
+MODES = [("fp32", "direct"), ("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "winograd88i8"),
+         ("fp32", "auto"), ("f16x3", "winograd48"), ("f64w", "auto"), ("i8x5", "auto")]
 # the explicit fp32 / f16x3 Winograd towers are outside the tolerance at trained magnitudes ("stress": 1.2e-3 to
 # 3.6e-3); AUTO measures that at load time and runs the fp64 Winograd domain instead (test_nn_accuracy_gpu.py)
-UNGUARDED = {("fp32", "winograd48"), ("fp32", "winograd88"), ("f16x3", "winograd48")}
+UNGUARDED = {("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "winograd88i8"), ("f16x3", "winograd48")}
 
 
 def _net(variant, precision="fp32", algo="auto"):
@@ -93,7 +94,7 @@ def test_batch_invariance(precision):
     assert float((p_16 - p_all[:16]).abs().max()) < 1e-4
 
 
-@pytest.mark.parametrize("precision", ["fp32", "f64w", "i8x5"])
+@pytest.mark.parametrize("precision", ["fp32", "f64w", "i8x5", "fp32-i8"])
 def test_wino88_batch_invariance(precision):
     """F(8x8) (one row per board): a board's outputs are the same bits at 20
     boards (padded to 32: 32-row GEMM tiles, k-tiles of 32), 80 / 96 (padded to
@@ -105,7 +106,8 @@ def test_wino88_batch_invariance(precision):
     rng = np.random.default_rng(88)
     codes = rng.integers(0, 13, size=(512, 64)) * (rng.random((512, 64)) < 0.4)
     planes = torch.from_numpy(codes_to_planes(codes)).cuda()
-    m = _net("peaked", "fp32", "winograd88") if precision == "fp32" else _net("peaked", precision, "auto")
+    m = (_net("peaked", "fp32", "winograd88") if precision == "fp32" else
+         _net("peaked", "fp32", "winograd88i8") if precision == "fp32-i8" else _net("peaked", precision, "auto"))
     p_l, v_l = m(planes)
     for lo, hi in ((0, 40), (20, 40), (0, 300), (0, 96), (16, 96)) + (((0, 1), (5, 8)) if precision != "fp32" else ()):
         p, v = m(planes[lo:hi])

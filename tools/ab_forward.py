@@ -2,7 +2,7 @@
 seeded boards, and the outputs saved for a bit-for-bit comparison of builds.
 
     KV_LIB_PATH=knightvision_amd/libkv_b.so python tools/ab_forward.py TAG 2048 256
-    (KV_PREC=f64w: the fp64 Winograd domain)
+    (KV_PREC=f64w: the fp64 Winograd domain; KV_ALGO=winograd88 etc.: an fp32 conv algorithm)
 """
 import os
 import sys
@@ -15,7 +15,7 @@ from knightvision_amd.model import ChessNet  # noqa: E402
 from knightvision_amd.weights import synthetic_state_dict  # noqa: E402
 
 tag = sys.argv[1]
-m = ChessNet(precision=os.environ.get("KV_PREC", "fp32"))
+m = ChessNet(precision=os.environ.get("KV_PREC", "fp32"), algo=os.environ.get("KV_ALGO", "auto"))
 m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synthetic_state_dict(42, "bn").items()})
 m.eval()
 net = m.kv_net(0)

@@ -10,7 +10,9 @@ digits d_i = round(r * 2^(7(i+1))) clamped to [-127, 127], remainder r carried
 with i + j <= s - 1 (s(s+1)/2 int8 GEMMs, exact in int32 over K = 512), summed
 per level and scaled back in fp64.
 
-Exponent modes for V: 'row' = exact max over the row's K channels; 'groupN'
+Mode prefix "f32" (e.g. f32row:4): the fp32 Winograd domain (U, V, M and
+the transforms rounded to fp32, as the fp32 F(8x8) tower) with only the GEMM
+from digits. Exponent modes for V: 'row' = exact max over the row's K channels; 'groupN'
 = one exponent per N-channel group; 'bound' = per board, from max |y| of the
 board's activations times the point's transform gain sum|B^T|.
 
@@ -87,14 +89,26 @@ def ozaki_gemm(V, U, s, mode, gain, ymax):
 
 def conv(x, w, s, mode):
     B, _, _, Cin = x.shape
+    f32 = mode.startswith("f32")  # the fp32 Winograd domain: U, V, M and both transforms fp32
+    if f32:
+        mode = mode[3:] or "row"
     U = np.einsum("ak,oikl,bl->abio", G, w, G).reshape(100, Cin, -1).transpose(0, 2, 1)  # [100][Cout][Cin]
     xp = np.zeros((B, 10, 10, Cin))
     xp[:, 1:9, 1:9] = x
-    V = np.einsum("ai,bicq->bacq", BT, xp)
-    V = np.einsum("bj,xajq->xabq", BT, V).reshape(B, 100, Cin)
+    if f32:
+        U = U.astype(F32).astype(np.float64)
+        V = np.einsum("ai,bicq->bacq", BT.astype(F32), xp.astype(F32)).astype(F32)
+        V = np.einsum("bj,xajq->xabq", BT.astype(F32), V).astype(F32).reshape(B, 100, Cin).astype(np.float64)
+    else:
+        V = np.einsum("ai,bicq->bacq", BT, xp)
+        V = np.einsum("bj,xajq->xabq", BT, V).reshape(B, 100, Cin)
     gain = np.outer(np.abs(BT).sum(1), np.abs(BT).sum(1)).reshape(100)
     ymax = np.abs(x).reshape(B, -1).max(1)
     M = ozaki_gemm(V, U, s, mode, gain, ymax).reshape(B, 10, 10, -1)
+    if f32:
+        M = M.astype(F32)
+        Y = np.einsum("ia,bacq->bicq", AT.astype(F32), M).astype(F32)
+        return np.einsum("jc,bicq->bijq", AT.astype(F32), Y).astype(F32).astype(np.float64)
     Y = np.einsum("ia,bacq->bicq", AT, M)
     return np.einsum("jc,bicq->bijq", AT, Y)
 
