@@ -1180,49 +1180,40 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     return KV_OK;
 }
 
-// ---- the fp32 domain on int8 digits (KV_PATH_WINO88_I8F32): the fp32 F(8x8) transforms, 4 digits ----
-template <bool RESID>
-static int launch_wino88i32_out(kv_net* net, int l, const float* M, int nb, int stride, const float* resid, float* Y,
-                                hipStream_t st) {
-    const float* W = net->w;
-    unsigned* evmax = (unsigned*)net->evmax8;
-    KV_REQUIRE(nb % 4 == 0, KV_EINVAL, "wino88i32: %d boards (a multiple of 4)", nb);
-    KV_HIP(hipMemsetAsync(evmax, 0, (size_t)kv::W88_XI * stride * sizeof(unsigned), st));
-    hipLaunchKernelGGL((kv::wino88i_outmax32_kernel<RESID>), dim3(512 / 128, nb), dim3(256), 0, st, M, stride,
-                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, evmax);
-    hipLaunchKernelGGL(kv::wino88i_in32_kernel, dim3(512 / 32, nb / 4), dim3(256), 0, st, Y, stride,
-                       (const unsigned*)evmax, net->V8, net->ev8);
-    KV_HIP(hipGetLastError());
-    return KV_OK;
+// ---- the fp32 domain on int8 digits (KV_PATH_WINO88_I8F32): the fp32 F(8x8) tower's own fused output /
+// input transform kernels (wino88_out_kernel writes the next fp32 V), then the slice kernel turns each V
+// row into 4 digits under its row exponent (it reads the whole row, so the exponent needs no second pass
+// over the activations) ----
+static int wino88i32_gemm_layer(kv_net* net, int l, int K, int rows, int stride, hipStream_t st) {
+    constexpr int D = kv::kI8DigitsF32;
+    const float* Vsrc = K == 256 ? (const float*)net->V256 : (const float*)net->V;
+    float* M = (float*)net->Mw;
+    int rc = K == 256 ? launch_wino88i_slice<256, D>(Vsrc, rows, stride, kv::W88_XI, net->V8, net->ev8, st)
+                      : launch_wino88i_slice<512, D>(Vsrc, rows, stride, kv::W88_XI, net->V8, net->ev8, st);
+    if (rc) return rc;
+    const int8_t* U = net->U88i32 + net->uoff88[l] * D;
+    const int* eu = net->eu88i32 + net->euoff[l];
+    return K == 256 ? launch_wino88i_gemm<256, D>(net->V8, net->ev8, U, eu, M, rows, stride, st)
+                    : launch_wino88i_gemm<512, D>(net->V8, net->ev8, U, eu, M, rows, stride, st);
 }
 
 static int wino88i32_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
-    constexpr int D = kv::kI8DigitsF32;
     const int rows = nb, stride = rows;
-    float* M = (float*)net->Mw;
-    const int8_t* U = net->U88i32;
+    float* V = (float*)net->V;
+    const float* M = (const float*)net->Mw;
     int rc;
-    // conv2: the stem wrote the fp32 V (256 channels); its digits by the slice kernel
-    if ((rc = launch_wino88i_slice<256, D>((const float*)net->V256, rows, stride, kv::W88_XI, net->V8, net->ev8, st)))
-        return rc;
-    if ((rc = launch_wino88i_gemm<256, D>(net->V8, net->ev8, U + net->uoff88[1] * D, net->eu88i32 + net->euoff[1], M,
-                                          rows, stride, st)))
-        return rc;
-    if ((rc = launch_wino88i32_out<false>(net, 1, M, nb, stride, nullptr, net->X, st))) return rc;
+    if ((rc = wino88i32_gemm_layer(net, 1, 256, rows, stride, st))) return rc;
+    if ((rc = launch_wino88_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st))) return rc;
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
     for (int r = 0; r < 5; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         const bool m = mark && r == 2;
         if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-        if ((rc = launch_wino88i_gemm<512, D>(net->V8, net->ev8, U + net->uoff88[l1] * D,
-                                              net->eu88i32 + net->euoff[l1], M, rows, stride, st)))
-            return rc;
+        if ((rc = wino88i32_gemm_layer(net, l1, 512, rows, stride, st))) return rc;
         if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
-        if ((rc = launch_wino88i32_out<false>(net, l1, M, nb, stride, nullptr, net->T, st))) return rc;
-        if ((rc = launch_wino88i_gemm<512, D>(net->V8, net->ev8, U + net->uoff88[l2] * D,
-                                              net->eu88i32 + net->euoff[l2], M, rows, stride, st)))
-            return rc;
-        rc = r < 4 ? launch_wino88i32_out<true>(net, l2, M, nb, stride, net->X, net->X, st)
+        if ((rc = launch_wino88_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st))) return rc;
+        if ((rc = wino88i32_gemm_layer(net, l2, 512, rows, stride, st))) return rc;
+        rc = r < 4 ? launch_wino88_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
                    : launch_wino88_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
         if (rc) return rc;
     }

@@ -386,97 +386,16 @@ __global__ __launch_bounds__(256) void wino88i_in_kernel(const float* __restrict
 }
 
 // ---- the fp32 Winograd domain with int8-digit GEMMs (KV_PATH_WINO88_I8F32) ----
-// The fp32 F(8x8) tower's arithmetic (kv_wino88.h: fp32 U rounded once from fp64, fp32 transforms,
-// fp32 M and activations) with each GEMM taken from 4 int8 digits per value: the product of the
+// The fp32 F(8x8) tower's arithmetic (kv_wino88.h: fp32 transforms, V, M and activations; U as
+// 4 digits of the fp64 U) with each GEMM taken from 4 int8 digits per value: the product of the
 // 28-bit truncated rows is exact (int32 levels, fp64 combine) and rounded to fp32 once, where the
 // fp32 MFMA GEMM rounds after every product. 10 int8 MFMAs per point product against one fp32 one at
-// 1/32 the rate. The kernels mirror the fp64-domain pair above.
+// 1/32 the rate.
 
-// output transform (fp32) + BN (+ residual) + ReLU -> Y, the next V rows reduced to each point's
-// max |V| over the workgroup's 128 channels -> atomicMax into evmax[xi][board] (float bits)
-template <bool RESID>
-__global__ __launch_bounds__(256) void wino88i_outmax32_kernel(const float* __restrict__ M, int rows,
-                                                               const float* __restrict__ scale,
-                                                               const float* __restrict__ shift, const float* resid,
-                                                               float* Y, unsigned* __restrict__ evmax) {
-    __shared__ unsigned red[4][2][5][16];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
-    const int c = blockIdx.x * 128 + w * 32 + (lane & 31), b = blockIdx.y;
-    float t2[10][4];
-    {
-        float x2[4][8];
-        wino88_out_plane_half<RESID, true>(M, rows, b, c, h, scale[c], shift[c], resid, Y, x2);
-        wino88_input_cols(x2, h, t2);
-    }
-#pragma unroll
-    for (int aa = 0; aa < 5; ++aa) {
-        float o[10];
-        wino88_input_row(t2, h, aa, o);
-        unsigned v[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = j < 10 ? __float_as_uint(o[j]) & 0x7fffffffu : 0u;
-#pragma unroll
-        for (int st = 0; st < 4; ++st) {  // halving over offsets 8, 4, 2, 1: lane keeps index lane & 15
-            const int off = 8 >> st;
-            const bool up = (lane & off) != 0;
-#pragma unroll
-            for (int i = 0; i < off; ++i) {
-                const unsigned mine = up ? v[off + i] : v[i];
-                const unsigned other = (unsigned)__shfl_xor((int)(up ? v[i] : v[off + i]), off, 64);
-                v[i] = mine > other ? mine : other;
-            }
-        }
-        const unsigned o16 = (unsigned)__shfl_xor((int)v[0], 16, 64);
-        const unsigned m = v[0] > o16 ? v[0] : o16;
-        if ((lane & 16) == 0 && (lane & 15) < 10) red[w][h][aa][lane & 15] = m;
-    }
-    __syncthreads();
-    if (threadIdx.x < 100) {
-        const int xi = threadIdx.x, a = xi / 10, bb = xi % 10, hh = a / 5, aa = a % 5;
-        unsigned m = 0;
-#pragma unroll
-        for (int ww = 0; ww < 4; ++ww) m = red[ww][hh][aa][bb] > m ? red[ww][hh][aa][bb] : m;
-        if (m) atomicMax(evmax + (size_t)xi * rows + b, m);
-    }
-}
-
-// the input transform (fp32) of Y and its 4 digits (layout and workgroup shape of wino88i_in_kernel)
-__global__ __launch_bounds__(256) void wino88i_in32_kernel(const float* __restrict__ X, int rows,
-                                                           const unsigned* __restrict__ evmax,
-                                                           int8_t* __restrict__ V8n, int* __restrict__ ex) {
-    constexpr int C = 512, D = kI8DigitsF32;
-    __shared__ int exs[4][100];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
-    const int kc = blockIdx.x, c = kc * 32 + (lane & 31), b = blockIdx.y * 4 + w;
-    for (int i = threadIdx.x; i < 400; i += 256) {
-        const int bw = i / 100, xi = i % 100, bb = blockIdx.y * 4 + bw;
-        const int e = i8_row_exponent_f32(evmax[(size_t)xi * rows + bb]);
-        exs[bw][xi] = e;
-        if (kc == 0) ex[(size_t)xi * rows + bb] = e;
-    }
-    float x2[4][8];
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) x2[ii][j] = X[((size_t)b * 64 + (4 * h + ii) * 8 + j) * C + c];
-    float t2[10][4];
-    wino88_input_cols(x2, h, t2);
-    __syncthreads();
-#pragma unroll
-    for (int aa = 0; aa < 5; ++aa) {
-        float o[10];
-        wino88_input_row(t2, h, aa, o);
-        const int a = 5 * h + aa;
-#pragma unroll
-        for (int bb = 0; bb < 10; ++bb) {
-            const int xi = a * 10 + bb;
-            int dg[D];
-            i8_digits<D>(o[bb], exs[w][xi], dg);
-            int8_t* dst = V8n + ((((size_t)xi * (C / 32) + kc) * D) * rows + b) * 32 + (lane & 31);
-#pragma unroll
-            for (int d = 0; d < D; ++d) dst[(size_t)d * rows * 32] = (int8_t)dg[d];
-        }
-    }
-}
+// The fp32 tower's own fused output / input transform kernels (kv_wino88.h) write the next fp32 V,
+// and wino88i_slice_kernel<K, float, 4> turns it into digits. (An output kernel computing only the
+// row maxima plus a second input-transform pass writing the digits, mirroring the fp64 pair above, ran
+// 294-356 + 220 us per layer at 2,048 boards against ~180 + the slice's time:
+// profiles/r04_i8f32_outmax_form.log.)
 
 }  // namespace kv
