@@ -590,6 +590,9 @@ def main():
             "roofline": {"bound": "mfma",
                          "kernel": kname + kdesc,
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "operations": ("int8 multiply-adds of the digit products (2 operations each) against the "
+                                        "dense int8 MFMA peak" if path in I8_DIGIT_PRODUCTS else
+                                        "fp64 MFMA FLOP" if path == 3 else "fp32 MFMA FLOP"),
                          "frac": (achieved / peak) if achieved else None,
                          "traffic": traffic, "traffic_source": ("profiles/" + traffic_src) if traffic_src else None,
                          "avg_launch_ms": conv_ms, "boards_per_launch": bpl,

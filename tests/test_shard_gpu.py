@@ -187,8 +187,10 @@ def test_bench_json_line_contract():
         assert k in d["roofline"], k
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in d["cpu_baseline"], k
-    c = d["calibration"]  # the conv paths the run used, chosen by the load-time calibration (random-init: F(8x8))
-    assert c["calibrated"] and c["path_large"] == "winograd88" and c["path_small"] == "direct"
+    c = d["calibration"]  # the conv paths the run used, chosen by the load-time calibration (random-init: the
+    # fp32 F(8x8) tower on int8-digit GEMMs)
+    assert c["calibrated"] and c["path_large"] == "winograd88_i8f32" and c["path_small"] == "direct"
+    assert d["conv_path"] == "winograd88_i8f32" and d["roofline"]["peak"] == 5000.0  # int8 operations vs the int8 peak
     assert d["trained_weights_path"]["value"] > 0
 
 
