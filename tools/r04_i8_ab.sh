@@ -9,7 +9,7 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 280 --timeout-method threa
     > gpurun_out/r04_i8_exact.log 2>&1
 : > gpurun_out/r04_i8_ab.log
 for e in $AB_ENVS; do
-    env $e KV_PREC=i8x5 timeout -k 10 200 python -u tools/ab_forward.py "$e" 2048 256 128 >> gpurun_out/r04_i8_ab.log 2>&1
+    env $e KV_PREC=${AB_PREC:-i8x5} KV_ALGO=${AB_ALGO:-auto} timeout -k 10 200 python -u tools/ab_forward.py "$e" 2048 256 128 >> gpurun_out/r04_i8_ab.log 2>&1
 done
 cd /tmp && export TMPDIR=/tmp KV_PREC=i8x5
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/r04_i8_prof" -o run -- \
