@@ -309,7 +309,7 @@ def gemm_label(path: int, rows: int, split: int):
                     "Winograd F(8x8,3x3) GEMM layer: two launches, both inside the timed events)")
         return name, desc
     if path == 6:
-        return "wino88i_gemm_kernel<512,4,true,float>", (
+        return "wino88i_gemm_kernel<512,4,true,float,true>", (
             " (residual-tower Winograd F(8x8,3x3) GEMMs of the fp32 tower from 4 int8 digits per value: 10 "
             "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 tiles)")
     if path == 5:

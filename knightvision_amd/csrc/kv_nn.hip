@@ -1097,11 +1097,12 @@ static int wino88d_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 
 // ---- F(8x8) on int8 digits (kv_wino88i.h): the fp64 tower's transforms, V64 sliced into digits
 // before each GEMM ----
+// (4 digits: the fp32 domain's row-line layout)
 template <int K, int D = kv::kI8Digits, class T>
 static int launch_wino88i_slice(const T* src, int n, int slab_rows, int nslab, int8_t* dst, int* ex,
                                 hipStream_t st) {
     const int waves = n * nslab;
-    hipLaunchKernelGGL((kv::wino88i_slice_kernel<K, T, D>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st,
+    hipLaunchKernelGGL((kv::wino88i_slice_kernel<K, T, D, D == kv::kI8DigitsF32>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st,
                        src, n, slab_rows, nslab, dst, ex);
     KV_HIP(hipGetLastError());
     return KV_OK;
@@ -1121,7 +1122,8 @@ template <int K, int D = kv::kI8Digits, class OutT = double>
 static int launch_wino88i_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, OutT* M, int rows,
                                int stride, hipStream_t st) {
     using T = kv::Wino88iTile<D>;
-    auto kern = i8_spread() ? kv::wino88i_gemm_kernel<K, D, true, OutT> : kv::wino88i_gemm_kernel<K, D, false, OutT>;
+    constexpr bool RL = D == kv::kI8DigitsF32;  // 4 digits: row lines
+    auto kern = i8_spread() ? kv::wino88i_gemm_kernel<K, D, true, OutT, RL> : kv::wino88i_gemm_kernel<K, D, false, OutT, RL>;
     KV_HIP(lds_opt_in((const void*)kern, (int)T::BYTES));
     const int nwg = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
     KV_REQUIRE(rows % T::WM == 0 && stride % T::WM == 0 && nwg % 8 == 0, KV_EINVAL,
@@ -1182,13 +1184,13 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 
 // ---- the fp32 domain on int8 digits (KV_PATH_WINO88_I8F32): the fp32 F(8x8) tower's own fused output /
 // input transform kernels (wino88_out_kernel writes the next fp32 V), then the slice kernel turns each V
-// row into 4 digits under its row exponent (it reads the whole row, so the exponent needs no second pass
-// over the activations) ----
-// (mark: the engine's timing hook brackets the GEMM, the dominant kernel, without the slice)
+// row into 4 digits under its row exponent, in the row-line layout (it reads the whole row, so the exponent
+// needs no second pass over the activations) ----
+// (mark: the engine's timing hook brackets the GEMM, the dominant kernel)
 static int wino88i32_gemm_layer(kv_net* net, int l, int K, int rows, int stride, bool mark, hipStream_t st) {
     constexpr int D = kv::kI8DigitsF32;
-    const float* Vsrc = K == 256 ? (const float*)net->V256 : (const float*)net->V;
     float* M = (float*)net->Mw;
+    const float* Vsrc = K == 256 ? (const float*)net->V256 : (const float*)net->V;
     int rc = K == 256 ? launch_wino88i_slice<256, D>(Vsrc, rows, stride, kv::W88_XI, net->V8, net->ev8, st)
                       : launch_wino88i_slice<512, D>(Vsrc, rows, stride, kv::W88_XI, net->V8, net->ev8, st);
     if (rc) return rc;

@@ -74,12 +74,15 @@ __device__ inline void i8_digits(T v, int e, int (&d)[D]) {
 // [32 kc, 32 kc + 32) goes to plane (x, kc, d) of dst -- 32 bytes at
 // (((x * K/32 + kc) * 5 + d) * slab_rows + r) * 32 -- and the exponent to
 // ex[x * slab_rows + r]. One wave per row; lane l holds channels
-// [l * K/64, (l + 1) * K/64).
-template <int K, class T, int D>
+// [l * K/64, (l + 1) * K/64). RL (row lines, 4 digits only): digit d of the
+// 32 channels goes to (((x * K/32 + kc) * slab_rows + r) * 4 + d) * 32 instead
+// -- the 4 digits of one row's chunk are one 128-byte line.
+template <int K, class T, int D, bool RL = false>
 __global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict__ src, int n, int slab_rows,
                                                             int nslab, int8_t* __restrict__ dst,
                                                             int* __restrict__ ex) {
     static_assert(K == 256 || K == 512, "rows of 256 or 512 channels");
+    static_assert(!RL || D == 4, "row lines hold 4 digits");
     constexpr int CPL = K / 64;  // 4 or 8 channels per lane
     const int lane = threadIdx.x & 63;
     const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -117,10 +120,11 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict_
         for (int d = 0; d < D; ++d) pk[d] |= (unsigned long long)(unsigned char)(signed char)dg[d] << (8 * i);
     }
     const int c = lane * CPL, kc = c / 32;
-    int8_t* o = dst + ((((size_t)x * (K / 32) + kc) * D) * slab_rows + r) * 32 + (c % 32);
+    int8_t* o = RL ? dst + (((size_t)x * (K / 32) + kc) * slab_rows + r) * (D * 32) + (c % 32)
+                   : dst + ((((size_t)x * (K / 32) + kc) * D) * slab_rows + r) * 32 + (c % 32);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-        int8_t* od = o + (size_t)d * slab_rows * 32;
+        int8_t* od = o + (size_t)d * (RL ? 32 : slab_rows * 32);
         if constexpr (CPL == 8)
             *(unsigned long long*)od = pk[d];
         else
@@ -152,10 +156,20 @@ struct Wino88iTile {
 
 __device__ inline int i8_lds_half(int row, int h) { return 16 * (h ^ ((row >> 3) & 1)); }
 
+// RL layout in LDS: row r of an operand is its 128-byte line (16-byte chunk c = 2 d + half of digit d),
+// chunk c at position c ^ ((r >> 1) & 7): a ds_read_b128 lane group (rows {0-3, 12-15, 20-27} or {4-11,
+// 16-19, 28-31} of a 32-row block, one chunk) hits 16 distinct 16-byte bank groups -- even rows in the
+// first 128 bytes of the 256-byte bank window, odd rows in the second, 8 distinct positions each. (A
+// chunk-major image with one base + 256 d per digit needs lanes 128 bytes apart in the copy: the GEMM
+// ran 551 us against 523, profiles/r04_i8f32_rowlines_ab.log.)
+__device__ inline int i8_rl_off(int row, int chunk) { return row * 128 + 16 * (chunk ^ ((row >> 1) & 7)); }
+
 // M[xi] (fp64 [xi][stride rows][cout]) = V[xi] x U[xi]^T from the digits (see the header comment).
 // V8: planes [xi][K/32][5][stride][32], U8: [xi][K/32][5][cout][32]. XCD-aware tile order as kv_wino.h's
-// wino_gemm_kernel.
-template <int K, int S, bool SPREAD = true, class OutT = double>
+// wino_gemm_kernel. RL (4 digits): row lines [xi][K/32][stride][4][32] and [xi][K/32][cout][4][32] -- a
+// stage of a tile is one contiguous 16 KiB block per operand, and one workgroup of the fused output
+// kernel (one board) writes whole lines.
+template <int K, int S, bool SPREAD = true, class OutT = double, bool RL = false>
 __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restrict__ V8,
                                                             const int* __restrict__ ev,
                                                             const int8_t* __restrict__ U8,
@@ -167,6 +181,7 @@ __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restr
     constexpr int MT = T::MT, NT = T::NT, WM = T::WM, WN = T::WN, GL = T::GL;
     constexpr int NK = K / 32;
     static_assert(GL == S && GL * (T::THREADS / 64) * 1024 == T::STAGE, "stage split");
+    static_assert(!RL || S == 4, "row lines hold 4 digits");
 
     extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8[];
     char* const L0 = (char*)lds_i8;
@@ -187,12 +202,26 @@ __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restr
     // lane's offset is wave-uniform.
     const int op = (wave * GL) / (4 * S);
     const size_t rstride = op ? (size_t)cout : (size_t)stride;
-    const int8_t* gbase = op ? U8 + (((size_t)xi * NK) * kI8Digits * cout + n_base) * 32
-                             : V8 + (((size_t)xi * NK) * kI8Digits * stride + r_base) * 32;
+    const size_t tbase = RL ? (op ? (size_t)n_base : (size_t)r_base) * 4 : (op ? n_base : r_base);  // RL: 128 B rows
+    const int8_t* gbase = op ? U8 + (((size_t)xi * NK) * kI8Digits * cout + tbase) * 32
+                             : V8 + (((size_t)xi * NK) * kI8Digits * stride + tbase) * 32;
     const size_t sstep = (size_t)kI8Digits * rstride * 32;  // the next 32-k chunk
     const int lane_off = (lane >> 1) * 32 + 16 * ((lane & 1) ^ ((lane >> 4) & 1));
+    // RL: piece q covers operand q / 16, rows 8 (q % 16) .. +7 (1 KiB contiguous in both places); lane l
+    // fills position l & 7 of LDS row 8 (q % 16) + l / 8 from source chunk (l & 7) ^ (row >> 1 & 7)
+    const int rl_off0 = (lane >> 3) * 128 + 16 * ((lane & 7) ^ (lane >> 4));
+    const int rl_off1 = (lane >> 3) * 128 + 16 * ((lane & 7) ^ (lane >> 4) ^ 4);
     auto issue1 = [&](int g, int kt, int buf) {  // this wave's piece g of stage kt
         const int q = wave * GL + g, d = (q % (4 * S)) / 4, rg = q % 4;
+        if constexpr (RL) {
+            const int rg8 = q % 16;
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(gbase + kt * sstep + (size_t)rg8 * 1024 + ((rg8 & 1) ? rl_off1 : rl_off0)),
+                (__attribute__((address_space(3))) void*)(L0 + buf * T::STAGE + op * kI8Digits * T::PLANE +
+                                                          rg8 * 1024),
+                16, 0, 0);
+            return;
+        }
         __builtin_amdgcn_global_load_lds(
             (const void*)(gbase + kt * sstep + ((size_t)d * rstride + rg * 32) * 32 + lane_off),
             (__attribute__((address_space(3))) void*)(L0 + buf * T::STAGE + op * kI8Digits * T::PLANE +
@@ -213,6 +242,15 @@ __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restr
     for (int nt = 0; nt < NT; ++nt) {
         const int bcol = wn * NT * 32 + nt * 32 + lr;
         boff[nt] = kI8Digits * T::PLANE + bcol * 32 + i8_lds_half(bcol, lh);
+    }
+    // RL: the fragment of digit i is chunk 2 i + half of the row's line
+    int aoffr[S], boffr[NT][S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        aoffr[i] = i8_rl_off(arow, 2 * i + lh);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+            boffr[nt][i] = kI8Digits * T::PLANE + i8_rl_off(wn * NT * 32 + nt * 32 + lr, 2 * i + lh);
     }
 
     i32x16_t acc[S][MT][NT];
@@ -239,12 +277,13 @@ __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restr
         // profiles/r04_i8_glds_spread_ab.log)
         i8x16_t a[S];
 #pragma unroll
-        for (int i = 0; i < S; ++i) a[i] = *(const i8x16_t*)(buf + aoff + i * T::PLANE);
+        for (int i = 0; i < S; ++i) a[i] = *(const i8x16_t*)(buf + (RL ? aoffr[i] : aoff + i * T::PLANE));
 #pragma unroll
         for (int j = 0; j < S; ++j) {
             i8x16_t b[NT];
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt) b[nt] = *(const i8x16_t*)(buf + boff[nt] + j * T::PLANE);
+            for (int nt = 0; nt < NT; ++nt)
+                b[nt] = *(const i8x16_t*)(buf + (RL ? boffr[nt][j] : boff[nt] + j * T::PLANE));
 #pragma unroll
             for (int i = 0; i + j < S; ++i)
 #pragma unroll
@@ -392,10 +431,12 @@ __global__ __launch_bounds__(256) void wino88i_in_kernel(const float* __restrict
 // fp32 MFMA GEMM rounds after every product. 10 int8 MFMAs per point product against one fp32 one at
 // 1/32 the rate.
 
-// The fp32 tower's own fused output / input transform kernels (kv_wino88.h) write the next fp32 V,
-// and wino88i_slice_kernel<K, float, 4> turns it into digits. (An output kernel computing only the
-// row maxima plus a second input-transform pass writing the digits, mirroring the fp64 pair above, ran
-// 294-356 + 220 us per layer at 2,048 boards against ~180 + the slice's time:
-// profiles/r04_i8f32_outmax_form.log.)
+// The fp32 tower's own fused output / input transform kernels (kv_wino88.h) write the next fp32 V, and
+// wino88i_slice_kernel<K, float, 4, true> turns it into row-line digits (one wave per row: whole lines).
+// Dropped forms (profiles/r04_i8f32_outmax_form.log, profiles/r04_i8f32_fused_out.log): an output kernel
+// computing only the row maxima plus a second input-transform pass writing the digits (294-356 + 220 us
+// per layer at 2,048 boards), and one 512-thread workgroup per board keeping V in registers and reducing
+// the row maxima in the workgroup (436-511 us: at 246 VGPRs one workgroup per CU, its load, transform
+// and store phases serialised), against 142-238 + 165 us for the out kernel + slice.
 
 }  // namespace kv

@@ -14,7 +14,7 @@ KERNELS = {
     "wino_gemm": ("wino_gemm_kernel<512,2,2,1,2,16,36>", "wino_gemm_kernel<512,2,2,1,2,16,36>"),
     "wino48_gemm": ("wino_gemm_kernel<512,4,2,1,2,32,60>", "wino_gemm_kernel<512,4,2,1,2,32,60>"),
     "wino88_gemm": ("wino_gemm_kernel<512,4,2,1,2,32,100>", "wino_gemm_kernel<512,4,2,1,2,32,100>"),
-    "i8f32_gemm": ("wino88i_gemm_kernel<512,4,true,float>", "wino88i_gemm_kernel<512,4,true,float>"),
+    "i8f32_gemm": ("wino88i_gemm_kernel<512,4,true,float,true>", "wino88i_gemm_kernel<512,4,true,float,true>"),
     "i8_gemm": ("wino88i_gemm_kernel<512,5,true,double>", "wino88i_gemm_kernel<512,5,true,double>"),
 }
 
