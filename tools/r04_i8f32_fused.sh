@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: the fused kernel and KV_I8F32_FUSED were dropped after this measurement, profiles/r04_i8f32_fused_out.log)
 # fp32 tower on int8 digits, fused output kernel (wino88i32_out_kernel, row-line digit layout): the
 # bit-exact GEMM test, the fused-vs-slice bit-identity test and the tower's accuracy / invariance tests,
 # then forward timing with KV_I8F32_FUSED=1 / 0 alternating, a kernel trace of the fused form, and the
