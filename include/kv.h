@@ -300,9 +300,9 @@ int kv_dev_py_random(int device, const uint64_t* seeds, int n, int count, double
  * and U [100][512][K] fp64 (K 256 or 512, rows a multiple of 128) are split into
  * `digits` int8 digits by the product's slice kernel and multiplied by its GEMM
  * kernel: M [100][rows][512] (digits 5: KV_PREC_I8X5's fp64 M; 4: the fp32
- * domain's (KV_ALGO_WINOGRAD88_I8) fp32 M, widened); v_digits (digit planes
- * [100][K/32][digits][rows][32]) and v_exp [100][rows] (either may be NULL)
- * return V's digits and row exponents. */
+ * domain's (KV_ALGO_WINOGRAD88_I8) fp32 M, widened); v_digits (5 digits: planes
+ * [100][K/32][5][rows][32]; 4 digits: row lines [100][K/32][rows][4][32]) and
+ * v_exp [100][rows] (either may be NULL) return V's digits and row exponents. */
 int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, int digits, double* M,
                    int8_t* v_digits, int* v_exp);
 
