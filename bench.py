@@ -613,18 +613,19 @@ def main():
         out["calibration"] = dict(m["calibration"], note=(
             "the network's conv paths for these weights: fp32 + AUTO measures its candidates at load time against an "
             "fp64 forward on 64 seeded boards and keeps the fastest within max |dlogit| 4e-5 / |dvalue| 4e-6 "
-            "(F(8x8) fp32 with int8-digit GEMMs, F(8x8) fp32, F(4x8) fp32, the fp64 Winograd domain on int8 digits, "
-            "else on fp64 MFMA); errors are max |x - fp64|"))
+            "(F(8x8) fp32 with int8-digit GEMMs, the fp64 Winograd domain on int8 digits, else on fp64 MFMA); "
+            "errors are max |x - fp64|"))
         out["conv_path"] = PATH_NAMES.get(path)
         out["conv_arithmetic"] = {
-            6: "fp32 network (fp32 activations, fp32 Winograd transforms, U, V and M); each Winograd GEMM the exact "
-               "product of the fp32 operands' 28-bit truncations (4 int8 digits per value per row exponent, 10 "
-               "v_mfma_i32_32x32x32_i8 chains, int32 accumulation without rounding, fp64 combine), rounded to fp32 "
-               "once -- closer to the fp64 result than fp32 MFMA accumulation (calibration errors above; "
-               "fp32_winograd88 is the fp32 MFMA tower)",
+            6: "fp32 network (fp32 activations, fp32 Winograd transforms, U, V and M); each Winograd GEMM on int8 "
+               "digits: per-row 28-bit block fixed point (4 int8 digits per value under its row's exponent), the 10 "
+               "digit pairs i + j <= 3 of 16 as v_mfma_i32_32x32x32_i8 chains, exact int32 levels, exact combine, one "
+               "rounding to fp32 -- closer to the fp64 result than fp32 MFMA accumulation (calibration errors above; "
+               "per-element bound vs the fp64 product tested; fp32_winograd88 is the fp32 MFMA tower)",
             2: "fp32 network, Winograd GEMMs on v_mfma_f32_32x32x2_f32",
             1: "fp32 network, Winograd F(4x8) GEMMs on v_mfma_f32_32x32x2_f32",
-            5: "fp32 activations, fp64 Winograd domain, GEMMs from 5 int8 digits per value",
+            5: "fp32 activations, fp64 Winograd domain, GEMMs on 5 int8 digits per value (per-row 35-bit block fixed "
+               "point, 15 of 25 digit pairs, exact int32 levels, exact fp64 combine)",
             3: "fp32 activations, fp64 Winograd domain on v_mfma_f64",
             0: "fp32 direct implicit-GEMM convs"}.get(path)
         if pg_info is not None:

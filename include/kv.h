@@ -84,7 +84,8 @@ int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv);
  *                matrix cores: every V / U row scaled by a power of two and
  *                split into 5 int8 digits, the 15 digit products of weight
  *                >= 2^-28 accumulated exactly in int32 and combined in fp64
- *                (the exact dot product of the 35-bit truncated rows); logits
+ *                (per-row 35-bit block fixed point, 15 of 25 digit pairs: within
+ *                ~2^-36 of the fp64 product per element); logits
  *                as close to fp64 as KV_PREC_F64W's, at every batch size (the
  *                fp32 AUTO fallback for trained weights before F64W).
  * Values 1 and 2 (bf16x3 / bf16x6) were retired in round 4: KV_EINVAL. */
@@ -96,20 +97,22 @@ int kv_net_set_precision(kv_net* net, int precision);
 /* Algorithm of the fp32 3x3 convs with Cin 256/512:
  * KV_ALGO_AUTO      per weight load, the fastest path whose logits / values are
  *                   within 4e-5 / 4e-6 of an fp64 forward on 64 calibration
- *                   boards: > 16 boards F(8x8) fp32 with int8-digit GEMMs
- *                   (KV_ALGO_WINOGRAD88_I8), else F(8x8) fp32, else F(4x8)
- *                   fp32, else the fp64 Winograd domain on int8 digits
- *                   (KV_PREC_I8X5), else on fp64 MFMA; <= 16 boards direct
- *                   (split-K), else F(8x8) fp64 (kv_net_calibration reports it)
+ *                   boards (the initial position, 16 positions of reference
+ *                   self-play, 47 seeded random ones): > 16 boards F(8x8) fp32
+ *                   with int8-digit GEMMs (KV_ALGO_WINOGRAD88_I8), else the
+ *                   fp64 Winograd domain on int8 digits (KV_PREC_I8X5), else
+ *                   on fp64 MFMA; <= 16 boards direct (split-K), else F(8x8)
+ *                   fp64 (kv_net_calibration reports it)
  * KV_ALGO_DIRECT    implicit GEMM over the 9 taps (exact fp32 products)
  * KV_ALGO_WINOGRAD48 F(4x8,3x3): 60 GEMMs of 2 tiles x Cin x Cout per board,
  *                   4.8x fewer FLOPs than direct (fp32 and f16x3)
  * KV_ALGO_WINOGRAD88 F(8x8,3x3): 100 GEMMs of 1 tile x Cin x Cout per board,
  *                   5.76x fewer FLOPs than direct (fp32; f16x3 runs F(4x8))
  * KV_ALGO_WINOGRAD88_I8 the F(8x8) fp32 tower (fp32 U, V, M, transforms) with
- *                   each GEMM the exact product of 4 int8 digits per value
- *                   (28-bit rows, int32 levels, fp64 combine, one rounding to
- *                   fp32) on v_mfma_i32_32x32x32_i8
+ *                   each GEMM on 4 int8 digits per value: per-row 28-bit
+ *                   block fixed point, the 10 digit pairs i + j <= 3, exact
+ *                   int32 levels, one rounding to fp32, on
+ *                   v_mfma_i32_32x32x32_i8
  * Value 2 (F(4x4)) was retired in round 4: KV_EINVAL. Setting the precision or
  * the algorithm of a loaded net re-prepares it (synchronous).
  * Results are batch-invariant inside a class (<= 16 boards, > 16 boards). */
@@ -305,6 +308,18 @@ int kv_dev_py_random(int device, const uint64_t* seeds, int n, int count, double
  * v_exp [100][rows] (either may be NULL) return V's digits and row exponents. */
 int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, int digits, double* M,
                    int8_t* v_digits, int* v_exp);
+/* The fp32 tower's residual output kernel on int8 digits (KV_ALGO_WINOGRAD88_I8): M [100][rows][512] fp32
+ * (rows a multiple of 128), folded BN scale / shift [512], resid [rows][64][512] or NULL -> Y
+ * [rows][64][512] (= ReLU(A^T M A * scale + shift (+ resid))) and the next conv's V as row-line digits
+ * [100][16][rows][4][32] with row exponents [100][rows]. fused 1: the product's one-kernel form
+ * (wino88i32_out_kernel); 0: wino88_out_kernel's fp32 V then the slice kernel (bit-identical). */
+int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scale, const float* shift,
+                         const float* resid, int fused, float* Y, int8_t* v_digits, int* v_exp);
+/* Timing / A-B harness of the fp32 tower's int8-digit GEMM on seeded random digits (rows boards, K 256 or
+ * 512): variant 0 the round-4 kernel, 1.. round-5 forms (persistent / per-tile, k per stage, ring depth);
+ * avg_us = mean HIP-event time of `iters` launches; M_out [100][rows][512] (optional) for a bit-for-bit
+ * comparison of the variants. */
+int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, float* avg_us, float* M_out);
 
 /* ------------------------------------------------------- data pipeline ---
  * Full-rules chess (python-chess 1.999 semantics, csrc/kv_chess.cpp) for the

@@ -1133,6 +1133,28 @@ static int launch_wino88i_gemm(const int8_t* V8, const int* ev, const int8_t* U8
     return KV_OK;
 }
 
+// the fp32 tower's int8-digit GEMM, round-5 form (kv_wino88i.h wino88i32_gemm_kernel): persistent
+// workgroups, one per CU (grid a multiple of 8, at most the tile count), or one tile each (persist false)
+template <int K, int KS, int NBUF>
+static int launch_wino88i32_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
+                                 int rows, int stride, bool persist, hipStream_t st) {
+    using T = kv::I8G32<KS, NBUF>;
+    auto kern = kv::wino88i32_gemm_kernel<K, KS, NBUF>;
+    KV_HIP(lds_opt_in((const void*)kern, (int)T::BYTES));
+    const int ntiles = kv::W88_XI * (rows / T::WN) * (512 / T::WM);
+    KV_REQUIRE(rows % T::WN == 0 && stride % T::WN == 0 && ntiles % 8 == 0, KV_EINVAL,
+               "wino88i32 gemm: rows %d / stride %d vs tile %d", rows, stride, T::WN);
+    int grid = ntiles;
+    if (persist) {
+        const int cus = device_cus();
+        const int g = cus >= 8 ? (cus / 8) * 8 : 8;
+        grid = g < ntiles ? g : ntiles;
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(T::THREADS), T::BYTES, st, V8, ev, U8, eu, M, rows, stride);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
 // conv l's output transform into Y (fp32), then the next conv's digit planes from Y (kv_wino88i.h)
 template <bool RESID>
 static int launch_wino88i_out(kv_net* net, int l, const double* M, int nb, int stride, const float* resid, float* Y,
@@ -1182,21 +1204,45 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     return KV_OK;
 }
 
-// ---- the fp32 domain on int8 digits (KV_PATH_WINO88_I8F32): the fp32 F(8x8) tower's own fused output /
-// input transform kernels (wino88_out_kernel writes the next fp32 V), then the slice kernel turns each V
-// row into 4 digits under its row exponent, in the row-line layout (it reads the whole row, so the exponent
-// needs no second pass over the activations) ----
-// (mark: the engine's timing hook brackets the GEMM, the dominant kernel)
-static int wino88i32_gemm_layer(kv_net* net, int l, int K, int rows, int stride, bool mark, hipStream_t st) {
+// ---- the fp32 domain on int8 digits (KV_PATH_WINO88_I8F32): the fp32 F(8x8) tower's transforms; each
+// residual conv's output kernel (wino88i32_out_kernel, one workgroup per board) writes the next conv's V
+// directly as row-line digits under its row exponents. conv2's V256 (from the stem, 256 channels) goes
+// through the slice kernel. KV_I8F32_SLICE=1 (A/B probe): the round-4 form, wino88_out_kernel's fp32 V
+// + the slice kernel for every conv (the same digits, bit for bit) ----
+static bool i8f32_slice_form() {
+    static const bool v = [] {
+        const char* e = getenv("KV_I8F32_SLICE");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+template <bool RESID, bool WRITE_Y>
+static int launch_wino88i32_out(kv_net* net, int l, const float* M, int nb, int stride, const float* resid,
+                                float* Y, int8_t* V8, int* ev, hipStream_t st) {
+    const float* W = net->w;
+    hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y>), dim3(nb), dim3(1024), 0, st, M, stride,
+                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, V8, ev);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+// conv l's GEMM; slice: V (fp32) -> digits first. (mark: the engine's timing hook brackets the slice, when
+// there is one, and the GEMM)
+static int wino88i32_gemm_layer(kv_net* net, int l, int K, int rows, int stride, bool slice, bool mark,
+                                hipStream_t st) {
     constexpr int D = kv::kI8DigitsF32;
     float* M = (float*)net->Mw;
-    const float* Vsrc = K == 256 ? (const float*)net->V256 : (const float*)net->V;
-    int rc = K == 256 ? launch_wino88i_slice<256, D>(Vsrc, rows, stride, kv::W88_XI, net->V8, net->ev8, st)
+    int rc;
+    if (mark && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
+    if (slice) {
+        const float* Vsrc = K == 256 ? (const float*)net->V256 : (const float*)net->V;
+        rc = K == 256 ? launch_wino88i_slice<256, D>(Vsrc, rows, stride, kv::W88_XI, net->V8, net->ev8, st)
                       : launch_wino88i_slice<512, D>(Vsrc, rows, stride, kv::W88_XI, net->V8, net->ev8, st);
-    if (rc) return rc;
+        if (rc) return rc;
+    }
     const int8_t* U = net->U88i32 + net->uoff88[l] * D;
     const int* eu = net->eu88i32 + net->euoff[l];
-    if (mark && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
     rc = K == 256 ? launch_wino88i_gemm<256, D>(net->V8, net->ev8, U, eu, M, rows, stride, st)
                   : launch_wino88i_gemm<512, D>(net->V8, net->ev8, U, eu, M, rows, stride, st);
     if (rc) return rc;
@@ -1208,18 +1254,26 @@ static int wino88i32_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     const int rows = nb, stride = rows;
     float* V = (float*)net->V;
     const float* M = (const float*)net->Mw;
+    const bool sf = i8f32_slice_form();
     int rc;
-    if ((rc = wino88i32_gemm_layer(net, 1, 256, rows, stride, false, st))) return rc;
-    if ((rc = launch_wino88_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st))) return rc;
+    if ((rc = wino88i32_gemm_layer(net, 1, 256, rows, stride, true, false, st))) return rc;
+    rc = sf ? launch_wino88_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st)
+            : launch_wino88i32_out<false, true>(net, 1, M, nb, stride, nullptr, net->X, net->V8, net->ev8, st);
+    if (rc) return rc;
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
     for (int r = 0; r < 5; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         const bool m = mark && r == 2;
-        if ((rc = wino88i32_gemm_layer(net, l1, 512, rows, stride, m, st))) return rc;
-        if ((rc = launch_wino88_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st))) return rc;
-        if ((rc = wino88i32_gemm_layer(net, l2, 512, rows, stride, false, st))) return rc;
-        rc = r < 4 ? launch_wino88_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
-                   : launch_wino88_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
+        if ((rc = wino88i32_gemm_layer(net, l1, 512, rows, stride, sf, m, st))) return rc;
+        rc = sf ? launch_wino88_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st)
+                : launch_wino88i32_out<false, false>(net, l1, M, nb, stride, nullptr, nullptr, net->V8, net->ev8, st);
+        if (rc) return rc;
+        if ((rc = wino88i32_gemm_layer(net, l2, 512, rows, stride, sf, false, st))) return rc;
+        if (r == 4)
+            rc = launch_wino88_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
+        else
+            rc = sf ? launch_wino88_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
+                    : launch_wino88i32_out<true, true>(net, l2, M, nb, stride, net->X, net->X, net->V8, net->ev8, st);
         if (rc) return rc;
     }
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
@@ -1545,9 +1599,31 @@ static void release_unused(kv_net* net) {
 constexpr int kCalibBoards = 64;
 constexpr double kCalibTolLogit = 4e-5, kCalibTolValue = 4e-6;
 
-// the calibration boards: seeded random positions, 40 % of squares occupied by
-// any of the 12 pieces (the parity tests' board distribution), board 0 the
-// initial position
+// 16 positions the reference's own self-play reached (tests/golden/movegen.npz, states 7406, 6656, 6615, 3572, 5535, 8179, 411, 2546, 318, 1022, 55, 3355, 5618, 1459, 1713, 4805, generated by
+// tests/golden/make_golden.py from scripts/self_play.py games): 3-6 pieces (sparse endgames), 10-13,
+// 21-28 and full middlegames
+static const int8_t kCalibReal[16][64] = {
+    {0, 7, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 5, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1},
+    {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 7, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 6, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {4, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 7, 0, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 6, 0, 0, 0, 0, 1, 0, 0, 4, 0, 0, 0, 0, 0, 0, 0, 0},
+    {0, 0, 0, 0, 4, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 6, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 7, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 5},
+    {0, 0, 0, 0, 10, 0, 0, 0, 0, 0, 0, 0, 7, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 6, 0, 0, 0, 0, 10, 0, 0, 6, 0, 0, 6, 0, 9, 0, 0, 0, 0, 1, 0, 0, 0, 4, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 3, 0, 0},
+    {0, 0, 0, 0, 0, 0, 4, 0, 7, 0, 0, 0, 0, 12, 12, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 12, 0, 0, 0, 12, 0, 0, 0, 0, 0, 0, 0, 6, 0, 0, 6, 0, 6, 0, 0, 0, 0, 6, 0, 0, 0, 6, 6, 0, 0, 0, 3, 0, 0, 0, 0, 0},
+    {0, 0, 0, 0, 0, 0, 7, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 10, 0, 0, 0, 2, 0, 0, 0, 12, 12, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 11, 5, 0, 0, 0, 0, 12, 0, 0, 0, 0, 1, 0, 0, 6, 0, 0, 0, 0, 0, 0, 0, 0},
+    {0, 0, 0, 0, 0, 7, 0, 0, 0, 0, 5, 6, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 3, 0, 0, 0, 10, 12, 0, 0, 0, 0, 0, 0, 0, 6, 0, 0, 12, 6, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 5, 0, 0, 0, 0, 0},
+    {0, 2, 10, 0, 0, 0, 0, 0, 0, 12, 0, 0, 7, 0, 0, 0, 8, 0, 0, 12, 12, 12, 0, 10, 0, 0, 0, 0, 0, 0, 0, 6, 12, 0, 0, 0, 6, 4, 12, 12, 0, 0, 0, 11, 0, 4, 0, 5, 11, 0, 0, 1, 0, 6, 0, 6, 0, 0, 0, 3, 0, 0, 3, 0},
+    {0, 0, 0, 0, 7, 0, 0, 9, 0, 0, 9, 0, 0, 0, 12, 0, 10, 11, 12, 10, 0, 0, 0, 0, 0, 0, 0, 2, 0, 8, 5, 12, 12, 12, 0, 6, 0, 0, 0, 6, 0, 0, 0, 0, 1, 0, 0, 3, 6, 0, 0, 0, 0, 0, 0, 0, 0, 0, 4, 0, 3, 0, 0, 0},
+    {9, 0, 4, 0, 7, 10, 0, 9, 0, 0, 0, 12, 11, 12, 0, 12, 11, 0, 0, 0, 12, 0, 12, 0, 12, 0, 0, 0, 0, 0, 6, 0, 0, 0, 0, 0, 8, 6, 0, 0, 6, 0, 0, 0, 0, 0, 0, 6, 0, 6, 0, 6, 6, 0, 0, 2, 3, 5, 4, 0, 1, 0, 5, 3},
+    {9, 0, 10, 0, 7, 0, 11, 9, 12, 12, 12, 12, 0, 0, 0, 12, 0, 0, 0, 0, 0, 12, 0, 0, 8, 0, 0, 0, 12, 0, 12, 6, 6, 0, 6, 0, 6, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 6, 0, 0, 4, 0, 6, 3, 11, 5, 4, 0, 0, 0, 5, 0},
+    {9, 0, 10, 8, 7, 10, 11, 0, 12, 0, 12, 0, 12, 12, 12, 0, 0, 0, 11, 0, 0, 0, 0, 9, 0, 12, 0, 0, 0, 0, 0, 12, 6, 6, 0, 12, 6, 0, 0, 0, 0, 0, 5, 0, 0, 5, 0, 0, 3, 0, 6, 6, 0, 6, 6, 6, 0, 0, 4, 2, 1, 4, 3, 0},
+    {9, 11, 10, 8, 0, 10, 0, 9, 12, 12, 12, 12, 12, 7, 12, 12, 0, 0, 0, 0, 0, 12, 0, 11, 0, 5, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 6, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 6, 6, 6, 6, 4, 6, 6, 6, 3, 0, 4, 2, 1, 0, 5, 3},
+    {9, 11, 10, 8, 7, 10, 11, 9, 12, 12, 12, 12, 12, 12, 12, 12, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 6, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 6, 6, 0, 6, 6, 6, 6, 6, 3, 5, 4, 2, 1, 4, 5, 3},
+    {9, 0, 10, 0, 7, 10, 11, 0, 0, 0, 8, 0, 12, 0, 12, 9, 12, 12, 11, 0, 0, 12, 0, 0, 0, 0, 12, 4, 0, 6, 0, 12, 0, 0, 6, 0, 0, 0, 6, 6, 5, 0, 0, 0, 0, 0, 0, 0, 6, 6, 0, 6, 6, 0, 0, 0, 3, 0, 4, 2, 1, 0, 5, 3},
+};
+
+// the calibration boards: board 0 the initial position, boards 1-16 the real positions above, the rest
+// seeded random positions, 40 % of squares occupied by any of the 12 pieces (the parity tests' board
+// distribution)
 static void calib_boards(int8_t* b) {
     uint64_t s = 0x4b56414d44ull;
     auto next = [&]() {  // splitmix64
@@ -1565,6 +1641,7 @@ static void calib_boards(int8_t* b) {
                                      0, 0,  0,  0, 0, 0,  0,  0, 0,  0,  0,  0,  0,  0,  0,  0,
                                      6, 6,  6,  6, 6, 6,  6,  6, 3,  5,  4,  2,  1,  4,  5,  3};
     memcpy(b, start, 64);
+    memcpy(b + 64, kCalibReal, sizeof kCalibReal);
 }
 
 struct Ref64Bufs {
@@ -1645,10 +1722,11 @@ static int net_calibrate(kv_net* net) {
     if ((rc = ref64_forward(net, boards, kCalibBoards, r)) || (rc = net_reserve(net, kCalibBoards))) return fail(rc);
     const auto within = [&](double el, double ev) { return el <= kCalibTolLogit && ev <= kCalibTolValue; };
     // > 16 boards
-    const int cands[5] = {KV_PATH_WINO88_I8F32, KV_PATH_WINO88, KV_PATH_WINO48, KV_PATH_WINO88_I8,
-                          KV_PATH_WINO88_F64};
+    // (F(8x8) and F(4x8) on fp32 MFMA are never within the budget when the int8-digit fp32 tower is not:
+    // on every weight set measured they are further from fp64 -- DESIGN.md; they stay explicit algos)
+    const int cands[3] = {KV_PATH_WINO88_I8F32, KV_PATH_WINO88_I8, KV_PATH_WINO88_F64};
     net->auto_small = KV_PATH_DIRECT;
-    for (int i = 0; i < 5; ++i) {
+    for (int i = 0; i < 3; ++i) {
         const int p = cands[i];
         if ((rc = ensure_path(net, p))) return fail(rc);
         net->auto_large = p;
@@ -1683,10 +1761,11 @@ static int net_prepare(kv_net* net) {
     if (net->precision == KV_PREC_FP32 && net->algo == KV_ALGO_AUTO) {
         const char* e = getenv("KV_CALIBRATE");  // "0": skip, AUTO keeps F(8x8) / direct (timing probes only)
         if (!(e && e[0] == '0')) return net_calibrate(net);
-        net->calib = kv_calib{};
         net->auto_large = KV_PATH_WINO88;
         net->auto_small = KV_PATH_DIRECT;
     }
+    // no calibration for this setting: kv_net_calibration must not report an earlier one's errors
+    net->calib = kv_calib{};
     int rc;
     if ((rc = ensure_path(net, path_for(net, 1))) || (rc = ensure_path(net, path_for(net, 1024)))) return rc;
     release_unused(net);
@@ -1743,9 +1822,15 @@ int kv_net_set_algo(kv_net* net, int algo) {
     KV_REQUIRE(algo == KV_ALGO_AUTO || algo == KV_ALGO_DIRECT || algo == KV_ALGO_WINOGRAD48 ||
                    algo == KV_ALGO_WINOGRAD88 || algo == KV_ALGO_WINOGRAD88_I8,
                KV_EINVAL, "kv_net_set_algo: unknown algo %d", algo);
-    if (net->algo == algo) return KV_OK;
+    if (net->algo == algo && (!net->loaded || net->built[path_for(net, 1024)])) return KV_OK;
+    const int prev = net->algo;
     net->algo = algo;
-    return net_prepare(net);
+    const int rc = net_prepare(net);
+    if (rc) {  // keep the setting whose weights the net holds; a retry with the same value rebuilds
+        net->algo = prev;
+        if (net->loaded && !net->built[path_for(net, 1024)]) (void)net_prepare(net);
+    }
+    return rc;
 }
 
 int kv_net_set_precision(kv_net* net, int precision) {
@@ -1757,9 +1842,15 @@ int kv_net_set_precision(kv_net* net, int precision) {
                    precision == KV_PREC_I8X5,
                KV_EINVAL,
                "kv_net_set_precision: unknown precision %d", precision);
-    if (net->precision == precision) return KV_OK;
+    if (net->precision == precision && (!net->loaded || net->built[path_for(net, 1024)])) return KV_OK;
+    const int prev = net->precision;
     net->precision = precision;
-    return net_prepare(net);
+    const int rc = net_prepare(net);
+    if (rc) {  // as kv_net_set_algo
+        net->precision = prev;
+        if (net->loaded && !net->built[path_for(net, 1024)]) (void)net_prepare(net);
+    }
+    return rc;
 }
 
 int kv_net_calibration(kv_net* net, kv_calib* out) {
@@ -1866,6 +1957,127 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
     }
     if (v_digits) KV_HIP(hipMemcpy(v_digits, v8.p, nv * digits, hipMemcpyDeviceToHost));
     if (v_exp) KV_HIP(hipMemcpy(v_exp, ev.p, (size_t)kv::W88_XI * rows * sizeof(int), hipMemcpyDeviceToHost));
+    return KV_OK;
+}
+
+int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scale, const float* shift,
+                         const float* resid, int fused, float* Y, int8_t* v_digits, int* v_exp) {
+    KV_REQUIRE(M && scale && shift && Y && v_digits && v_exp && rows > 0 && rows % 128 == 0, KV_EINVAL,
+               "kv_dev_wino88i32_out: bad arguments (rows %d must be a multiple of 128)", rows);
+    KV_HIP(hipSetDevice(device));
+    const size_t nm = (size_t)kv::W88_XI * rows * 512, ny = (size_t)rows * 64 * 512;
+    kv::DevBuf<float> dm, dsc, dsh, dy, dv;
+    kv::DevBuf<int8_t> v8;
+    kv::DevBuf<int> ev;
+    KV_HIP(dm.alloc(nm));
+    KV_HIP(dsc.alloc(512));
+    KV_HIP(dsh.alloc(512));
+    KV_HIP(dy.alloc(ny));
+    KV_HIP(dv.alloc(nm));
+    KV_HIP(v8.alloc(nm * kv::kI8DigitsF32));
+    KV_HIP(ev.alloc((size_t)kv::W88_XI * rows));
+    KV_HIP(hipMemcpy(dm.p, M, nm * sizeof(float), hipMemcpyHostToDevice));
+    KV_HIP(hipMemcpy(dsc.p, scale, 512 * sizeof(float), hipMemcpyHostToDevice));
+    KV_HIP(hipMemcpy(dsh.p, shift, 512 * sizeof(float), hipMemcpyHostToDevice));
+    if (resid)
+        KV_HIP(hipMemcpy(dy.p, resid, ny * sizeof(float), hipMemcpyHostToDevice));
+    else
+        KV_HIP(hipMemset(dy.p, 0, ny * sizeof(float)));
+    const float* sc = dsc.p;
+    const float* sh = dsh.p;
+    // Y doubles as the residual (in place, as the tower runs it)
+    if (fused) {
+        if (resid)
+            hipLaunchKernelGGL((kv::wino88i32_out_kernel<true, true>), dim3(rows), dim3(1024), 0, 0, dm.p, rows, sc,
+                               sh, dy.p, dy.p, v8.p, ev.p);
+        else
+            hipLaunchKernelGGL((kv::wino88i32_out_kernel<false, true>), dim3(rows), dim3(1024), 0, 0, dm.p, rows, sc,
+                               sh, nullptr, dy.p, v8.p, ev.p);
+        KV_HIP(hipGetLastError());
+    } else {
+        if (resid)
+            hipLaunchKernelGGL((kv::wino88_out_kernel<true, true, true>), dim3(512 / 256, rows), dim3(256), 0, 0,
+                               dm.p, rows, sc, sh, dy.p, dy.p, dv.p);
+        else
+            hipLaunchKernelGGL((kv::wino88_out_kernel<false, true, true>), dim3(512 / 256, rows), dim3(256), 0, 0,
+                               dm.p, rows, sc, sh, nullptr, dy.p, dv.p);
+        KV_HIP(hipGetLastError());
+        int rc = launch_wino88i_slice<512, kv::kI8DigitsF32>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
+        if (rc) return rc;
+    }
+    KV_HIP(hipDeviceSynchronize());
+    KV_HIP(hipMemcpy(Y, dy.p, ny * sizeof(float), hipMemcpyDeviceToHost));
+    KV_HIP(hipMemcpy(v_digits, v8.p, nm * kv::kI8DigitsF32, hipMemcpyDeviceToHost));
+    KV_HIP(hipMemcpy(v_exp, ev.p, (size_t)kv::W88_XI * rows * sizeof(int), hipMemcpyDeviceToHost));
+    return KV_OK;
+}
+
+__global__ void i8_fill_kernel(int8_t* d, size_t n_lines, int* e, size_t ne, unsigned seed) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_lines * 128) {  // byte 32 d + c of a line: digit d (0: [-127, 127], else [-64, 64])
+        unsigned h = (unsigned)(i * 2654435761u) ^ seed;
+        h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+        const int dg = (int)((i >> 5) & 3);
+        d[i] = (int8_t)(dg == 0 ? (int)(h % 255u) - 127 : (int)(h % 129u) - 64);
+    }
+    if (i < ne) e[i] = (int)((i * 7u + seed) % 7u) - 3;
+}
+
+int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, float* avg_us, float* M_out) {
+    KV_REQUIRE(rows > 0 && rows % 128 == 0 && (K == 256 || K == 512) && iters > 0 && avg_us, KV_EINVAL,
+               "kv_dev_i8gemm_bench: bad arguments");
+    KV_HIP(hipSetDevice(device));
+    const size_t lv = (size_t)kv::W88_XI * (K / 32) * rows, lu = (size_t)kv::W88_XI * (K / 32) * 512;
+    const size_t nm = (size_t)kv::W88_XI * rows * 512;
+    kv::DevBuf<int8_t> v8, u8;
+    kv::DevBuf<int> ev, eu;
+    kv::DevBuf<float> m;
+    KV_HIP(v8.alloc(lv * 128));
+    KV_HIP(u8.alloc(lu * 128));
+    KV_HIP(ev.alloc((size_t)kv::W88_XI * rows));
+    KV_HIP(eu.alloc((size_t)kv::W88_XI * 512));
+    KV_HIP(m.alloc(nm));
+    hipLaunchKernelGGL(i8_fill_kernel, dim3((unsigned)((lv * 128 + 255) / 256)), dim3(256), 0, 0, v8.p, lv, ev.p,
+                       (size_t)kv::W88_XI * rows, 1234u);
+    hipLaunchKernelGGL(i8_fill_kernel, dim3((unsigned)((lu * 128 + 255) / 256)), dim3(256), 0, 0, u8.p, lu, eu.p,
+                       (size_t)kv::W88_XI * 512, 99u);
+    KV_HIP(hipGetLastError());
+    constexpr int D = kv::kI8DigitsF32;
+    auto run = [&]() -> int {
+        const bool k5 = K == 512;
+        switch (variant) {
+            case 0: return k5 ? launch_wino88i_gemm<512, D>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0)
+                               : launch_wino88i_gemm<256, D>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0);
+            case 1: return k5 ? launch_wino88i32_gemm<512, 32, 3>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0)
+                              : launch_wino88i32_gemm<256, 32, 3>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);
+            case 2: return k5 ? launch_wino88i32_gemm<512, 32, 3>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, false, 0)
+                              : launch_wino88i32_gemm<256, 32, 3>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, false, 0);
+            case 3: return k5 ? launch_wino88i32_gemm<512, 32, 4>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0)
+                              : launch_wino88i32_gemm<256, 32, 4>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);
+            case 4: return k5 ? launch_wino88i32_gemm<512, 64, 2>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0)
+                              : launch_wino88i32_gemm<256, 64, 2>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);
+            case 5: return k5 ? launch_wino88i32_gemm<512, 64, 2>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, false, 0)
+                              : launch_wino88i32_gemm<256, 64, 2>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, false, 0);
+            default: KV_REQUIRE(false, KV_EINVAL, "kv_dev_i8gemm_bench: variant %d", variant);
+        }
+    };
+    int rc;
+    for (int w = 0; w < 2; ++w)
+        if ((rc = run())) return rc;
+    hipEvent_t e0, e1;
+    KV_HIP(hipEventCreate(&e0));
+    KV_HIP(hipEventCreate(&e1));
+    KV_HIP(hipEventRecord(e0, 0));
+    for (int it = 0; it < iters; ++it)
+        if ((rc = run())) return rc;
+    KV_HIP(hipEventRecord(e1, 0));
+    KV_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    KV_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *avg_us = 1000.f * ms / iters;
+    if (M_out) KV_HIP(hipMemcpy(M_out, m.p, nm * sizeof(float), hipMemcpyDeviceToHost));
     return KV_OK;
 }
 

@@ -13,9 +13,15 @@
 //     M = 2^(e_v + e_u - 14) * sum_{l < S} 2^(-7l) * sum_{i+j=l} (D_i . E_j)
 // where each D_i . E_j is one v_mfma_i32_32x32x32_i8 chain over K (exact in
 // int32: |level l| <= 5 * 512 * 127^2 < 2^31), and the five level sums are
-// combined in fp64 exactly (at most 51 significant bits). The result is the
-// exact dot product of the digit-truncated rows: no rounding anywhere in the
-// GEMM, so it is independent of k order, tile shape and batch by construction.
+// combined in fp64 exactly (at most 51 significant bits). What it computes:
+// per-row 35-bit block fixed point (each value cut to the multiples of
+// 2^(e-36) of its row's exponent), the 15 digit pairs i + j <= 4 of the 25
+// (the 10 dropped pairs weigh < 2^-42 of the row maxima's product each), exact
+// int32 levels, one exact fp64 combine. Nothing in the GEMM rounds, so M is
+// independent of k order, tile shape and batch by construction. Its distance
+// from the fp64 product of the unsplit rows is bounded per element by the
+// truncation (|rest| <= 2^-36 per value) plus the dropped pairs:
+// tests/test_wino_i8_gpu.py::test_i8_gemm_within_derived_bound_of_fp64_product.
 // 15 int8 products at 32x the fp32 MFMA rate (the int8 rate is 2x bf16's)
 // against v_mfma_f64 at half the fp32 rate: a ~4x higher ceiling than the fp64
 // GEMM it replaces, at the same accuracy (host emulation on the stress weights:
@@ -28,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kv_common.h"
+#include "kv_wino88.h"   // w88_bt, wino88_out_plane
 #include "kv_wino88d.h"  // f64x2
 
 namespace kv {
@@ -331,10 +338,10 @@ __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restr
 
 // max over the 32 lanes of this half of v[0..9] (16 shuffles): lanes with (lane & 16) == 0 and
 // (lane & 15) < 10 return the max of index lane & 15
-__device__ inline unsigned i8_half_max10(const double (&o)[10], int lane) {
+__device__ inline unsigned i8_half_max10(const unsigned (&v10)[10], int lane) {
     unsigned v[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = j < 10 ? (unsigned)(__double_as_longlong(o[j]) >> 32) & 0x7fffffffu : 0u;
+    for (int j = 0; j < 16; ++j) v[j] = j < 10 ? v10[j] : 0u;
 #pragma unroll
     for (int st = 0; st < 4; ++st) {  // halving over offsets 8, 4, 2, 1: lane keeps index lane & 15
         const int off = 8 >> st;
@@ -348,6 +355,14 @@ __device__ inline unsigned i8_half_max10(const double (&o)[10], int lane) {
     }
     const unsigned o16 = (unsigned)__shfl_xor((int)v[0], 16, 64);
     return v[0] > o16 ? v[0] : o16;
+}
+
+// the same over the high words of |o| (doubles)
+__device__ inline unsigned i8_half_max10(const double (&o)[10], int lane) {
+    unsigned v[10];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) v[j] = (unsigned)(__double_as_longlong(o[j]) >> 32) & 0x7fffffffu;
+    return i8_half_max10(v, lane);
 }
 
 template <bool RESID>
@@ -424,19 +439,312 @@ __global__ __launch_bounds__(256) void wino88i_in_kernel(const float* __restrict
     }
 }
 
+// ---- the fp32 tower's GEMM on 4 int8 digits, round 5 (wino88i32_gemm_kernel) ----
+// The same products as wino88i_gemm_kernel<K, 4, ., float, true> -- exact int32 levels, one rounding to fp32 --
+// with four changes, none of which changes a bit of M:
+//  * operands swapped: A = U (32 output channels per wave), B = V (2 x 32 boards), so the accumulator's 4
+//    consecutive registers are 4 consecutive output channels of one board and the epilogue writes M with
+//    16-byte stores (8 per wave instead of 32 dword stores);
+//  * the level combine in integers first: H = 128 L0 + L1 and L = 128 L2 + L3 are exact in int32 (|L0| <=
+//    K 127^2 < 2^23, |L1| <= 2 K 127 64, |L2| <= K (2 127 64 + 64^2), |L3| <= K (2 127 64 + 2 64^2), all at
+//    K = 512), then m = 2^14 H + L in fp64 (< 2^46: exact) -- the same value as the fp64 chain
+//    L0 + L1/128 + L2/128^2 + L3/128^3 times 2^21, so the same fp32 after ldexp and the one rounding;
+//  * persistent workgroups: one per CU, each walking a contiguous run of its XCD's share of the tile order
+//    (the XCD-aware order of wino88i_gemm_kernel), with the copy ring running across tiles -- the next tile's
+//    first stages are in flight during this tile's last stages and its epilogue;
+//  * the row exponents of a tile (128 of V, 128 of U) come into LDS by one more global_load_lds piece with
+//    the tile's first stage and are read into registers after that stage's barrier (an ordinary load's
+//    first use, or an LDS read in the epilogue, makes hipcc wait vmcnt(0) on the ring).
+// KS: k per stage (32 or 64: one barrier per KS), NBUF: ring buffers (prefetch distance NBUF - 1).
+template <int KS, int NBUF>
+struct I8G32 {
+    static constexpr int THREADS = 512, WM = 128, WN = 128;  // WM output channels x WN boards
+    static constexpr int NCH = KS / 32;                      // 32-k chunks per stage
+    static constexpr int CHB = 128 * 128;                    // one operand's chunk: 128 rows x 128-B lines
+    static constexpr int STAGE = 2 * NCH * CHB;              // [op U, V][chunk][row][128 B]
+    static constexpr int GL = STAGE / 1024 / (THREADS / 64); // global_load_lds pieces per wave and stage
+    static constexpr int EXP = NBUF * STAGE;                 // 2 x (128 + 128) exponents (tile parity)
+    static constexpr size_t BYTES = (size_t)NBUF * STAGE + 2048;
+    static constexpr int NS = 8;                             // epilogue stores per wave
+};
+
+template <int K, int KS, int NBUF>
+__global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __restrict__ V8,
+                                                             const int* __restrict__ ev,
+                                                             const int8_t* __restrict__ U8,
+                                                             const int* __restrict__ eu, float* __restrict__ M,
+                                                             int rows, int stride) {
+    using T = I8G32<KS, NBUF>;
+    constexpr int NK = K / KS, NCH = T::NCH, GL = T::GL, PD = NBUF - 1;
+    static_assert(GL * 8 * 1024 == T::STAGE && GL % 4 == 0, "stage split");
+    extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8g[];
+    char* const L0 = (char*)lds_i8g;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;  // 32 output channels, 64 boards
+    const int RT = rows / T::WN, CT = 512 / T::WM;
+    const int ntiles = kv::W88_XI * RT * CT;
+    // this workgroup's tiles: XCD group x = blockIdx % 8 owns [x T8, (x + 1) T8) of the tile order; its P
+    // workgroups take every P-th tile of that run (gridDim = ntiles: one tile each, the plain XCD order)
+    const int T8 = ntiles >> 3, P = (int)gridDim.x >> 3;
+    const int tfirst = (int)(blockIdx.x & 7) * T8 + (int)(blockIdx.x >> 3);
+    const int tend = (int)(blockIdx.x & 7) * T8 + T8;
+    const int ntile_wg = tfirst < tend ? (tend - tfirst + P - 1) / P : 0;
+    const int nstage = ntile_wg * NK;
+
+    // piece q = wave * GL + g: operand q / (16 NCH) (U: waves 0-3, V: waves 4-7), chunk (q / 16) % NCH,
+    // rows 8 (q % 16) .. +7; lane l fills position l & 7 of LDS row 8 (q % 16) + l / 8 from source chunk
+    // (l & 7) ^ (row >> 1 & 7) (the row-line image of wino88i_gemm_kernel)
+    const int op = wave >> 2;
+    const int rl_off0 = (lane >> 3) * 128 + 16 * ((lane & 7) ^ (lane >> 4));
+    const int rl_off1 = (lane >> 3) * 128 + 16 * ((lane & 7) ^ (lane >> 4) ^ 4);
+    const size_t cstride = (size_t)(op ? stride : 512) * 128;  // the next 32-k chunk of an operand
+    auto tile_of = [&](int n, int& xi, int& n_base, int& r_base) {  // n-th tile of this workgroup
+        const int idx = tfirst + n * P;
+        xi = idx / (CT * RT);
+        n_base = (idx % CT) * T::WM;
+        r_base = ((idx / CT) % RT) * T::WN;
+    };
+    // a tile's operand base (this wave's operand) and exponent-piece source (lanes 0-31: ev, 32-63: eu)
+    auto tile_base = [&](int n, const int8_t*& gb, const int*& es) {
+        int xi, n_base, r_base;
+        tile_of(n, xi, n_base, r_base);
+        gb = op ? V8 + (((size_t)xi * (K / 32)) * stride + r_base) * 128
+                : U8 + (((size_t)xi * (K / 32)) * 512 + n_base) * 128;
+        const bool lo = lane < 32;
+        es = (lo ? ev : eu) + (lo ? (size_t)xi * stride + r_base : (size_t)xi * 512 + n_base) + 4 * (lane & 31);
+    };
+    // pieces g0 .. g1 - 1 of stage kt of the tile at gb (exponents first when ex != nullptr), into buffer buf
+    auto issue = [&](const int8_t* gb, int kt, int buf, int g0, int g1) {
+        const int8_t* gk = gb + (size_t)(kt * NCH) * cstride;
+#pragma unroll
+        for (int g = g0; g < g1; ++g) {
+            const int q = wave * GL + g, rg8 = q % 16, ch = (q / 16) % NCH;
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(gk + (size_t)ch * cstride + (size_t)rg8 * 1024 + ((rg8 & 1) ? rl_off1 : rl_off0)),
+                (__attribute__((address_space(3))) void*)(L0 + buf * T::STAGE + (op * NCH + ch) * T::CHB +
+                                                          rg8 * 1024),
+                16, 0, 0);
+        }
+    };
+    auto issue_exp = [&](const int* es, int n) {
+        __builtin_amdgcn_global_load_lds((const void*)es,
+                                         (__attribute__((address_space(3))) void*)(L0 + T::EXP + (n & 1) * 1024),
+                                         16, 0, 0);
+    };
+
+    // fragments: A = U digit i of channel row wm * 32 + (lane & 31), B = V digit j of board row
+    // wn * 64 + nt * 32 + (lane & 31); the 16-byte chunk 2 i + (lane >> 5) of the row's line
+    const int lr = lane & 31, lh = lane >> 5;
+    int aoff[4], boff[2][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        aoff[i] = i8_rl_off(wm * 32 + lr, 2 * i + lh);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) boff[nt][i] = NCH * T::CHB + i8_rl_off(wn * 64 + nt * 32 + lr, 2 * i + lh);
+    }
+
+    const int8_t *gb_cur = nullptr, *gb_nxt = nullptr;
+    const int *es_cur = nullptr, *es_nxt = nullptr;
+    if (ntile_wg > 0) {
+        tile_base(0, gb_cur, es_cur);
+        if (wave == 0) issue_exp(es_cur, 0);
+        for (int k = 0; k < PD && k < NK; ++k) issue(gb_cur, k, k % NBUF, 0, GL);
+    }
+    int s = 0, bcur = 0, bpre = PD % NBUF;  // ring buffers of stage s and of stage s + PD
+    for (int n = 0; n < ntile_wg; ++n) {
+        if (n + 1 < ntile_wg) tile_base(n + 1, gb_nxt, es_nxt);
+        i32x16_t acc[4][2];
+#pragma unroll
+        for (int l = 0; l < 4; ++l)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) acc[l][nt] = i32x16_t{};
+        int evr[2];     // ev - 35 of the wave's two 32-board blocks (this lane's board)
+        int euv[4][4];  // eu of this lane's 16 output channels
+        for (int kt = 0; kt < NK; ++kt, ++s, bcur = bcur + 1 == NBUF ? 0 : bcur + 1,
+                                     bpre = bpre + 1 == NBUF ? 0 : bpre + 1) {
+            // stage s has landed once only the batches issued after it may be outstanding: the next PD - 1
+            // stages' (those that exist) and, in a tile's first PD stages after an epilogue, its NS stores
+            const int ahead = nstage - 1 - s < PD - 1 ? nstage - 1 - s : PD - 1;
+            const bool st = n > 0 && kt < PD;
+            if (PD == 2) {
+                if (ahead == 1) {
+                    if (st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL + T::NS) : "memory");
+                    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+                } else {
+                    if (st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T::NS) : "memory");
+                    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+            } else {  // PD == 3
+                if (ahead == 2) {
+                    if (st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL + T::NS) : "memory");
+                    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL) : "memory");
+                } else if (ahead == 1) {
+                    if (st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL + T::NS) : "memory");
+                    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+                } else {
+                    if (st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T::NS) : "memory");
+                    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+            }
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (kt == 0) {  // the tile's exponents landed with its first stage: ev of the 2 boards, eu of 16 channels
+                const int* ex = (const int*)(L0 + T::EXP + (n & 1) * 1024);
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) evr[nt] = ex[wn * 64 + nt * 32 + lr] - 35;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj) euv[k][jj] = ex[128 + wm * 32 + 8 * k + 4 * lh + jj];
+            }
+            const char* buf = L0 + bcur * T::STAGE;
+            const bool more = s + PD < nstage;
+#pragma unroll
+            for (int ch = 0; ch < NCH; ++ch) {
+                const char* cb = buf + ch * T::CHB;
+                i8x16_t a[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) a[i] = *(const i8x16_t*)(cb + aoff[i]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    i8x16_t b[2];
+#pragma unroll
+                    for (int nt = 0; nt < 2; ++nt) b[nt] = *(const i8x16_t*)(cb + boff[nt][j]);
+#pragma unroll
+                    for (int i = 0; i + j < 4; ++i)
+#pragma unroll
+                        for (int nt = 0; nt < 2; ++nt)
+                            acc[i + j][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[nt], acc[i + j][nt], 0, 0, 0);
+                    // stage s + PD's copies (this tile's or the next one's), one group per (chunk, B digit)
+                    // between the MFMA groups; the next tile's exponents ahead of its first stage
+                    if (more) {
+                        constexpr int PER = GL / (4 * NCH);
+                        const int g0 = (ch * 4 + j) * PER;
+                        const bool nx = kt + PD >= NK;
+                        if (nx && kt + PD == NK && g0 == 0 && wave == 0) issue_exp(es_nxt, n + 1);
+                        issue(nx ? gb_nxt : gb_cur, nx ? kt + PD - NK : kt + PD, bpre, g0, g0 + PER);
+                    }
+                }
+            }
+        }
+        // epilogue (registers only; the ring keeps loading the next tile)
+        int xi, n_base, r_base;
+        tile_of(n, xi, n_base, r_base);
+        gb_cur = gb_nxt;
+        es_cur = es_nxt;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            const int bl = wn * 64 + nt * 32 + lr;
+            const int eb = evr[nt];
+            float* mrow = M + ((size_t)xi * stride + r_base + bl) * 512 + n_base + wm * 32 + 4 * lh;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float o[4];
+                const int* ec = euv[k];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int r = 4 * k + jj;
+                    const int hi = acc[0][nt][r] * 128 + acc[1][nt][r];
+                    const int lo = acc[2][nt][r] * 128 + acc[3][nt][r];
+                    const double m = __builtin_fma((double)hi, 16384.0, (double)lo);  // exact
+                    o[jj] = (float)ldexp(m, eb + ec[jj]);
+                }
+                *(float4*)(mrow + 8 * k) = make_float4(o[0], o[1], o[2], o[3]);
+            }
+        }
+    }
+}
+
 // ---- the fp32 Winograd domain with int8-digit GEMMs (KV_PATH_WINO88_I8F32) ----
 // The fp32 F(8x8) tower's arithmetic (kv_wino88.h: fp32 transforms, V, M and activations; U as
-// 4 digits of the fp64 U) with each GEMM taken from 4 int8 digits per value: the product of the
-// 28-bit truncated rows is exact (int32 levels, fp64 combine) and rounded to fp32 once, where the
-// fp32 MFMA GEMM rounds after every product. 10 int8 MFMAs per point product against one fp32 one at
+// 4 digits of the fp64 U) with each GEMM taken from 4 int8 digits per value: per-row 28-bit block
+// fixed point (each value cut to the multiples of 2^(e-29) of its row's exponent e), the 10 digit pairs
+// i + j <= 3 of the 16, exact int32 levels, combined exactly and rounded to fp32 once -- where the fp32
+// MFMA GEMM rounds after every product. An fp32 value within 2^-4 of its row's max keeps all its bits; one
+// 2^-k below keeps 28 - k (the bound test: tests/test_wino_i8_gpu.py). 10 int8 MFMAs per point product against one fp32 one at
 // 1/32 the rate.
 
-// The fp32 tower's own fused output / input transform kernels (kv_wino88.h) write the next fp32 V, and
-// wino88i_slice_kernel<K, float, 4, true> turns it into row-line digits (one wave per row: whole lines).
-// Dropped forms (profiles/r04_i8f32_outmax_form.log, profiles/r04_i8f32_fused_out.log): an output kernel
-// computing only the row maxima plus a second input-transform pass writing the digits (294-356 + 220 us
-// per layer at 2,048 boards), and one 512-thread workgroup per board keeping V in registers and reducing
-// the row maxima in the workgroup (436-511 us: at 246 VGPRs one workgroup per CU, its load, transform
-// and store phases serialised), against 142-238 + 165 us for the out kernel + slice.
+// wino88i32_out_kernel: the fp32 tower's output transform + BN (+ residual) + ReLU -> Y (optional), then
+// the next conv's V as row-line digits under each row's exponent -- what wino88_out_kernel's fp32 V
+// followed by wino88i_slice_kernel<512, float, 4, true> gives, bit for bit, without V's HBM round trip.
+// One 512-thread workgroup per board, thread = channel, so the 512 channels of a row (the exponent's
+// domain) are in one workgroup. V is computed twice from the column pass, which stays in registers (80
+// floats): once for the row maxima (a halving shuffle reduction per wave, then LDS over the 8 waves), once
+// for the digits -- the same fmaf chains on the same inputs, so the same bits. A thread's 4 digits of a
+// point go through a 4x4 byte transpose within its lane quad (two DPP exchanges + v_perm), so every lane
+// stores one dword and each half-wave writes one whole 128-byte line.
+// (Round 4 dropped a form that kept all 100 V values in registers for the reduction: 246 VGPRs, one
+// workgroup per CU, 436-511 us per layer against 142-238 + 165 us for the out kernel + slice,
+// profiles/r04_i8f32_fused_out.log; and an output kernel computing only the row maxima plus a second
+// input-transform pass, 294-356 + 220 us, profiles/r04_i8f32_outmax_form.log.)
+
+// lane quad q = lane & 3 holds P = digits 0..3 of its channel (byte d = digit d); returns digit q of the
+// quad's 4 channels (byte j = channel 4 (lane / 4) + j)
+__device__ inline unsigned i8_quad_transpose(unsigned P, int lane) {
+    const unsigned q1 = (unsigned)__builtin_amdgcn_mov_dpp((int)P, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+    // even lane: [P.0 q1.0 P.2 q1.2], odd: [q1.1 P.1 q1.3 P.3]
+    const unsigned R = __builtin_amdgcn_perm(q1, P, (lane & 1) ? 0x03070105u : 0x06020400u);
+    const unsigned r2 = (unsigned)__builtin_amdgcn_mov_dpp((int)R, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+    // lanes 0, 1 of the quad: [R.0 R.1 r2.0 r2.1], lanes 2, 3: [r2.2 r2.3 R.2 R.3]
+    return __builtin_amdgcn_perm(r2, R, (lane & 2) ? 0x03020706u : 0x05040100u);
+}
+
+template <bool RESID, bool WRITE_Y>
+__global__ __launch_bounds__(1024) void wino88i32_out_kernel(const float* __restrict__ M, int rows,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift, const float* resid,
+                                                             float* Y, int8_t* __restrict__ V8, int* __restrict__ ex) {
+#pragma clang fp contract(off)
+    constexpr int NK = 512 / 32;
+    __shared__ unsigned red[16][2][5][16];
+    __shared__ int exs[100];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+    const int c = w * 32 + (lane & 31), b = blockIdx.x;
+    float t2[10][4];  // B10^T of the plane's columns 4h .. 4h+3
+    {
+        float x2[4][8];
+        wino88_out_plane_half<RESID, WRITE_Y>(M, rows, b, c, h, scale[c], shift[c], resid, Y, x2);
+        wino88_input_cols(x2, h, t2);
+    }
+#pragma unroll
+    for (int aa = 0; aa < 5; ++aa) {
+        float o[10];
+        wino88_input_row(t2, h, aa, o);
+        unsigned m[10];
+#pragma unroll
+        for (int bb = 0; bb < 10; ++bb) m[bb] = __float_as_uint(o[bb]) & 0x7fffffffu;
+        const unsigned r = i8_half_max10(m, lane);
+        if ((lane & 16) == 0 && (lane & 15) < 10) red[w][h][aa][lane & 15] = r;
+    }
+    __syncthreads();
+    if (threadIdx.x < 100) {
+        const int xi = threadIdx.x, a = xi / 10, bb = xi % 10, hh = a / 5, aa = a % 5;
+        unsigned m = 0;
+#pragma unroll
+        for (int ww = 0; ww < 16; ++ww) m = red[ww][hh][aa][bb] > m ? red[ww][hh][aa][bb] : m;
+        const int e = i8_row_exponent_f32(m);
+        exs[xi] = e;
+        ex[(size_t)xi * rows + b] = e;
+    }
+    __syncthreads();
+    // row line (xi, kc = w, b): 128 bytes, digit d of channel 32 kc + i at byte 32 d + i
+    const int q = lane & 3;
+    int8_t* dst0 = V8 + ((size_t)w * rows + b) * 128 + q * 32 + (c & 28);
+#pragma unroll
+    for (int aa = 0; aa < 5; ++aa) {
+        float o[10];
+        wino88_input_row(t2, h, aa, o);
+        const int a = 5 * h + aa;
+#pragma unroll
+        for (int bb = 0; bb < 10; ++bb) {
+            const int xi = a * 10 + bb;
+            int dg[kI8DigitsF32];
+            i8_digits<kI8DigitsF32>(o[bb], exs[xi], dg);
+            const unsigned P = (dg[0] & 0xff) | (dg[1] & 0xff) << 8 | (dg[2] & 0xff) << 16 | (unsigned)dg[3] << 24;
+            *(unsigned*)(dst0 + (size_t)xi * NK * rows * 128) = i8_quad_transpose(P, lane);
+        }
+    }
+}
 
 }  // namespace kv

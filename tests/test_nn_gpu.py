@@ -116,8 +116,8 @@ def test_wino88_batch_invariance(precision):
 
 @pytest.mark.parametrize("variant", ["peaked", "stress"])
 def test_i8_digits_track_fp64_domain(variant):
-    """The int8-digit GEMMs (KV_PREC_I8X5) compute the exact dot products of
-    35-bit truncated rows, so the tower lands on the fp64-MFMA tower's outputs to
+    """The int8-digit GEMMs (KV_PREC_I8X5: per-row 35-bit block fixed point, 15 of 25 digit pairs, exact
+    int32 levels) are within ~2^-36 of the fp64 products, so the tower lands on the fp64-MFMA tower's outputs to
     within the truncation (~2^-35 of each row's magnitude) and the fp32 rounding
     of the activations between layers it can flip: logits within 1e-5 (a few
     fp32 ulps of the peaked set's logits, which reach ~30) of KV_PREC_F64W's at

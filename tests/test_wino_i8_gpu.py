@@ -1,8 +1,9 @@
 """KV_PREC_I8X5's slice and GEMM kernels (csrc/kv_wino88i.h) through
 kv_dev_wino88i, bit for bit against the numpy restatement (tests/_i8_digits.py):
-the digits and row exponents of V, and M -- the exact dot products of the
-digit-truncated rows, so any lane-mapping or accumulation slip shows as a
-differing bit. 4 digits (the fp32 domain) use the row-line layout
+the digits and row exponents of V, and M -- per-row block fixed point, the
+digit pairs i + j < digits, exact int32 levels -- so any lane-mapping or
+accumulation slip shows as a differing bit; and M against the fp64 product
+of the unsplit operands within the bound the arithmetic implies. 4 digits (the fp32 domain) use the row-line layout
 [xi][K/32][row][4][32]; 5 digits the planes [xi][K/32][5][row][32]."""
 import ctypes as C
 
@@ -47,3 +48,95 @@ def test_i8_gemm_bit_exact(K, rows, digits):
         want = want.transpose(0, 1, 3, 2, 4)
     assert np.array_equal(dg.reshape(want.shape), want)
     assert np.array_equal(M.view(np.uint64), Mr.view(np.uint64)), float(np.abs(M - Mr).max())
+
+
+def _out(M, scale, shift, resid, fused):
+    from knightvision_amd import _lib
+    L = _lib.lib()
+    R = M.shape[1]
+    Y = np.zeros((R, 64, 512), dtype=np.float32)
+    dg = np.zeros((100, 16, R, 4, 32), dtype=np.int8)
+    ex = np.zeros((100, R), dtype=np.int32)
+    P = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
+    rp = P(np.ascontiguousarray(resid), C.c_float) if resid is not None else None
+    _lib.check(L.kv_dev_wino88i32_out(0, P(np.ascontiguousarray(M), C.c_float), R, P(scale, C.c_float),
+                                      P(shift, C.c_float), rp, int(fused), P(Y, C.c_float), P(dg, C.c_int8),
+                                      P(ex, C.c_int32)), "kv_dev_wino88i32_out")
+    return Y, dg, ex
+
+
+@pytest.mark.parametrize("rows,resid", [(128, False), (128, True), (256, True)])
+def test_i8f32_out_kernel_writes_the_slice_kernels_digits(rows, resid):
+    """wino88i32_out_kernel (output transform + BN (+ residual) + ReLU, then the next V's row-line digits in
+    one kernel) == wino88_out_kernel's fp32 V + wino88i_slice_kernel, bit for bit: Y, every digit and every
+    row exponent. Board 5 is all zero after the ReLU (its V rows: exponent 0, digits 0); every 7th
+    channel sits 2^-12 below the others."""
+    rng = np.random.default_rng(rows + resid)
+    M = (rng.standard_normal((100, rows, 512)) * 0.3).astype(np.float32)
+    M[:, 5, :] = 0.0
+    scale = (0.5 + rng.random(512)).astype(np.float32)
+    scale[::7] *= np.float32(2.0 ** -12)  # channels far below the row max
+    shift = (rng.standard_normal(512) * 0.1).astype(np.float32)
+    shift = -np.abs(shift)  # M = 0 (and resid = 0) on board 5: ReLU(shift) = 0
+    R = (np.abs(rng.standard_normal((rows, 64, 512))) * 0.5).astype(np.float32) if resid else None
+    if resid:
+        R[5] = 0.0
+    Yf, df, ef = _out(M, scale, shift, R, True)
+    Ys, ds, es = _out(M, scale, shift, R, False)
+    assert np.array_equal(Yf.view(np.uint32), Ys.view(np.uint32))
+    assert np.array_equal(ef, es)
+    assert np.array_equal(df, ds)
+    assert (ef[:, 5] == 0).all() and not df[:, :, 5].any()
+    assert len(np.unique(ef)) > 3  # exponents actually vary across rows
+
+
+def _error_bound(V, U, digits, M):
+    """Per-element bound of |M - V U^T| for the kernel's arithmetic (V U^T in fp64 from the unsplit
+    operands): each operand row is scaled by 2^-e (|a| 2^-e < 1) and cut to `digits` base-128 digits, so
+    a 2^-e = sum_i d_i 2^-7(i+1) + rho, |rho| <= rho_max = 2^-(7 digits + 1); the GEMM keeps the digit pairs
+    i + j < digits and drops the rest. Hence
+        |M - V U^T| <= 2^(ev + eu) [rho_max (sum |a 2^-ev| + sum |b 2^-eu|) + 3 K rho_max^2
+                                   + sum_{i + j >= digits} |d_i| . |e_j| 2^-7(i+j+2)]
+                       + the one rounding of M (2^-24 |M| in fp32, 2^-53 in fp64)."""
+    K = V.shape[-1]
+    ev, eu = D.row_exponents(V), D.row_exponents(U)
+    dv, du = np.abs(D.split(V, ev, digits).astype(np.float64)), np.abs(D.split(U, eu, digits).astype(np.float64))
+    rho = 2.0 ** -(7 * digits + 1)
+    an = np.abs(np.ldexp(V, (-ev[..., None]).astype(np.int32))).sum(-1)
+    bn = np.abs(np.ldexp(U, (-eu[..., None]).astype(np.int32))).sum(-1)
+    b = rho * (an[:, :, None] + bn[:, None, :]) + 3 * K * rho * rho
+    for i in range(digits):
+        for j in range(digits):
+            if i + j >= digits:
+                b = b + np.matmul(dv[i], np.swapaxes(du[j], 1, 2)) * 2.0 ** (-7 * (i + j + 2))
+    b = np.ldexp(b, (ev[:, :, None] + eu[:, None, :]).astype(np.int32))
+    return b + np.abs(M) * (2.0 ** -24 if digits == 4 else 2.0 ** -53)
+
+
+@pytest.mark.parametrize("digits", [4, 5])
+def test_i8_gemm_within_derived_bound_of_fp64_product(digits):
+    """M of the int8-digit GEMM against an fp64 matmul of the UNSPLIT operands, on adversarial rows:
+    channels spread over 2^-30 .. 1 of their row's max (so most values keep far fewer than the block's 28 /
+    35 bits), all-equal rows, rows with one large channel, and sign-alternating rows. Every element must be
+    within the bound derived from the arithmetic (_error_bound): per-row block fixed point of 7 x digits
+    bits, digit pairs i + j < digits, exact int32 levels, one rounding."""
+    rng = np.random.default_rng(40 + digits)
+    X, R, K = 100, 128, 512
+    V = np.where(rng.random((X, R, K)) < 0.5, -1.0, 1.0) * np.exp2(-30.0 * rng.random((X, R, K)))
+    V *= np.exp2(rng.integers(-12, 12, size=(X, R, 1)))
+    V[:, 0] = 0.75                        # all-equal rows
+    V[:, 1] = 1e-9
+    V[:, 1, 7] = 3.0                      # one large channel, the rest 2^-31 below it
+    V[:, 2] = np.where(np.arange(K) % 2 == 0, 1.0, -1.0) * (1 + 2.0 ** -20)
+    U = rng.standard_normal((X, 512, K)) * np.exp2(-10.0 * rng.random((X, 512, K)))
+    U[:, 3] = -0.3                        # an all-equal weight row
+    if digits == 4:
+        V, U = V.astype(np.float32).astype(np.float64), U.astype(np.float32).astype(np.float64)
+    M, _, _ = _run(V, U, digits)
+    M64 = np.matmul(V, np.swapaxes(U, 1, 2))
+    bound = _error_bound(V, U, digits, M)
+    err = np.abs(M - M64)
+    ratio = err / np.maximum(bound, 1e-300)
+    print(f"digits {digits}: max |M - VU^T| / bound = {ratio.max():.3f}, max |err| / |M| (|M| > 0) = "
+          f"{(err / np.where(np.abs(M64) > 0, np.abs(M64), np.inf)).max():.2e}")
+    assert (err <= bound).all(), float(ratio.max())
