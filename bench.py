@@ -46,12 +46,15 @@ FLOP_RES_CONV_PER_BOARD = 301989888   # one 3x3 512->512 conv on 8x8 (2*64*512*4
 FLOP_WINO48_GEMM_PER_BOARD = 62914560  # its Winograd F(4x8,3x3) GEMMs: 2 * 2 tiles * 60 * 512 * 512
 FLOP_WINO88_GEMM_PER_BOARD = 52428800  # the fp32 default, F(8x8,3x3) GEMMs: 2 * 1 tile * 100 * 512 * 512
 FP32_MFMA_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md, f32-input MFMA (dense)
-FP64_MFMA_PEAK_TFLOPS = 78.6          # AMD's MI355X FP64 matrix figure (the guides give no f64 row; measured in
-                                      # profiles/r04_f64_mfma_peak.log)
+FP64_MFMA_PEAK_TFLOPS = 78.6          # AMD's MI355X FP64 matrix spec figure (the guides give no f64 row; not
+                                      # measured here)
 PATH_NAMES = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3",
               5: "winograd88_i8", 6: "winograd88_i8f32"}  # KV_PATH_*
 BF16_MFMA_PEAK_TFLOPS = 2500.0        # dense bf16 MFMA
-I8_MFMA_PEAK_TOPS = 5000.0            # dense int8 MFMA: 2x the bf16 rate (cdna_hip_programming.md, MFMA rate per dtype)
+I8_MFMA_PEAK_TOPS = 5000.0            # dense int8 MFMA: 2x the bf16 rate (cdna_hip_programming.md, MFMA rate per dtype);
+                                      # v_mfma_i32_32x32x32_i8 back to back measured 4.1 POPS at the clock the chip
+                                      # holds under it (profiles/r04_mfma_rate.log)
+I8_MFMA_MEASURED_TOPS = 4098.0
 I8_DIGIT_PRODUCTS = {5: 15, 6: 10}    # int8 GEMMs per Winograd GEMM: digit pairs i + j < 5 (KV_PREC_I8X5, fp64
                                       # domain) / < 4 (KV_ALGO_WINOGRAD88_I8, fp32 domain)
 
@@ -70,10 +73,13 @@ def parse():
                          "Winograd F(8x8,3x3) fp32 for the random-init weights)")
     ap.add_argument("--compare-direct", type=int, default=0,
                     help="also measure the fp32 direct implicit-GEMM tower ('fp32_direct'; ~40 s per step at C3)")
+    ap.add_argument("--weights", choices=["init", "stress"], default="init",
+                    help="synthetic weights of the headline run: init (random init, the reference's untrained "
+                         "network) or stress (trained-network magnitudes, weights.stress_state_dict)")
     ap.add_argument("--trained-steps", type=int, default=2,
-                    help="fp32 headline: also time this many moves with the fp64 Winograd domain on int8 digits "
-                         "(KV_PREC_I8X5, the AUTO path for trained-magnitude weights), reported under "
-                         "'trained_weights_path'; 0 to skip")
+                    help="also time this many moves on the stress weights (trained-network magnitudes: AUTO "
+                         "chooses the fp64 Winograd domain on int8 digits there, and the priors are peaked, so the "
+                         "trees take their own shapes), reported under 'trained_weights_path'; 0 to skip")
     ap.add_argument("--f64w-steps", type=int, default=0,
                     help="also time this many moves with the fp64 Winograd domain on fp64 MFMA (KV_PREC_F64W), "
                          "reported under 'f64w_path'")
@@ -402,8 +408,8 @@ def main():
                 print(f"bench: {what} {done}/{n}{el}", file=sys.stderr, flush=True)
 
     def measure(precision, algo="auto", sims=sims, steps=steps, warmup=warmup, keep=False, tag="main",
-                eval_mode="faithful"):
-        eng = SelfPlayEngine(synthetic_state_dict(42, "init"), slots=G, n_games=1 << 40, seed=42, max_moves=None,
+                eval_mode="faithful", weights="init"):
+        eng = SelfPlayEngine(synthetic_state_dict(42, weights), slots=G, n_games=1 << 40, seed=42, max_moves=None,
                              batch=16, sims=sims, game_id_base=rank, game_id_stride=world,
                              eval_mode=(EVAL_LAZY if (eval_mode == "lazy" and sims == 0) else
                                         EVAL_HASH if (eval_mode == "hash" and sims > 0) else EVAL_FAITHFUL),
@@ -439,7 +445,7 @@ def main():
                    conv_ms=d["res_conv_ms"] / max(d["res_conv_launches"], 1), dom_flop=s1["dom_flop"],
                    dom_algo=s1["dom_algo"], dom_path=s1["dom_path"], dom_split=s1["dom_split"],
                    tree_overflows=s1["tree_overflows"], steps=steps, warmup=warmup)
-        if tag == "main":
+        if tag in ("main", "trained"):
             out["calibration"] = eng.calibration()
         if keep:  # the timed region's experience, left in HBM for the gather (MCTS: with pi)
             out["recs_dev"], out["gms"] = eng.records_device(), eng.games()
@@ -447,7 +453,17 @@ def main():
         eng.close()
         return out
 
-    m = measure(args.precision, args.algo, keep=True, eval_mode=args.eval)
+    m = measure(args.precision, args.algo, keep=True, eval_mode=args.eval, weights=args.weights)
+    calib_ranks = None
+    if world > 1:  # every rank must run the same conv path (the calibration is per process)
+        calib_ranks = [None] * world
+        dist.all_gather_object(calib_ranks, {"rank": rank, "path_large": m["calibration"]["path_large"],
+                                             "path_small": m["calibration"]["path_small"],
+                                             "err_logit": m["calibration"]["err_logit"],
+                                             "err_value": m["calibration"]["err_value"]})
+        paths = {(c["path_large"], c["path_small"]) for c in calib_ranks}
+        if len(paths) != 1:
+            raise SystemExit(f"bench.py: ranks chose different conv paths {calib_ranks}")
     dt, plies, games_done, nn_rows, sims_done, conv_ms = (m[k] for k in ("dt", "plies", "games_done", "nn_rows",
                                                                           "sims", "conv_ms"))
 
@@ -492,8 +508,9 @@ def main():
     if args.compare_direct and args.precision == "fp32" and m["dom_path"] != 0:
         direct = measure("fp32", "direct", steps=1, warmup=1, tag="direct")
     trained = None
-    if args.trained_steps > 0 and args.precision == "fp32" and m["dom_path"] != 5:
-        trained = measure("i8x5", steps=args.trained_steps, warmup=args.alt_warmup, tag="i8x5")
+    if args.trained_steps > 0 and args.precision == "fp32" and args.weights != "stress":
+        trained = measure("fp32", "auto", steps=args.trained_steps, warmup=args.alt_warmup, tag="trained",
+                          weights="stress")
     f64w = None
     if args.f64w_steps > 0 and args.precision == "fp32" and m["dom_path"] != 3:
         f64w = measure("f64w", steps=args.f64w_steps, warmup=args.alt_warmup, tag="f64w")
@@ -547,7 +564,8 @@ def main():
             "metric": metric, "value": value, "unit": unit, "n_gpus": world, "steps": steps, "warmup": warmup,
             "ms_per_step": dt * 1e3 / steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": args.precision,
-            "data": "synthetic (random-init weights seed 42, self-play from the start position, per-game seeds)",
+            "data": (f"synthetic ({'random-init' if args.weights == 'init' else 'trained-magnitude (stress)'} weights "
+                     "seed 42, self-play from the start position, per-game seeds)"),
             "config": {"workload": wl + (" (BASELINE configs[2], C3)" if (mcts and G == 2048 and sims == 800) else ""),
                        "slots_per_gpu": G, "sims_per_move": sims, "nn_batch": G, "parallelism": f"games sharded x{world}",
                        "step": "one move of every slot (the whole search + the committed move)" if mcts else
@@ -588,7 +606,13 @@ def main():
             "mean_plies_per_game": mean_len,
             "tree_overflows": m["tree_overflows"],
             "roofline": {"bound": "mfma",
-                         "kernel": kname + kdesc,
+                         "kernel": kname + kdesc + (
+                             "; GEMM only: the operands' int8 digits come from the previous output kernel "
+                             "(wino88i32_out_kernel, which writes them instead of fp32 V; conv2's from a slice "
+                             "kernel)" if path == 6 else ""),
+                         "measured_peak_note": (f"v_mfma_i32_32x32x32_i8 back to back: {I8_MFMA_MEASURED_TOPS:.0f} "
+                                                "TOPS at the clock held (profiles/r04_mfma_rate.log)"
+                                                if path in I8_DIGIT_PRODUCTS else None),
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "operations": ("int8 multiply-adds of the digit products (2 operations each) against the "
                                         "dense int8 MFMA peak" if path in I8_DIGIT_PRODUCTS else
@@ -630,22 +654,31 @@ def main():
             0: "fp32 direct implicit-GEMM convs"}.get(path)
         if pg_info is not None:
             out["process_group"] = pg_info
+        if calib_ranks is not None:
+            out["calibration_ranks"] = calib_ranks
         if trained is not None:
+            tp = trained["dom_path"]
             t_ach = (FLOP_WINO88_GEMM_PER_BOARD * bpl / (trained["conv_ms"] * 1e-3) / 1e12) \
                 if trained["conv_ms"] > 0 else None
             out["trained_weights_path"] = {
-                "note": "the same workload on the fp64 Winograd domain with the GEMMs on int8 digits (KV_PREC_I8X5): "
-                        "the path AUTO runs for weights at trained magnitudes, where no fp32 Winograd tower holds the "
-                        "1e-4 logit tolerance (learn-loop weights after 20 iterations: F(8x8) fp32 1.0e-4 / value "
-                        "3.4e-5; the stress set 3.8e-3; tests/test_nn_accuracy_gpu.py, profiles/r04_*accuracy*)",
+                "note": "the same workload on the stress weights (weights.stress_state_dict: trained-network "
+                        "magnitudes, BN statistics of the data, logits of std 4 -- what a checkpoint looks like, "
+                        "scripts/self_play.py:71-77) under fp32 + AUTO: no fp32 Winograd tower holds the 1e-4 "
+                        "logit tolerance there, so the calibration picks the fp64 Winograd domain with int8-digit "
+                        "GEMMs; the peaked priors give the trees their own shapes",
+                "weights": "stress", "conv_path": PATH_NAMES.get(tp),
+                "calibration": {k: trained["calibration"][k] for k in ("path_large", "path_small", "err_logit",
+                                                                      "err_value", "ms")},
                 "value": (trained["sims"] if mcts else trained["plies"]) / trained["dt"], "unit": unit,
                 "steps": trained["steps"], "warmup": trained["warmup"],
                 "ms_per_step": trained["dt"] * 1e3 / trained["steps"],
-                "dominant_kernel": gemm_label(5, G, 0)[0], "res_gemm_avg_launch_ms": trained["conv_ms"],
-                "res_gemm_fp64_equiv_tflops": t_ach,
-                "res_gemm_i8_tops": (t_ach * I8_DIGIT_PRODUCTS[5]) if t_ach else None, "peak_i8_tops": I8_MFMA_PEAK_TOPS,
-                "res_gemm_frac_i8": (t_ach * I8_DIGIT_PRODUCTS[5] / I8_MFMA_PEAK_TOPS) if t_ach else None,
-                "res_gemm_over_fp64_mfma_peak": (t_ach / FP64_MFMA_PEAK_TFLOPS) if t_ach else None}
+                "dominant_kernel": gemm_label(tp, G, 0)[0], "res_gemm_avg_launch_ms": trained["conv_ms"],
+                "res_gemm_fp64_equiv_tflops": t_ach if tp == 5 else None,
+                "res_gemm_i8_tops": (t_ach * I8_DIGIT_PRODUCTS[tp]) if (t_ach and tp in I8_DIGIT_PRODUCTS) else None,
+                "peak_i8_tops": I8_MFMA_PEAK_TOPS,
+                "res_gemm_frac_i8": (t_ach * I8_DIGIT_PRODUCTS[tp] / I8_MFMA_PEAK_TOPS)
+                if (t_ach and tp in I8_DIGIT_PRODUCTS) else None,
+                "res_gemm_over_fp64_mfma_peak": (t_ach / FP64_MFMA_PEAK_TFLOPS) if (t_ach and tp == 5) else None}
         if f64w is not None:
             f_ach = (FLOP_WINO88_GEMM_PER_BOARD * bpl / (f64w["conv_ms"] * 1e-3) / 1e12) if f64w["conv_ms"] > 0 \
                 else None

@@ -305,14 +305,16 @@ int kv_dev_py_random(int device, const uint64_t* seeds, int n, int count, double
  * kernel: M [100][rows][512] (digits 5: KV_PREC_I8X5's fp64 M; 4: the fp32
  * domain's (KV_ALGO_WINOGRAD88_I8) fp32 M, widened); v_digits (5 digits: planes
  * [100][K/32][5][rows][32]; 4 digits: row lines [100][K/32][rows][4][32]) and
- * v_exp [100][rows] (either may be NULL) return V's digits and row exponents. */
-int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, int digits, double* M,
+ * v_exp [100][rows] (either may be NULL) return V's digits and row exponents. seg 1 (4 digits, K 512):
+ * V's exponents per 256-channel segment (v_exp [100][2][rows]), the fp32 tower's default form. */
+int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, int digits, int seg, double* M,
                    int8_t* v_digits, int* v_exp);
 /* The fp32 tower's residual output kernel on int8 digits (KV_ALGO_WINOGRAD88_I8): M [100][rows][512] fp32
  * (rows a multiple of 128), folded BN scale / shift [512], resid [rows][64][512] or NULL -> Y
  * [rows][64][512] (= ReLU(A^T M A * scale + shift (+ resid))) and the next conv's V as row-line digits
- * [100][16][rows][4][32] with row exponents [100][rows]. fused 1: the product's one-kernel form
- * (wino88i32_out_kernel); 0: wino88_out_kernel's fp32 V then the slice kernel (bit-identical). */
+ * [100][16][rows][4][32] with row exponents [100][rows]. fused bit 0 set: the product's one-kernel form
+ * (wino88i32_out_kernel), clear: wino88_out_kernel's fp32 V then the slice kernel (bit-identical); bit 1:
+ * exponents per 256-channel segment ([100][2][rows]) instead of per row. */
 int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scale, const float* shift,
                          const float* resid, int fused, float* Y, int8_t* v_digits, int* v_exp);
 /* Timing / A-B harness of the fp32 tower's int8-digit GEMM on seeded random digits (rows boards, K 256 or

@@ -111,7 +111,7 @@ def _declare(L):
         "kv_dev_dirichlet": ([i, P(C.c_uint64), i, C.c_double, i, i, P(C.c_double), P(i64), P(C.c_double)], i),
         "kv_dev_py_random": ([i, P(C.c_uint64), i, i, P(C.c_double)], i),
         "kv_host_libm": ([i, P(C.c_double), P(C.c_double), i, P(C.c_double)], i),
-        "kv_dev_wino88i": ([i, P(C.c_double), i, P(C.c_double), i, i, P(C.c_double), P(C.c_int8), P(i)], i),
+        "kv_dev_wino88i": ([i, P(C.c_double), i, P(C.c_double), i, i, i, P(C.c_double), P(C.c_int8), P(i)], i),
         "kv_dev_i8gemm_bench": ([i, i, i, i, i, P(C.c_float), P(C.c_float)], i),
         "kv_dev_wino88i32_out": ([i, P(C.c_float), i, P(C.c_float), P(C.c_float), P(C.c_float), i, P(C.c_float),
                                   P(C.c_int8), P(i)], i),

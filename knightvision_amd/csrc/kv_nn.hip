@@ -804,7 +804,7 @@ static int net_reserve(kv_net* net, int nb_pad) {
     KV_HIP(hipMalloc(&net->V256, (size_t)cap * kWs256Board));
     KV_HIP(hipMalloc(&net->vmax, (size_t)12 * cap * sizeof(unsigned)));
     KV_HIP(hipMalloc(&net->V8, (size_t)cap * kv::W88_XI * 512 * kv::kI8Digits));
-    KV_HIP(hipMalloc(&net->ev8, (size_t)cap * kv::W88_XI * sizeof(int)));
+    KV_HIP(hipMalloc(&net->ev8, (size_t)cap * kv::W88_XI * 2 * sizeof(int)));  // 2: segment exponents
     KV_HIP(hipMalloc(&net->evmax8, (size_t)cap * kv::W88_XI * sizeof(unsigned)));
     if (!net->slab)  // 48 splits x 16 boards x 64 px x 512 channels
         KV_HIP(hipMalloc(&net->slab, (size_t)(144 / kSplitKt) * kSplitMaxBoards * 64 * 512 * 4));
@@ -1098,12 +1098,13 @@ static int wino88d_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 // ---- F(8x8) on int8 digits (kv_wino88i.h): the fp64 tower's transforms, V64 sliced into digits
 // before each GEMM ----
 // (4 digits: the fp32 domain's row-line layout)
-template <int K, int D = kv::kI8Digits, class T>
+// (NSEG 2: V's exponents per 256-channel segment, K 512 only)
+template <int K, int D = kv::kI8Digits, class T, int NSEG = 1>
 static int launch_wino88i_slice(const T* src, int n, int slab_rows, int nslab, int8_t* dst, int* ex,
                                 hipStream_t st) {
     const int waves = n * nslab;
-    hipLaunchKernelGGL((kv::wino88i_slice_kernel<K, T, D, D == kv::kI8DigitsF32>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st,
-                       src, n, slab_rows, nslab, dst, ex);
+    hipLaunchKernelGGL((kv::wino88i_slice_kernel<K, T, D, D == kv::kI8DigitsF32, NSEG>),
+                       dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, src, n, slab_rows, nslab, dst, ex);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -1135,11 +1136,11 @@ static int launch_wino88i_gemm(const int8_t* V8, const int* ev, const int8_t* U8
 
 // the fp32 tower's int8-digit GEMM, round-5 form (kv_wino88i.h wino88i32_gemm_kernel): persistent
 // workgroups, one per CU (grid a multiple of 8, at most the tile count), or one tile each (persist false)
-template <int K, int KS, int NBUF>
+template <int K, int KS, int NBUF, int NSEG = 1>
 static int launch_wino88i32_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
                                  int rows, int stride, bool persist, hipStream_t st) {
     using T = kv::I8G32<KS, NBUF>;
-    auto kern = kv::wino88i32_gemm_kernel<K, KS, NBUF>;
+    auto kern = kv::wino88i32_gemm_kernel<K, KS, NBUF, NSEG>;
     KV_HIP(lds_opt_in((const void*)kern, (int)T::BYTES));
     const int ntiles = kv::W88_XI * (rows / T::WN) * (512 / T::WM);
     KV_REQUIRE(rows % T::WN == 0 && stride % T::WN == 0 && ntiles % 8 == 0, KV_EINVAL,
@@ -1205,26 +1206,55 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 }
 
 // ---- the fp32 domain on int8 digits (KV_PATH_WINO88_I8F32): the fp32 F(8x8) tower's transforms; each
-// residual conv's output kernel (wino88i32_out_kernel, one workgroup per board) writes the next conv's V
-// directly as row-line digits under its row exponents. conv2's V256 (from the stem, 256 channels) goes
-// through the slice kernel. KV_I8F32_SLICE=1 (A/B probe): the round-4 form, wino88_out_kernel's fp32 V
-// + the slice kernel for every conv (the same digits, bit for bit) ----
-static bool i8f32_slice_form() {
-    static const bool v = [] {
-        const char* e = getenv("KV_I8F32_SLICE");
-        return e && e[0] == '1';
+// residual conv's output kernel (wino88i32_out_kernel) writes the next conv's V directly as row-line digits.
+// conv2's V256 (from the stem, 256 channels) goes through the slice kernel. Forms (read once from the
+// environment; A/B probes, the defaults are the measured fastest):
+//   KV_I8F32_SEG   0 (default): V's exponents per row (one 512-channel output workgroup per board); 1: per
+//                  256-channel segment -- the output kernel's workgroup is 256 channels of a board, two per
+//                  CU -- and the GEMM combines the two segments
+//   KV_I8F32_SLICE 1: wino88_out_kernel's fp32 V + the slice kernel (the round-4 form; the same digits)
+//   KV_I8F32_GEMM  r4: the round-4 GEMM kernel (per-row exponents only); else the round-5 persistent one ----
+struct I8f32Form {
+    bool seg = false, slice = false, r4 = false;
+};
+static const I8f32Form& i8f32_form() {
+    static const I8f32Form f = [] {
+        I8f32Form x;
+        const char* e = getenv("KV_I8F32_SEG");
+        x.seg = e && e[0] == '1';
+        e = getenv("KV_I8F32_SLICE");
+        x.slice = e && e[0] == '1';
+        e = getenv("KV_I8F32_GEMM");
+        x.r4 = e && !strcmp(e, "r4") && !x.seg;
+        return x;
     }();
-    return v;
+    return f;
 }
 
 template <bool RESID, bool WRITE_Y>
 static int launch_wino88i32_out(kv_net* net, int l, const float* M, int nb, int stride, const float* resid,
-                                float* Y, int8_t* V8, int* ev, hipStream_t st) {
+                                float* Y, int8_t* V8, int* ev, bool seg, hipStream_t st) {
     const float* W = net->w;
-    hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y>), dim3(nb), dim3(1024), 0, st, M, stride,
-                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, V8, ev);
+    if (seg)
+        hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y, 256>), dim3(2, nb), dim3(512), 0, st, M, stride,
+                           W + net->off.scale[l], W + net->off.shift[l], resid, Y, V8, ev);
+    else
+        hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y, 512>), dim3(1, nb), dim3(1024), 0, st, M, stride,
+                           W + net->off.scale[l], W + net->off.shift[l], resid, Y, V8, ev);
     KV_HIP(hipGetLastError());
     return KV_OK;
+}
+
+// the fp32 tower's int8-digit GEMM of one conv (K 256: one segment, per-row exponents)
+template <int K>
+static int i8f32_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M, int rows, int stride,
+                      bool seg, hipStream_t st) {
+    constexpr int D = kv::kI8DigitsF32;
+    const I8f32Form& f = i8f32_form();
+    if constexpr (K == 512)
+        if (seg) return launch_wino88i32_gemm<K, 32, 3, 2>(V8, ev, U8, eu, M, rows, stride, true, st);
+    if (f.r4) return launch_wino88i_gemm<K, D>(V8, ev, U8, eu, M, rows, stride, st);
+    return launch_wino88i32_gemm<K, 32, 3, 1>(V8, ev, U8, eu, M, rows, stride, true, st);
 }
 
 // conv l's GEMM; slice: V (fp32) -> digits first. (mark: the engine's timing hook brackets the slice, when
@@ -1232,19 +1262,21 @@ static int launch_wino88i32_out(kv_net* net, int l, const float* M, int nb, int 
 static int wino88i32_gemm_layer(kv_net* net, int l, int K, int rows, int stride, bool slice, bool mark,
                                 hipStream_t st) {
     constexpr int D = kv::kI8DigitsF32;
+    const bool seg = K == 512 && i8f32_form().seg;
     float* M = (float*)net->Mw;
     int rc;
     if (mark && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
     if (slice) {
         const float* Vsrc = K == 256 ? (const float*)net->V256 : (const float*)net->V;
         rc = K == 256 ? launch_wino88i_slice<256, D>(Vsrc, rows, stride, kv::W88_XI, net->V8, net->ev8, st)
+             : seg    ? launch_wino88i_slice<512, D, float, 2>(Vsrc, rows, stride, kv::W88_XI, net->V8, net->ev8, st)
                       : launch_wino88i_slice<512, D>(Vsrc, rows, stride, kv::W88_XI, net->V8, net->ev8, st);
         if (rc) return rc;
     }
     const int8_t* U = net->U88i32 + net->uoff88[l] * D;
     const int* eu = net->eu88i32 + net->euoff[l];
-    rc = K == 256 ? launch_wino88i_gemm<256, D>(net->V8, net->ev8, U, eu, M, rows, stride, st)
-                  : launch_wino88i_gemm<512, D>(net->V8, net->ev8, U, eu, M, rows, stride, st);
+    rc = K == 256 ? i8f32_gemm<256>(net->V8, net->ev8, U, eu, M, rows, stride, false, st)
+                  : i8f32_gemm<512>(net->V8, net->ev8, U, eu, M, rows, stride, seg, st);
     if (rc) return rc;
     if (mark && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
     return KV_OK;
@@ -1254,11 +1286,11 @@ static int wino88i32_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     const int rows = nb, stride = rows;
     float* V = (float*)net->V;
     const float* M = (const float*)net->Mw;
-    const bool sf = i8f32_slice_form();
+    const bool sf = i8f32_form().slice, seg = i8f32_form().seg;
     int rc;
     if ((rc = wino88i32_gemm_layer(net, 1, 256, rows, stride, true, false, st))) return rc;
     rc = sf ? launch_wino88_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st)
-            : launch_wino88i32_out<false, true>(net, 1, M, nb, stride, nullptr, net->X, net->V8, net->ev8, st);
+            : launch_wino88i32_out<false, true>(net, 1, M, nb, stride, nullptr, net->X, net->V8, net->ev8, seg, st);
     if (rc) return rc;
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
     for (int r = 0; r < 5; ++r) {
@@ -1266,14 +1298,16 @@ static int wino88i32_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
         const bool m = mark && r == 2;
         if ((rc = wino88i32_gemm_layer(net, l1, 512, rows, stride, sf, m, st))) return rc;
         rc = sf ? launch_wino88_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st)
-                : launch_wino88i32_out<false, false>(net, l1, M, nb, stride, nullptr, nullptr, net->V8, net->ev8, st);
+                : launch_wino88i32_out<false, false>(net, l1, M, nb, stride, nullptr, nullptr, net->V8, net->ev8, seg,
+                                                     st);
         if (rc) return rc;
         if ((rc = wino88i32_gemm_layer(net, l2, 512, rows, stride, sf, false, st))) return rc;
         if (r == 4)
             rc = launch_wino88_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
         else
             rc = sf ? launch_wino88_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
-                    : launch_wino88i32_out<true, true>(net, l2, M, nb, stride, net->X, net->X, net->V8, net->ev8, st);
+                    : launch_wino88i32_out<true, true>(net, l2, M, nb, stride, net->X, net->X, net->V8, net->ev8, seg,
+                                                       st);
         if (rc) return rc;
     }
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
@@ -1903,11 +1937,13 @@ int kv_net_forward_boards_legal(kv_net* net, const int8_t* boards_dev, int B, co
     return rc;
 }
 
-int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, int digits, double* M,
+int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, int digits, int seg, double* M,
                    int8_t* v_digits, int* v_exp) {
-    KV_REQUIRE(V && U && M && rows > 0 && rows % 128 == 0 && (K == 256 || K == 512) && (digits == 4 || digits == 5),
+    KV_REQUIRE(V && U && M && rows > 0 && rows % 128 == 0 && (K == 256 || K == 512) && (digits == 4 || digits == 5) &&
+                   (!seg || (digits == 4 && K == 512)),
                KV_EINVAL, "kv_dev_wino88i: bad arguments (rows %d must be a multiple of 128, K %d 256 or 512, "
-               "digits %d 4 or 5)", rows, K, digits);
+               "digits %d 4 or 5, segments %d only with 4 digits and K 512)", rows, K, digits, seg);
+    const int nseg = seg ? 2 : 1;
     KV_HIP(hipSetDevice(device));
     const size_t nv = (size_t)kv::W88_XI * rows * K, nu = (size_t)kv::W88_XI * 512 * K;
     const size_t nm = (size_t)kv::W88_XI * rows * 512;
@@ -1921,7 +1957,7 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
     KV_HIP(dmf.alloc(nm));
     KV_HIP(v8.alloc(nv * digits));
     KV_HIP(u8.alloc(nu * digits));
-    KV_HIP(ev.alloc((size_t)kv::W88_XI * rows));
+    KV_HIP(ev.alloc((size_t)kv::W88_XI * rows * nseg));
     KV_HIP(eu.alloc((size_t)kv::W88_XI * 512));
     KV_HIP(hipMemcpy(dv.p, V, nv * sizeof(double), hipMemcpyHostToDevice));
     KV_HIP(hipMemcpy(du.p, U, nu * sizeof(double), hipMemcpyHostToDevice));
@@ -1941,10 +1977,11 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
                       : launch_wino88i_slice<512, D>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0);
         if (!rc)
             rc = K == 256 ? launch_wino88i_slice<256, D>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0)
+                 : seg    ? launch_wino88i_slice<512, D, double, 2>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0)
                           : launch_wino88i_slice<512, D>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
-        if (!rc)
-            rc = K == 256 ? launch_wino88i_gemm<256, D>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, 0)
-                          : launch_wino88i_gemm<512, D>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, 0);
+        if (!rc)  // the product's GEMM for this exponent form (i8f32_gemm)
+            rc = K == 256 ? i8f32_gemm<256>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, false, 0)
+                          : i8f32_gemm<512>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, seg != 0, 0);
     }
     if (rc) return rc;
     KV_HIP(hipDeviceSynchronize());
@@ -1956,7 +1993,7 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
         for (size_t i = 0; i < nm; ++i) M[i] = mf[i];
     }
     if (v_digits) KV_HIP(hipMemcpy(v_digits, v8.p, nv * digits, hipMemcpyDeviceToHost));
-    if (v_exp) KV_HIP(hipMemcpy(v_exp, ev.p, (size_t)kv::W88_XI * rows * sizeof(int), hipMemcpyDeviceToHost));
+    if (v_exp) KV_HIP(hipMemcpy(v_exp, ev.p, (size_t)kv::W88_XI * rows * nseg * sizeof(int), hipMemcpyDeviceToHost));
     return KV_OK;
 }
 
@@ -1975,7 +2012,8 @@ int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scal
     KV_HIP(dy.alloc(ny));
     KV_HIP(dv.alloc(nm));
     KV_HIP(v8.alloc(nm * kv::kI8DigitsF32));
-    KV_HIP(ev.alloc((size_t)kv::W88_XI * rows));
+    const bool seg = (fused & 2) != 0;
+    KV_HIP(ev.alloc((size_t)kv::W88_XI * rows * 2));
     KV_HIP(hipMemcpy(dm.p, M, nm * sizeof(float), hipMemcpyHostToDevice));
     KV_HIP(hipMemcpy(dsc.p, scale, 512 * sizeof(float), hipMemcpyHostToDevice));
     KV_HIP(hipMemcpy(dsh.p, shift, 512 * sizeof(float), hipMemcpyHostToDevice));
@@ -1986,13 +2024,22 @@ int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scal
     const float* sc = dsc.p;
     const float* sh = dsh.p;
     // Y doubles as the residual (in place, as the tower runs it)
-    if (fused) {
-        if (resid)
-            hipLaunchKernelGGL((kv::wino88i32_out_kernel<true, true>), dim3(rows), dim3(1024), 0, 0, dm.p, rows, sc,
-                               sh, dy.p, dy.p, v8.p, ev.p);
-        else
-            hipLaunchKernelGGL((kv::wino88i32_out_kernel<false, true>), dim3(rows), dim3(1024), 0, 0, dm.p, rows, sc,
-                               sh, nullptr, dy.p, v8.p, ev.p);
+    if (fused & 1) {
+        if (resid) {
+            if (seg)
+                hipLaunchKernelGGL((kv::wino88i32_out_kernel<true, true, 256>), dim3(2, rows), dim3(512), 0, 0, dm.p,
+                                   rows, sc, sh, dy.p, dy.p, v8.p, ev.p);
+            else
+                hipLaunchKernelGGL((kv::wino88i32_out_kernel<true, true, 512>), dim3(1, rows), dim3(1024), 0, 0, dm.p,
+                                   rows, sc, sh, dy.p, dy.p, v8.p, ev.p);
+        } else {
+            if (seg)
+                hipLaunchKernelGGL((kv::wino88i32_out_kernel<false, true, 256>), dim3(2, rows), dim3(512), 0, 0, dm.p,
+                                   rows, sc, sh, nullptr, dy.p, v8.p, ev.p);
+            else
+                hipLaunchKernelGGL((kv::wino88i32_out_kernel<false, true, 512>), dim3(1, rows), dim3(1024), 0, 0,
+                                   dm.p, rows, sc, sh, nullptr, dy.p, v8.p, ev.p);
+        }
         KV_HIP(hipGetLastError());
     } else {
         if (resid)
@@ -2002,13 +2049,14 @@ int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scal
             hipLaunchKernelGGL((kv::wino88_out_kernel<false, true, true>), dim3(512 / 256, rows), dim3(256), 0, 0,
                                dm.p, rows, sc, sh, nullptr, dy.p, dv.p);
         KV_HIP(hipGetLastError());
-        int rc = launch_wino88i_slice<512, kv::kI8DigitsF32>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
+        int rc = seg ? launch_wino88i_slice<512, kv::kI8DigitsF32, float, 2>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0)
+                     : launch_wino88i_slice<512, kv::kI8DigitsF32>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
         if (rc) return rc;
     }
     KV_HIP(hipDeviceSynchronize());
     KV_HIP(hipMemcpy(Y, dy.p, ny * sizeof(float), hipMemcpyDeviceToHost));
     KV_HIP(hipMemcpy(v_digits, v8.p, nm * kv::kI8DigitsF32, hipMemcpyDeviceToHost));
-    KV_HIP(hipMemcpy(v_exp, ev.p, (size_t)kv::W88_XI * rows * sizeof(int), hipMemcpyDeviceToHost));
+    KV_HIP(hipMemcpy(v_exp, ev.p, (size_t)kv::W88_XI * rows * (seg ? 2 : 1) * sizeof(int), hipMemcpyDeviceToHost));
     return KV_OK;
 }
 
@@ -2034,11 +2082,11 @@ int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, flo
     kv::DevBuf<float> m;
     KV_HIP(v8.alloc(lv * 128));
     KV_HIP(u8.alloc(lu * 128));
-    KV_HIP(ev.alloc((size_t)kv::W88_XI * rows));
+    KV_HIP(ev.alloc((size_t)kv::W88_XI * rows * 2));
     KV_HIP(eu.alloc((size_t)kv::W88_XI * 512));
     KV_HIP(m.alloc(nm));
     hipLaunchKernelGGL(i8_fill_kernel, dim3((unsigned)((lv * 128 + 255) / 256)), dim3(256), 0, 0, v8.p, lv, ev.p,
-                       (size_t)kv::W88_XI * rows, 1234u);
+                       (size_t)kv::W88_XI * rows * 2, 1234u);
     hipLaunchKernelGGL(i8_fill_kernel, dim3((unsigned)((lu * 128 + 255) / 256)), dim3(256), 0, 0, u8.p, lu, eu.p,
                        (size_t)kv::W88_XI * 512, 99u);
     KV_HIP(hipGetLastError());
@@ -2058,6 +2106,9 @@ int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, flo
                               : launch_wino88i32_gemm<256, 64, 2>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);
             case 5: return k5 ? launch_wino88i32_gemm<512, 64, 2>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, false, 0)
                               : launch_wino88i32_gemm<256, 64, 2>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, false, 0);
+            case 6:  // segment exponents (K 512): a different M from the same digits (timing only)
+                KV_REQUIRE(k5, KV_EINVAL, "kv_dev_i8gemm_bench: variant 6 needs K 512");
+                return launch_wino88i32_gemm<512, 32, 3, 2>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);
             default: KV_REQUIRE(false, KV_EINVAL, "kv_dev_i8gemm_bench: variant %d", variant);
         }
     };

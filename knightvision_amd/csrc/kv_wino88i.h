@@ -83,13 +83,15 @@ __device__ inline void i8_digits(T v, int e, int (&d)[D]) {
 // ex[x * slab_rows + r]. One wave per row; lane l holds channels
 // [l * K/64, (l + 1) * K/64). RL (row lines, 4 digits only): digit d of the
 // 32 channels goes to (((x * K/32 + kc) * slab_rows + r) * 4 + d) * 32 instead
-// -- the 4 digits of one row's chunk are one 128-byte line.
-template <int K, class T, int D, bool RL = false>
+// -- the 4 digits of one row's chunk are one 128-byte line. NSEG = 2 (K = 512 only): one exponent per
+// 256-channel segment instead of per row (lanes 0-31 hold segment 0), at ex[(x * 2 + seg) * slab_rows + r].
+template <int K, class T, int D, bool RL = false, int NSEG = 1>
 __global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict__ src, int n, int slab_rows,
                                                             int nslab, int8_t* __restrict__ dst,
                                                             int* __restrict__ ex) {
     static_assert(K == 256 || K == 512, "rows of 256 or 512 channels");
     static_assert(!RL || D == 4, "row lines hold 4 digits");
+    static_assert(NSEG == 1 || (NSEG == 2 && K == 512), "segments of 256 channels");
     constexpr int CPL = K / 64;  // 4 or 8 channels per lane
     const int lane = threadIdx.x & 63;
     const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -112,12 +114,13 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict_
         m = hw > m ? hw : m;
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
+    for (int o = 64 / (2 * NSEG); o > 0; o >>= 1) {
         const unsigned t = (unsigned)__shfl_xor((int)m, o, 64);
         m = t > m ? t : m;
     }
     const int e = sizeof(T) == 8 ? i8_row_exponent(m) : i8_row_exponent_f32(m);
-    if (lane == 0) ex[row] = e;
+    if (NSEG == 1 && lane == 0) ex[row] = e;
+    if (NSEG == 2 && (lane & 31) == 0) ex[((size_t)x * 2 + (lane >> 5)) * slab_rows + r] = e;
     unsigned long long pk[D] = {};
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
@@ -463,12 +466,17 @@ struct I8G32 {
     static constexpr int CHB = 128 * 128;                    // one operand's chunk: 128 rows x 128-B lines
     static constexpr int STAGE = 2 * NCH * CHB;              // [op U, V][chunk][row][128 B]
     static constexpr int GL = STAGE / 1024 / (THREADS / 64); // global_load_lds pieces per wave and stage
-    static constexpr int EXP = NBUF * STAGE;                 // 2 x (128 + 128) exponents (tile parity)
-    static constexpr size_t BYTES = (size_t)NBUF * STAGE + 2048;
+    static constexpr int EXP = NBUF * STAGE;                 // 2 x 2 KiB of exponents (tile parity)
+    static constexpr size_t BYTES = (size_t)NBUF * STAGE + 4096;
     static constexpr int NS = 8;                             // epilogue stores per wave
 };
 
-template <int K, int KS, int NBUF>
+// NSEG: V's exponents per 256-channel segment (K / 256 of them, ev[(xi * NSEG + seg)][row]: the output
+// kernel that writes V sees 256 channels of a board) instead of per row (1). Each segment's levels are
+// combined exactly (2^14 H + L, fp64) and scaled by its exponent; the segments' scaled values add in fp64 in
+// segment order (one fp64 rounding, 2^-53: deterministic, so still batch-invariant), then the one rounding to
+// fp32. NSEG = 1 is bit-identical to wino88i_gemm_kernel.
+template <int K, int KS, int NBUF, int NSEG = 1>
 __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __restrict__ V8,
                                                              const int* __restrict__ ev,
                                                              const int8_t* __restrict__ U8,
@@ -477,6 +485,8 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
     using T = I8G32<KS, NBUF>;
     constexpr int NK = K / KS, NCH = T::NCH, GL = T::GL, PD = NBUF - 1;
     static_assert(GL * 8 * 1024 == T::STAGE && GL % 4 == 0, "stage split");
+    static_assert(NSEG == 1 || (NSEG == 2 && K == 512 && NK % 2 == 0), "256-channel segments");
+    constexpr int NEP = NSEG == 1 ? 1 : 2;  // exponent pieces per tile (items of 128 ints: ev segs, eu)
     extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8g[];
     char* const L0 = (char*)lds_i8g;
 
@@ -505,14 +515,21 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
         n_base = (idx % CT) * T::WM;
         r_base = ((idx / CT) % RT) * T::WN;
     };
-    // a tile's operand base (this wave's operand) and exponent-piece source (lanes 0-31: ev, 32-63: eu)
-    auto tile_base = [&](int n, const int8_t*& gb, const int*& es) {
+    // a tile's operand base (this wave's operand) and exponent-piece sources: item i of the exponent slot
+    // (128 ints at byte 512 i) is ev of segment i for i < NSEG, then eu (repeated to fill the last piece);
+    // piece p carries items 2p (lanes 0-31) and 2p + 1 (lanes 32-63)
+    auto tile_base = [&](int n, const int8_t*& gb, const int* (&es)[NEP]) {
         int xi, n_base, r_base;
         tile_of(n, xi, n_base, r_base);
         gb = op ? V8 + (((size_t)xi * (K / 32)) * stride + r_base) * 128
                 : U8 + (((size_t)xi * (K / 32)) * 512 + n_base) * 128;
-        const bool lo = lane < 32;
-        es = (lo ? ev : eu) + (lo ? (size_t)xi * stride + r_base : (size_t)xi * 512 + n_base) + 4 * (lane & 31);
+#pragma unroll
+        for (int p = 0; p < NEP; ++p) {
+            const int item = 2 * p + (lane >> 5);
+            const bool isv = item < NSEG;
+            es[p] = (isv ? ev : eu) + (isv ? ((size_t)xi * NSEG + item) * stride + r_base
+                                           : (size_t)xi * 512 + n_base) + 4 * (lane & 31);
+        }
     };
     // pieces g0 .. g1 - 1 of stage kt of the tile at gb (exponents first when ex != nullptr), into buffer buf
     auto issue = [&](const int8_t* gb, int kt, int buf, int g0, int g1) {
@@ -527,10 +544,12 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
                 16, 0, 0);
         }
     };
-    auto issue_exp = [&](const int* es, int n) {
-        __builtin_amdgcn_global_load_lds((const void*)es,
-                                         (__attribute__((address_space(3))) void*)(L0 + T::EXP + (n & 1) * 1024),
-                                         16, 0, 0);
+    auto issue_exp = [&](const int* const* es, int n) {
+#pragma unroll
+        for (int p = 0; p < NEP; ++p)
+            __builtin_amdgcn_global_load_lds(
+                (const void*)es[p], (__attribute__((address_space(3))) void*)(L0 + T::EXP + (n & 1) * 2048 + p * 1024),
+                16, 0, 0);
     };
 
     // fragments: A = U digit i of channel row wm * 32 + (lane & 31), B = V digit j of board row
@@ -545,7 +564,7 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
     }
 
     const int8_t *gb_cur = nullptr, *gb_nxt = nullptr;
-    const int *es_cur = nullptr, *es_nxt = nullptr;
+    const int *es_cur[NEP] = {}, *es_nxt[NEP] = {};
     if (ntile_wg > 0) {
         tile_base(0, gb_cur, es_cur);
         if (wave == 0) issue_exp(es_cur, 0);
@@ -559,8 +578,9 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
         for (int l = 0; l < 4; ++l)
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt) acc[l][nt] = i32x16_t{};
-        int evr[2];     // ev - 35 of the wave's two 32-board blocks (this lane's board)
-        int euv[4][4];  // eu of this lane's 16 output channels
+        int evr[NSEG][2];  // ev - 35 of the wave's two 32-board blocks (this lane's board), per segment
+        int euv[4][4];     // eu of this lane's 16 output channels
+        double sacc[NSEG == 2 ? 2 : 1][NSEG == 2 ? 16 : 1];  // segment 0, scaled (NSEG 2)
         for (int kt = 0; kt < NK; ++kt, ++s, bcur = bcur + 1 == NBUF ? 0 : bcur + 1,
                                      bpre = bpre + 1 == NBUF ? 0 : bpre + 1) {
             // stage s has landed once only the batches issued after it may be outstanding: the next PD - 1
@@ -590,13 +610,15 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             if (kt == 0) {  // the tile's exponents landed with its first stage: ev of the 2 boards, eu of 16 channels
-                const int* ex = (const int*)(L0 + T::EXP + (n & 1) * 1024);
+                const int* ex = (const int*)(L0 + T::EXP + (n & 1) * 2048);
 #pragma unroll
-                for (int nt = 0; nt < 2; ++nt) evr[nt] = ex[wn * 64 + nt * 32 + lr] - 35;
+                for (int sg = 0; sg < NSEG; ++sg)
+#pragma unroll
+                    for (int nt = 0; nt < 2; ++nt) evr[sg][nt] = ex[sg * 128 + wn * 64 + nt * 32 + lr] - 35;
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
 #pragma unroll
-                    for (int jj = 0; jj < 4; ++jj) euv[k][jj] = ex[128 + wm * 32 + 8 * k + 4 * lh + jj];
+                    for (int jj = 0; jj < 4; ++jj) euv[k][jj] = ex[NSEG * 128 + wm * 32 + 8 * k + 4 * lh + jj];
             }
             const char* buf = L0 + bcur * T::STAGE;
             const bool more = s + PD < nstage;
@@ -627,16 +649,34 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
                     }
                 }
             }
+            if constexpr (NSEG == 2) {
+              if (kt == NK / 2 - 1) {  // segment 0 done: its exact value, scaled, then restart
+#pragma unroll
+                for (int nt = 0; nt < 2; ++nt) {
+                    const double sc = ldexp(1.0, evr[0][nt]);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int hi = acc[0][nt][r] * 128 + acc[1][nt][r];
+                        const int lo = acc[2][nt][r] * 128 + acc[3][nt][r];
+                        sacc[nt][r] = __builtin_fma((double)hi, 16384.0, (double)lo) * sc;  // exact
+                    }
+#pragma unroll
+                    for (int l = 0; l < 4; ++l) acc[l][nt] = i32x16_t{};
+                }
+              }
+            }
         }
         // epilogue (registers only; the ring keeps loading the next tile)
         int xi, n_base, r_base;
         tile_of(n, xi, n_base, r_base);
         gb_cur = gb_nxt;
-        es_cur = es_nxt;
+#pragma unroll
+        for (int p = 0; p < NEP; ++p) es_cur[p] = es_nxt[p];
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
             const int bl = wn * 64 + nt * 32 + lr;
-            const int eb = evr[nt];
+            const int eb = evr[NSEG - 1][nt];
+            const double sc1 = ldexp(1.0, eb);
             float* mrow = M + ((size_t)xi * stride + r_base + bl) * 512 + n_base + wm * 32 + 4 * lh;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -648,7 +688,10 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
                     const int hi = acc[0][nt][r] * 128 + acc[1][nt][r];
                     const int lo = acc[2][nt][r] * 128 + acc[3][nt][r];
                     const double m = __builtin_fma((double)hi, 16384.0, (double)lo);  // exact
-                    o[jj] = (float)ldexp(m, eb + ec[jj]);
+                    if constexpr (NSEG == 2)  // segment 1 scaled (exact) plus segment 0: one fp64 rounding
+                        o[jj] = (float)ldexp(__builtin_fma(m, sc1, sacc[nt][r]), ec[jj]);
+                    else
+                        o[jj] = (float)ldexp(m, eb + ec[jj]);
                 }
                 *(float4*)(mrow + 8 * k) = make_float4(o[0], o[1], o[2], o[3]);
             }
@@ -690,17 +733,23 @@ __device__ inline unsigned i8_quad_transpose(unsigned P, int lane) {
     return __builtin_amdgcn_perm(r2, R, (lane & 2) ? 0x03020706u : 0x05040100u);
 }
 
-template <bool RESID, bool WRITE_Y>
-__global__ __launch_bounds__(1024) void wino88i32_out_kernel(const float* __restrict__ M, int rows,
-                                                             const float* __restrict__ scale,
-                                                             const float* __restrict__ shift, const float* resid,
-                                                             float* Y, int8_t* __restrict__ V8, int* __restrict__ ex) {
+// CW channels per workgroup (2 CW threads: a plane split over lanes l, l ^ 32): 512 -- the row's exponent
+// over all its channels, one workgroup per board -- or 256 -- one exponent per 256-channel segment
+// (ex[(xi * 2 + seg) * rows + b]), two workgroups per board, so a CU holds two of them and one's loads
+// overlap the other's transforms and reductions.
+template <bool RESID, bool WRITE_Y, int CW>
+__global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __restrict__ M, int rows,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ shift, const float* resid,
+                                                               float* Y, int8_t* __restrict__ V8,
+                                                               int* __restrict__ ex) {
 #pragma clang fp contract(off)
-    constexpr int NK = 512 / 32;
-    __shared__ unsigned red[16][2][5][16];
+    static_assert(CW == 512 || CW == 256, "a row or a 256-channel segment per workgroup");
+    constexpr int NK = 512 / 32, NW = CW / 32, NSEG = 512 / CW;
+    __shared__ unsigned red[NW][2][5][16];
     __shared__ int exs[100];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
-    const int c = w * 32 + (lane & 31), b = blockIdx.x;
+    const int seg = blockIdx.x, c = seg * CW + w * 32 + (lane & 31), b = blockIdx.y;
     float t2[10][4];  // B10^T of the plane's columns 4h .. 4h+3
     {
         float x2[4][8];
@@ -722,15 +771,15 @@ __global__ __launch_bounds__(1024) void wino88i32_out_kernel(const float* __rest
         const int xi = threadIdx.x, a = xi / 10, bb = xi % 10, hh = a / 5, aa = a % 5;
         unsigned m = 0;
 #pragma unroll
-        for (int ww = 0; ww < 16; ++ww) m = red[ww][hh][aa][bb] > m ? red[ww][hh][aa][bb] : m;
+        for (int ww = 0; ww < NW; ++ww) m = red[ww][hh][aa][bb] > m ? red[ww][hh][aa][bb] : m;
         const int e = i8_row_exponent_f32(m);
         exs[xi] = e;
-        ex[(size_t)xi * rows + b] = e;
+        ex[((size_t)xi * NSEG + seg) * rows + b] = e;
     }
     __syncthreads();
-    // row line (xi, kc = w, b): 128 bytes, digit d of channel 32 kc + i at byte 32 d + i
+    // row line (xi, kc = c / 32, b): 128 bytes, digit d of channel 32 kc + i at byte 32 d + i
     const int q = lane & 3;
-    int8_t* dst0 = V8 + ((size_t)w * rows + b) * 128 + q * 32 + (c & 28);
+    int8_t* dst0 = V8 + ((size_t)(c >> 5) * rows + b) * 128 + q * 32 + (c & 28);
 #pragma unroll
     for (int aa = 0; aa < 5; ++aa) {
         float o[10];

@@ -1,6 +1,7 @@
-"""numpy restatement of KV_PREC_I8X5's digit split and integer GEMM
-(knightvision_amd/csrc/kv_wino88i.h) for the tests: the same fp64 operations
-in the same order, so digits, exponents and M compare bit for bit."""
+"""numpy restatement of the int8-digit split and integer GEMMs
+(knightvision_amd/csrc/kv_wino88i.h: KV_PREC_I8X5's 5 digits, the fp32 tower's 4, with per-row or
+per-256-channel-segment exponents) for the tests: the same operations in the same order, so digits,
+exponents and M compare bit for bit."""
 import numpy as np
 
 DIGITS = 5
@@ -31,6 +32,36 @@ def pack(d):
     """digits [DIGITS][X][R][K] -> the product's digit planes [X][K/32][DIGITS][R][32] int8."""
     D, X, R, K = d.shape
     return d.reshape(D, X, R, K // 32, 32).transpose(1, 3, 0, 2, 4).copy()
+
+
+def gemm_seg(V, U):
+    """The fp32 tower's GEMM with V's exponents per 256-channel segment (4 digits, K 512; wino88i32_gemm_kernel
+    NSEG 2): each segment's levels combined exactly (2^14 H + L) and scaled by 2^(ev_s - 35), segment 1 added
+    to segment 0 in fp64 (one rounding), times 2^eu, rounded to fp32. -> (M [X][R][C] widened, V digits
+    [4][X][R][K], V exponents [X][2][R])."""
+    X, R, K = V.shape
+    assert K == 512
+    eu = row_exponents(U)
+    du = split(U, eu, 4).astype(np.float64)
+    evs, dvs, total = [], [], None
+    for sg in range(2):
+        Vs = V[:, :, 256 * sg:256 * (sg + 1)]
+        ev = row_exponents(Vs)
+        dv = split(Vs, ev, 4)
+        fv, fu = dv.astype(np.float64), du[:, :, :, 256 * sg:256 * (sg + 1)]
+        lev = []
+        for l in range(4):
+            acc = np.zeros((X, R, U.shape[1]))
+            for i in range(l + 1):
+                acc += np.matmul(fv[i], np.swapaxes(fu[l - i], 1, 2))
+            lev.append(acc)
+        m = (lev[0] * 128 + lev[1]) * 16384.0 + (lev[2] * 128 + lev[3])  # exact: < 2^46
+        part = np.ldexp(m, (ev[:, :, None] - 35).astype(np.int32))     # exact
+        total = part if total is None else total + part                  # one fp64 rounding
+        evs.append(ev)
+        dvs.append(dv)
+    M = np.ldexp(total, eu[:, None, :].astype(np.int32)).astype(np.float32).astype(np.float64)
+    return M, np.concatenate(dvs, axis=-1), np.stack(evs, axis=1)
 
 
 def gemm(V, U, digits=DIGITS):

@@ -15,16 +15,16 @@ from tests import _i8_digits as D
 pytestmark = pytest.mark.gpu
 
 
-def _run(V, U, digits=D.DIGITS):
+def _run(V, U, digits=D.DIGITS, seg=0):
     from knightvision_amd import _lib
     L = _lib.lib()
     X, R, K = V.shape
     M = np.zeros((X, R, 512))
     dg = np.zeros((X, K // 32, digits, R, 32), dtype=np.int8)
-    ex = np.zeros((X, R), dtype=np.int32)
+    ex = np.zeros((X, 2, R) if seg else (X, R), dtype=np.int32)
     P = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
     _lib.check(L.kv_dev_wino88i(0, P(np.ascontiguousarray(V), C.c_double), R, P(np.ascontiguousarray(U), C.c_double),
-                                K, digits, P(M, C.c_double), P(dg, C.c_int8), P(ex, C.c_int32)), "kv_dev_wino88i")
+                                K, digits, seg, P(M, C.c_double), P(dg, C.c_int8), P(ex, C.c_int32)), "kv_dev_wino88i")
     return M, dg, ex
 
 
@@ -50,43 +50,64 @@ def test_i8_gemm_bit_exact(K, rows, digits):
     assert np.array_equal(M.view(np.uint64), Mr.view(np.uint64)), float(np.abs(M - Mr).max())
 
 
-def _out(M, scale, shift, resid, fused):
+@pytest.mark.parametrize("rows", [128, 256])
+def test_i8f32_segment_gemm_bit_exact(rows):
+    """The fp32 tower's GEMM with V's exponents per 256-channel segment (KV_I8F32_SEG=1): digits, the two
+    segment exponents of every row and M bit for bit against the numpy restatement (tests/_i8_digits.gemm_seg),
+    including rows whose two halves sit 2^20 apart and a row with one all-zero half."""
+    rng = np.random.default_rng(rows + 7)
+    V = rng.standard_normal((100, rows, 512)) * np.exp2(rng.integers(-20, 20, size=(100, rows, 1)))
+    V[:, 4, 256:] *= 2.0 ** -20
+    V[:, 5, :256] = 0.0
+    U = rng.standard_normal((100, 512, 512)) * 0.05
+    V, U = V.astype(np.float32).astype(np.float64), U.astype(np.float32).astype(np.float64)
+    M, dg, ex = _run(V, U, 4, seg=1)
+    Mr, dv, evr = D.gemm_seg(V, U)
+    assert np.array_equal(ex, evr.astype(np.int32))
+    assert (ex[:, 1, 4] < ex[:, 0, 4]).all() and (ex[:, 0, 5] == 0).all()
+    assert np.array_equal(dg.reshape(100, 16, rows, 4, 32), D.pack(dv).transpose(0, 1, 3, 2, 4))
+    assert np.array_equal(M.view(np.uint64), Mr.view(np.uint64)), float(np.abs(M - Mr).max())
+
+
+def _out(M, scale, shift, resid, flags):
     from knightvision_amd import _lib
     L = _lib.lib()
     R = M.shape[1]
     Y = np.zeros((R, 64, 512), dtype=np.float32)
     dg = np.zeros((100, 16, R, 4, 32), dtype=np.int8)
-    ex = np.zeros((100, R), dtype=np.int32)
+    ex = np.zeros((100, 2, R) if flags & 2 else (100, R), dtype=np.int32)
     P = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
     rp = P(np.ascontiguousarray(resid), C.c_float) if resid is not None else None
     _lib.check(L.kv_dev_wino88i32_out(0, P(np.ascontiguousarray(M), C.c_float), R, P(scale, C.c_float),
-                                      P(shift, C.c_float), rp, int(fused), P(Y, C.c_float), P(dg, C.c_int8),
+                                      P(shift, C.c_float), rp, int(flags), P(Y, C.c_float), P(dg, C.c_int8),
                                       P(ex, C.c_int32)), "kv_dev_wino88i32_out")
     return Y, dg, ex
 
 
-@pytest.mark.parametrize("rows,resid", [(128, False), (128, True), (256, True)])
-def test_i8f32_out_kernel_writes_the_slice_kernels_digits(rows, resid):
+@pytest.mark.parametrize("rows,resid,seg", [(128, False, 0), (128, True, 0), (256, True, 0), (128, True, 2),
+                                            (256, False, 2)])
+def test_i8f32_out_kernel_writes_the_slice_kernels_digits(rows, resid, seg):
     """wino88i32_out_kernel (output transform + BN (+ residual) + ReLU, then the next V's row-line digits in
     one kernel) == wino88_out_kernel's fp32 V + wino88i_slice_kernel, bit for bit: Y, every digit and every
-    row exponent. Board 5 is all zero after the ReLU (its V rows: exponent 0, digits 0); every 7th
-    channel sits 2^-12 below the others."""
-    rng = np.random.default_rng(rows + resid)
+    exponent (per row, or per 256-channel segment: seg 2). Board 5 is all zero after the ReLU (its V rows:
+    exponent 0, digits 0); every 7th channel sits 2^-12 below the others."""
+    rng = np.random.default_rng(rows + resid + seg)
     M = (rng.standard_normal((100, rows, 512)) * 0.3).astype(np.float32)
     M[:, 5, :] = 0.0
     scale = (0.5 + rng.random(512)).astype(np.float32)
     scale[::7] *= np.float32(2.0 ** -12)  # channels far below the row max
+    scale[256:] *= np.float32(2.0 ** -5)  # the two segments at different scales
     shift = (rng.standard_normal(512) * 0.1).astype(np.float32)
     shift = -np.abs(shift)  # M = 0 (and resid = 0) on board 5: ReLU(shift) = 0
     R = (np.abs(rng.standard_normal((rows, 64, 512))) * 0.5).astype(np.float32) if resid else None
     if resid:
         R[5] = 0.0
-    Yf, df, ef = _out(M, scale, shift, R, True)
-    Ys, ds, es = _out(M, scale, shift, R, False)
+    Yf, df, ef = _out(M, scale, shift, R, 1 | seg)
+    Ys, ds, es = _out(M, scale, shift, R, seg)
     assert np.array_equal(Yf.view(np.uint32), Ys.view(np.uint32))
     assert np.array_equal(ef, es)
     assert np.array_equal(df, ds)
-    assert (ef[:, 5] == 0).all() and not df[:, :, 5].any()
+    assert (ef[..., 5] == 0).all() and not df[:, :, 5].any()
     assert len(np.unique(ef)) > 3  # exponents actually vary across rows
 
 
