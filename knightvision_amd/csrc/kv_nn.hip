@@ -1136,11 +1136,11 @@ static int launch_wino88i_gemm(const int8_t* V8, const int* ev, const int8_t* U8
 
 // the fp32 tower's int8-digit GEMM, round-5 form (kv_wino88i.h wino88i32_gemm_kernel): persistent
 // workgroups, one per CU (grid a multiple of 8, at most the tile count), or one tile each (persist false)
-template <int K, int KS, int NBUF, int NSEG = 1>
+template <int K, int KS, int NBUF, int NSEG = 1, int ABL = 0, bool DEFER = false>
 static int launch_wino88i32_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
                                  int rows, int stride, bool persist, hipStream_t st) {
     using T = kv::I8G32<KS, NBUF>;
-    auto kern = kv::wino88i32_gemm_kernel<K, KS, NBUF, NSEG>;
+    auto kern = kv::wino88i32_gemm_kernel<K, KS, NBUF, NSEG, ABL, DEFER>;
     KV_HIP(lds_opt_in((const void*)kern, (int)T::BYTES));
     const int ntiles = kv::W88_XI * (rows / T::WN) * (512 / T::WM);
     KV_REQUIRE(rows % T::WN == 0 && stride % T::WN == 0 && ntiles % 8 == 0, KV_EINVAL,
@@ -1213,9 +1213,11 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 //                  256-channel segment -- the output kernel's workgroup is 256 channels of a board, two per
 //                  CU -- and the GEMM combines the two segments
 //   KV_I8F32_SLICE 1: wino88_out_kernel's fp32 V + the slice kernel (the round-4 form; the same digits)
-//   KV_I8F32_GEMM  r4: the round-4 GEMM kernel (per-row exponents only); else the round-5 persistent one ----
+//   KV_I8F32_GEMM  p: the round-5 persistent GEMM (wino88i32_gemm_kernel, bit-identical, measured 5 %
+//                  slower: profiles/r05_i8gemm_variants.log); default the 128x128-tile wino88i_gemm_kernel
+//                  (per-row exponents; the segment form always runs wino88i32_gemm_kernel) ----
 struct I8f32Form {
-    bool seg = false, slice = false, r4 = false;
+    bool seg = false, slice = false, r4 = true;
 };
 static const I8f32Form& i8f32_form() {
     static const I8f32Form f = [] {
@@ -1225,7 +1227,7 @@ static const I8f32Form& i8f32_form() {
         e = getenv("KV_I8F32_SLICE");
         x.slice = e && e[0] == '1';
         e = getenv("KV_I8F32_GEMM");
-        x.r4 = e && !strcmp(e, "r4") && !x.seg;
+        x.r4 = !(e && !strcmp(e, "p")) && !x.seg;
         return x;
     }();
     return f;
@@ -2109,6 +2111,24 @@ int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, flo
             case 6:  // segment exponents (K 512): a different M from the same digits (timing only)
                 KV_REQUIRE(k5, KV_EINVAL, "kv_dev_i8gemm_bench: variant 6 needs K 512");
                 return launch_wino88i32_gemm<512, 32, 3, 2>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);
+            case 7:  // ablation: variant 1 without the M stores (timing only)
+                KV_REQUIRE(k5, KV_EINVAL, "kv_dev_i8gemm_bench: variant 7 needs K 512");
+                return launch_wino88i32_gemm<512, 32, 3, 1, 1>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);
+            case 8:  // ablation: variant 1 without the operand copies (timing only)
+                KV_REQUIRE(k5, KV_EINVAL, "kv_dev_i8gemm_bench: variant 8 needs K 512");
+                return launch_wino88i32_gemm<512, 32, 3, 1, 2>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);
+            case 9:  // ablation: variant 4 (64-k stages) without the operand copies (timing only)
+                KV_REQUIRE(k5, KV_EINVAL, "kv_dev_i8gemm_bench: variant 9 needs K 512");
+                return launch_wino88i32_gemm<512, 64, 2, 1, 2>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);
+            case 10:  // variant 1 with the M stores deferred past the next tile's first copies
+                return k5 ? launch_wino88i32_gemm<512, 32, 3, 1, 0, true>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0)
+                          : launch_wino88i32_gemm<256, 32, 3, 1, 0, true>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);
+            case 11:  // variant 3 (4 buffers) deferred
+                return k5 ? launch_wino88i32_gemm<512, 32, 4, 1, 0, true>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0)
+                          : launch_wino88i32_gemm<256, 32, 4, 1, 0, true>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);
+            case 12:  // variant 4 (64-k stages) deferred
+                return k5 ? launch_wino88i32_gemm<512, 64, 2, 1, 0, true>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0)
+                          : launch_wino88i32_gemm<256, 64, 2, 1, 0, true>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);
             default: KV_REQUIRE(false, KV_EINVAL, "kv_dev_i8gemm_bench: variant %d", variant);
         }
     };

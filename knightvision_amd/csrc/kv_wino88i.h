@@ -476,7 +476,12 @@ struct I8G32 {
 // combined exactly (2^14 H + L, fp64) and scaled by its exponent; the segments' scaled values add in fp64 in
 // segment order (one fp64 rounding, 2^-53: deterministic, so still batch-invariant), then the one rounding to
 // fp32. NSEG = 1 is bit-identical to wino88i_gemm_kernel.
-template <int K, int KS, int NBUF, int NSEG = 1>
+// ABL (timing ablations of kv_dev_i8gemm_bench only; M is wrong): 1 no M stores (the values kept live),
+// 2 no operand copies (the waits and barriers stay; LDS holds whatever it held).
+// DEFER: a tile's 8 M stores per wave wait in registers until the next tile's first stage has issued its
+// copies, so no vmcnt wait of the next tile's first PD + 1 stages has to retire them (the stores are older
+// than every copy such a wait needs otherwise; vmcnt counts in issue order).
+template <int K, int KS, int NBUF, int NSEG = 1, int ABL = 0, bool DEFER = false>
 __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __restrict__ V8,
                                                              const int* __restrict__ ev,
                                                              const int8_t* __restrict__ U8,
@@ -533,6 +538,7 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
     };
     // pieces g0 .. g1 - 1 of stage kt of the tile at gb (exponents first when ex != nullptr), into buffer buf
     auto issue = [&](const int8_t* gb, int kt, int buf, int g0, int g1) {
+        if (ABL == 2) return;
         const int8_t* gk = gb + (size_t)(kt * NCH) * cstride;
 #pragma unroll
         for (int g = g0; g < g1; ++g) {
@@ -571,6 +577,14 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
         for (int k = 0; k < PD && k < NK; ++k) issue(gb_cur, k, k % NBUF, 0, GL);
     }
     int s = 0, bcur = 0, bpre = PD % NBUF;  // ring buffers of stage s and of stage s + PD
+    float4 pend[2][4];  // DEFER: the previous tile's M rows
+    float* prow[2] = {nullptr, nullptr};
+    auto store_pend = [&]() {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) *(float4*)(prow[nt] + 8 * k) = pend[nt][k];
+    };
     for (int n = 0; n < ntile_wg; ++n) {
         if (n + 1 < ntile_wg) tile_base(n + 1, gb_nxt, es_nxt);
         i32x16_t acc[4][2];
@@ -586,7 +600,7 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
             // stage s has landed once only the batches issued after it may be outstanding: the next PD - 1
             // stages' (those that exist) and, in a tile's first PD stages after an epilogue, its NS stores
             const int ahead = nstage - 1 - s < PD - 1 ? nstage - 1 - s : PD - 1;
-            const bool st = n > 0 && kt < PD;
+            const bool st = DEFER ? (n > 0 && kt >= 1 && kt <= PD) : (n > 0 && kt < PD);
             if (PD == 2) {
                 if (ahead == 1) {
                     if (st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL + T::NS) : "memory");
@@ -649,6 +663,7 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
                     }
                 }
             }
+            if (DEFER && kt == 0 && n > 0) store_pend();  // after this stage's copies (stage s + PD's)
             if constexpr (NSEG == 2) {
               if (kt == NK / 2 - 1) {  // segment 0 done: its exact value, scaled, then restart
 #pragma unroll
@@ -693,10 +708,17 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
                     else
                         o[jj] = (float)ldexp(m, eb + ec[jj]);
                 }
-                *(float4*)(mrow + 8 * k) = make_float4(o[0], o[1], o[2], o[3]);
+                if (ABL == 1)
+                    asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
+                else if (DEFER)
+                    pend[nt][k] = make_float4(o[0], o[1], o[2], o[3]);
+                else
+                    *(float4*)(mrow + 8 * k) = make_float4(o[0], o[1], o[2], o[3]);
             }
+            if (DEFER) prow[nt] = mrow;
         }
     }
+    if (DEFER && ntile_wg > 0) store_pend();
 }
 
 // ---- the fp32 Winograd domain with int8-digit GEMMs (KV_PATH_WINO88_I8F32) ----
@@ -712,15 +734,55 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
 // the next conv's V as row-line digits under each row's exponent -- what wino88_out_kernel's fp32 V
 // followed by wino88i_slice_kernel<512, float, 4, true> gives, bit for bit, without V's HBM round trip.
 // One 512-thread workgroup per board, thread = channel, so the 512 channels of a row (the exponent's
-// domain) are in one workgroup. V is computed twice from the column pass, which stays in registers (80
-// floats): once for the row maxima (a halving shuffle reduction per wave, then LDS over the 8 waves), once
-// for the digits -- the same fmaf chains on the same inputs, so the same bits. A thread's 4 digits of a
-// point go through a 4x4 byte transpose within its lane quad (two DPP exchanges + v_perm), so every lane
-// stores one dword and each half-wave writes one whole 128-byte line.
+// domain) are in one workgroup. Each (board, channel) plane is split over lanes l and l ^ 32 (the
+// transforms' half exchanges are v_permlane32_swap), so a lane keeps its 50 V values in registers across
+// the exponent barrier: the row maxima (DPP max per half-wave, then LDS over the waves), the exponents, then
+// the digits of the kept values -- the same fmaf chains on the same inputs as wino88_out_kernel + the slice
+// kernel, so the same bits. A thread's 4 digits of a point go through a 4x4 byte transpose within its lane
+// quad (two DPP exchanges + v_perm), so every lane stores one dword and each half-wave writes one whole
+// 128-byte line.
 // (Round 4 dropped a form that kept all 100 V values in registers for the reduction: 246 VGPRs, one
 // workgroup per CU, 436-511 us per layer against 142-238 + 165 us for the out kernel + slice,
 // profiles/r04_i8f32_fused_out.log; and an output kernel computing only the row maxima plus a second
 // input-transform pass, 294-356 + 220 us, profiles/r04_i8f32_outmax_form.log.)
+
+// max over the 32 lanes of each half-wave of v, by DPP-modified max operations (no selects, no LDS-pipe
+// shuffle): xor 1 and xor 2 within quads, the half-row and row mirrors (every lane then holds its 16-lane
+// row's max), then row_bcast:15 into rows 1 and 3 -- lanes 16-31 end with the max of lanes 0-31, lanes
+// 48-63 with the max of lanes 32-63.
+__device__ inline unsigned i8_half_max_dpp(unsigned v) {
+    // old = 0 (the identity of an unsigned max) so the compiler folds each DPP move into its max
+    unsigned t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);  // quad_perm 1,0,3,2
+    v = v > t ? v : t;
+    t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);  // quad_perm 2,3,0,1
+    v = v > t ? v : t;
+    t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, true);  // row_half_mirror
+    v = v > t ? v : t;
+    t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, true);  // row_mirror
+    v = v > t ? v : t;
+    t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    return v > t ? v : t;
+}
+
+// The 4 digits of an fp32 v under exponent e (i8_digits<4>) packed into one dword, digit d in byte d: each
+// rint(t) as t + 1.5 * 2^23 (|t| <= 128: the add rounds to the integer, ties to even, as rintf) whose low byte
+// is the digit's two's complement; q - 1.5 * 2^23 is rint(t) exactly, so t - rint(t) and the x128 are the
+// same operations as i8_digits's -- the same digits, without the float -> int conversions.
+__device__ inline unsigned i8_digits4_packed(float v, int e) {
+#pragma clang fp contract(off)
+    constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23
+    float t = ldexpf(v, 7 - e);
+    unsigned q[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float qf = t + kMagic;
+        q[i] = __float_as_uint(qf);
+        if (i < 3) t = (t - (qf - kMagic)) * 128.0f;
+    }
+    const unsigned lo = __builtin_amdgcn_perm(q[1], q[0], 0x0c0c0400u);  // [q0.b0, q1.b0, 0, 0]
+    const unsigned hi = __builtin_amdgcn_perm(q[3], q[2], 0x0c0c0400u);
+    return lo | hi << 16;
+}
 
 // lane quad q = lane & 3 holds P = digits 0..3 of its channel (byte d = digit d); returns digit q of the
 // quad's 4 channels (byte j = channel 4 (lane / 4) + j)
@@ -746,25 +808,33 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
 #pragma clang fp contract(off)
     static_assert(CW == 512 || CW == 256, "a row or a 256-channel segment per workgroup");
     constexpr int NK = 512 / 32, NW = CW / 32, NSEG = 512 / CW;
-    __shared__ unsigned red[NW][2][5][16];
+    __shared__ __attribute__((aligned(16))) unsigned red[NW][2][5][16];
     __shared__ int exs[100];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
     const int seg = blockIdx.x, c = seg * CW + w * 32 + (lane & 31), b = blockIdx.y;
-    float t2[10][4];  // B10^T of the plane's columns 4h .. 4h+3
+    float vk[5][10];  // this half's 50 V values (rows 5h .. 5h+4), kept across the exponent barrier
     {
-        float x2[4][8];
-        wino88_out_plane_half<RESID, WRITE_Y>(M, rows, b, c, h, scale[c], shift[c], resid, Y, x2);
-        wino88_input_cols(x2, h, t2);
+        float t2[10][4];  // B10^T of the plane's columns 4h .. 4h+3
+        {
+            float x2[4][8];
+            wino88_out_plane_half<RESID, WRITE_Y>(M, rows, b, c, h, scale[c], shift[c], resid, Y, x2);
+            wino88_input_cols(x2, h, t2);
+        }
+#pragma unroll
+        for (int aa = 0; aa < 5; ++aa) wino88_input_row(t2, h, aa, vk[aa]);
     }
 #pragma unroll
     for (int aa = 0; aa < 5; ++aa) {
-        float o[10];
-        wino88_input_row(t2, h, aa, o);
+        const float (&o)[10] = vk[aa];
         unsigned m[10];
 #pragma unroll
-        for (int bb = 0; bb < 10; ++bb) m[bb] = __float_as_uint(o[bb]) & 0x7fffffffu;
-        const unsigned r = i8_half_max10(m, lane);
-        if ((lane & 16) == 0 && (lane & 15) < 10) red[w][h][aa][lane & 15] = r;
+        for (int bb = 0; bb < 10; ++bb) m[bb] = i8_half_max_dpp(__float_as_uint(o[bb]) & 0x7fffffffu);
+        if ((lane & 31) == 16) {  // this half's 10 maxima, written by one lane
+            uint4* rr = (uint4*)&red[w][h][aa][0];
+            rr[0] = make_uint4(m[0], m[1], m[2], m[3]);
+            rr[1] = make_uint4(m[4], m[5], m[6], m[7]);
+            *(uint2*)&red[w][h][aa][8] = make_uint2(m[8], m[9]);
+        }
     }
     __syncthreads();
     if (threadIdx.x < 100) {
@@ -779,19 +849,17 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
     __syncthreads();
     // row line (xi, kc = c / 32, b): 128 bytes, digit d of channel 32 kc + i at byte 32 d + i
     const int q = lane & 3;
-    int8_t* dst0 = V8 + ((size_t)(c >> 5) * rows + b) * 128 + q * 32 + (c & 28);
+    // 32-bit byte offsets (the digits of 100 x rows x 512 values < 2^32 bytes)
+    const unsigned off0 = ((unsigned)(c >> 5) * rows + b) * 128 + q * 32 + (c & 28), xstride = NK * rows * 128;
+    unsigned* const dst = (unsigned*)V8;
 #pragma unroll
     for (int aa = 0; aa < 5; ++aa) {
-        float o[10];
-        wino88_input_row(t2, h, aa, o);
         const int a = 5 * h + aa;
 #pragma unroll
         for (int bb = 0; bb < 10; ++bb) {
             const int xi = a * 10 + bb;
-            int dg[kI8DigitsF32];
-            i8_digits<kI8DigitsF32>(o[bb], exs[xi], dg);
-            const unsigned P = (dg[0] & 0xff) | (dg[1] & 0xff) << 8 | (dg[2] & 0xff) << 16 | (unsigned)dg[3] << 24;
-            *(unsigned*)(dst0 + (size_t)xi * NK * rows * 128) = i8_quad_transpose(P, lane);
+            const unsigned P = i8_digits4_packed(vk[aa][bb], exs[xi]);
+            dst[(off0 + (unsigned)xi * xstride) >> 2] = i8_quad_transpose(P, lane);
         }
     }
 }
