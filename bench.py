@@ -315,9 +315,10 @@ def gemm_label(path: int, rows: int, split: int):
                     "Winograd F(8x8,3x3) GEMM layer: two launches, both inside the timed events)")
         return name, desc
     if path == 6:
-        return "wino88i_gemm_kernel<512,4,true,float,true>", (
+        return "wino88i32_gemm_lag_kernel<512,false>", (
             " (residual-tower Winograd F(8x8,3x3) GEMMs of the fp32 tower from 4 int8 digits per value: 10 "
-            "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 tiles)")
+            "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 tiles, "
+            "each stage's last 6 MFMAs per wave under the next stage's first LDS reads)")
     if path == 5:
         return "wino88i_gemm_kernel<512,5,true,double>", (
             " (residual-tower Winograd F(8x8,3x3) GEMMs in the fp64 domain from 5 int8 digits per value: 15 "

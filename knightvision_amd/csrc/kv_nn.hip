@@ -1134,6 +1134,38 @@ static int launch_wino88i_gemm(const int8_t* V8, const int* ev, const int8_t* U8
     return KV_OK;
 }
 
+// the fp32 tower's int8-digit GEMM with the stage barrier in the middle of the stage (wino88i32_gemm_mid_kernel)
+template <int K>
+static int launch_wino88i32_gemm_mid(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
+                                     int rows, int stride, hipStream_t st) {
+    using T = kv::Wino88iTile<kv::kI8DigitsF32>;
+    constexpr int bytes = 4 * T::STAGE;
+    KV_HIP(lds_opt_in((const void*)kv::wino88i32_gemm_mid_kernel<K>, bytes));
+    const int nwg = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
+    KV_REQUIRE(rows % T::WM == 0 && stride % T::WM == 0 && nwg % 8 == 0, KV_EINVAL,
+               "wino gemm i8 (mid): rows %d / stride %d vs tile %d", rows, stride, T::WM);
+    hipLaunchKernelGGL(kv::wino88i32_gemm_mid_kernel<K>, dim3(nwg), dim3(T::THREADS), bytes, st, V8, ev, U8, eu, M,
+                       rows, 512, stride);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+// the lagging-half form (wino88i32_gemm_lag_kernel); STAG: only waves 0-3 lag
+template <int K, bool STAG>
+static int launch_wino88i32_gemm_lag(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
+                                     int rows, int stride, hipStream_t st) {
+    using T = kv::Wino88iTile<kv::kI8DigitsF32>;
+    constexpr int bytes = 3 * T::STAGE;
+    KV_HIP(lds_opt_in((const void*)kv::wino88i32_gemm_lag_kernel<K, STAG>, bytes));
+    const int nwg = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
+    KV_REQUIRE(rows % T::WM == 0 && stride % T::WM == 0 && nwg % 8 == 0, KV_EINVAL,
+               "wino gemm i8 (lag): rows %d / stride %d vs tile %d", rows, stride, T::WM);
+    hipLaunchKernelGGL((kv::wino88i32_gemm_lag_kernel<K, STAG>), dim3(nwg), dim3(T::THREADS), bytes, st, V8, ev, U8,
+                       eu, M, rows, 512, stride);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
 // the fp32 tower's int8-digit GEMM, round-5 form (kv_wino88i.h wino88i32_gemm_kernel): persistent
 // workgroups, one per CU (grid a multiple of 8, at most the tile count), or one tile each (persist false)
 template <int K, int KS, int NBUF, int NSEG = 1, int ABL = 0, bool DEFER = false>
@@ -1213,11 +1245,13 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 //                  256-channel segment -- the output kernel's workgroup is 256 channels of a board, two per
 //                  CU -- and the GEMM combines the two segments
 //   KV_I8F32_SLICE 1: wino88_out_kernel's fp32 V + the slice kernel (the round-4 form; the same digits)
-//   KV_I8F32_GEMM  p: the round-5 persistent GEMM (wino88i32_gemm_kernel, bit-identical, measured 5 %
-//                  slower: profiles/r05_i8gemm_variants.log); default the 128x128-tile wino88i_gemm_kernel
-//                  (per-row exponents; the segment form always runs wino88i32_gemm_kernel) ----
+//   KV_I8F32_GEMM  default: wino88i32_gemm_lag_kernel (128x128 tiles, each stage's last 6 MFMAs per wave run
+//                  after the next barrier, under the next stage's first LDS reads: 6 % faster than the round-4
+//                  kernel, bit-identical, profiles/r05_i8gemm_lag_ab.log); r4: the round-4
+//                  wino88i_gemm_kernel; p: the persistent wino88i32_gemm_kernel (5 % slower than r4,
+//                  profiles/r05_i8gemm_variants.log). The segment form always runs wino88i32_gemm_kernel ----
 struct I8f32Form {
-    bool seg = false, slice = false, r4 = true;
+    bool seg = false, slice = false, r4 = false, persist = false;
 };
 static const I8f32Form& i8f32_form() {
     static const I8f32Form f = [] {
@@ -1227,7 +1261,8 @@ static const I8f32Form& i8f32_form() {
         e = getenv("KV_I8F32_SLICE");
         x.slice = e && e[0] == '1';
         e = getenv("KV_I8F32_GEMM");
-        x.r4 = !(e && !strcmp(e, "p")) && !x.seg;
+        x.r4 = e && !strcmp(e, "r4") && !x.seg;
+        x.persist = e && !strcmp(e, "p");
         return x;
     }();
     return f;
@@ -1256,7 +1291,8 @@ static int i8f32_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const i
     if constexpr (K == 512)
         if (seg) return launch_wino88i32_gemm<K, 32, 3, 2>(V8, ev, U8, eu, M, rows, stride, true, st);
     if (f.r4) return launch_wino88i_gemm<K, D>(V8, ev, U8, eu, M, rows, stride, st);
-    return launch_wino88i32_gemm<K, 32, 3, 1>(V8, ev, U8, eu, M, rows, stride, true, st);
+    if (f.persist) return launch_wino88i32_gemm<K, 32, 3, 1>(V8, ev, U8, eu, M, rows, stride, true, st);
+    return launch_wino88i32_gemm_lag<K, false>(V8, ev, U8, eu, M, rows, stride, st);
 }
 
 // conv l's GEMM; slice: V (fp32) -> digits first. (mark: the engine's timing hook brackets the slice, when
@@ -2120,6 +2156,15 @@ int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, flo
             case 9:  // ablation: variant 4 (64-k stages) without the operand copies (timing only)
                 KV_REQUIRE(k5, KV_EINVAL, "kv_dev_i8gemm_bench: variant 9 needs K 512");
                 return launch_wino88i32_gemm<512, 64, 2, 1, 2>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);
+            case 13:  // the round-4 kernel with the barrier in the middle of each stage
+                return k5 ? launch_wino88i32_gemm_mid<512>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0)
+                          : launch_wino88i32_gemm_mid<256>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0);
+            case 14:  // every wave lags h2 by a barrier (3 buffers)
+                return k5 ? launch_wino88i32_gemm_lag<512, false>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0)
+                          : launch_wino88i32_gemm_lag<256, false>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0);
+            case 15:  // staggered: waves 0-3 lag, 4-7 do not
+                return k5 ? launch_wino88i32_gemm_lag<512, true>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0)
+                          : launch_wino88i32_gemm_lag<256, true>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0);
             case 10:  // variant 1 with the M stores deferred past the next tile's first copies
                 return k5 ? launch_wino88i32_gemm<512, 32, 3, 1, 0, true>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0)
                           : launch_wino88i32_gemm<256, 32, 3, 1, 0, true>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);

@@ -324,6 +324,311 @@ __global__ __launch_bounds__(512) void wino88i_gemm_kernel(const int8_t* __restr
     }
 }
 
+// wino88i_gemm_kernel<K, 4, ., float, true> with the stage barrier moved to the middle of the stage
+// (MID): a stage's MFMAs run in two halves (B digits 0-1: 14 of its 20 MFMAs per wave; 2-3: 6), and between
+// them the waves wait for the NEXT stage's copies, pass one barrier, and read that stage's A digits and first
+// B digit -- so those LDS reads run under the second half's MFMAs instead of after a barrier with both waves
+// of a SIMD idle. The ring has 4 buffers: stage kt + 3's copies go out after the barrier in the middle of
+// stage kt (all waves are then past stage kt - 1, whose buffer they refill), two per B digit of the second
+// half. Same products, same k order, same bits.
+template <int K>
+__global__ __launch_bounds__(512) void wino88i32_gemm_mid_kernel(const int8_t* __restrict__ V8,
+                                                                 const int* __restrict__ ev,
+                                                                 const int8_t* __restrict__ U8,
+                                                                 const int* __restrict__ eu, float* __restrict__ M,
+                                                                 int rows, int cout, int stride) {
+    constexpr int S = 4, NBUF = 4;
+    using T = Wino88iTile<S>;
+    constexpr int NT = T::NT, WM = T::WM, WN = T::WN, GL = T::GL;
+    constexpr int NK = K / 32;
+    static_assert(GL == 4 && NK >= 4, "4 pieces per wave and stage");
+
+    extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8m[];
+    char* const L0 = (char*)lds_i8m;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / T::WC, wn = wave % T::WC;
+    const int CT = cout / WN, RT = rows / WM;
+    const int nwg = (int)gridDim.x;  // a multiple of 8
+    const int idx = (int)(blockIdx.x & 7) * (nwg >> 3) + (int)(blockIdx.x >> 3);
+    const int xi = idx / (CT * RT);
+    const int n_base = (idx % CT) * WN;
+    const int r_base = ((idx / CT) % RT) * WM;
+
+    // copy pieces as wino88i_gemm_kernel's row-line path: piece q = wave * 4 + g covers operand q / 16,
+    // rows 8 (q % 16) .. +7
+    const int op = (wave * GL) / (4 * S);
+    const size_t rstride = op ? (size_t)cout : (size_t)stride;
+    const int8_t* gbase = op ? U8 + (((size_t)xi * NK) * cout + (size_t)n_base) * 128
+                             : V8 + (((size_t)xi * NK) * stride + (size_t)r_base) * 128;
+    const size_t sstep = rstride * 128;
+    const int rl_off0 = (lane >> 3) * 128 + 16 * ((lane & 7) ^ (lane >> 4));
+    const int rl_off1 = (lane >> 3) * 128 + 16 * ((lane & 7) ^ (lane >> 4) ^ 4);
+    auto issue1 = [&](int g, int kt) {
+        const int q = wave * GL + g, rg8 = q % 16;
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(gbase + kt * sstep + (size_t)rg8 * 1024 + ((rg8 & 1) ? rl_off1 : rl_off0)),
+            (__attribute__((address_space(3))) void*)(L0 + (kt % NBUF) * T::STAGE + op * S * T::PLANE + rg8 * 1024),
+            16, 0, 0);
+    };
+
+    const int lr = lane & 31, lh = lane >> 5;
+    const int arow = wm * 32 + lr;
+    int aoffr[S], boffr[NT][S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        aoffr[i] = i8_rl_off(arow, 2 * i + lh);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) boffr[nt][i] = S * T::PLANE + i8_rl_off(wn * NT * 32 + nt * 32 + lr, 2 * i + lh);
+    }
+
+    i32x16_t acc[S][NT];
+#pragma unroll
+    for (int l = 0; l < S; ++l)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[l][nt] = i32x16_t{};
+
+    // prologue: stages 0-2 in flight, stage 0 landed (this wave's copies, then every wave's), its A digits
+    // and first B digit read
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int g = 0; g < GL; ++g) issue1(g, k);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    i8x16_t a[S], b0[NT];
+#pragma unroll
+    for (int i = 0; i < S; ++i) a[i] = *(const i8x16_t*)(L0 + aoffr[i]);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) b0[nt] = *(const i8x16_t*)(L0 + boffr[nt][0]);
+
+    for (int kt = 0; kt < NK; ++kt) {
+        const char* buf = L0 + (kt % NBUF) * T::STAGE;
+        i8x16_t b1[NT], b2[NT], b3[NT];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) b1[nt] = *(const i8x16_t*)(buf + boffr[nt][1]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                acc[i][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b0[nt], acc[i][nt], 0, 0, 0);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) b2[nt] = *(const i8x16_t*)(buf + boffr[nt][2]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                acc[i + 1][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b1[nt], acc[i + 1][nt], 0, 0, 0);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) b3[nt] = *(const i8x16_t*)(buf + boffr[nt][3]);
+        // the A digits of stage kt that the second half still needs (i = 0, 1), before they are replaced
+        const i8x16_t a0 = a[0], a1 = a[1];
+        // middle: stage kt + 1 landed (only stage kt + 2's copies may still be in flight), then every wave
+        // is past stage kt - 1, whose buffer stage kt + 3's copies refill
+        if (kt + 1 < NK) {
+            if (kt + 2 < NK)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + 1 < NK) {
+            const char* nb = L0 + ((kt + 1) % NBUF) * T::STAGE;
+#pragma unroll
+            for (int i = 0; i < S; ++i) a[i] = *(const i8x16_t*)(nb + aoffr[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                acc[i + 2][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(i ? a1 : a0, b2[nt], acc[i + 2][nt], 0, 0, 0);
+        if (kt + 3 < NK) {
+            issue1(0, kt + 3);
+            issue1(1, kt + 3);
+        }
+        if (kt + 1 < NK) {
+            const char* nb = L0 + ((kt + 1) % NBUF) * T::STAGE;
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) b0[nt] = *(const i8x16_t*)(nb + boffr[nt][0]);
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+            acc[3][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b3[nt], acc[3][nt], 0, 0, 0);
+        if (kt + 3 < NK) {
+            issue1(2, kt + 3);
+            issue1(3, kt + 3);
+        }
+    }
+
+    // epilogue (as wino88i_gemm_kernel's): D col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+    const int* evx = ev + (size_t)xi * stride + r_base + wm * 32;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int col = n_base + wn * NT * 32 + nt * 32 + lr;
+        const int ec = eu[(size_t)xi * cout + col] - 14;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+            double m = (double)acc[S - 1][nt][r];
+#pragma unroll
+            for (int l = S - 2; l >= 0; --l) m = __builtin_fma(m, 0.0078125, (double)acc[l][nt][r]);  // exact
+            M[((size_t)xi * stride + r_base + wm * 32 + row) * cout + col] = (float)ldexp(m, evx[row] + ec);
+        }
+    }
+}
+
+// The same GEMM as one loop over stage barriers in which a wave's MFMAs for stage k are split in two
+// halves: h1(k) = B digits 0-1 (14 of 20 MFMAs per wave), h2(k) = B digits 2-3 (6). Two programs:
+//   LAG ("mid"): after barrier k it reads stage k's A digits and first B digit while it runs h2(k - 1)
+//     from registers (the A digits 0-1 and B digits 2-3 of stage k - 1, kept), then h1(k);
+//   plain: after barrier k it reads stage k's digits and runs h1(k) and h2(k).
+// Either way every LDS read of stage k happens between barriers k and k + 1, so stage k + 2's copies go into
+// stage k - 1's buffer right after barrier k (3 buffers, two stages in flight). STAG: waves 0-3 lag, waves
+// 4-7 do not -- the two waves of a SIMD then reach each barrier at different points of their MFMA streams
+// (one finishing a stage, one mid-stage), so one issues MFMAs while the other waits on its LDS reads; else
+// every wave lags. Same products, same bits.
+template <int K, bool STAG>
+__global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* __restrict__ V8,
+                                                                 const int* __restrict__ ev,
+                                                                 const int8_t* __restrict__ U8,
+                                                                 const int* __restrict__ eu, float* __restrict__ M,
+                                                                 int rows, int cout, int stride) {
+    constexpr int S = 4, NBUF = 3;
+    using T = Wino88iTile<S>;
+    constexpr int NT = T::NT, WM = T::WM, WN = T::WN, GL = T::GL;
+    constexpr int NK = K / 32;
+    static_assert(GL == 4 && NK >= 3, "4 pieces per wave and stage");
+
+    extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8l[];
+    char* const L0 = (char*)lds_i8l;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const bool lag = !STAG || wave < 4;  // wave-uniform
+    const int wm = wave / T::WC, wn = wave % T::WC;
+    const int CT = cout / WN, RT = rows / WM;
+    const int nwg = (int)gridDim.x;  // a multiple of 8
+    const int idx = (int)(blockIdx.x & 7) * (nwg >> 3) + (int)(blockIdx.x >> 3);
+    const int xi = idx / (CT * RT);
+    const int n_base = (idx % CT) * WN;
+    const int r_base = ((idx / CT) % RT) * WM;
+
+    const int op = (wave * GL) / (4 * S);
+    const size_t rstride = op ? (size_t)cout : (size_t)stride;
+    const int8_t* gbase = op ? U8 + (((size_t)xi * NK) * cout + (size_t)n_base) * 128
+                             : V8 + (((size_t)xi * NK) * stride + (size_t)r_base) * 128;
+    const size_t sstep = rstride * 128;
+    const int rl_off0 = (lane >> 3) * 128 + 16 * ((lane & 7) ^ (lane >> 4));
+    const int rl_off1 = (lane >> 3) * 128 + 16 * ((lane & 7) ^ (lane >> 4) ^ 4);
+    auto issue1 = [&](int g, int kt) {
+        const int q = wave * GL + g, rg8 = q % 16;
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(gbase + kt * sstep + (size_t)rg8 * 1024 + ((rg8 & 1) ? rl_off1 : rl_off0)),
+            (__attribute__((address_space(3))) void*)(L0 + (kt % NBUF) * T::STAGE + op * S * T::PLANE + rg8 * 1024),
+            16, 0, 0);
+    };
+
+    const int lr = lane & 31, lh = lane >> 5;
+    const int arow = wm * 32 + lr;
+    int aoffr[S], boffr[NT][S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        aoffr[i] = i8_rl_off(arow, 2 * i + lh);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) boffr[nt][i] = S * T::PLANE + i8_rl_off(wn * NT * 32 + nt * 32 + lr, 2 * i + lh);
+    }
+
+    i32x16_t acc[S][NT];
+#pragma unroll
+    for (int l = 0; l < S; ++l)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[l][nt] = i32x16_t{};
+    // h2 of the previous stage (lagging waves): its A digits 0-1 and B digits 2-3
+    i8x16_t pa0 = {}, pa1 = {}, pb2[NT] = {}, pb3[NT] = {};
+    auto h2 = [&](const i8x16_t& x0, const i8x16_t& x1, const i8x16_t (&y2)[NT], const i8x16_t (&y3)[NT]) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[2][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(x0, y2[nt], acc[2][nt], 0, 0, 0);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[3][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(x1, y2[nt], acc[3][nt], 0, 0, 0);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[3][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(x0, y3[nt], acc[3][nt], 0, 0, 0);
+    };
+
+    issue1(0, 0); issue1(1, 0); issue1(2, 0); issue1(3, 0);
+    issue1(0, 1); issue1(1, 1); issue1(2, 1); issue1(3, 1);
+    for (int kt = 0; kt < NK; ++kt) {
+        // stage kt landed: only stage kt + 1's copies may still be in flight
+        if (kt + 1 < NK)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const char* buf = L0 + (kt % NBUF) * T::STAGE;
+        i8x16_t a[S], b0[NT], b1[NT], b2[NT], b3[NT];
+#pragma unroll
+        for (int i = 0; i < S; ++i) a[i] = *(const i8x16_t*)(buf + aoffr[i]);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) b0[nt] = *(const i8x16_t*)(buf + boffr[nt][0]);
+        if (lag && kt > 0) h2(pa0, pa1, pb2, pb3);  // under the reads above
+        if (kt + 2 < NK) {  // stage kt + 2 into stage kt - 1's buffer
+            issue1(0, kt + 2);
+            issue1(1, kt + 2);
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) b1[nt] = *(const i8x16_t*)(buf + boffr[nt][1]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                acc[i][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b0[nt], acc[i][nt], 0, 0, 0);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) b2[nt] = *(const i8x16_t*)(buf + boffr[nt][2]);
+        if (kt + 2 < NK) {
+            issue1(2, kt + 2);
+            issue1(3, kt + 2);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+                acc[i + 1][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b1[nt], acc[i + 1][nt], 0, 0, 0);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) b3[nt] = *(const i8x16_t*)(buf + boffr[nt][3]);
+        if (lag) {  // h2(kt) after the next barrier
+            pa0 = a[0];
+            pa1 = a[1];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                pb2[nt] = b2[nt];
+                pb3[nt] = b3[nt];
+            }
+        } else {
+            h2(a[0], a[1], b2, b3);
+        }
+    }
+    if (lag) h2(pa0, pa1, pb2, pb3);
+
+    // epilogue (as wino88i_gemm_kernel's): D col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+    const int* evx = ev + (size_t)xi * stride + r_base + wm * 32;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int col = n_base + wn * NT * 32 + nt * 32 + lr;
+        const int ec = eu[(size_t)xi * cout + col] - 14;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+            double m = (double)acc[S - 1][nt][r];
+#pragma unroll
+            for (int l = S - 2; l >= 0; --l) m = __builtin_fma(m, 0.0078125, (double)acc[l][nt][r]);  // exact
+            M[((size_t)xi * stride + r_base + wm * 32 + row) * cout + col] = (float)ldexp(m, evx[row] + ec);
+        }
+    }
+}
+
 // The next conv's digits come from two kernels, each at the occupancy of the
 // fp64 out kernel (one workgroup = 128 channels of one board): the exponent of
 // a V row needs the largest magnitude over all 512 channels, i.e. over 4
