@@ -1151,17 +1151,17 @@ static int launch_wino88i32_gemm_mid(const int8_t* V8, const int* ev, const int8
 }
 
 // the lagging-half form (wino88i32_gemm_lag_kernel); STAG: only waves 0-3 lag
-template <int K, bool STAG>
+template <int K, bool STAG, int LJ = 2>
 static int launch_wino88i32_gemm_lag(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
                                      int rows, int stride, hipStream_t st) {
     using T = kv::Wino88iTile<kv::kI8DigitsF32>;
     constexpr int bytes = 3 * T::STAGE;
-    KV_HIP(lds_opt_in((const void*)kv::wino88i32_gemm_lag_kernel<K, STAG>, bytes));
+    KV_HIP(lds_opt_in((const void*)kv::wino88i32_gemm_lag_kernel<K, STAG, LJ>, bytes));
     const int nwg = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
     KV_REQUIRE(rows % T::WM == 0 && stride % T::WM == 0 && nwg % 8 == 0, KV_EINVAL,
                "wino gemm i8 (lag): rows %d / stride %d vs tile %d", rows, stride, T::WM);
-    hipLaunchKernelGGL((kv::wino88i32_gemm_lag_kernel<K, STAG>), dim3(nwg), dim3(T::THREADS), bytes, st, V8, ev, U8,
-                       eu, M, rows, 512, stride);
+    hipLaunchKernelGGL((kv::wino88i32_gemm_lag_kernel<K, STAG, LJ>), dim3(nwg), dim3(T::THREADS), bytes, st, V8, ev,
+                       U8, eu, M, rows, 512, stride);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -2165,6 +2165,12 @@ int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, flo
             case 15:  // staggered: waves 0-3 lag, 4-7 do not
                 return k5 ? launch_wino88i32_gemm_lag<512, true>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0)
                           : launch_wino88i32_gemm_lag<256, true>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0);
+            case 16:  // every wave lags B digits 1-3 (12 MFMAs) by a barrier
+                return k5 ? launch_wino88i32_gemm_lag<512, false, 1>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0)
+                          : launch_wino88i32_gemm_lag<256, false, 1>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0);
+            case 17:  // every wave lags B digit 3 (2 MFMAs)
+                return k5 ? launch_wino88i32_gemm_lag<512, false, 3>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0)
+                          : launch_wino88i32_gemm_lag<256, false, 3>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0);
             case 10:  // variant 1 with the M stores deferred past the next tile's first copies
                 return k5 ? launch_wino88i32_gemm<512, 32, 3, 1, 0, true>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0)
                           : launch_wino88i32_gemm<256, 32, 3, 1, 0, true>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, true, 0);

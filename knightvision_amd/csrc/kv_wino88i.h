@@ -490,7 +490,7 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_mid_kernel(const int8_t* _
 // 4-7 do not -- the two waves of a SIMD then reach each barrier at different points of their MFMA streams
 // (one finishing a stage, one mid-stage), so one issues MFMAs while the other waits on its LDS reads; else
 // every wave lags. Same products, same bits.
-template <int K, bool STAG>
+template <int K, bool STAG, int LJ = 2>
 __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* __restrict__ V8,
                                                                  const int* __restrict__ ev,
                                                                  const int8_t* __restrict__ U8,
@@ -500,7 +500,8 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* _
     using T = Wino88iTile<S>;
     constexpr int NT = T::NT, WM = T::WM, WN = T::WN, GL = T::GL;
     constexpr int NK = K / 32;
-    static_assert(GL == 4 && NK >= 3, "4 pieces per wave and stage");
+    constexpr int NA = S - LJ;  // A digits the lagging half uses (0 .. S - LJ - 1)
+    static_assert(GL == 4 && NK >= 3 && LJ >= 1 && LJ <= 3, "4 pieces per wave and stage; B digits LJ.. lag");
 
     extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8l[];
     char* const L0 = (char*)lds_i8l;
@@ -546,15 +547,16 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* _
     for (int l = 0; l < S; ++l)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[l][nt] = i32x16_t{};
-    // h2 of the previous stage (lagging waves): its A digits 0-1 and B digits 2-3
-    i8x16_t pa0 = {}, pa1 = {}, pb2[NT] = {}, pb3[NT] = {};
-    auto h2 = [&](const i8x16_t& x0, const i8x16_t& x1, const i8x16_t (&y2)[NT], const i8x16_t (&y3)[NT]) {
+    // h2 of a stage: B digits j >= LJ with the A digits i < S - j
+    i8x16_t pa[NA] = {}, pb[S - LJ][NT] = {};
+    auto h2 = [&](const i8x16_t (&x)[NA], const i8x16_t (&y)[S - LJ][NT]) {
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[2][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(x0, y2[nt], acc[2][nt], 0, 0, 0);
+        for (int j = LJ; j < S; ++j)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[3][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(x1, y2[nt], acc[3][nt], 0, 0, 0);
+            for (int i = 0; i + j < S; ++i)
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[3][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(x0, y3[nt], acc[3][nt], 0, 0, 0);
+                for (int nt = 0; nt < NT; ++nt)
+                    acc[i + j][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(x[i], y[j - LJ][nt], acc[i + j][nt], 0, 0, 0);
     };
 
     issue1(0, 0); issue1(1, 0); issue1(2, 0); issue1(3, 0);
@@ -568,49 +570,44 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* _
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         const char* buf = L0 + (kt % NBUF) * T::STAGE;
-        i8x16_t a[S], b0[NT], b1[NT], b2[NT], b3[NT];
+        i8x16_t a[S], b[S][NT];
 #pragma unroll
         for (int i = 0; i < S; ++i) a[i] = *(const i8x16_t*)(buf + aoffr[i]);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) b0[nt] = *(const i8x16_t*)(buf + boffr[nt][0]);
-        if (lag && kt > 0) h2(pa0, pa1, pb2, pb3);  // under the reads above
-        if (kt + 2 < NK) {  // stage kt + 2 into stage kt - 1's buffer
+        for (int nt = 0; nt < NT; ++nt) b[0][nt] = *(const i8x16_t*)(buf + boffr[nt][0]);
+        if (lag && kt > 0) h2(pa, pb);  // under the reads above
+        // stage kt + 2 into stage kt - 1's buffer, two pieces at the start, two after the first B digit
+        if (kt + 2 < NK) {
             issue1(0, kt + 2);
             issue1(1, kt + 2);
         }
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) b1[nt] = *(const i8x16_t*)(buf + boffr[nt][1]);
+        for (int j = 0; j < S; ++j) {
+            if (j + 1 < S) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-                acc[i][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b0[nt], acc[i][nt], 0, 0, 0);
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) b2[nt] = *(const i8x16_t*)(buf + boffr[nt][2]);
-        if (kt + 2 < NK) {
-            issue1(2, kt + 2);
-            issue1(3, kt + 2);
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-                acc[i + 1][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b1[nt], acc[i + 1][nt], 0, 0, 0);
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) b3[nt] = *(const i8x16_t*)(buf + boffr[nt][3]);
-        if (lag) {  // h2(kt) after the next barrier
-            pa0 = a[0];
-            pa1 = a[1];
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-                pb2[nt] = b2[nt];
-                pb3[nt] = b3[nt];
+                for (int nt = 0; nt < NT; ++nt) b[j + 1][nt] = *(const i8x16_t*)(buf + boffr[nt][j + 1]);
             }
-        } else {
-            h2(a[0], a[1], b2, b3);
+            if (j < LJ) {
+#pragma unroll
+                for (int i = 0; i + j < S; ++i)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+                        acc[i + j][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[j][nt], acc[i + j][nt], 0, 0, 0);
+            }
+            if (j == 0 && kt + 2 < NK) {
+                issue1(2, kt + 2);
+                issue1(3, kt + 2);
+            }
         }
+#pragma unroll
+        for (int i = 0; i < NA; ++i) pa[i] = a[i];
+#pragma unroll
+        for (int j = LJ; j < S; ++j)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) pb[j - LJ][nt] = b[j][nt];
+        if (!lag) h2(pa, pb);  // h2(kt) now
     }
-    if (lag) h2(pa0, pa1, pb2, pb3);
+    if (lag) h2(pa, pb);
 
     // epilogue (as wino88i_gemm_kernel's): D col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
     const int* evx = ev + (size_t)xi * stride + r_base + wm * 32;
