@@ -1150,6 +1150,22 @@ static int launch_wino88i32_gemm_mid(const int8_t* V8, const int* ev, const int8
     return KV_OK;
 }
 
+// KV_PREC_I8X5's GEMM with the lagging half (wino88i_gemm_lag5_kernel)
+template <int K, int LJ = 3>
+static int launch_wino88i_gemm_lag5(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, double* M,
+                                    int rows, int stride, hipStream_t st) {
+    using T = kv::Wino88iTile<kv::kI8Digits>;
+    constexpr int bytes = 3 * T::STAGE;
+    KV_HIP(lds_opt_in((const void*)kv::wino88i_gemm_lag5_kernel<K, LJ>, bytes));
+    const int nwg = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
+    KV_REQUIRE(rows % T::WM == 0 && stride % T::WM == 0 && nwg % 8 == 0, KV_EINVAL,
+               "wino gemm i8x5 (lag): rows %d / stride %d vs tile %d", rows, stride, T::WM);
+    hipLaunchKernelGGL((kv::wino88i_gemm_lag5_kernel<K, LJ>), dim3(nwg), dim3(T::THREADS), bytes, st, V8, ev, U8, eu,
+                       M, rows, 512, stride);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
 // the lagging-half form (wino88i32_gemm_lag_kernel); STAG: only waves 0-3 lag
 template <int K, bool STAG, int LJ = 2>
 static int launch_wino88i32_gemm_lag(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
@@ -1204,6 +1220,19 @@ static int launch_wino88i_out(kv_net* net, int l, const double* M, int nb, int s
     return KV_OK;
 }
 
+// KV_PREC_I8X5's GEMM: wino88i_gemm_lag5_kernel (the lagging half; bit-identical); KV_I8X5_GEMM=r4: the
+// round-4 wino88i_gemm_kernel<K, 5>
+template <int K>
+static int i8x5_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, double* M, int rows, int stride,
+                     hipStream_t st) {
+    static const bool r4 = [] {
+        const char* e = getenv("KV_I8X5_GEMM");
+        return e && !strcmp(e, "r4");
+    }();
+    if (r4) return launch_wino88i_gemm<K>(V8, ev, U8, eu, M, rows, stride, st);
+    return launch_wino88i_gemm_lag5<K>(V8, ev, U8, eu, M, rows, stride, st);
+}
+
 static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     const int rows = nb, stride = rows;
     double* M = (double*)net->Mw;
@@ -1212,7 +1241,7 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     // conv2: the stem wrote V64 (256 channels); its digits by the slice kernel
     if ((rc = launch_wino88i_slice<256>((const double*)net->V256, rows, stride, kv::W88_XI, net->V8, net->ev8, st)))
         return rc;
-    if ((rc = launch_wino88i_gemm<256>(net->V8, net->ev8, U + net->uoff88[1] * kv::kI8Digits,
+    if ((rc = i8x5_gemm<256>(net->V8, net->ev8, U + net->uoff88[1] * kv::kI8Digits,
                                        net->eu88i + net->euoff[1], M, rows, stride, st)))
         return rc;
     if ((rc = launch_wino88i_out<false>(net, 1, M, nb, stride, nullptr, net->X, st))) return rc;
@@ -1221,12 +1250,12 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         const bool m = mark && r == 2;
         if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-        if ((rc = launch_wino88i_gemm<512>(net->V8, net->ev8, U + net->uoff88[l1] * kv::kI8Digits,
+        if ((rc = i8x5_gemm<512>(net->V8, net->ev8, U + net->uoff88[l1] * kv::kI8Digits,
                                            net->eu88i + net->euoff[l1], M, rows, stride, st)))
             return rc;
         if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
         if ((rc = launch_wino88i_out<false>(net, l1, M, nb, stride, nullptr, net->T, st))) return rc;
-        if ((rc = launch_wino88i_gemm<512>(net->V8, net->ev8, U + net->uoff88[l2] * kv::kI8Digits,
+        if ((rc = i8x5_gemm<512>(net->V8, net->ev8, U + net->uoff88[l2] * kv::kI8Digits,
                                            net->eu88i + net->euoff[l2], M, rows, stride, st)))
             return rc;
         rc = r < 4 ? launch_wino88i_out<true>(net, l2, M, nb, stride, net->X, net->X, st)

@@ -76,6 +76,59 @@ __device__ inline void i8_digits(T v, int e, int (&d)[D]) {
     }
 }
 
+// max over the 32 lanes of each half-wave of v, by DPP-modified max operations (no selects, no LDS-pipe
+// shuffle): xor 1 and xor 2 within quads, the half-row and row mirrors (every lane then holds its 16-lane
+// row's max), then row_bcast:15 into rows 1 and 3 -- lanes 16-31 end with the max of lanes 0-31, lanes
+// 48-63 with the max of lanes 32-63.
+__device__ inline unsigned i8_half_max_dpp(unsigned v) {
+    // old = 0 (the identity of an unsigned max) so the compiler folds each DPP move into its max
+    unsigned t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);  // quad_perm 1,0,3,2
+    v = v > t ? v : t;
+    t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);  // quad_perm 2,3,0,1
+    v = v > t ? v : t;
+    t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, true);  // row_half_mirror
+    v = v > t ? v : t;
+    t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, true);  // row_mirror
+    v = v > t ? v : t;
+    t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    return v > t ? v : t;
+}
+
+// The 4 digits of an fp32 v under exponent e (i8_digits<4>) packed into one dword, digit d in byte d: each
+// rint(t) as t + 1.5 * 2^23 (|t| <= 128: the add rounds to the integer, ties to even, as rintf) whose low byte
+// is the digit's two's complement; q - 1.5 * 2^23 is rint(t) exactly, so t - rint(t) and the x128 are the
+// same operations as i8_digits's -- the same digits, without the float -> int conversions.
+__device__ inline unsigned i8_digits4_packed(float v, int e) {
+#pragma clang fp contract(off)
+    constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23
+    float t = ldexpf(v, 7 - e);
+    unsigned q[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float qf = t + kMagic;
+        q[i] = __float_as_uint(qf);
+        if (i < 3) t = (t - (qf - kMagic)) * 128.0f;
+    }
+    const unsigned lo = __builtin_amdgcn_perm(q[1], q[0], 0x0c0c0400u);  // [q0.b0, q1.b0, 0, 0]
+    const unsigned hi = __builtin_amdgcn_perm(q[3], q[2], 0x0c0c0400u);
+    return lo | hi << 16;
+}
+
+// lane quad q = lane & 3 holds P = digits 0..3 of its channel (byte d = digit d); returns digit q of the
+// quad's 4 channels (byte j = channel 4 (lane / 4) + j)
+__device__ inline unsigned i8_quad_transpose(unsigned P, int lane) {
+    const unsigned q1 = (unsigned)__builtin_amdgcn_mov_dpp((int)P, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+    // even lane: [P.0 q1.0 P.2 q1.2], odd: [q1.1 P.1 q1.3 P.3]
+    const unsigned R = __builtin_amdgcn_perm(q1, P, (lane & 1) ? 0x03070105u : 0x06020400u);
+    const unsigned r2 = (unsigned)__builtin_amdgcn_mov_dpp((int)R, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+    // lanes 0, 1 of the quad: [R.0 R.1 r2.0 r2.1], lanes 2, 3: [r2.2 r2.3 R.2 R.3]
+    return __builtin_amdgcn_perm(r2, R, (lane & 2) ? 0x03020706u : 0x05040100u);
+}
+
+// CW channels per workgroup (2 CW threads: a plane split over lanes l, l ^ 32): 512 -- the row's exponent
+// over all its channels, one workgroup per board -- or 256 -- one exponent per 256-channel segment
+// (ex[(xi * 2 + seg) * rows + b]), two workgroups per board, so a CU holds two of them and one's loads
+// overlap the other's transforms and reductions.
 // The digits and exponent of `nslab` slabs of n rows of K fp64 values: row r of
 // slab x is src[(x * slab_rows + r) * K ...]; digit d of its channels
 // [32 kc, 32 kc + 32) goes to plane (x, kc, d) of dst -- 32 bytes at
@@ -626,6 +679,146 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* _
     }
 }
 
+// KV_PREC_I8X5's GEMM (5 digits, digit planes, fp64 M) with wino88i32_gemm_lag_kernel's schedule: the
+// B digits j >= LJ of a stage (their pairs i + j <= 4) run after the next barrier, under that stage's first
+// LDS reads; stage k + 2's copies (5 pieces per wave) go into stage k - 1's buffer right after barrier k.
+// Same products, same bits as wino88i_gemm_kernel<K, 5, ., double>.
+template <int K, int LJ = 3>
+__global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __restrict__ V8,
+                                                                const int* __restrict__ ev,
+                                                                const int8_t* __restrict__ U8,
+                                                                const int* __restrict__ eu, double* __restrict__ M,
+                                                                int rows, int cout, int stride) {
+    constexpr int S = 5, NBUF = 3;
+    using T = Wino88iTile<S>;
+    constexpr int NT = T::NT, WM = T::WM, WN = T::WN, GL = T::GL;
+    constexpr int NK = K / 32;
+    constexpr int NA = S - LJ;
+    static_assert(GL == 5 && NK >= 3 && LJ >= 1 && LJ < S, "5 pieces per wave and stage");
+
+    extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8l5[];
+    char* const L0 = (char*)lds_i8l5;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / T::WC, wn = wave % T::WC;
+    const int CT = cout / WN, RT = rows / WM;
+    const int nwg = (int)gridDim.x;  // a multiple of 8
+    const int idx = (int)(blockIdx.x & 7) * (nwg >> 3) + (int)(blockIdx.x >> 3);
+    const int xi = idx / (CT * RT);
+    const int n_base = (idx % CT) * WN;
+    const int r_base = ((idx / CT) % RT) * WM;
+
+    // copy pieces as wino88i_gemm_kernel's planes path: piece q = wave * 5 + g covers operand q / 20, digit
+    // (q % 20) / 4, rows 32 (q % 4) .. +31; lane l fills LDS row 32 (q % 4) + l / 2, half l & 1 (swapped on
+    // bit 3 of the row)
+    const int op = (wave * GL) / (4 * S);
+    const size_t rstride = op ? (size_t)cout : (size_t)stride;
+    const int8_t* gbase = op ? U8 + (((size_t)xi * NK) * S * cout + (size_t)n_base) * 32
+                             : V8 + (((size_t)xi * NK) * S * stride + (size_t)r_base) * 32;
+    const size_t sstep = (size_t)S * rstride * 32;
+    const int lane_off = (lane >> 1) * 32 + 16 * ((lane & 1) ^ ((lane >> 4) & 1));
+    auto issue1 = [&](int g, int kt) {
+        const int q = wave * GL + g, d = (q % (4 * S)) / 4, rg = q % 4;
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(gbase + kt * sstep + ((size_t)d * rstride + rg * 32) * 32 + lane_off),
+            (__attribute__((address_space(3))) void*)(L0 + (kt % NBUF) * T::STAGE + op * S * T::PLANE + d * T::PLANE +
+                                                      rg * 1024),
+            16, 0, 0);
+    };
+
+    const int lr = lane & 31, lh = lane >> 5;
+    const int arow = wm * 32 + lr;
+    const int aoff = arow * 32 + i8_lds_half(arow, lh);
+    int boff[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int bcol = wn * NT * 32 + nt * 32 + lr;
+        boff[nt] = S * T::PLANE + bcol * 32 + i8_lds_half(bcol, lh);
+    }
+
+    i32x16_t acc[S][NT];
+#pragma unroll
+    for (int l = 0; l < S; ++l)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[l][nt] = i32x16_t{};
+    i8x16_t pa[NA] = {}, pb[S - LJ][NT] = {};
+    auto h2 = [&]() {
+#pragma unroll
+        for (int j = LJ; j < S; ++j)
+#pragma unroll
+            for (int i = 0; i + j < S; ++i)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    acc[i + j][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(pa[i], pb[j - LJ][nt], acc[i + j][nt], 0, 0, 0);
+    };
+
+#pragma unroll
+    for (int g = 0; g < GL; ++g) issue1(g, 0);
+#pragma unroll
+    for (int g = 0; g < GL; ++g) issue1(g, 1);
+    for (int kt = 0; kt < NK; ++kt) {
+        if (kt + 1 < NK)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const char* buf = L0 + (kt % NBUF) * T::STAGE;
+        i8x16_t a[S], b[NT];
+#pragma unroll
+        for (int i = 0; i < S; ++i) a[i] = *(const i8x16_t*)(buf + aoff + i * T::PLANE);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) b[nt] = *(const i8x16_t*)(buf + boff[nt]);
+        if (kt > 0) h2();  // the previous stage's lagging half, under the reads above
+        if (kt + 2 < NK) {
+            issue1(0, kt + 2);
+            issue1(1, kt + 2);
+        }
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            if (j > 0) {
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) b[nt] = *(const i8x16_t*)(buf + boff[nt] + j * T::PLANE);
+            }
+            if (j < LJ) {
+#pragma unroll
+                for (int i = 0; i + j < S; ++i)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+                        acc[i + j][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[nt], acc[i + j][nt], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) pb[j - LJ][nt] = b[nt];
+            }
+            if (j == 0 && kt + 2 < NK) {
+                issue1(2, kt + 2);
+                issue1(3, kt + 2);
+                issue1(4, kt + 2);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NA; ++i) pa[i] = a[i];
+    }
+    h2();
+
+    // epilogue (as wino88i_gemm_kernel's): D col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+    const int* evx = ev + (size_t)xi * stride + r_base + wm * 32;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int col = n_base + wn * NT * 32 + nt * 32 + lr;
+        const int ec = eu[(size_t)xi * cout + col] - 14;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+            double m = (double)acc[S - 1][nt][r];
+#pragma unroll
+            for (int l = S - 2; l >= 0; --l) m = __builtin_fma(m, 0.0078125, (double)acc[l][nt][r]);  // exact
+            M[((size_t)xi * stride + r_base + wm * 32 + row) * cout + col] = ldexp(m, evx[row] + ec);
+        }
+    }
+}
+
 // The next conv's digits come from two kernels, each at the occupancy of the
 // fp64 out kernel (one workgroup = 128 channels of one board): the exponent of
 // a V row needs the largest magnitude over all 512 channels, i.e. over 4
@@ -675,7 +868,7 @@ __global__ __launch_bounds__(256) void wino88i_outmax_kernel(const double* __res
                                                              const float* __restrict__ scale,
                                                              const float* __restrict__ shift, const float* resid,
                                                              float* Y, unsigned* __restrict__ evmax) {
-    __shared__ unsigned red[4][2][5][16];
+    __shared__ __attribute__((aligned(16))) unsigned red[4][2][5][16];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
     const int c = blockIdx.x * 128 + w * 32 + (lane & 31), b = blockIdx.y;
     double t2[10][4];
@@ -688,8 +881,16 @@ __global__ __launch_bounds__(256) void wino88i_outmax_kernel(const double* __res
     for (int aa = 0; aa < 5; ++aa) {
         double o[10];
         wino88d_input_row(t2, h, aa, o);
-        const unsigned m = i8_half_max10(o, lane);
-        if ((lane & 16) == 0 && (lane & 15) < 10) red[w][h][aa][lane & 15] = m;
+        unsigned m[10];
+#pragma unroll
+        for (int bb = 0; bb < 10; ++bb)
+            m[bb] = i8_half_max_dpp((unsigned)(__double_as_longlong(o[bb]) >> 32) & 0x7fffffffu);
+        if ((lane & 31) == 16) {  // this half's 10 maxima (high words), written by one lane
+            uint4* rr = (uint4*)&red[w][h][aa][0];
+            rr[0] = make_uint4(m[0], m[1], m[2], m[3]);
+            rr[1] = make_uint4(m[4], m[5], m[6], m[7]);
+            *(uint2*)&red[w][h][aa][8] = make_uint2(m[8], m[9]);
+        }
     }
     __syncthreads();
     if (threadIdx.x < 100) {
@@ -727,6 +928,8 @@ __global__ __launch_bounds__(256) void wino88i_in_kernel(const float* __restrict
     double t2[10][4];
     wino88d_input_cols(x2, h, t2);
     __syncthreads();
+    // (one byte store per digit: a lane-quad transpose into dword stores measured 3 % slower here,
+    // profiles/r05_i8x5_ab.log -- the kernel is bound by its fp64 transform and digit arithmetic)
 #pragma unroll
     for (int aa = 0; aa < 5; ++aa) {
         double o[10];
@@ -1048,59 +1251,6 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
 // profiles/r04_i8f32_fused_out.log; and an output kernel computing only the row maxima plus a second
 // input-transform pass, 294-356 + 220 us, profiles/r04_i8f32_outmax_form.log.)
 
-// max over the 32 lanes of each half-wave of v, by DPP-modified max operations (no selects, no LDS-pipe
-// shuffle): xor 1 and xor 2 within quads, the half-row and row mirrors (every lane then holds its 16-lane
-// row's max), then row_bcast:15 into rows 1 and 3 -- lanes 16-31 end with the max of lanes 0-31, lanes
-// 48-63 with the max of lanes 32-63.
-__device__ inline unsigned i8_half_max_dpp(unsigned v) {
-    // old = 0 (the identity of an unsigned max) so the compiler folds each DPP move into its max
-    unsigned t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);  // quad_perm 1,0,3,2
-    v = v > t ? v : t;
-    t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);  // quad_perm 2,3,0,1
-    v = v > t ? v : t;
-    t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, true);  // row_half_mirror
-    v = v > t ? v : t;
-    t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, true);  // row_mirror
-    v = v > t ? v : t;
-    t = (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
-    return v > t ? v : t;
-}
-
-// The 4 digits of an fp32 v under exponent e (i8_digits<4>) packed into one dword, digit d in byte d: each
-// rint(t) as t + 1.5 * 2^23 (|t| <= 128: the add rounds to the integer, ties to even, as rintf) whose low byte
-// is the digit's two's complement; q - 1.5 * 2^23 is rint(t) exactly, so t - rint(t) and the x128 are the
-// same operations as i8_digits's -- the same digits, without the float -> int conversions.
-__device__ inline unsigned i8_digits4_packed(float v, int e) {
-#pragma clang fp contract(off)
-    constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23
-    float t = ldexpf(v, 7 - e);
-    unsigned q[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const float qf = t + kMagic;
-        q[i] = __float_as_uint(qf);
-        if (i < 3) t = (t - (qf - kMagic)) * 128.0f;
-    }
-    const unsigned lo = __builtin_amdgcn_perm(q[1], q[0], 0x0c0c0400u);  // [q0.b0, q1.b0, 0, 0]
-    const unsigned hi = __builtin_amdgcn_perm(q[3], q[2], 0x0c0c0400u);
-    return lo | hi << 16;
-}
-
-// lane quad q = lane & 3 holds P = digits 0..3 of its channel (byte d = digit d); returns digit q of the
-// quad's 4 channels (byte j = channel 4 (lane / 4) + j)
-__device__ inline unsigned i8_quad_transpose(unsigned P, int lane) {
-    const unsigned q1 = (unsigned)__builtin_amdgcn_mov_dpp((int)P, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
-    // even lane: [P.0 q1.0 P.2 q1.2], odd: [q1.1 P.1 q1.3 P.3]
-    const unsigned R = __builtin_amdgcn_perm(q1, P, (lane & 1) ? 0x03070105u : 0x06020400u);
-    const unsigned r2 = (unsigned)__builtin_amdgcn_mov_dpp((int)R, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
-    // lanes 0, 1 of the quad: [R.0 R.1 r2.0 r2.1], lanes 2, 3: [r2.2 r2.3 R.2 R.3]
-    return __builtin_amdgcn_perm(r2, R, (lane & 2) ? 0x03020706u : 0x05040100u);
-}
-
-// CW channels per workgroup (2 CW threads: a plane split over lanes l, l ^ 32): 512 -- the row's exponent
-// over all its channels, one workgroup per board -- or 256 -- one exponent per 256-channel segment
-// (ex[(xi * 2 + seg) * rows + b]), two workgroups per board, so a CU holds two of them and one's loads
-// overlap the other's transforms and reductions.
 template <bool RESID, bool WRITE_Y, int CW>
 __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __restrict__ M, int rows,
                                                                const float* __restrict__ scale,
