@@ -138,10 +138,11 @@ def test_mcts_network_visits_identical_to_oracle_c3_first_move(variant):
     _compare_network_games(variant, slots=2048, n_check=8, sims=800, max_moves=None, steps=1)
 
 
-@pytest.mark.parametrize("variant", ["init", "peaked"])
+@pytest.mark.parametrize("variant", ["init", "peaked", "stress"])
 def test_mcts_network_visits_identical_to_oracle_c3_three_moves(variant):
     """C3, the headline config (2,048 slots x 800 sims): the first three moves of the first 8 games -- trees
-    that start from positions the search itself chose."""
+    that start from positions the search itself chose. "stress" (trained-network magnitudes): the AUTO path
+    there is the fp64 Winograd domain on int8 digits, and the peaked priors give the trees their own shapes."""
     _compare_network_games(variant, slots=2048, n_check=8, sims=800, max_moves=None, steps=3)
 
 
