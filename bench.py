@@ -320,9 +320,10 @@ def gemm_label(path: int, rows: int, split: int):
             "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 tiles, "
             "each stage's last 6 MFMAs per wave under the next stage's first LDS reads)")
     if path == 5:
-        return "wino88i_gemm_kernel<512,5,true,double>", (
+        return "wino88i_gemm_lag5_kernel<512,3>", (
             " (residual-tower Winograd F(8x8,3x3) GEMMs in the fp64 domain from 5 int8 digits per value: 15 "
-            "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, 128x128 tiles)")
+            "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, 128x128 tiles, each stage's last "
+            "MFMAs under the next stage's first LDS reads)")
     if path == 3:
         name = ("wino88d_gemm_kernel<512,2,4,4,2>" if rows % 128 == 0 else
                 "wino88d_gemm_kernel<512,1,4,4,2>" if rows % 64 == 0 else "wino88d_gemm_kernel<512,1,4,2,2>")

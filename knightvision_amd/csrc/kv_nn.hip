@@ -647,11 +647,13 @@ struct kv_net {
     unsigned* vmax = nullptr;  // f16x3: per-board max |V| of each conv's input, [12][cap]
     float* stemT = nullptr; // conv1 as [tap][piece][cout] (stem_kernel)
     float* v1wT = nullptr;  // value_fc1 weight as [k][o] (heads_kernel)
-    // Winograd workspaces (bytes per board: kWsBoard / kWs256Board), shared by every path
+    // Winograd workspaces, shared by the paths; each sized by net_reserve_ws for the paths this net has run
+    // (ws_cap: bytes allocated, grown only)
     void* V = nullptr;
     void* V256 = nullptr;   // conv2's input transform
     void* Mw = nullptr;
-    int8_t* V8 = nullptr;   // KV_PATH_WINO88_I8: V's digit planes [100][512/32][5][board][32], exponents [100][board]
+    int8_t* V8 = nullptr;   // the int8-digit paths: V's digit planes [100][512/32][digits][board][32]
+    size_t ws_cap[4] = {};  // V, Mw, V256, V8
     int* ev8 = nullptr;
     unsigned* evmax8 = nullptr;  // the next V's per-row max |V| (high words), [100][board]
     // fp32 + AUTO: the paths chosen by the last calibration (> 16 boards / <= 16)
@@ -671,10 +673,6 @@ struct kv_net {
     int dom_split = 0;  // F(8x8) fp32: points run as 128x128 tiles in the first launch (100: one launch)
     double dom_flop = 0;
 };
-
-// workspace bytes per board: the largest path's V / M (F(8x8) in fp64: 100 points x 512 doubles;
-// F(4x8): 120 rows x 512 floats; F(8x8) fp32: 100 x 512 floats)
-constexpr size_t kWsBoard = (size_t)100 * 512 * 8, kWs256Board = (size_t)100 * 256 * 8;
 
 // Small batches (<= 16 boards: the sequential reference path, batch-16
 // schedules) have far fewer output tiles than CUs: split K into groups of 3
@@ -786,11 +784,8 @@ static int net_reserve(kv_net* net, int nb_pad) {
     if (nb_pad <= net->cap) return KV_OK;
     int cap = nb_pad < 64 ? 64 : nb_pad;
     (void)hipFree(net->x16); (void)hipFree(net->X); (void)hipFree(net->T); (void)hipFree(net->pfeat);
-    (void)hipFree(net->V); (void)hipFree(net->Mw); (void)hipFree(net->V256); (void)hipFree(net->vmax);
-    (void)hipFree(net->V8); (void)hipFree(net->ev8); (void)hipFree(net->evmax8);
+    (void)hipFree(net->vmax); (void)hipFree(net->ev8); (void)hipFree(net->evmax8);
     net->x16 = net->X = net->T = net->pfeat = nullptr;
-    net->V = net->Mw = net->V256 = nullptr;
-    net->V8 = nullptr;
     net->ev8 = nullptr;
     net->evmax8 = nullptr;
     net->vmax = nullptr;
@@ -799,11 +794,7 @@ static int net_reserve(kv_net* net, int nb_pad) {
     KV_HIP(hipMalloc(&net->X, (size_t)cap * 64 * 512 * 4));
     KV_HIP(hipMalloc(&net->T, (size_t)cap * 64 * 512 * 4));
     KV_HIP(hipMalloc(&net->pfeat, (size_t)cap * 128 * 4));
-    KV_HIP(hipMalloc(&net->V, (size_t)cap * kWsBoard));
-    KV_HIP(hipMalloc(&net->Mw, (size_t)cap * kWsBoard));
-    KV_HIP(hipMalloc(&net->V256, (size_t)cap * kWs256Board));
     KV_HIP(hipMalloc(&net->vmax, (size_t)12 * cap * sizeof(unsigned)));
-    KV_HIP(hipMalloc(&net->V8, (size_t)cap * kv::W88_XI * 512 * kv::kI8Digits));
     KV_HIP(hipMalloc(&net->ev8, (size_t)cap * kv::W88_XI * 2 * sizeof(int)));  // 2: segment exponents
     KV_HIP(hipMalloc(&net->evmax8, (size_t)cap * kv::W88_XI * sizeof(unsigned)));
     if (!net->slab)  // 48 splits x 16 boards x 64 px x 512 channels
@@ -1381,6 +1372,45 @@ static int wino88i32_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
     return KV_OK;
 }
 
+// Winograd workspace bytes per board of a conv path: V (the residual convs' input transform), M (the GEMM
+// output), V256 (conv2's input transform), V8 (the digit planes). F(4x8): 2 rows per board of 60 points;
+// F(8x8): 1 row of 100 points; fp64 on the fp64 domains (the 5-digit one keeps no fp64 V: its output kernel
+// writes the digits)
+struct WsNeed {
+    size_t b[4];
+};
+static WsNeed ws_need(int path) {
+    constexpr size_t f = 4, d = 8, R48 = 2 * kv::W48_XI, P88 = kv::W88_XI;
+    switch (path) {
+        case KV_PATH_WINO48:
+        case KV_PATH_WINO48_F16X3: return {{R48 * 512 * f, R48 * 512 * f, R48 * 256 * f, 0}};
+        case KV_PATH_WINO88: return {{P88 * 512 * f, P88 * 512 * f, P88 * 256 * f, 0}};
+        case KV_PATH_WINO88_F64: return {{P88 * 512 * d, P88 * 512 * d, P88 * 256 * d, 0}};
+        case KV_PATH_WINO88_I8: return {{0, P88 * 512 * d, P88 * 256 * d, P88 * 512 * kv::kI8Digits}};
+        case KV_PATH_WINO88_I8F32:
+            return {{i8f32_form().slice ? P88 * 512 * f : 0, P88 * 512 * f, P88 * 256 * f,
+                     P88 * 512 * kv::kI8DigitsF32}};
+        default: return {{0, 0, 0, 0}};  // direct: the split-K slab only
+    }
+}
+
+// grow the workspaces to what `path` needs at net->cap boards (a buffer only ever grows, so a forward on
+// another path never shrinks one under the first)
+static int net_reserve_ws(kv_net* net, int path) {
+    void** buf[4] = {&net->V, &net->Mw, &net->V256, (void**)&net->V8};
+    const WsNeed n = ws_need(path);
+    for (int i = 0; i < 4; ++i) {
+        const size_t need = n.b[i] * (size_t)net->cap;
+        if (need <= net->ws_cap[i]) continue;
+        (void)hipFree(*buf[i]);
+        *buf[i] = nullptr;
+        net->ws_cap[i] = 0;
+        KV_HIP(hipMalloc(buf[i], need));
+        net->ws_cap[i] = need;
+    }
+    return KV_OK;
+}
+
 // Winograd tower on `path`: conv2 and the 5 residual blocks (conv1 output in
 // net->T, or conv2's input transform already in net->V256 when v256_ready)
 static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hipStream_t st) {
@@ -1433,6 +1463,8 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     const int path = path_for(net, nb);
     KV_REQUIRE(net->built[path], KV_EINVAL, "kv_net: conv path %d has no weights (load the net after choosing it)",
                path);
+    KV_REQUIRE(nb_pad <= net->cap, KV_EINVAL, "kv_net: %d boards over the reserved %d", nb_pad, net->cap);
+    if ((rc = net_reserve_ws(net, path))) return rc;
     if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
     if (path == KV_PATH_WINO48_F16X3)
         KV_HIP(hipMemsetAsync(net->vmax, 0, (size_t)12 * net->cap * sizeof(unsigned), st));

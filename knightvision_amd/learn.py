@@ -74,6 +74,7 @@ def selfplay_shard(model, n_games: int, iteration: int, device, *, sims=0, max_m
                         precision=precision, eval_mode=batched_eval_mode() if sims == 0 else 0) as eng:
         eng.run()
         selfplay_shard.last_calibration = eng.calibration()  # the conv paths these weights ran on
+        selfplay_shard.last_stats = eng.stats()
         return eng.records(), eng.games()
 
 
@@ -234,6 +235,9 @@ def reinforcement_loop(model, iterations: int, games_per_iter: int, device, *, e
         cal = getattr(selfplay_shard, "last_calibration", None)
         if cal is not None:  # fp32 AUTO: the self-play network's conv path for this iteration's weights
             st["nn_path"] = cal["path_large"]
+        es = getattr(selfplay_shard, "last_stats", None)
+        if es is not None:  # this rank's engine: plies and MCTS simulations (the throughput a path flip moves)
+            st.update(plies=int(es["plies"]), sims=int(es["sims"]))
         model.train()
         data = extend_dataset(data, recs, games, dev)
         st.update(records=int(data[0].shape[0]) if data is not None else 0,

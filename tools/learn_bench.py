@@ -64,6 +64,10 @@ def main():
                           "train_samples_per_s": cnt.item() / tr_s if tr_s else None,
                           "val_loss": last.get("val_loss"), "records": last["records"], "wall_s": wall,
                           "nn_path_per_iteration": [st.get("nn_path") for st in stats],
+                          # rank 0's self-play per iteration (sims/s with --sims > 0, else plies/s): the spread a
+                          # change of conv path between iterations would show
+                          "selfplay_rate_per_iteration": [
+                              round((st.get("sims") or st.get("plies", 0)) / st["selfplay_s"], 1) for st in stats],
                           "data": "synthetic"}), flush=True)
     if world > 1:
         dist.barrier()
