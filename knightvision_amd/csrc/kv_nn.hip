@@ -780,7 +780,12 @@ static int net_pad(const kv_net* net, int B) {
     }
 }
 
+// boards per forward: the output / input kernels index the Winograd workspaces with 32-bit offsets (the
+// 5-digit planes of 100 x boards x 512 values: 256,000 bytes per board)
+constexpr int kMaxBoards = 16384;
+
 static int net_reserve(kv_net* net, int nb_pad) {
+    KV_REQUIRE(nb_pad <= kMaxBoards, KV_EINVAL, "kv_net: %d boards per forward (at most %d)", nb_pad, kMaxBoards);
     if (nb_pad <= net->cap) return KV_OK;
     int cap = nb_pad < 64 ? 64 : nb_pad;
     (void)hipFree(net->x16); (void)hipFree(net->X); (void)hipFree(net->T); (void)hipFree(net->pfeat);

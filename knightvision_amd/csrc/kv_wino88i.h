@@ -94,6 +94,23 @@ __device__ inline unsigned i8_half_max_dpp(unsigned v) {
     return v > t ? v : t;
 }
 
+// i8_digits<D> of an fp64 v with each rint(t) as t + 1.5 * 2^52 (|t| <= 128: the add rounds to the integer,
+// ties to even, as rint) -- q[i]'s low byte is digit i's two's complement; q - 1.5 * 2^52 is rint(t) exactly, so
+// the remainders are i8_digits's: the same digits with full-rate fp64 adds instead of v_rndne_f64 +
+// v_cvt_i32_f64
+template <int D>
+__device__ inline void i8_digits_magic(double v, int e, unsigned (&q)[D]) {
+#pragma clang fp contract(off)
+    constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
+    double t = ldexp(v, 7 - e);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        const double qf = t + kMagic;
+        q[i] = (unsigned)__double_as_longlong(qf);
+        if (i + 1 < D) t = (t - (qf - kMagic)) * 128.0;
+    }
+}
+
 // The 4 digits of an fp32 v under exponent e (i8_digits<4>) packed into one dword, digit d in byte d: each
 // rint(t) as t + 1.5 * 2^23 (|t| <= 128: the add rounds to the integer, ties to even, as rintf) whose low byte
 // is the digit's two's complement; q - 1.5 * 2^23 is rint(t) exactly, so t - rint(t) and the x128 are the
@@ -834,35 +851,6 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
 //     the same fp32 inputs: the same bits) and its 5 digits under the row
 //     exponents -- what wino88i_slice_kernel makes of that V64.
 
-// max over the 32 lanes of this half of v[0..9] (16 shuffles): lanes with (lane & 16) == 0 and
-// (lane & 15) < 10 return the max of index lane & 15
-__device__ inline unsigned i8_half_max10(const unsigned (&v10)[10], int lane) {
-    unsigned v[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = j < 10 ? v10[j] : 0u;
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {  // halving over offsets 8, 4, 2, 1: lane keeps index lane & 15
-        const int off = 8 >> st;
-        const bool up = (lane & off) != 0;
-#pragma unroll
-        for (int i = 0; i < off; ++i) {
-            const unsigned mine = up ? v[off + i] : v[i];
-            const unsigned other = (unsigned)__shfl_xor((int)(up ? v[i] : v[off + i]), off, 64);
-            v[i] = mine > other ? mine : other;
-        }
-    }
-    const unsigned o16 = (unsigned)__shfl_xor((int)v[0], 16, 64);
-    return v[0] > o16 ? v[0] : o16;
-}
-
-// the same over the high words of |o| (doubles)
-__device__ inline unsigned i8_half_max10(const double (&o)[10], int lane) {
-    unsigned v[10];
-#pragma unroll
-    for (int j = 0; j < 10; ++j) v[j] = (unsigned)(__double_as_longlong(o[j]) >> 32) & 0x7fffffffu;
-    return i8_half_max10(v, lane);
-}
-
 template <bool RESID>
 __global__ __launch_bounds__(256) void wino88i_outmax_kernel(const double* __restrict__ M, int rows,
                                                              const float* __restrict__ scale,
@@ -928,8 +916,13 @@ __global__ __launch_bounds__(256) void wino88i_in_kernel(const float* __restrict
     double t2[10][4];
     wino88d_input_cols(x2, h, t2);
     __syncthreads();
+    // 32-bit byte offsets (the digit planes of 100 x rows x 512 values, 5 digits: < 2^32 bytes): one base
+    // register + a 32-bit offset per store
+    const unsigned off0 = ((unsigned)kc * kI8Digits * rows + b) * 32 + (lane & 31);
+    const unsigned dstride = (unsigned)rows * 32, xstride = (C / 32) * kI8Digits * dstride;
     // (one byte store per digit: a lane-quad transpose into dword stores measured 3 % slower here,
-    // profiles/r05_i8x5_ab.log -- the kernel is bound by its fp64 transform and digit arithmetic)
+    // profiles/r05_i8x5_ab.log -- the kernel is bound by its fp64 transform and digit arithmetic; the digits
+    // by magic-number adds: profiles/r05_i8x5_magic_ab.log)
 #pragma unroll
     for (int aa = 0; aa < 5; ++aa) {
         double o[10];
@@ -938,11 +931,10 @@ __global__ __launch_bounds__(256) void wino88i_in_kernel(const float* __restrict
 #pragma unroll
         for (int bb = 0; bb < 10; ++bb) {
             const int xi = a * 10 + bb;
-            int dg[kI8Digits];
-            i8_digits<kI8Digits>(o[bb], exs[w][xi], dg);
-            int8_t* dst = V8n + ((((size_t)xi * (C / 32) + kc) * kI8Digits) * rows + b) * 32 + (lane & 31);
+            unsigned dg[kI8Digits];
+            i8_digits_magic<kI8Digits>(o[bb], exs[w][xi], dg);
 #pragma unroll
-            for (int d = 0; d < kI8Digits; ++d) dst[(size_t)d * rows * 32] = (int8_t)dg[d];
+            for (int d = 0; d < kI8Digits; ++d) V8n[off0 + (unsigned)xi * xstride + (unsigned)d * dstride] = (int8_t)dg[d];
         }
     }
 }
