@@ -59,22 +59,27 @@ def fwd(sd,planes,m,tabs,vp,gp,op,seq):
         h=cbr(x,f"res_blocks.{r}.conv1",f"res_blocks.{r}.bn1"); x=cbr(h,f"res_blocks.{r}.conv2",f"res_blocks.{r}.bn2",res=x)
     sdt={k:torch.from_numpy(v) for k,v in t.items()}
     return _heads(sdt, torch.from_numpy(x.transpose(0,3,1,2).astype(np.float64)))
-variant=sys.argv[1]; nb=int(sys.argv[2])
-sd=synthetic_state_dict(42,variant)
-rng=np.random.default_rng(5); codes=rng.integers(0,13,size=(nb,64))*(rng.random((nb,64))<0.4)
-planes=codes_to_planes(codes)
-p64,v64=torch_ref.forward({k:torch.from_numpy(np.asarray(v,dtype=np.float64)) for k,v in sd.items()},torch.from_numpy(planes.astype(np.float64)))
-p64=p64.numpy(); v64=v64.numpy().reshape(-1)
-T88=toom_cook(P88,8); T44=toom_cook(P44,4)
-D=np.float64
-cases=[("F88 all fp32 seq",8,T88,F32,F32,F32,True),
-       ("F88 V,U f32; GEMM f64; M,out f64",8,T88,F32,F32,D,False),
-       ("F88 V f64,U f32; GEMM f64; out f64",8,T88,D,F32,D,False),
-       ("F88 V f32,U f64; GEMM f64; out f64",8,T88,F32,D,D,False),
-       ("F88 all f64",8,T88,D,D,D,False),
-       ("F88 V,U,GEMM f64; M,out f32",8,T88,D,D,F32,False),
-       ("F44 all fp32 seq",4,T44,F32,F32,F32,True),
-       ("F44 V,U f32, GEMM f64, out f64",4,T44,F32,F32,D,False)]
-for name,m,tabs,vp,gp,op,seq in cases:
-    p,v=fwd(sd,planes,m,tabs,vp,gp,op,seq)
-    print(f"{variant} {name:40s} dlogit {np.abs(p-p64).max():.3e} dvalue {np.abs(v-v64).max():.3e}",flush=True)
+def main():
+    variant=sys.argv[1]; nb=int(sys.argv[2])
+    sd=synthetic_state_dict(42,variant)
+    rng=np.random.default_rng(5); codes=rng.integers(0,13,size=(nb,64))*(rng.random((nb,64))<0.4)
+    planes=codes_to_planes(codes)
+    p64,v64=torch_ref.forward({k:torch.from_numpy(np.asarray(v,dtype=np.float64)) for k,v in sd.items()},torch.from_numpy(planes.astype(np.float64)))
+    p64=p64.numpy(); v64=v64.numpy().reshape(-1)
+    T88=toom_cook(P88,8); T44=toom_cook(P44,4)
+    D=np.float64
+    cases=[("F88 all fp32 seq",8,T88,F32,F32,F32,True),
+           ("F88 V,U f32; GEMM f64; M,out f64",8,T88,F32,F32,D,False),
+           ("F88 V f64,U f32; GEMM f64; out f64",8,T88,D,F32,D,False),
+           ("F88 V f32,U f64; GEMM f64; out f64",8,T88,F32,D,D,False),
+           ("F88 all f64",8,T88,D,D,D,False),
+           ("F88 V,U,GEMM f64; M,out f32",8,T88,D,D,F32,False),
+           ("F44 all fp32 seq",4,T44,F32,F32,F32,True),
+           ("F44 V,U f32, GEMM f64, out f64",4,T44,F32,F32,D,False)]
+    for name,m,tabs,vp,gp,op,seq in cases:
+        p,v=fwd(sd,planes,m,tabs,vp,gp,op,seq)
+        print(f"{variant} {name:40s} dlogit {np.abs(p-p64).max():.3e} dvalue {np.abs(v-v64).max():.3e}",flush=True)
+
+
+if __name__ == "__main__":
+    main()
