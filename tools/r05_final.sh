@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 5, final code: the whole -m gpu suite, smoke(), the driver's bench command, the C2 line, and the driver
+# command's kernel trace (rocprofv3 --kernel-trace --stats)
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+O=$R/gpurun_out/${1:-r05_final2}
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_suite.log 2>&1
+echo suite-done
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+echo smoke-done
+timeout -k 10 500 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.log 2> $O/bench.err
+echo bench-done
