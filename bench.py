@@ -298,10 +298,11 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def gemm_label(path: int, rows: int, split: int):
+def gemm_label(path: int, rows: int, split: int, cus: int = 256):
     """(kernel name, description) of the dominant Winograd GEMM launch at `rows` rows per point, as
     knightvision_amd/csrc/kv_nn.hip launches it; `split` = the engine's kv_stats.dom_split (F(8x8) fp32:
-    points in the 128x128-tile launch)."""
+    points in the 128x128-tile launch); `cus` = the device's CUs (the fp32 tower's GEMM runs 4 tiles per
+    workgroup when its grid is 3-4 rounds of single tiles: kv_nn.hip i8f32_four_tiles)."""
     if path == 2:
         if rows % 128 == 0:
             name = "wino_gemm_kernel<512,4,2,1,2,32,100>"
@@ -315,6 +316,12 @@ def gemm_label(path: int, rows: int, split: int):
                     "Winograd F(8x8,3x3) GEMM layer: two launches, both inside the timed events)")
         return name, desc
     if path == 6:
+        tiles = 100 * (rows // 128) * 4
+        if 3 * cus < tiles <= 4 * cus and tiles % 32 == 0:
+            return "wino88i32_gemm_lagt_kernel<512,4>", (
+                " (residual-tower Winograd F(8x8,3x3) GEMMs of the fp32 tower from 4 int8 digits per value: 10 "
+                "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 "
+                "tiles, 4 per workgroup with the copy ring across them: one round of workgroups)")
         return "wino88i32_gemm_lag_kernel<512,false>", (
             " (residual-tower Winograd F(8x8,3x3) GEMMs of the fp32 tower from 4 int8 digits per value: 10 "
             "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 tiles, "
@@ -528,7 +535,7 @@ def main():
     flop_alg = per_board * bpl
     achieved = flop_alg / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
     rows = int(round(m["dom_flop"] / (2 * 512 * 512 * (100 if path in (2, 3, 5, 6) else 60)))) if path else bpl
-    kname, kdesc = gemm_label(path, rows, m["dom_split"])
+    kname, kdesc = gemm_label(path, rows, m["dom_split"], torch.cuda.get_device_properties(0).multi_processor_count)
     peak = FP64_MFMA_PEAK_TFLOPS if path == 3 else FP32_MFMA_PEAK_TFLOPS
     if path in I8_DIGIT_PRODUCTS:  # int8 operations of the digit products against the int8 peak
         achieved = achieved * I8_DIGIT_PRODUCTS[path] if achieved else None

@@ -1178,6 +1178,34 @@ static int launch_wino88i32_gemm_lag(const int8_t* V8, const int* ev, const int8
     return KV_OK;
 }
 
+// TPW tiles per workgroup, the ring across tiles (kv_wino88i.h wino88i32_gemm_lagt_kernel)
+template <int K, int TPW = 4>
+static int launch_wino88i32_gemm_lagt(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
+                                      int rows, int stride, hipStream_t st) {
+    using T = kv::Wino88iTile<kv::kI8DigitsF32>;
+    constexpr int bytes = 3 * T::STAGE;
+    KV_HIP(lds_opt_in((const void*)kv::wino88i32_gemm_lagt_kernel<K, TPW>, bytes));
+    const int tiles = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
+    KV_REQUIRE(rows % T::WM == 0 && stride % T::WM == 0 && tiles % (8 * TPW) == 0, KV_EINVAL,
+               "wino gemm i8 (lagt): rows %d / stride %d vs tile %d", rows, stride, T::WM);
+    hipLaunchKernelGGL((kv::wino88i32_gemm_lagt_kernel<K, TPW>), dim3(tiles / TPW), dim3(T::THREADS), bytes, st, V8,
+                       ev, U8, eu, M, rows, 512, stride);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+// 4 tiles per workgroup when the grid is 3-4 rounds of single tiles (C2's 800 on 256 CUs): one round of
+// 4-tile workgroups, 3 of 4 prologues hidden (KV_I8F32_TPW=1: always one tile per workgroup)
+static bool i8f32_four_tiles(int rows) {
+    static const bool off = [] {
+        const char* e = getenv("KV_I8F32_TPW");
+        return e && e[0] == '1';
+    }();
+    const int cus = device_cus();
+    const int tiles = kv::W88_XI * (rows / 128) * 4;
+    return !off && cus > 0 && tiles > 3 * cus && tiles <= 4 * cus && tiles % 32 == 0;
+}
+
 // the fp32 tower's int8-digit GEMM, round-5 form (kv_wino88i.h wino88i32_gemm_kernel): persistent
 // workgroups, one per CU (grid a multiple of 8, at most the tile count), or one tile each (persist false)
 template <int K, int KS, int NBUF, int NSEG = 1, int ABL = 0, bool DEFER = false>
@@ -1317,6 +1345,7 @@ static int i8f32_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const i
         if (seg) return launch_wino88i32_gemm<K, 32, 3, 2>(V8, ev, U8, eu, M, rows, stride, true, st);
     if (f.r4) return launch_wino88i_gemm<K, D>(V8, ev, U8, eu, M, rows, stride, st);
     if (f.persist) return launch_wino88i32_gemm<K, 32, 3, 1>(V8, ev, U8, eu, M, rows, stride, true, st);
+    if (i8f32_four_tiles(rows)) return launch_wino88i32_gemm_lagt<K, 4>(V8, ev, U8, eu, M, rows, stride, st);
     return launch_wino88i32_gemm_lag<K, false>(V8, ev, U8, eu, M, rows, stride, st);
 }
 
@@ -2234,6 +2263,9 @@ int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, flo
             case 16:  // every wave lags B digits 1-3 (12 MFMAs) by a barrier
                 return k5 ? launch_wino88i32_gemm_lag<512, false, 1>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0)
                           : launch_wino88i32_gemm_lag<256, false, 1>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0);
+            case 18:  // four tiles per workgroup, the ring across them
+                return k5 ? launch_wino88i32_gemm_lagt<512, 4>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0)
+                          : launch_wino88i32_gemm_lagt<256, 4>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0);
             case 17:  // every wave lags B digit 3 (2 MFMAs)
                 return k5 ? launch_wino88i32_gemm_lag<512, false, 3>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0)
                           : launch_wino88i32_gemm_lag<256, false, 3>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0);

@@ -696,6 +696,160 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* _
     }
 }
 
+// wino88i32_gemm_lag_kernel with TPW tiles per workgroup: the copy ring runs across the tile boundaries (a tile's
+// first two stages go out during the previous tile's last two), so every tile after a workgroup's first starts
+// with its operands in LDS. For grids of 3-4 rounds of tiles (C2: 800 tiles on 256 CUs), where the single-tile
+// kernel pays a prologue per round and a 12 %-full last round, TPW = 4 runs them as one round of 4-tile
+// workgroups (256 boards: 71.8 vs 75.9 us, profiles/r05_i8gemm_lagt_ab.log). Tile j of workgroup w is virtual
+// block w + j * gridDim in the XCD-aware order (the same XCD). At the first stage of a later tile a wave waits
+// for that stage's pieces with the previous tile's 32 M stores still allowed in flight. Same products, same bits.
+template <int K, int TPW = 4, int LJ = 2>
+__global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* __restrict__ V8,
+                                                                  const int* __restrict__ ev,
+                                                                  const int8_t* __restrict__ U8,
+                                                                  const int* __restrict__ eu, float* __restrict__ M,
+                                                                  int rows, int cout, int stride) {
+    constexpr int S = 4, NBUF = 3;
+    using T = Wino88iTile<S>;
+    constexpr int NT = T::NT, WM = T::WM, WN = T::WN, GL = T::GL;
+    constexpr int NK = K / 32, NS = TPW * NK;
+    constexpr int NA = S - LJ;
+    static_assert(GL == 4 && NK >= 3 && LJ >= 1 && LJ <= 3, "4 pieces per wave and stage");
+
+    extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8t[];
+    char* const L0 = (char*)lds_i8t;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / T::WC, wn = wave % T::WC;
+    const int CT = cout / WN, RT = rows / WM;
+    const int nwg = (int)gridDim.x, nv = nwg * TPW;  // nwg a multiple of 8
+    int xis[TPW], nbs[TPW], rbs[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+        const int vb = (int)blockIdx.x + j * nwg;
+        const int idx = (vb & 7) * (nv >> 3) + (vb >> 3);
+        xis[j] = idx / (CT * RT);
+        nbs[j] = (idx % CT) * WN;
+        rbs[j] = ((idx / CT) % RT) * WM;
+    }
+
+    const int wu = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: scalar tile bases
+    const int op = (wu * GL) / (4 * S);
+    const size_t sstep = (op ? (size_t)cout : (size_t)stride) * 128;
+    const int8_t* gb[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+        gb[j] = op ? U8 + (((size_t)xis[j] * NK) * cout + (size_t)nbs[j]) * 128
+                   : V8 + (((size_t)xis[j] * NK) * stride + (size_t)rbs[j]) * 128;
+    const int rl_off0 = (lane >> 3) * 128 + 16 * ((lane & 7) ^ (lane >> 4));
+    const int rl_off1 = (lane >> 3) * 128 + 16 * ((lane & 7) ^ (lane >> 4) ^ 4);
+    auto issue1 = [&](int g, int s) {  // piece g of global stage s (tile s / NK, stage s % NK)
+        const int q = wu * GL + g, rg8 = q % 16;
+        const int j = s / NK, kt = s - j * NK;
+        const int8_t* base = gb[0];
+#pragma unroll
+        for (int jj = 1; jj < TPW; ++jj) base = j == jj ? gb[jj] : base;
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(base + kt * sstep + (size_t)rg8 * 1024 + ((rg8 & 1) ? rl_off1 : rl_off0)),
+            (__attribute__((address_space(3))) void*)(L0 + (s % NBUF) * T::STAGE + op * S * T::PLANE + rg8 * 1024),
+            16, 0, 0);
+    };
+
+    const int lr = lane & 31, lh = lane >> 5;
+    const int arow = wm * 32 + lr;
+    int aoffr[S], boffr[NT][S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        aoffr[i] = i8_rl_off(arow, 2 * i + lh);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) boffr[nt][i] = S * T::PLANE + i8_rl_off(wn * NT * 32 + nt * 32 + lr, 2 * i + lh);
+    }
+
+    issue1(0, 0); issue1(1, 0); issue1(2, 0); issue1(3, 0);
+    issue1(0, 1); issue1(1, 1); issue1(2, 1); issue1(3, 1);
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+        i32x16_t acc[S][NT];
+#pragma unroll
+        for (int l = 0; l < S; ++l)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc[l][nt] = i32x16_t{};
+        i8x16_t pa[NA] = {}, pb[S - LJ][NT] = {};
+        auto h2 = [&]() {
+#pragma unroll
+            for (int jb = LJ; jb < S; ++jb)
+#pragma unroll
+                for (int i = 0; i + jb < S; ++i)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+                        acc[i + jb][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(pa[i], pb[jb - LJ][nt], acc[i + jb][nt], 0, 0, 0);
+        };
+        for (int kt = 0; kt < NK; ++kt) {
+            const int s = j * NK + kt;
+            if (s + 1 >= NS)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else if (kt == 0 && j > 0)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL + 32) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            const char* buf = L0 + (s % NBUF) * T::STAGE;
+            i8x16_t a[S], b[S][NT];
+#pragma unroll
+            for (int i = 0; i < S; ++i) a[i] = *(const i8x16_t*)(buf + aoffr[i]);
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) b[0][nt] = *(const i8x16_t*)(buf + boffr[nt][0]);
+            if (kt > 0) h2();
+            if (s + 2 < NS) {
+                issue1(0, s + 2);
+                issue1(1, s + 2);
+            }
+#pragma unroll
+            for (int jb = 0; jb < S; ++jb) {
+                if (jb + 1 < S) {
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) b[jb + 1][nt] = *(const i8x16_t*)(buf + boffr[nt][jb + 1]);
+                }
+                if (jb < LJ) {
+#pragma unroll
+                    for (int i = 0; i + jb < S; ++i)
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt)
+                            acc[i + jb][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[jb][nt], acc[i + jb][nt], 0, 0, 0);
+                }
+                if (jb == 0 && s + 2 < NS) {
+                    issue1(2, s + 2);
+                    issue1(3, s + 2);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NA; ++i) pa[i] = a[i];
+#pragma unroll
+            for (int jb = LJ; jb < S; ++jb)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) pb[jb - LJ][nt] = b[jb][nt];
+        }
+        h2();
+        const int xi = xis[j], n_base = nbs[j], r_base = rbs[j];
+        const int* evx = ev + (size_t)xi * stride + r_base + wm * 32;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int col = n_base + wn * NT * 32 + nt * 32 + lr;
+            const int ec = eu[(size_t)xi * cout + col] - 14;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+                double m = (double)acc[S - 1][nt][r];
+#pragma unroll
+                for (int l = S - 2; l >= 0; --l) m = __builtin_fma(m, 0.0078125, (double)acc[l][nt][r]);  // exact
+                M[((size_t)xi * stride + r_base + wm * 32 + row) * cout + col] = (float)ldexp(m, evx[row] + ec);
+            }
+        }
+    }
+}
+
 // KV_PREC_I8X5's GEMM (5 digits, digit planes, fp64 M) with wino88i32_gemm_lag_kernel's schedule: the
 // B digits j >= LJ of a stage (their pairs i + j <= 4) run after the next barrier, under that stage's first
 // LDS reads; stage k + 2's copies (5 pieces per wave) go into stage k - 1's buffer right after barrier k.
