@@ -317,11 +317,14 @@ def gemm_label(path: int, rows: int, split: int, cus: int = 256):
         return name, desc
     if path == 6:
         tiles = 100 * (rows // 128) * 4
-        if 3 * cus < tiles <= 4 * cus and tiles % 32 == 0:
-            return "wino88i32_gemm_lagt_kernel<512,4>", (
-                " (residual-tower Winograd F(8x8,3x3) GEMMs of the fp32 tower from 4 int8 digits per value: 10 "
-                "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 "
-                "tiles, 4 per workgroup with the copy ring across them: one round of workgroups)")
+        single = -(-tiles // cus)
+        for t in (5, 4):  # kv_nn.hip i8f32_tiles_per_wg
+            if tiles % (8 * t) == 0 and -(-(tiles // t) // cus) * t <= single:
+                return f"wino88i32_gemm_lagt_kernel<512,{t}>", (
+                    " (residual-tower Winograd F(8x8,3x3) GEMMs of the fp32 tower from 4 int8 digits per value: 10 "
+                    "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 "
+                    f"tiles, {t} per workgroup with the copy ring across them, each stage's last 6 MFMAs per wave "
+                    "under the next stage's first LDS reads)")
         return "wino88i32_gemm_lag_kernel<512,false>", (
             " (residual-tower Winograd F(8x8,3x3) GEMMs of the fp32 tower from 4 int8 digits per value: 10 "
             "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 tiles, "

@@ -1179,7 +1179,7 @@ static int launch_wino88i32_gemm_lag(const int8_t* V8, const int* ev, const int8
 }
 
 // TPW tiles per workgroup, the ring across tiles (kv_wino88i.h wino88i32_gemm_lagt_kernel)
-template <int K, int TPW = 4>
+template <int K, int TPW>
 static int launch_wino88i32_gemm_lagt(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
                                       int rows, int stride, hipStream_t st) {
     using T = kv::Wino88iTile<kv::kI8DigitsF32>;
@@ -1194,16 +1194,26 @@ static int launch_wino88i32_gemm_lagt(const int8_t* V8, const int* ev, const int
     return KV_OK;
 }
 
-// 4 tiles per workgroup when the grid is 3-4 rounds of single tiles (C2's 800 on 256 CUs): one round of
-// 4-tile workgroups, 3 of 4 prologues hidden (KV_I8F32_TPW=1: always one tile per workgroup)
-static bool i8f32_four_tiles(int rows) {
+// tiles per workgroup for the fp32 tower's GEMM: t in {5, 4} when ceil(tiles / (t CUs)) t -- the tile-times of
+// t-tile workgroups in whole rounds -- is no more than the single-tile grid's ceil(tiles / CUs) (then the same
+// or fewer tile-times, and t - 1 of t prologues hidden), else 1. C3's 6,400 tiles on 256 CUs: 5 rounds of
+// 5-tile workgroups (25 tile-times either way: 497 vs 511 us); C2's 800: one round of 4-tile workgroups (4
+// tile-times either way: 72 vs 76 us). KV_I8F32_TPW=1: always one tile per workgroup.
+static int i8f32_tiles_per_wg(int rows) {
     static const bool off = [] {
         const char* e = getenv("KV_I8F32_TPW");
         return e && e[0] == '1';
     }();
     const int cus = device_cus();
     const int tiles = kv::W88_XI * (rows / 128) * 4;
-    return !off && cus > 0 && tiles > 3 * cus && tiles <= 4 * cus && tiles % 32 == 0;
+    if (off || cus <= 0) return 1;
+    const int single = (tiles + cus - 1) / cus;
+    for (int t = 5; t >= 4; --t) {
+        if (tiles % (8 * t)) continue;
+        const int wgs = tiles / t;
+        if ((wgs + cus - 1) / cus * t <= single) return t;
+    }
+    return 1;
 }
 
 // the fp32 tower's int8-digit GEMM, round-5 form (kv_wino88i.h wino88i32_gemm_kernel): persistent
@@ -1345,7 +1355,9 @@ static int i8f32_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const i
         if (seg) return launch_wino88i32_gemm<K, 32, 3, 2>(V8, ev, U8, eu, M, rows, stride, true, st);
     if (f.r4) return launch_wino88i_gemm<K, D>(V8, ev, U8, eu, M, rows, stride, st);
     if (f.persist) return launch_wino88i32_gemm<K, 32, 3, 1>(V8, ev, U8, eu, M, rows, stride, true, st);
-    if (i8f32_four_tiles(rows)) return launch_wino88i32_gemm_lagt<K, 4>(V8, ev, U8, eu, M, rows, stride, st);
+    const int tpw = i8f32_tiles_per_wg(rows);
+    if (tpw == 5) return launch_wino88i32_gemm_lagt<K, 5>(V8, ev, U8, eu, M, rows, stride, st);
+    if (tpw == 4) return launch_wino88i32_gemm_lagt<K, 4>(V8, ev, U8, eu, M, rows, stride, st);
     return launch_wino88i32_gemm_lag<K, false>(V8, ev, U8, eu, M, rows, stride, st);
 }
 
@@ -2266,6 +2278,9 @@ int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, flo
             case 18:  // four tiles per workgroup, the ring across them
                 return k5 ? launch_wino88i32_gemm_lagt<512, 4>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0)
                           : launch_wino88i32_gemm_lagt<256, 4>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0);
+            case 19:  // five (2,048 rows: exactly 5 rounds)
+                return k5 ? launch_wino88i32_gemm_lagt<512, 5>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0)
+                          : launch_wino88i32_gemm_lagt<256, 5>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0);
             case 17:  // every wave lags B digit 3 (2 MFMAs)
                 return k5 ? launch_wino88i32_gemm_lag<512, false, 3>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0)
                           : launch_wino88i32_gemm_lag<256, false, 3>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, 0);

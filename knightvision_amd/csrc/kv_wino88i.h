@@ -698,12 +698,14 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* _
 
 // wino88i32_gemm_lag_kernel with TPW tiles per workgroup: the copy ring runs across the tile boundaries (a tile's
 // first two stages go out during the previous tile's last two), so every tile after a workgroup's first starts
-// with its operands in LDS. For grids of 3-4 rounds of tiles (C2: 800 tiles on 256 CUs), where the single-tile
-// kernel pays a prologue per round and a 12 %-full last round, TPW = 4 runs them as one round of 4-tile
-// workgroups (256 boards: 71.8 vs 75.9 us, profiles/r05_i8gemm_lagt_ab.log). Tile j of workgroup w is virtual
+// with its operands in LDS. kv_nn.hip picks TPW so the workgroups fill whole rounds in no more tile-times than
+// single tiles: C3's 6,400 tiles as 5 rounds of 5-tile workgroups (497 vs 511 us), C2's 800 as one round of
+// 4-tile workgroups (72 vs 76 us; profiles/r05_i8gemm_lagt_ab.log, r05_i8gemm_tpw5_ab.log). The tile loop is
+// unrolled (a runtime count recomputing tile coordinates per copy ran 13 % slower,
+// profiles/r05_i8gemm_tpw_runtime_ab.log). Tile j of workgroup w is virtual
 // block w + j * gridDim in the XCD-aware order (the same XCD). At the first stage of a later tile a wave waits
 // for that stage's pieces with the previous tile's 32 M stores still allowed in flight. Same products, same bits.
-template <int K, int TPW = 4, int LJ = 2>
+template <int K, int TPW, int LJ = 2>
 __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* __restrict__ V8,
                                                                   const int* __restrict__ ev,
                                                                   const int8_t* __restrict__ U8,

@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from knightvision_amd import _lib  # noqa: E402
 
 VARIANTS = [int(v) for v in os.environ.get("I8_VARIANTS", "0,14,16,17").split(",")]
-SAME_M = {1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 16, 17, 18}  # 6: segment exponents (another M); 7-9: timing ablations (no stores / no copies)
+SAME_M = {1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19}  # 6: segment exponents (another M); 7-9: timing ablations (no stores / no copies)
 L = _lib.lib()
 rows_list = [int(a) for a in sys.argv[1:]] or [2048, 256]
 for K in (512,):
