@@ -1078,7 +1078,8 @@ __global__ __launch_bounds__(256) void wino88i_in_kernel(const float* __restrict
     const unsigned dstride = (unsigned)rows * 32, xstride = (C / 32) * kI8Digits * dstride;
     // (one byte store per digit: a lane-quad transpose into dword stores measured 3 % slower here,
     // profiles/r05_i8x5_ab.log -- the kernel is bound by its fp64 transform and digit arithmetic; the digits
-    // by magic-number adds: profiles/r05_i8x5_magic_ab.log)
+    // by magic-number adds: profiles/r05_i8x5_magic_ab.log; non-temporal byte stores -- 32-byte pieces of
+    // lines -- made the forward 28 % slower: profiles/r05_i8x5_nt_ab.log)
 #pragma unroll
     for (int aa = 0; aa < 5; ++aa) {
         double o[10];
@@ -1459,7 +1460,10 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
         for (int bb = 0; bb < 10; ++bb) {
             const int xi = a * 10 + bb;
             const unsigned P = i8_digits4_packed(vk[aa][bb], exs[xi]);
-            dst[(off0 + (unsigned)xi * xstride) >> 2] = i8_quad_transpose(P, lane);
+            // non-temporal: the digits are read once, by the next GEMM (forward -1.2 % at 2,048 boards against
+            // plain stores, bit-identical; the GEMM's M stored non-temporal instead slowed the output kernel that
+            // reads it: profiles/r05_out_nt_ab.log)
+            __builtin_nontemporal_store(i8_quad_transpose(P, lane), &dst[(off0 + (unsigned)xi * xstride) >> 2]);
         }
     }
 }
