@@ -49,13 +49,13 @@ FP32_MFMA_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md, f32-input MFMA (den
 FP64_MFMA_PEAK_TFLOPS = 78.6          # AMD's MI355X FP64 matrix spec figure (the guides give no f64 row; not
                                       # measured here)
 PATH_NAMES = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3",
-              5: "winograd88_i8", 6: "winograd88_i8f32"}  # KV_PATH_*
+              5: "winograd88_i8", 6: "winograd88_i8f32", 7: "winograd88_i8f32v"}  # KV_PATH_*
 BF16_MFMA_PEAK_TFLOPS = 2500.0        # dense bf16 MFMA
 I8_MFMA_PEAK_TOPS = 5000.0            # dense int8 MFMA: 2x the bf16 rate (cdna_hip_programming.md, MFMA rate per dtype);
                                       # v_mfma_i32_32x32x32_i8 back to back measured 4.1 POPS at the clock the chip
                                       # holds under it (profiles/r04_mfma_rate.log)
 I8_MFMA_MEASURED_TOPS = 4098.0
-I8_DIGIT_PRODUCTS = {5: 15, 6: 10}    # int8 GEMMs per Winograd GEMM: digit pairs i + j < 5 (KV_PREC_I8X5, fp64
+I8_DIGIT_PRODUCTS = {5: 15, 6: 10, 7: 10}    # int8 GEMMs per Winograd GEMM: digit pairs i + j < 5 (KV_PREC_I8X5, fp64
                                       # domain) / < 4 (KV_ALGO_WINOGRAD88_I8, fp32 domain)
 
 
@@ -315,7 +315,7 @@ def gemm_label(path: int, rows: int, split: int, cus: int = 256):
             desc = (f" points 0-{split - 1} + wino_gemm_kernel<512,2,2,1,2,16,100> points {split}-99 (residual-tower "
                     "Winograd F(8x8,3x3) GEMM layer: two launches, both inside the timed events)")
         return name, desc
-    if path == 6:
+    if path in (6, 7):  # 7: the same GEMM (fp64 input transforms)
         tiles = 100 * (rows // 128) * 4
         single = -(-tiles // cus)
         for t in (5, 4):  # kv_nn.hip i8f32_tiles_per_wg
@@ -621,7 +621,10 @@ def main():
                          "kernel": kname + kdesc + (
                              "; GEMM only: the operands' int8 digits come from the previous output kernel "
                              "(wino88i32_out_kernel, which writes them instead of fp32 V; conv2's from a slice "
-                             "kernel)" if path == 6 else ""),
+                             "kernel)" if path == 6 else
+                             "; GEMM only: the operands' int8 digits come from the previous output kernel "
+                             "(wino88i32v_out_kernel: the fp64 input transform of the fp32 activation, cut to 4 digits; "
+                             "conv2's from a slice kernel)" if path == 7 else ""),
                          "measured_peak_note": (f"v_mfma_i32_32x32x32_i8 back to back: {I8_MFMA_MEASURED_TOPS:.0f} "
                                                 "TOPS at the clock held (profiles/r04_mfma_rate.log)"
                                                 if path in I8_DIGIT_PRODUCTS else None),

@@ -100,7 +100,9 @@ int kv_net_set_precision(kv_net* net, int precision);
  *                   boards (the initial position, 16 positions of reference
  *                   self-play, 47 seeded random ones): > 16 boards F(8x8) fp32
  *                   with int8-digit GEMMs (KV_ALGO_WINOGRAD88_I8), else the
- *                   fp64 Winograd domain on int8 digits (KV_PREC_I8X5), else
+ *                   same with fp64 input transforms (KV_ALGO_WINOGRAD88_I8V),
+ *                   else the fp64 Winograd domain on int8 digits
+ *                   (KV_PREC_I8X5), else
  *                   on fp64 MFMA; <= 16 boards direct (split-K), else F(8x8)
  *                   fp64 (kv_net_calibration reports it)
  * KV_ALGO_DIRECT    implicit GEMM over the 9 taps (exact fp32 products)
@@ -113,6 +115,9 @@ int kv_net_set_precision(kv_net* net, int precision);
  *                   block fixed point, the 10 digit pairs i + j <= 3, exact
  *                   int32 levels, one rounding to fp32, on
  *                   v_mfma_i32_32x32x32_i8
+ * KV_ALGO_WINOGRAD88_I8V the same tower with each conv's V the fp64 input
+ *                   transform of its fp32 input, cut to 4 digits from fp64
+ *                   (M, the output transform and the activations stay fp32)
  * Value 2 (F(4x4)) was retired in round 4: KV_EINVAL. Setting the precision or
  * the algorithm of a loaded net re-prepares it (synchronous).
  * Results are batch-invariant inside a class (<= 16 boards, > 16 boards). */
@@ -121,6 +126,7 @@ int kv_net_set_precision(kv_net* net, int precision);
 #define KV_ALGO_WINOGRAD48 3
 #define KV_ALGO_WINOGRAD88 4
 #define KV_ALGO_WINOGRAD88_I8 5
+#define KV_ALGO_WINOGRAD88_I8V 6
 int kv_net_set_algo(kv_net* net, int algo);
 /* conv paths (what a forward runs) */
 #define KV_PATH_DIRECT 0
@@ -130,7 +136,8 @@ int kv_net_set_algo(kv_net* net, int algo);
 #define KV_PATH_WINO48_F16X3 4
 #define KV_PATH_WINO88_I8 5
 #define KV_PATH_WINO88_I8F32 6
-#define KV_NPATH 7
+#define KV_PATH_WINO88_I8F32V 7
+#define KV_NPATH 8
 typedef struct {
     int calibrated;      /* 1: the last load / setting ran the fp32 AUTO calibration */
     int path_large;      /* KV_PATH_* of batches > 16 boards (also without calibration) */
@@ -314,7 +321,9 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
  * [rows][64][512] (= ReLU(A^T M A * scale + shift (+ resid))) and the next conv's V as row-line digits
  * [100][16][rows][4][32] with row exponents [100][rows]. fused bit 0 set: the product's one-kernel form
  * (wino88i32_out_kernel), clear: wino88_out_kernel's fp32 V then the slice kernel (bit-identical); bit 1:
- * exponents per 256-channel segment ([100][2][rows]) instead of per row. */
+ * exponents per 256-channel segment ([100][2][rows]) instead of per row; bit 2 (KV_ALGO_WINOGRAD88_I8V's V,
+ * per row): with bit 0 the one-kernel wino88i32v_out_kernel, without it wino88_out_kernel's Y, then
+ * wino88d_in_kernel's fp64 V and the slice kernel (bit-identical). */
 int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scale, const float* shift,
                          const float* resid, int fused, float* Y, int8_t* v_digits, int* v_exp);
 /* Timing / A-B harness of the fp32 tower's int8-digit GEMM on seeded random digits (rows boards, K 256 or

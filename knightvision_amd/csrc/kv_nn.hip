@@ -611,6 +611,7 @@ __global__ void planes_to_nhwc16_kernel(const float* __restrict__ planes, int nb
 //   KV_PATH_WINO48_F16X3 F(4x8) with the f16x3 split GEMM
 //   KV_PATH_WINO88_I8  F(8x8), fp64 Winograd domain, GEMMs on int8 digits (kv_wino88i.h)
 //   KV_PATH_WINO88_I8F32 F(8x8), fp32 Winograd domain, GEMMs on int8 digits (kv_wino88i.h)
+//   KV_PATH_WINO88_I8F32V the same with fp64 input transforms (V cut to digits from fp64)
 // fp32 + KV_ALGO_AUTO picks its paths per weight load (kv_net_calibration).
 constexpr int kNPath = KV_NPATH;
 
@@ -640,7 +641,7 @@ struct kv_net {
     double* U88d = nullptr; // F(8x8), fp64 [100][Cout][Cin] (KV_PATH_WINO88_F64)
     int8_t* U88i = nullptr; // F(8x8) int8 digit planes [100][Cin/32][5][Cout][32] (KV_PATH_WINO88_I8)
     int* eu88i = nullptr;   // their row exponents [100][Cout]
-    int8_t* U88i32 = nullptr;  // the same with 4 digits (KV_PATH_WINO88_I8F32)
+    int8_t* U88i32 = nullptr;  // the same with 4 digits (KV_PATH_WINO88_I8F32 and _I8F32V)
     int* eu88i32 = nullptr;
     size_t euoff[12] = {};
     bool built[kNPath] = {};
@@ -688,6 +689,7 @@ static int path_for(const kv_net* net, int B) {
     if (net->precision == KV_PREC_F64W) return KV_PATH_WINO88_F64;
     if (net->precision == KV_PREC_I8X5) return KV_PATH_WINO88_I8;
     if (net->precision == KV_PREC_FP32 && net->algo == KV_ALGO_WINOGRAD88_I8) return KV_PATH_WINO88_I8F32;
+    if (net->precision == KV_PREC_FP32 && net->algo == KV_ALGO_WINOGRAD88_I8V) return KV_PATH_WINO88_I8F32V;
     if (net->precision == KV_PREC_F16X3) {
         if (net->algo == KV_ALGO_DIRECT || (net->algo == KV_ALGO_AUTO && small)) return KV_PATH_DIRECT;
         return KV_PATH_WINO48_F16X3;
@@ -775,7 +777,8 @@ static int net_pad(const kv_net* net, int B) {
         }
         case KV_PATH_DIRECT: return (B + 3) & ~3;
         case KV_PATH_WINO88_I8:
-        case KV_PATH_WINO88_I8F32: return (B + 127) & ~127;  // the int8 GEMM's 128-row tiles
+        case KV_PATH_WINO88_I8F32:
+        case KV_PATH_WINO88_I8F32V: return (B + 127) & ~127;  // the int8 GEMM's 128-row tiles
         default: return (B + 31) & ~31;
     }
 }
@@ -1345,6 +1348,17 @@ static int launch_wino88i32_out(kv_net* net, int l, const float* M, int nb, int 
     return KV_OK;
 }
 
+// KV_PATH_WINO88_I8F32V's output kernel (per-row exponents, the next V from the fp64 input transform)
+template <bool RESID, bool WRITE_Y>
+static int launch_wino88i32v_out(kv_net* net, int l, const float* M, int nb, int stride, const float* resid,
+                                 float* Y, int8_t* V8, int* ev, hipStream_t st) {
+    const float* W = net->w;
+    hipLaunchKernelGGL((kv::wino88i32v_out_kernel<RESID, WRITE_Y>), dim3(1, nb), dim3(1024), 0, st, M, stride,
+                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, V8, ev);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
 // the fp32 tower's int8-digit GEMM of one conv (K 256: one segment, per-row exponents)
 template <int K>
 static int i8f32_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M, int rows, int stride,
@@ -1361,16 +1375,21 @@ static int i8f32_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const i
     return launch_wino88i32_gemm_lag<K, false>(V8, ev, U8, eu, M, rows, stride, st);
 }
 
-// conv l's GEMM; slice: V (fp32) -> digits first. (mark: the engine's timing hook brackets the slice, when
-// there is one, and the GEMM)
-static int wino88i32_gemm_layer(kv_net* net, int l, int K, int rows, int stride, bool slice, bool mark,
+// conv l's GEMM; slice: V (fp32; v64: conv2's fp64 V256) -> digits first. (mark: the engine's timing hook
+// brackets the slice, when there is one, and the GEMM)
+static int wino88i32_gemm_layer(kv_net* net, int l, int K, int rows, int stride, bool slice, bool mark, bool v64,
                                 hipStream_t st) {
     constexpr int D = kv::kI8DigitsF32;
-    const bool seg = K == 512 && i8f32_form().seg;
+    const bool seg = K == 512 && i8f32_form().seg && !v64;
     float* M = (float*)net->Mw;
     int rc;
     if (mark && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-    if (slice) {
+    if (slice && v64) {
+        KV_REQUIRE(K == 256, KV_EINVAL, "wino88i32v: the output kernels write the digits of K 512");
+        if ((rc = launch_wino88i_slice<256, D>((const double*)net->V256, rows, stride, kv::W88_XI, net->V8, net->ev8,
+                                               st)))
+            return rc;
+    } else if (slice) {
         const float* Vsrc = K == 256 ? (const float*)net->V256 : (const float*)net->V;
         rc = K == 256 ? launch_wino88i_slice<256, D>(Vsrc, rows, stride, kv::W88_XI, net->V8, net->ev8, st)
              : seg    ? launch_wino88i_slice<512, D, float, 2>(Vsrc, rows, stride, kv::W88_XI, net->V8, net->ev8, st)
@@ -1386,32 +1405,37 @@ static int wino88i32_gemm_layer(kv_net* net, int l, int K, int rows, int stride,
     return KV_OK;
 }
 
-static int wino88i32_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
+// v64 (KV_PATH_WINO88_I8F32V): conv2's V256 is fp64 (the stem's / wino88d_in_kernel's) and every output
+// kernel is wino88i32v_out_kernel (the slice and segment forms do not apply)
+static int wino88i32_blocks(kv_net* net, int nb, bool mark, bool v64, hipStream_t st) {
     const int rows = nb, stride = rows;
     float* V = (float*)net->V;
     const float* M = (const float*)net->Mw;
-    const bool sf = i8f32_form().slice, seg = i8f32_form().seg;
+    const bool sf = i8f32_form().slice && !v64, seg = i8f32_form().seg && !v64;
+    int8_t* V8 = net->V8;
+    int* ev = net->ev8;
     int rc;
-    if ((rc = wino88i32_gemm_layer(net, 1, 256, rows, stride, true, false, st))) return rc;
-    rc = sf ? launch_wino88_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st)
-            : launch_wino88i32_out<false, true>(net, 1, M, nb, stride, nullptr, net->X, net->V8, net->ev8, seg, st);
+    if ((rc = wino88i32_gemm_layer(net, 1, 256, rows, stride, true, false, v64, st))) return rc;
+    rc = v64  ? launch_wino88i32v_out<false, true>(net, 1, M, nb, stride, nullptr, net->X, V8, ev, st)
+         : sf ? launch_wino88_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st)
+              : launch_wino88i32_out<false, true>(net, 1, M, nb, stride, nullptr, net->X, V8, ev, seg, st);
     if (rc) return rc;
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
     for (int r = 0; r < 5; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         const bool m = mark && r == 2;
-        if ((rc = wino88i32_gemm_layer(net, l1, 512, rows, stride, sf, m, st))) return rc;
-        rc = sf ? launch_wino88_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st)
-                : launch_wino88i32_out<false, false>(net, l1, M, nb, stride, nullptr, nullptr, net->V8, net->ev8, seg,
-                                                     st);
+        if ((rc = wino88i32_gemm_layer(net, l1, 512, rows, stride, sf, m, v64, st))) return rc;
+        rc = v64  ? launch_wino88i32v_out<false, false>(net, l1, M, nb, stride, nullptr, nullptr, V8, ev, st)
+             : sf ? launch_wino88_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st)
+                  : launch_wino88i32_out<false, false>(net, l1, M, nb, stride, nullptr, nullptr, V8, ev, seg, st);
         if (rc) return rc;
-        if ((rc = wino88i32_gemm_layer(net, l2, 512, rows, stride, sf, false, st))) return rc;
+        if ((rc = wino88i32_gemm_layer(net, l2, 512, rows, stride, sf, false, v64, st))) return rc;
         if (r == 4)
             rc = launch_wino88_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
         else
-            rc = sf ? launch_wino88_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
-                    : launch_wino88i32_out<true, true>(net, l2, M, nb, stride, net->X, net->X, net->V8, net->ev8, seg,
-                                                       st);
+            rc = v64  ? launch_wino88i32v_out<true, true>(net, l2, M, nb, stride, net->X, net->X, V8, ev, st)
+                 : sf ? launch_wino88_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
+                      : launch_wino88i32_out<true, true>(net, l2, M, nb, stride, net->X, net->X, V8, ev, seg, st);
         if (rc) return rc;
     }
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
@@ -1436,6 +1460,7 @@ static WsNeed ws_need(int path) {
         case KV_PATH_WINO88_I8F32:
             return {{i8f32_form().slice ? P88 * 512 * f : 0, P88 * 512 * f, P88 * 256 * f,
                      P88 * 512 * kv::kI8DigitsF32}};
+        case KV_PATH_WINO88_I8F32V: return {{0, P88 * 512 * f, P88 * 256 * d, P88 * 512 * kv::kI8DigitsF32}};
         default: return {{0, 0, 0, 0}};  // direct: the split-K slab only
     }
 }
@@ -1464,8 +1489,8 @@ static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hi
     net->dom_path = path;
     net->dom_launches = 1;
     if (path == KV_PATH_WINO88 || path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8 ||
-        path == KV_PATH_WINO88_I8F32) {
-        const bool f64 = path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8;
+        path == KV_PATH_WINO88_I8F32 || path == KV_PATH_WINO88_I8F32V) {
+        const bool f64 = path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8 || path == KV_PATH_WINO88_I8F32V;
         if (!v256_ready) {
             if (f64)
                 hipLaunchKernelGGL(kv::wino88d_in_kernel<256>, dim3(1, nb_pad), dim3(256), 0, st, net->T, nb_pad,
@@ -1475,7 +1500,8 @@ static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hi
                                    (float*)net->V256);
             KV_HIP(hipGetLastError());
         }
-        if ((rc = path == KV_PATH_WINO88_I8F32 ? wino88i32_blocks(net, nb_pad, true, st)
+        if ((rc = path == KV_PATH_WINO88_I8F32    ? wino88i32_blocks(net, nb_pad, true, false, st)
+                  : path == KV_PATH_WINO88_I8F32V ? wino88i32_blocks(net, nb_pad, true, true, st)
                   : path == KV_PATH_WINO88_I8  ? wino88i_blocks(net, nb_pad, true, st)
                   : path == KV_PATH_WINO88_F64 ? wino88d_blocks(net, nb_pad, true, st)
                                                : wino88_blocks(net, nb_pad, true, st)))
@@ -1520,7 +1546,7 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
         if (path == KV_PATH_WINO88 || path == KV_PATH_WINO88_I8F32)
             hipLaunchKernelGGL(kv::stem_kernel<4>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], (float*)net->V256, nb_pad, nullptr);
-        else if (path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8)
+        else if (path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8 || path == KV_PATH_WINO88_I8F32V)
             hipLaunchKernelGGL(kv::stem_kernel<5>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], (float*)net->V256, nb_pad, nullptr);
         else if (path == KV_PATH_WINO48 || path == KV_PATH_WINO48_F16X3)
@@ -1624,6 +1650,11 @@ static size_t wino_offsets(size_t* uoff, int nxi) {
 // (once per load; a path not used is never allocated)
 static int ensure_path(kv_net* net, int path) {
     if (net->built[path]) return KV_OK;
+    if (path == KV_PATH_WINO88_I8F32V) {  // the fp32 tower's 4-digit U
+        const int rc = ensure_path(net, KV_PATH_WINO88_I8F32);
+        if (rc == KV_OK) net->built[path] = true;
+        return rc;
+    }
     const auto each_conv = [&](auto&& launch) {
         for (int l = 1; l < 12; ++l) {
             const size_t n = (size_t)kv::kConv[l].cout * kv::kConv[l].cin;
@@ -1754,7 +1785,8 @@ static void release_unused(kv_net* net) {
         net->eu88i = nullptr;
         net->built[KV_PATH_WINO88_I8] = false;
     }
-    if (!keep[KV_PATH_WINO88_I8F32]) {
+    if (!keep[KV_PATH_WINO88_I8F32V]) net->built[KV_PATH_WINO88_I8F32V] = false;
+    if (!keep[KV_PATH_WINO88_I8F32] && !keep[KV_PATH_WINO88_I8F32V]) {
         (void)hipFree(net->U88i32);
         (void)hipFree(net->eu88i32);
         net->U88i32 = nullptr;
@@ -1903,9 +1935,9 @@ static int net_calibrate(kv_net* net) {
     // > 16 boards
     // (F(8x8) and F(4x8) on fp32 MFMA are never within the budget when the int8-digit fp32 tower is not:
     // on every weight set measured they are further from fp64 -- DESIGN.md; they stay explicit algos)
-    const int cands[3] = {KV_PATH_WINO88_I8F32, KV_PATH_WINO88_I8, KV_PATH_WINO88_F64};
+    const int cands[4] = {KV_PATH_WINO88_I8F32, KV_PATH_WINO88_I8F32V, KV_PATH_WINO88_I8, KV_PATH_WINO88_F64};
     net->auto_small = KV_PATH_DIRECT;
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < 4; ++i) {
         const int p = cands[i];
         if ((rc = ensure_path(net, p))) return fail(rc);
         net->auto_large = p;
@@ -1999,7 +2031,7 @@ int kv_net_set_algo(kv_net* net, int algo) {
     KV_REQUIRE(algo != 2, KV_EINVAL, "kv_net_set_algo: KV_ALGO 2 (Winograd F(4x4)) was retired; use "
                                      "KV_ALGO_WINOGRAD48 or KV_ALGO_WINOGRAD88");
     KV_REQUIRE(algo == KV_ALGO_AUTO || algo == KV_ALGO_DIRECT || algo == KV_ALGO_WINOGRAD48 ||
-                   algo == KV_ALGO_WINOGRAD88 || algo == KV_ALGO_WINOGRAD88_I8,
+                   algo == KV_ALGO_WINOGRAD88 || algo == KV_ALGO_WINOGRAD88_I8 || algo == KV_ALGO_WINOGRAD88_I8V,
                KV_EINVAL, "kv_net_set_algo: unknown algo %d", algo);
     if (net->algo == algo && (!net->loaded || net->built[path_for(net, 1024)])) return KV_OK;
     const int prev = net->algo;
@@ -2157,7 +2189,8 @@ int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scal
     KV_HIP(dy.alloc(ny));
     KV_HIP(dv.alloc(nm));
     KV_HIP(v8.alloc(nm * kv::kI8DigitsF32));
-    const bool seg = (fused & 2) != 0;
+    const bool seg = (fused & 2) != 0, v64 = (fused & 4) != 0;
+    KV_REQUIRE(!(seg && v64), KV_EINVAL, "kv_dev_wino88i32_out: fp64 V (bit 2) has per-row exponents only");
     KV_HIP(ev.alloc((size_t)kv::W88_XI * rows * 2));
     KV_HIP(hipMemcpy(dm.p, M, nm * sizeof(float), hipMemcpyHostToDevice));
     KV_HIP(hipMemcpy(dsc.p, scale, 512 * sizeof(float), hipMemcpyHostToDevice));
@@ -2169,7 +2202,29 @@ int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scal
     const float* sc = dsc.p;
     const float* sh = dsh.p;
     // Y doubles as the residual (in place, as the tower runs it)
-    if (fused & 1) {
+    if (v64 && (fused & 1)) {
+        if (resid)
+            hipLaunchKernelGGL((kv::wino88i32v_out_kernel<true, true>), dim3(1, rows), dim3(1024), 0, 0, dm.p, rows, sc,
+                               sh, dy.p, dy.p, v8.p, ev.p);
+        else
+            hipLaunchKernelGGL((kv::wino88i32v_out_kernel<false, true>), dim3(1, rows), dim3(1024), 0, 0, dm.p, rows,
+                               sc, sh, nullptr, dy.p, v8.p, ev.p);
+        KV_HIP(hipGetLastError());
+    } else if (v64) {  // Y, then fp64 V from Y, then its digits
+        if (resid)
+            hipLaunchKernelGGL((kv::wino88_out_kernel<true, true, false>), dim3(512 / 256, rows), dim3(256), 0, 0,
+                               dm.p, rows, sc, sh, dy.p, dy.p, nullptr);
+        else
+            hipLaunchKernelGGL((kv::wino88_out_kernel<false, true, false>), dim3(512 / 256, rows), dim3(256), 0, 0,
+                               dm.p, rows, sc, sh, nullptr, dy.p, nullptr);
+        kv::DevBuf<double> dv64;
+        KV_HIP(dv64.alloc(nm));
+        hipLaunchKernelGGL(kv::wino88d_in_kernel<512>, dim3(512 / 256, rows), dim3(256), 0, 0, dy.p, rows, dv64.p);
+        KV_HIP(hipGetLastError());
+        const int rc = launch_wino88i_slice<512, kv::kI8DigitsF32>(dv64.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
+        if (rc) return rc;
+        KV_HIP(hipDeviceSynchronize());
+    } else if (fused & 1) {
         if (resid) {
             if (seg)
                 hipLaunchKernelGGL((kv::wino88i32_out_kernel<true, true, 256>), dim3(2, rows), dim3(512), 0, 0, dm.p,

@@ -1468,4 +1468,115 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
     }
 }
 
+// ---- the fp32 tower with fp64 input transforms (KV_PATH_WINO88_I8F32V) ----
+// The same tower as KV_PATH_WINO88_I8F32 (fp32 M, output transform and activations, the 4-digit GEMM)
+// except that every conv's V is the fp64 input transform of its fp32 input, cut to 4 digits from fp64:
+// on learn-loop weights the fp32 input transform is what sets the fp32 tower's value error
+// (profiles/r05_learn_stage_emulate.log).
+
+// fp64 transform row 5h + aa of a plane split over lanes l, l ^ 32, from the half's 4 columns after the
+// half exchange (xc[kk][i] = pixel (i, 4h + kk)): the fma chains of wino88d_input_cols + wino88d_input_row
+// on the same inputs -- so the same bits as wino88d_input_plane -- one transform row at a time (each
+// column's w88d_bt is taken for rows aa and 5 + aa only), so no 10x4 fp64 intermediate is live.
+__device__ inline void wino88d_input_row_of_cols(float (&xc)[4][8], int aa, double (&o)[10]) {
+    // opaque to the compiler per row: otherwise it keeps the 32 widened values (64 VGPRs) live across the
+    // rows and both passes instead of widening them again, and spills
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(xc[kk][i]));
+    double row[10];
+    row[0] = 0.0;
+    row[9] = 0.0;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+        double col[10], t[10];
+        col[0] = 0.0;
+        col[9] = 0.0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) col[1 + i] = (double)xc[kk][i];
+        w88d_bt(col, t);
+        double lo = t[aa], hi = t[5 + aa];
+        half_swap(lo, hi);
+        row[1 + kk] = lo;
+        row[5 + kk] = hi;
+    }
+    w88d_bt(row, o);
+}
+
+// wino88i32v_out_kernel: wino88i32_out_kernel<RESID, WRITE_Y, 512> with the next conv's V taken as the fp64
+// input transform of the fp32 activation (what wino88d_in_kernel + wino88i_slice_kernel<512, double, 4,
+// true> give, bit for bit). 50 fp64 V values per lane do not fit beside the rest at 1,024 threads, so the
+// lane keeps its 32 fp32 activations across the exponent barrier instead and transforms them twice: once
+// for the row maxima (the high words of |V|), once for the digits (magic-number fp64 rint).
+template <bool RESID, bool WRITE_Y>
+__global__ __launch_bounds__(1024) void wino88i32v_out_kernel(const float* __restrict__ M, int rows,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift, const float* resid,
+                                                              float* Y, int8_t* __restrict__ V8, int* __restrict__ ex) {
+    constexpr int NK = 512 / 32, NW = 16;
+    __shared__ __attribute__((aligned(16))) unsigned red[NW][2][5][16];
+    __shared__ int exs[100];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+    const int c = w * 32 + (lane & 31), b = blockIdx.y;
+    float xc[4][8];  // the half's columns 4h .. 4h+3, all 8 rows (after the half exchange)
+    {
+        float x2[4][8];
+        wino88_out_plane_half<RESID, WRITE_Y>(M, rows, b, c, h, scale[c], shift[c], resid, Y, x2);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+            for (int ii = 0; ii < 4; ++ii) {
+                float lo = x2[ii][kk], hi = x2[ii][4 + kk];
+                half_swap(lo, hi);
+                xc[kk][ii] = lo;
+                xc[kk][4 + ii] = hi;
+            }
+    }
+#pragma unroll
+    for (int aa = 0; aa < 5; ++aa) {
+        double o[10];
+        wino88d_input_row_of_cols(xc, aa, o);
+        unsigned m[10];
+#pragma unroll
+        for (int bb = 0; bb < 10; ++bb)
+            m[bb] = i8_half_max_dpp((unsigned)(__double_as_longlong(o[bb]) >> 32) & 0x7fffffffu);
+        if ((lane & 31) == 16) {
+            uint4* rr = (uint4*)&red[w][h][aa][0];
+            rr[0] = make_uint4(m[0], m[1], m[2], m[3]);
+            rr[1] = make_uint4(m[4], m[5], m[6], m[7]);
+            *(uint2*)&red[w][h][aa][8] = make_uint2(m[8], m[9]);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 100) {
+        const int xi = threadIdx.x, a = xi / 10, bb = xi % 10, hh = a / 5, aa = a % 5;
+        unsigned m = 0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) m = red[ww][hh][aa][bb] > m ? red[ww][hh][aa][bb] : m;
+        const int e = i8_row_exponent(m);
+        exs[xi] = e;
+        ex[(size_t)xi * rows + b] = e;
+    }
+    __syncthreads();
+    const int q = lane & 3;
+    const unsigned off0 = ((unsigned)(c >> 5) * rows + b) * 128 + q * 32 + (c & 28), xstride = NK * rows * 128;
+    unsigned* const dst = (unsigned*)V8;
+#pragma unroll
+    for (int aa = 0; aa < 5; ++aa) {
+        double o[10];
+        wino88d_input_row_of_cols(xc, aa, o);
+        const int a = 5 * h + aa;
+#pragma unroll
+        for (int bb = 0; bb < 10; ++bb) {
+            const int xi = a * 10 + bb;
+            unsigned dq[4];
+            i8_digits_magic<4>(o[bb], exs[xi], dq);
+            const unsigned P = __builtin_amdgcn_perm(dq[1], dq[0], 0x0c0c0400u) |
+                               __builtin_amdgcn_perm(dq[3], dq[2], 0x0c0c0400u) << 16;
+            __builtin_nontemporal_store(i8_quad_transpose(P, lane), &dst[(off0 + (unsigned)xi * xstride) >> 2]);
+        }
+    }
+}
+
 }  // namespace kv

@@ -235,6 +235,9 @@ def reinforcement_loop(model, iterations: int, games_per_iter: int, device, *, e
         cal = getattr(selfplay_shard, "last_calibration", None)
         if cal is not None:  # fp32 AUTO: the self-play network's conv path for this iteration's weights
             st["nn_path"] = cal["path_large"]
+            if cal.get("calibrated"):  # the load-time calibration (inside selfplay_s) and its candidates' errors
+                st["calib_ms"] = cal["ms"]
+                st["calib_err"] = {k: (cal["err_logit"][k], cal["err_value"][k]) for k in cal["err_logit"]}
         es = getattr(selfplay_shard, "last_stats", None)
         if es is not None:  # this rank's engine: plies and MCTS simulations (the throughput a path flip moves)
             st.update(plies=int(es["plies"]), sims=int(es["sims"]))

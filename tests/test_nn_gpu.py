@@ -16,12 +16,13 @@ TOL_P, TOL_V = 1e-4, 1e-5
 # (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x8,3x3) / fp32 Winograd F(8x8,3x3) / fp32 auto
 # (the calibrated choice every product caller runs) / f16x3 Winograd F(4x8) / F(8x8) with the fp64 Winograd domain
 # on fp64 MFMA / the same domain with the GEMMs on int8 digits; ("fp32", "winograd88i8") the fp32 F(8x8) tower with
-# its GEMMs on int8 digits
+# its GEMMs on int8 digits, ("fp32", "winograd88i8v") the same with fp64 input transforms
 MODES = [("fp32", "direct"), ("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "winograd88i8"),
-         ("fp32", "auto"), ("f16x3", "winograd48"), ("f64w", "auto"), ("i8x5", "auto")]
+         ("fp32", "winograd88i8v"), ("fp32", "auto"), ("f16x3", "winograd48"), ("f64w", "auto"), ("i8x5", "auto")]
 # the explicit fp32 / f16x3 Winograd towers are outside the tolerance at trained magnitudes ("stress": 1.2e-3 to
 # 3.6e-3); AUTO measures that at load time and runs the fp64 Winograd domain instead (test_nn_accuracy_gpu.py)
-UNGUARDED = {("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "winograd88i8"), ("f16x3", "winograd48")}
+UNGUARDED = {("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "winograd88i8"), ("fp32", "winograd88i8v"),
+             ("f16x3", "winograd48")}
 
 
 def _net(variant, precision="fp32", algo="auto"):

@@ -57,3 +57,23 @@ def test_gemm_matches_fp64_to_the_truncation():
     ref = np.matmul(V, np.swapaxes(U, 1, 2))
     scale = np.abs(V).max(axis=2)[:, :, None] * np.abs(U).max(axis=2)[:, None, :] * 512
     assert (np.abs(M - ref) <= scale * 2.0 ** -33).all()
+
+
+def test_f88_input_transform_restatement_matches_the_kernel_constants():
+    """tests/_wino_emul.bt88 (B10^T derived exactly from the points) == the coefficients of
+    csrc/kv_wino88d.h's w88d_bt fma chains, entry for entry -- the GPU test of wino88i32v_out_kernel checks its
+    digits against numpy's fp64 transform with this matrix."""
+    import os
+    import re
+    from tests._wino_emul import bt88
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "knightvision_amd", "csrc", "kv_wino88d.h")).read()
+    body = src[src.index("void w88d_bt"):]
+    body = body[:body.index("\n}")]
+    M = np.zeros((10, 10))
+    rows = re.findall(r"o\[(\d)\] = (.*);", body)
+    assert len(rows) == 10
+    for a, expr in rows:
+        for c, i in re.findall(r"(-?[\d.]+(?:e-?\d+)?),? ?\*? ?d\[(\d)\]", expr):
+            M[int(a), int(i)] = float(c)
+    assert np.array_equal(M, bt88())

@@ -111,6 +111,45 @@ def test_i8f32_out_kernel_writes_the_slice_kernels_digits(rows, resid, seg):
     assert len(np.unique(ef)) > 3  # exponents actually vary across rows
 
 
+@pytest.mark.parametrize("rows,resid", [(128, False), (128, True), (256, True)])
+def test_i8f32v_out_kernel_writes_the_fp64_transforms_digits(rows, resid):
+    """wino88i32v_out_kernel (KV_ALGO_WINOGRAD88_I8V: output transform + BN (+ residual) + ReLU in fp32, then
+    the next V as the fp64 input transform of that activation, cut to 4 row-line digits) == wino88_out_kernel's
+    Y + wino88d_in_kernel's fp64 V + wino88i_slice_kernel, bit for bit: Y, every digit, every exponent. Then the
+    digits against numpy's fp64 transform of the same Y: each value within half a unit of the 28-bit block
+    (2^(e-29)) plus fp64 rounding, each exponent the rule's on numpy's row max."""
+    from tests._wino_emul import input_transform_f64
+    rng = np.random.default_rng(rows + 11 * resid)
+    M = (rng.standard_normal((100, rows, 512)) * 0.3).astype(np.float32)
+    M[:, 5, :] = 0.0
+    scale = (0.5 + rng.random(512)).astype(np.float32)
+    scale[::7] *= np.float32(2.0 ** -12)
+    shift = -np.abs(rng.standard_normal(512) * 0.1).astype(np.float32)
+    R = (np.abs(rng.standard_normal((rows, 64, 512))) * 0.5).astype(np.float32) if resid else None
+    if resid:
+        R[5] = 0.0
+    Yf, df, ef = _out(M, scale, shift, R, 1 | 4)
+    Ys, ds, es = _out(M, scale, shift, R, 4)
+    assert np.array_equal(Yf.view(np.uint32), Ys.view(np.uint32))
+    assert np.array_equal(ef, es)
+    assert np.array_equal(df, ds)
+    assert (ef[:, 5] == 0).all() and not df[:, :, 5].any()
+    # the fp32 form's digits differ (the fp32 transform rounds): the fp64 transform is what ran
+    _, d32, _ = _out(M, scale, shift, R, 1)
+    assert not np.array_equal(df, d32)
+    V = input_transform_f64(Yf.astype(np.float64))              # [100][rows][512]
+    dec = np.zeros_like(V)
+    dg = df.astype(np.float64).transpose(0, 2, 1, 4, 3)           # [100][rows][16][32][4]
+    for d in range(4):
+        dec += dg[..., d].reshape(100, rows, 512) * 2.0 ** (-7 * (d + 1))
+    dec = np.ldexp(dec, ef[:, :, None])
+    mx = np.abs(V).max(-1)
+    e_np = np.where(mx > 0, np.frexp(mx)[1] + (np.frexp(mx)[0] * 2 >= 255 / 128), 0)
+    assert np.array_equal(ef, e_np.astype(np.int32))
+    tol = np.ldexp(1.0, ef - 29)[:, :, None] + 1e-12 * mx[:, :, None]
+    assert (np.abs(dec - V) <= tol).all(), float((np.abs(dec - V) / tol).max())
+
+
 def _error_bound(V, U, digits, M):
     """Per-element bound of |M - V U^T| for the kernel's arithmetic (V U^T in fp64 from the unsplit
     operands): each operand row is scaled by 2^-e (|a| 2^-e < 1) and cut to `digits` base-128 digits, so

@@ -1,7 +1,7 @@
-"""Per-kernel summary (calls, total/avg/min/max ns, share) from a rocprofv3
-rocpd SQLite database, in the column layout of rocprofv3's kernel_stats.csv.
+"""Kernel statistics (calls, average / total duration) from a rocprofv3 rocpd SQLite database (the
+--kernel-trace output when no csv format is asked for): the same columns as --stats' kernel_stats.csv.
 
-    python tools/rocpd_stats.py gpurun_out/prof/x_results.db [out.csv]
+    python tools/rocpd_stats.py gpurun_out/x/prof/run_results.db [out.csv]
 """
 import csv
 import sqlite3
@@ -10,23 +10,21 @@ import sys
 
 def stats(db):
     c = sqlite3.connect(db)
-    rows = c.execute("select name, count(*), sum(duration), avg(duration), min(duration), max(duration) "
-                     "from kernels group by name order by sum(duration) desc").fetchall()
-    tot = sum(r[2] for r in rows) or 1
-    return [(n, k, s, a, lo, hi, 100.0 * s / tot) for n, k, s, a, lo, hi in rows]
-
-
-def main():
-    rows = stats(sys.argv[1])
-    hdr = ["Name", "Calls", "TotalDurationNs", "AverageNs", "MinNs", "MaxNs", "Percentage"]
-    if len(sys.argv) > 2:
-        with open(sys.argv[2], "w", newline="") as f:
-            w = csv.writer(f, quoting=csv.QUOTE_NONNUMERIC)
-            w.writerow(hdr)
-            w.writerows(rows)
-    for n, k, s, a, lo, hi, p in rows[:20]:
-        print(f"{p:6.2f}% {k:6d} avg {a / 1e3:9.2f} us  {n[:110]}")
+    names = [r[0] for r in c.execute("select name from sqlite_master where type='table'")]
+    kd = next(n for n in names if n.startswith("rocpd_kernel_dispatch"))
+    ks = next(n for n in names if n.startswith("rocpd_info_kernel_symbol"))
+    rows = c.execute(f"select s.kernel_name, count(*), avg(d.end - d.start), sum(d.end - d.start) from {kd} d "
+                     f"join {ks} s on d.kernel_id = s.id group by s.kernel_name order by 4 desc").fetchall()
+    tot = sum(r[3] for r in rows)
+    return [(n, k, a, s, 100.0 * s / tot) for n, k, a, s in rows]
 
 
 if __name__ == "__main__":
-    main()
+    out = stats(sys.argv[1])
+    if len(sys.argv) > 2:
+        with open(sys.argv[2], "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["Name", "Calls", "AverageNs", "TotalDurationNs", "Percentage"])
+            w.writerows(out)
+    for n, k, a, s, p in out:
+        print(f"{n[:100]:100s} {k:6d} {a / 1e3:9.1f} us {p:6.2f} %")
