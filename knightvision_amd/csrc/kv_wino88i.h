@@ -1474,10 +1474,15 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
 // on learn-loop weights the fp32 input transform is what sets the fp32 tower's value error
 // (profiles/r05_learn_stage_emulate.log).
 
-// fp64 transform row 5h + aa of a plane split over lanes l, l ^ 32, from the half's 4 columns after the
-// half exchange (xc[kk][i] = pixel (i, 4h + kk)): the fma chains of wino88d_input_cols + wino88d_input_row
-// on the same inputs -- so the same bits as wino88d_input_plane -- one transform row at a time (each
-// column's w88d_bt is taken for rows aa and 5 + aa only), so no 10x4 fp64 intermediate is live.
+// Transform rows of the two halves at step aa: one +-p row pair of w88d_bt's even / odd form, (1, 2), (3, 4),
+// (5, 6), (7, 8), or (0, 9) at aa = 0 -- half 0 takes the first, half 1 the second.
+__device__ inline int w88v_row(int h, int aa) { return aa == 0 ? 9 * h : 2 * aa - 1 + h; }
+
+// fp64 transform row w88v_row(h, aa) of a plane split over lanes l, l ^ 32, from the half's 4 columns after
+// the half exchange (xc[kk][i] = pixel (i, 4h + kk)): the fma chains of wino88d_input_cols +
+// wino88d_input_row on the same inputs -- so the same bits as wino88d_input_plane -- one transform row pair
+// at a time (each column's w88d_bt is taken for that pair only, which shares its even / odd halves), so no
+// 10x4 fp64 intermediate is live.
 __device__ inline void wino88d_input_row_of_cols(float (&xc)[4][8], int aa, double (&o)[10]) {
     // opaque to the compiler per row: otherwise it keeps the 32 widened values (64 VGPRs) live across the
     // rows and both passes instead of widening them again, and spills
@@ -1496,7 +1501,7 @@ __device__ inline void wino88d_input_row_of_cols(float (&xc)[4][8], int aa, doub
 #pragma unroll
         for (int i = 0; i < 8; ++i) col[1 + i] = (double)xc[kk][i];
         w88d_bt(col, t);
-        double lo = t[aa], hi = t[5 + aa];
+        double lo = t[w88v_row(0, aa)], hi = t[w88v_row(1, aa)];
         half_swap(lo, hi);
         row[1 + kk] = lo;
         row[5 + kk] = hi;
@@ -1549,8 +1554,9 @@ __global__ __launch_bounds__(1024) void wino88i32v_out_kernel(const float* __res
         }
     }
     __syncthreads();
-    if (threadIdx.x < 100) {
-        const int xi = threadIdx.x, a = xi / 10, bb = xi % 10, hh = a / 5, aa = a % 5;
+    if (threadIdx.x < 100) {  // point row a came from half hh at step aa (w88v_row)
+        const int xi = threadIdx.x, a = xi / 10, bb = xi % 10;
+        const int hh = a == 9 ? 1 : (a == 0 ? 0 : (a - 1) & 1), aa = (a == 0 || a == 9) ? 0 : (a + 1) >> 1;
         unsigned m = 0;
 #pragma unroll
         for (int ww = 0; ww < NW; ++ww) m = red[ww][hh][aa][bb] > m ? red[ww][hh][aa][bb] : m;
@@ -1566,7 +1572,7 @@ __global__ __launch_bounds__(1024) void wino88i32v_out_kernel(const float* __res
     for (int aa = 0; aa < 5; ++aa) {
         double o[10];
         wino88d_input_row_of_cols(xc, aa, o);
-        const int a = 5 * h + aa;
+        const int a = w88v_row(h, aa);
 #pragma unroll
         for (int bb = 0; bb < 10; ++bb) {
             const int xi = a * 10 + bb;

@@ -68,6 +68,12 @@ def main():
                           # change of conv path between iterations would show
                           "selfplay_rate_per_iteration": [
                               round((st.get("sims") or st.get("plies", 0)) / st["selfplay_s"], 1) for st in stats],
+                          "selfplay_s_per_iteration": [round(st["selfplay_s"], 3) for st in stats],
+                          "sims_per_iteration": [st.get("sims") for st in stats],
+                          "plies_per_iteration": [st.get("plies") for st in stats],
+                          "calib_ms_per_iteration": [round(st["calib_ms"]) if "calib_ms" in st else None
+                                                     for st in stats],
+                          "calib_err_per_iteration": [st.get("calib_err") for st in stats],
                           "data": "synthetic"}), flush=True)
     if world > 1:
         dist.barrier()
