@@ -49,13 +49,14 @@ FP32_MFMA_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md, f32-input MFMA (den
 FP64_MFMA_PEAK_TFLOPS = 78.6          # AMD's MI355X FP64 matrix spec figure (the guides give no f64 row; not
                                       # measured here)
 PATH_NAMES = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3",
-              5: "winograd88_i8", 6: "winograd88_i8f32", 7: "winograd88_i8f32v"}  # KV_PATH_*
+              5: "winograd88_i8", 6: "winograd88_i8f32", 7: "winograd88_i8f32v",
+              8: "winograd88_i8r"}  # KV_PATH_*
 BF16_MFMA_PEAK_TFLOPS = 2500.0        # dense bf16 MFMA
 I8_MFMA_PEAK_TOPS = 5000.0            # dense int8 MFMA: 2x the bf16 rate (cdna_hip_programming.md, MFMA rate per dtype);
                                       # v_mfma_i32_32x32x32_i8 back to back measured 4.1 POPS at the clock the chip
                                       # holds under it (profiles/r04_mfma_rate.log)
 I8_MFMA_MEASURED_TOPS = 4098.0
-I8_DIGIT_PRODUCTS = {5: 15, 6: 10, 7: 10}    # int8 GEMMs per Winograd GEMM: digit pairs i + j < 5 (KV_PREC_I8X5, fp64
+I8_DIGIT_PRODUCTS = {5: 15, 6: 10, 7: 10, 8: 13}    # int8 GEMMs per Winograd GEMM: digit pairs i + j < 5 (KV_PREC_I8X5, fp64
                                       # domain) / < 4 (KV_ALGO_WINOGRAD88_I8, fp32 domain)
 
 
@@ -67,7 +68,7 @@ def parse():
     ap.add_argument("--mode", choices=["mcts", "ref"], default=os.environ.get("KV_BENCH_MODE", "mcts"))
     ap.add_argument("--slots", type=int, default=2048)
     ap.add_argument("--sims", type=int, default=800)
-    ap.add_argument("--precision", choices=["fp32", "f16x3", "f64w", "i8x5"], default="fp32")
+    ap.add_argument("--precision", choices=["fp32", "f16x3", "f64w", "i8x5", "i8r4"], default="fp32")
     ap.add_argument("--algo", choices=["auto", "direct", "winograd48", "winograd88", "winograd88i8"], default="auto",
                     help="conv algorithm of the fp32 tower (auto: the library's calibrated choice per weight load -- "
                          "Winograd F(8x8,3x3) fp32 for the random-init weights)")
@@ -329,8 +330,13 @@ def gemm_label(path: int, rows: int, split: int, cus: int = 256):
             " (residual-tower Winograd F(8x8,3x3) GEMMs of the fp32 tower from 4 int8 digits per value: 10 "
             "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 tiles, "
             "each stage's last 6 MFMAs per wave under the next stage's first LDS reads)")
+    if path == 8:
+        return "wino88i_gemm_lag5_kernel<512,2,4,8>", (
+            " (residual-tower Winograd F(8x8,3x3) GEMMs in the fp64 domain from 4 radix-256 int8 digits per value: "
+            "the 13 pairs i + j <= 4, v_mfma_i32_32x32x32_i8 chains with exact int32 accumulation, 128x128 tiles, "
+            "each stage's last B digits under the next stage's first LDS reads)")
     if path == 5:
-        return "wino88i_gemm_lag5_kernel<512,3>", (
+        return "wino88i_gemm_lag5_kernel<512,3,5,7>", (
             " (residual-tower Winograd F(8x8,3x3) GEMMs in the fp64 domain from 5 int8 digits per value: 15 "
             "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, 128x128 tiles, each stage's last "
             "MFMAs under the next stage's first LDS reads)")
@@ -665,6 +671,9 @@ def main():
             1: "fp32 network, Winograd F(4x8) GEMMs on v_mfma_f32_32x32x2_f32",
             5: "fp32 activations, fp64 Winograd domain, GEMMs on 5 int8 digits per value (per-row 35-bit block fixed "
                "point, 15 of 25 digit pairs, exact int32 levels, exact fp64 combine)",
+            8: "fp32 activations, fp64 Winograd domain, GEMMs on 4 radix-256 int8 digits per value (per-row 31-bit "
+               "block fixed point, 13 of 16 digit pairs, exact int32 levels, fp64 combine)",
+            7: "fp32 network with fp64 input transforms (V cut to 4 int8 digits from fp64); GEMMs as path 6",
             3: "fp32 activations, fp64 Winograd domain on v_mfma_f64",
             0: "fp32 direct implicit-GEMM convs"}.get(path)
         if pg_info is not None:
@@ -680,7 +689,8 @@ def main():
                         "magnitudes, BN statistics of the data, logits of std 4 -- what a checkpoint looks like, "
                         "scripts/self_play.py:71-77) under fp32 + AUTO: no fp32 Winograd tower holds the 1e-4 "
                         "logit tolerance there, so the calibration picks the fp64 Winograd domain with int8-digit "
-                        "GEMMs; the peaked priors give the trees their own shapes",
+                        "GEMMs (4 radix-256 digits when they hold the budget, else 5 radix-128 ones); the peaked "
+                        "priors give the trees their own shapes",
                 "weights": "stress", "conv_path": PATH_NAMES.get(tp),
                 "calibration": {k: trained["calibration"][k] for k in ("path_large", "path_small", "err_logit",
                                                                       "err_value", "ms")},

@@ -88,11 +88,17 @@ int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv);
  *                ~2^-36 of the fp64 product per element); logits
  *                as close to fp64 as KV_PREC_F64W's, at every batch size (the
  *                fp32 AUTO fallback for trained weights before F64W).
+ * KV_PREC_I8R4   the same fp64 domain with 4 radix-256 digits per value
+ *                (31-bit block fixed point: N = rint(a 2^(31-e)) split into
+ *                balanced bytes) and the 13 digit pairs i + j <= 4 of 16:
+ *                13 int8 GEMMs instead of 15 over 4 digit planes instead of
+ *                5 (AUTO's candidate before KV_PREC_I8X5).
  * Values 1 and 2 (bf16x3 / bf16x6) were retired in round 4: KV_EINVAL. */
 #define KV_PREC_FP32 0
 #define KV_PREC_F16X3 3
 #define KV_PREC_F64W 4
 #define KV_PREC_I8X5 5
+#define KV_PREC_I8R4 6
 int kv_net_set_precision(kv_net* net, int precision);
 /* Algorithm of the fp32 3x3 convs with Cin 256/512:
  * KV_ALGO_AUTO      per weight load, the fastest path whose logits / values are
@@ -101,7 +107,8 @@ int kv_net_set_precision(kv_net* net, int precision);
  *                   self-play, 47 seeded random ones): > 16 boards F(8x8) fp32
  *                   with int8-digit GEMMs (KV_ALGO_WINOGRAD88_I8), else the
  *                   same with fp64 input transforms (KV_ALGO_WINOGRAD88_I8V),
- *                   else the fp64 Winograd domain on int8 digits
+ *                   else the fp64 Winograd domain on 4 radix-256 int8
+ *                   digits (KV_PREC_I8R4), else on 5 radix-128 ones
  *                   (KV_PREC_I8X5), else
  *                   on fp64 MFMA; <= 16 boards direct (split-K), else F(8x8)
  *                   fp64 (kv_net_calibration reports it)
@@ -137,7 +144,8 @@ int kv_net_set_algo(kv_net* net, int algo);
 #define KV_PATH_WINO88_I8 5
 #define KV_PATH_WINO88_I8F32 6
 #define KV_PATH_WINO88_I8F32V 7
-#define KV_NPATH 8
+#define KV_PATH_WINO88_I8R 8
+#define KV_NPATH 9
 typedef struct {
     int calibrated;      /* 1: the last load / setting ran the fp32 AUTO calibration */
     int path_large;      /* KV_PATH_* of batches > 16 boards (also without calibration) */
@@ -313,7 +321,8 @@ int kv_dev_py_random(int device, const uint64_t* seeds, int n, int count, double
  * domain's (KV_ALGO_WINOGRAD88_I8) fp32 M, widened); v_digits (5 digits: planes
  * [100][K/32][5][rows][32]; 4 digits: row lines [100][K/32][rows][4][32]) and
  * v_exp [100][rows] (either may be NULL) return V's digits and row exponents. seg 1 (4 digits, K 512):
- * V's exponents per 256-channel segment (v_exp [100][2][rows]), the fp32 tower's default form. */
+ * V's exponents per 256-channel segment (v_exp [100][2][rows]), the fp32 tower's A/B form. seg 2 (4 digits):
+ * KV_PREC_I8R4's 4 radix-256 digit planes [100][K/32][4][rows][32], its GEMM and fp64 M. */
 int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, int digits, int seg, double* M,
                    int8_t* v_digits, int* v_exp);
 /* The fp32 tower's residual output kernel on int8 digits (KV_ALGO_WINOGRAD88_I8): M [100][rows][512] fp32

@@ -42,9 +42,10 @@ class Stats(C.Structure):
                 ("dom_path", C.c_int64), ("dom_split", C.c_int64)]
 
 
-NPATH = 8  # KV_NPATH
+NPATH = 9  # KV_NPATH
 PATHS = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3",
-         5: "winograd88_i8", 6: "winograd88_i8f32", 7: "winograd88_i8f32v"}  # KV_PATH_*
+         5: "winograd88_i8", 6: "winograd88_i8f32", 7: "winograd88_i8f32v",
+         8: "winograd88_i8r"}  # KV_PATH_*
 
 
 class Calib(C.Structure):

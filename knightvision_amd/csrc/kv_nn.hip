@@ -612,6 +612,7 @@ __global__ void planes_to_nhwc16_kernel(const float* __restrict__ planes, int nb
 //   KV_PATH_WINO88_I8  F(8x8), fp64 Winograd domain, GEMMs on int8 digits (kv_wino88i.h)
 //   KV_PATH_WINO88_I8F32 F(8x8), fp32 Winograd domain, GEMMs on int8 digits (kv_wino88i.h)
 //   KV_PATH_WINO88_I8F32V the same with fp64 input transforms (V cut to digits from fp64)
+//   KV_PATH_WINO88_I8R F(8x8), fp64 Winograd domain, GEMMs on 4 radix-256 digits (13 of 16 pairs)
 // fp32 + KV_ALGO_AUTO picks its paths per weight load (kv_net_calibration).
 constexpr int kNPath = KV_NPATH;
 
@@ -643,6 +644,8 @@ struct kv_net {
     int* eu88i = nullptr;   // their row exponents [100][Cout]
     int8_t* U88i32 = nullptr;  // the same with 4 digits (KV_PATH_WINO88_I8F32 and _I8F32V)
     int* eu88i32 = nullptr;
+    int8_t* U88r = nullptr;    // 4 radix-256 digit planes [100][Cin/32][4][Cout][32] (KV_PATH_WINO88_I8R)
+    int* eu88r = nullptr;
     size_t euoff[12] = {};
     bool built[kNPath] = {};
     unsigned* vmax = nullptr;  // f16x3: per-board max |V| of each conv's input, [12][cap]
@@ -688,6 +691,7 @@ static int path_for(const kv_net* net, int B) {
     const bool small = B <= kSplitMaxBoards;
     if (net->precision == KV_PREC_F64W) return KV_PATH_WINO88_F64;
     if (net->precision == KV_PREC_I8X5) return KV_PATH_WINO88_I8;
+    if (net->precision == KV_PREC_I8R4) return KV_PATH_WINO88_I8R;
     if (net->precision == KV_PREC_FP32 && net->algo == KV_ALGO_WINOGRAD88_I8) return KV_PATH_WINO88_I8F32;
     if (net->precision == KV_PREC_FP32 && net->algo == KV_ALGO_WINOGRAD88_I8V) return KV_PATH_WINO88_I8F32V;
     if (net->precision == KV_PREC_F16X3) {
@@ -777,6 +781,7 @@ static int net_pad(const kv_net* net, int B) {
         }
         case KV_PATH_DIRECT: return (B + 3) & ~3;
         case KV_PATH_WINO88_I8:
+        case KV_PATH_WINO88_I8R:
         case KV_PATH_WINO88_I8F32:
         case KV_PATH_WINO88_I8F32V: return (B + 127) & ~127;  // the int8 GEMM's 128-row tiles
         default: return (B + 31) & ~31;
@@ -1098,11 +1103,12 @@ static int wino88d_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 // before each GEMM ----
 // (4 digits: the fp32 domain's row-line layout)
 // (NSEG 2: V's exponents per 256-channel segment, K 512 only)
-template <int K, int D = kv::kI8Digits, class T, int NSEG = 1>
+// (R8: KV_PATH_WINO88_I8R's 4 radix-256 digit planes of fp64 rows)
+template <int K, int D = kv::kI8Digits, class T, int NSEG = 1, bool R8 = false>
 static int launch_wino88i_slice(const T* src, int n, int slab_rows, int nslab, int8_t* dst, int* ex,
                                 hipStream_t st) {
     const int waves = n * nslab;
-    hipLaunchKernelGGL((kv::wino88i_slice_kernel<K, T, D, D == kv::kI8DigitsF32, NSEG>),
+    hipLaunchKernelGGL((kv::wino88i_slice_kernel<K, T, D, D == kv::kI8DigitsF32 && !R8, NSEG, R8>),
                        dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, src, n, slab_rows, nslab, dst, ex);
     KV_HIP(hipGetLastError());
     return KV_OK;
@@ -1149,18 +1155,18 @@ static int launch_wino88i32_gemm_mid(const int8_t* V8, const int* ev, const int8
     return KV_OK;
 }
 
-// KV_PREC_I8X5's GEMM with the lagging half (wino88i_gemm_lag5_kernel)
-template <int K, int LJ = 3>
+// KV_PREC_I8X5's GEMM with the lagging half (wino88i_gemm_lag5_kernel); S = 4, RB = 8: KV_PATH_WINO88_I8R's
+template <int K, int LJ = 3, int S = kv::kI8Digits, int RB = 7>
 static int launch_wino88i_gemm_lag5(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, double* M,
                                     int rows, int stride, hipStream_t st) {
-    using T = kv::Wino88iTile<kv::kI8Digits>;
+    using T = kv::Wino88iTile<S>;
     constexpr int bytes = 3 * T::STAGE;
-    KV_HIP(lds_opt_in((const void*)kv::wino88i_gemm_lag5_kernel<K, LJ>, bytes));
+    KV_HIP(lds_opt_in((const void*)kv::wino88i_gemm_lag5_kernel<K, LJ, S, RB>, bytes));
     const int nwg = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
     KV_REQUIRE(rows % T::WM == 0 && stride % T::WM == 0 && nwg % 8 == 0, KV_EINVAL,
                "wino gemm i8x5 (lag): rows %d / stride %d vs tile %d", rows, stride, T::WM);
-    hipLaunchKernelGGL((kv::wino88i_gemm_lag5_kernel<K, LJ>), dim3(nwg), dim3(T::THREADS), bytes, st, V8, ev, U8, eu,
-                       M, rows, 512, stride);
+    hipLaunchKernelGGL((kv::wino88i_gemm_lag5_kernel<K, LJ, S, RB>), dim3(nwg), dim3(T::THREADS), bytes, st, V8, ev, U8,
+                       eu, M, rows, 512, stride);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -1241,18 +1247,23 @@ static int launch_wino88i32_gemm(const int8_t* V8, const int* ev, const int8_t* 
     return KV_OK;
 }
 
-// conv l's output transform into Y (fp32), then the next conv's digit planes from Y (kv_wino88i.h)
+// conv l's output transform into Y (fp32), then the next conv's digit planes from Y (kv_wino88i.h); r8: 4
+// radix-256 digit planes (KV_PATH_WINO88_I8R)
 template <bool RESID>
 static int launch_wino88i_out(kv_net* net, int l, const double* M, int nb, int stride, const float* resid, float* Y,
-                              hipStream_t st) {
+                              bool r8, hipStream_t st) {
     const float* W = net->w;
     unsigned* evmax = (unsigned*)net->evmax8;
     KV_HIP(hipMemsetAsync(evmax, 0, (size_t)kv::W88_XI * stride * sizeof(unsigned), st));
     hipLaunchKernelGGL((kv::wino88i_outmax_kernel<RESID>), dim3(512 / 128, nb), dim3(256), 0, st, M, stride,
                        W + net->off.scale[l], W + net->off.shift[l], resid, Y, evmax);
     KV_REQUIRE(nb % 4 == 0, KV_EINVAL, "wino88i: %d boards (a multiple of 4)", nb);
-    hipLaunchKernelGGL(kv::wino88i_in_kernel, dim3(512 / 32, nb / 4), dim3(256), 0, st, Y, stride,
-                       (const unsigned*)evmax, net->V8, net->ev8);
+    if (r8)
+        hipLaunchKernelGGL(kv::wino88i_in_kernel<true>, dim3(512 / 32, nb / 4), dim3(256), 0, st, Y, stride,
+                           (const unsigned*)evmax, net->V8, net->ev8);
+    else
+        hipLaunchKernelGGL(kv::wino88i_in_kernel<false>, dim3(512 / 32, nb / 4), dim3(256), 0, st, Y, stride,
+                           (const unsigned*)evmax, net->V8, net->ev8);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -1270,32 +1281,48 @@ static int i8x5_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const in
     return launch_wino88i_gemm_lag5<K>(V8, ev, U8, eu, M, rows, stride, st);
 }
 
-static int wino88i_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
+// KV_PATH_WINO88_I8R's GEMM: the lag kernel on 4 radix-256 digit planes, 13 pairs (B digits 2-3 lag)
+constexpr int kI8rLJ = 2;
+template <int K>
+static int i8r_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, double* M, int rows, int stride,
+                    hipStream_t st) {
+    return launch_wino88i_gemm_lag5<K, kI8rLJ, 4, 8>(V8, ev, U8, eu, M, rows, stride, st);
+}
+
+// the fp64 domain on int8 digits; r8: KV_PATH_WINO88_I8R (4 radix-256 digits) instead of 5 radix-128 ones
+static int wino88i_blocks(kv_net* net, int nb, bool mark, bool r8, hipStream_t st) {
     const int rows = nb, stride = rows;
     double* M = (double*)net->Mw;
-    const int8_t* U = net->U88i;
+    const int8_t* U = r8 ? net->U88r : net->U88i;
+    const int* eu = r8 ? net->eu88r : net->eu88i;
+    const int D = r8 ? 4 : kv::kI8Digits;
+    auto gemm = [&](int l, bool k256) {
+        const int8_t* Ul = U + net->uoff88[l] * D;
+        const int* el = eu + net->euoff[l];
+        if (r8)
+            return k256 ? i8r_gemm<256>(net->V8, net->ev8, Ul, el, M, rows, stride, st)
+                        : i8r_gemm<512>(net->V8, net->ev8, Ul, el, M, rows, stride, st);
+        return k256 ? i8x5_gemm<256>(net->V8, net->ev8, Ul, el, M, rows, stride, st)
+                    : i8x5_gemm<512>(net->V8, net->ev8, Ul, el, M, rows, stride, st);
+    };
     int rc;
     // conv2: the stem wrote V64 (256 channels); its digits by the slice kernel
-    if ((rc = launch_wino88i_slice<256>((const double*)net->V256, rows, stride, kv::W88_XI, net->V8, net->ev8, st)))
-        return rc;
-    if ((rc = i8x5_gemm<256>(net->V8, net->ev8, U + net->uoff88[1] * kv::kI8Digits,
-                                       net->eu88i + net->euoff[1], M, rows, stride, st)))
-        return rc;
-    if ((rc = launch_wino88i_out<false>(net, 1, M, nb, stride, nullptr, net->X, st))) return rc;
+    rc = r8 ? launch_wino88i_slice<256, 4, double, 1, true>((const double*)net->V256, rows, stride, kv::W88_XI, net->V8,
+                                                            net->ev8, st)
+            : launch_wino88i_slice<256>((const double*)net->V256, rows, stride, kv::W88_XI, net->V8, net->ev8, st);
+    if (rc) return rc;
+    if ((rc = gemm(1, true))) return rc;
+    if ((rc = launch_wino88i_out<false>(net, 1, M, nb, stride, nullptr, net->X, r8, st))) return rc;
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
     for (int r = 0; r < 5; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         const bool m = mark && r == 2;
         if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-        if ((rc = i8x5_gemm<512>(net->V8, net->ev8, U + net->uoff88[l1] * kv::kI8Digits,
-                                           net->eu88i + net->euoff[l1], M, rows, stride, st)))
-            return rc;
+        if ((rc = gemm(l1, false))) return rc;
         if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
-        if ((rc = launch_wino88i_out<false>(net, l1, M, nb, stride, nullptr, net->T, st))) return rc;
-        if ((rc = i8x5_gemm<512>(net->V8, net->ev8, U + net->uoff88[l2] * kv::kI8Digits,
-                                           net->eu88i + net->euoff[l2], M, rows, stride, st)))
-            return rc;
-        rc = r < 4 ? launch_wino88i_out<true>(net, l2, M, nb, stride, net->X, net->X, st)
+        if ((rc = launch_wino88i_out<false>(net, l1, M, nb, stride, nullptr, net->T, r8, st))) return rc;
+        if ((rc = gemm(l2, false))) return rc;
+        rc = r < 4 ? launch_wino88i_out<true>(net, l2, M, nb, stride, net->X, net->X, r8, st)
                    : launch_wino88d_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
         if (rc) return rc;
     }
@@ -1457,6 +1484,7 @@ static WsNeed ws_need(int path) {
         case KV_PATH_WINO88: return {{P88 * 512 * f, P88 * 512 * f, P88 * 256 * f, 0}};
         case KV_PATH_WINO88_F64: return {{P88 * 512 * d, P88 * 512 * d, P88 * 256 * d, 0}};
         case KV_PATH_WINO88_I8: return {{0, P88 * 512 * d, P88 * 256 * d, P88 * 512 * kv::kI8Digits}};
+        case KV_PATH_WINO88_I8R: return {{0, P88 * 512 * d, P88 * 256 * d, P88 * 512 * 4}};
         case KV_PATH_WINO88_I8F32:
             return {{i8f32_form().slice ? P88 * 512 * f : 0, P88 * 512 * f, P88 * 256 * f,
                      P88 * 512 * kv::kI8DigitsF32}};
@@ -1489,8 +1517,9 @@ static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hi
     net->dom_path = path;
     net->dom_launches = 1;
     if (path == KV_PATH_WINO88 || path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8 ||
-        path == KV_PATH_WINO88_I8F32 || path == KV_PATH_WINO88_I8F32V) {
-        const bool f64 = path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8 || path == KV_PATH_WINO88_I8F32V;
+        path == KV_PATH_WINO88_I8R || path == KV_PATH_WINO88_I8F32 || path == KV_PATH_WINO88_I8F32V) {
+        const bool f64 = path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8 || path == KV_PATH_WINO88_I8R ||
+                         path == KV_PATH_WINO88_I8F32V;
         if (!v256_ready) {
             if (f64)
                 hipLaunchKernelGGL(kv::wino88d_in_kernel<256>, dim3(1, nb_pad), dim3(256), 0, st, net->T, nb_pad,
@@ -1502,7 +1531,8 @@ static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hi
         }
         if ((rc = path == KV_PATH_WINO88_I8F32    ? wino88i32_blocks(net, nb_pad, true, false, st)
                   : path == KV_PATH_WINO88_I8F32V ? wino88i32_blocks(net, nb_pad, true, true, st)
-                  : path == KV_PATH_WINO88_I8  ? wino88i_blocks(net, nb_pad, true, st)
+                  : path == KV_PATH_WINO88_I8  ? wino88i_blocks(net, nb_pad, true, false, st)
+                  : path == KV_PATH_WINO88_I8R ? wino88i_blocks(net, nb_pad, true, true, st)
                   : path == KV_PATH_WINO88_F64 ? wino88d_blocks(net, nb_pad, true, st)
                                                : wino88_blocks(net, nb_pad, true, st)))
             return rc;
@@ -1546,7 +1576,8 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
         if (path == KV_PATH_WINO88 || path == KV_PATH_WINO88_I8F32)
             hipLaunchKernelGGL(kv::stem_kernel<4>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], (float*)net->V256, nb_pad, nullptr);
-        else if (path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8 || path == KV_PATH_WINO88_I8F32V)
+        else if (path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8 || path == KV_PATH_WINO88_I8R ||
+                 path == KV_PATH_WINO88_I8F32V)
             hipLaunchKernelGGL(kv::stem_kernel<5>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], (float*)net->V256, nb_pad, nullptr);
         else if (path == KV_PATH_WINO48 || path == KV_PATH_WINO48_F16X3)
@@ -1705,13 +1736,14 @@ static int ensure_path(kv_net* net, int path) {
             break;
         }
         case KV_PATH_WINO88_I8:
+        case KV_PATH_WINO88_I8R:
         case KV_PATH_WINO88_I8F32: {
             // U64 per layer (from the fp64 set when it is built, else into a one-layer scratch), then its digits
-            // (5 for the fp64 domain, 4 for the fp32 one)
-            const bool f32 = path == KV_PATH_WINO88_I8F32;
-            const int D = f32 ? kv::kI8DigitsF32 : kv::kI8Digits;
-            int8_t*& Ud = f32 ? net->U88i32 : net->U88i;
-            int*& Ue = f32 ? net->eu88i32 : net->eu88i;
+            // (5 for the fp64 domain, 4 radix-256 ones for its I8R form, 4 row-line ones for the fp32 tower)
+            const bool f32 = path == KV_PATH_WINO88_I8F32, r8 = path == KV_PATH_WINO88_I8R;
+            const int D = f32 || r8 ? 4 : kv::kI8Digits;
+            int8_t*& Ud = f32 ? net->U88i32 : r8 ? net->U88r : net->U88i;
+            int*& Ue = f32 ? net->eu88i32 : r8 ? net->eu88r : net->eu88i;
             const size_t tot = wino_offsets(net->uoff88, kv::W88_XI);
             size_t tot_co = 0;
             for (int l = 1; l < 12; ++l) {
@@ -1735,6 +1767,9 @@ static int ensure_path(kv_net* net, int path) {
                 if (f32)
                     rc = ci == 256 ? launch_wino88i_slice<256, kv::kI8DigitsF32>(U64, co, co, kv::W88_XI, dst, ex, 0)
                                    : launch_wino88i_slice<512, kv::kI8DigitsF32>(U64, co, co, kv::W88_XI, dst, ex, 0);
+                else if (r8)
+                    rc = ci == 256 ? launch_wino88i_slice<256, 4, double, 1, true>(U64, co, co, kv::W88_XI, dst, ex, 0)
+                                   : launch_wino88i_slice<512, 4, double, 1, true>(U64, co, co, kv::W88_XI, dst, ex, 0);
                 else
                     rc = ci == 256 ? launch_wino88i_slice<256>(U64, co, co, kv::W88_XI, dst, ex, 0)
                                    : launch_wino88i_slice<512>(U64, co, co, kv::W88_XI, dst, ex, 0);
@@ -1784,6 +1819,13 @@ static void release_unused(kv_net* net) {
         net->U88i = nullptr;
         net->eu88i = nullptr;
         net->built[KV_PATH_WINO88_I8] = false;
+    }
+    if (!keep[KV_PATH_WINO88_I8R]) {
+        (void)hipFree(net->U88r);
+        (void)hipFree(net->eu88r);
+        net->U88r = nullptr;
+        net->eu88r = nullptr;
+        net->built[KV_PATH_WINO88_I8R] = false;
     }
     if (!keep[KV_PATH_WINO88_I8F32V]) net->built[KV_PATH_WINO88_I8F32V] = false;
     if (!keep[KV_PATH_WINO88_I8F32] && !keep[KV_PATH_WINO88_I8F32V]) {
@@ -1935,9 +1977,10 @@ static int net_calibrate(kv_net* net) {
     // > 16 boards
     // (F(8x8) and F(4x8) on fp32 MFMA are never within the budget when the int8-digit fp32 tower is not:
     // on every weight set measured they are further from fp64 -- DESIGN.md; they stay explicit algos)
-    const int cands[4] = {KV_PATH_WINO88_I8F32, KV_PATH_WINO88_I8F32V, KV_PATH_WINO88_I8, KV_PATH_WINO88_F64};
+    const int cands[5] = {KV_PATH_WINO88_I8F32, KV_PATH_WINO88_I8F32V, KV_PATH_WINO88_I8R, KV_PATH_WINO88_I8,
+                          KV_PATH_WINO88_F64};
     net->auto_small = KV_PATH_DIRECT;
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 5; ++i) {
         const int p = cands[i];
         if ((rc = ensure_path(net, p))) return fail(rc);
         net->auto_large = p;
@@ -2050,7 +2093,7 @@ int kv_net_set_precision(kv_net* net, int precision) {
                "kv_net_set_precision: precision %d (bf16x3 / bf16x6) was retired; use KV_PREC_FP32, KV_PREC_F16X3 "
                "or KV_PREC_F64W", precision);
     KV_REQUIRE(precision == KV_PREC_FP32 || precision == KV_PREC_F16X3 || precision == KV_PREC_F64W ||
-                   precision == KV_PREC_I8X5,
+                   precision == KV_PREC_I8X5 || precision == KV_PREC_I8R4,
                KV_EINVAL,
                "kv_net_set_precision: unknown precision %d", precision);
     if (net->precision == precision && (!net->loaded || net->built[path_for(net, 1024)])) return KV_OK;
@@ -2117,10 +2160,12 @@ int kv_net_forward_boards_legal(kv_net* net, const int8_t* boards_dev, int B, co
 int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, int digits, int seg, double* M,
                    int8_t* v_digits, int* v_exp) {
     KV_REQUIRE(V && U && M && rows > 0 && rows % 128 == 0 && (K == 256 || K == 512) && (digits == 4 || digits == 5) &&
-                   (!seg || (digits == 4 && K == 512)),
+                   (!seg || (seg == 1 && digits == 4 && K == 512) || (seg == 2 && digits == 4)),
                KV_EINVAL, "kv_dev_wino88i: bad arguments (rows %d must be a multiple of 128, K %d 256 or 512, "
-               "digits %d 4 or 5, segments %d only with 4 digits and K 512)", rows, K, digits, seg);
-    const int nseg = seg ? 2 : 1;
+               "digits %d 4 or 5, seg %d: 1 only with 4 digits and K 512, 2 (radix 256) only with 4 digits)", rows,
+               K, digits, seg);
+    const bool r8 = seg == 2;
+    const int nseg = seg == 1 ? 2 : 1;
     KV_HIP(hipSetDevice(device));
     const size_t nv = (size_t)kv::W88_XI * rows * K, nu = (size_t)kv::W88_XI * 512 * K;
     const size_t nm = (size_t)kv::W88_XI * rows * 512;
@@ -2139,7 +2184,16 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
     KV_HIP(hipMemcpy(dv.p, V, nv * sizeof(double), hipMemcpyHostToDevice));
     KV_HIP(hipMemcpy(du.p, U, nu * sizeof(double), hipMemcpyHostToDevice));
     int rc;
-    if (digits == 5) {  // the fp64 domain: fp64 M
+    if (r8) {  // KV_PATH_WINO88_I8R: 4 radix-256 digit planes, 13 pairs, fp64 M
+        rc = K == 256 ? launch_wino88i_slice<256, 4, double, 1, true>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0)
+                      : launch_wino88i_slice<512, 4, double, 1, true>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0);
+        if (!rc)
+            rc = K == 256 ? launch_wino88i_slice<256, 4, double, 1, true>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0)
+                          : launch_wino88i_slice<512, 4, double, 1, true>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
+        if (!rc)
+            rc = K == 256 ? i8r_gemm<256>(v8.p, ev.p, u8.p, eu.p, dm.p, rows, rows, 0)
+                          : i8r_gemm<512>(v8.p, ev.p, u8.p, eu.p, dm.p, rows, rows, 0);
+    } else if (digits == 5) {  // the fp64 domain: fp64 M
         rc = K == 256 ? launch_wino88i_slice<256>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0)
                       : launch_wino88i_slice<512>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0);
         if (!rc)
@@ -2162,7 +2216,7 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
     }
     if (rc) return rc;
     KV_HIP(hipDeviceSynchronize());
-    if (digits == 5) {
+    if (digits == 5 || r8) {
         KV_HIP(hipMemcpy(M, dm.p, nm * sizeof(double), hipMemcpyDeviceToHost));
     } else {
         std::vector<float> mf(nm);
@@ -2403,6 +2457,8 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->eu88i);
     (void)hipFree(net->U88i32);
     (void)hipFree(net->eu88i32);
+    (void)hipFree(net->U88r);
+    (void)hipFree(net->eu88r);
     (void)hipFree(net->V8);
     (void)hipFree(net->ev8);
     (void)hipFree(net->evmax8);

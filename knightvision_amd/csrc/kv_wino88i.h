@@ -63,6 +63,25 @@ __device__ inline int i8_row_exponent_f32(unsigned m) {
     return (int)(m >> 23) - 126 + ((m & 0x7F0000u) == 0x7F0000u ? 1 : 0);
 }
 
+// Radix-256 form (KV_PATH_WINO88_I8R: 4 digits of 8 bits): e with max < 127/128 2^e (one more than the
+// plain rule when the max's top 7 fraction bits are >= 126), so every N = rint(v 2^(31-e)) has |N| < 127/128
+// 2^31 and its balanced base-256 digits d_0 (most significant) .. d_3, N = sum_i d_i 2^(8 (3 - i)), are all
+// in [-128, 127] with |d_0| <= 127: v ~ 2^(e-7) sum_i d_i 2^(-8 i), 31-bit block fixed point.
+__device__ inline int i8_row_exponent_r8(unsigned m) {
+    if (!m) return 0;
+    return (int)(m >> 20) - 1022 + ((m & 0xFE000u) >= 0xFC000u ? 1 : 0);
+}
+
+// the 4 radix-256 digits of v under e, packed: byte k = d_(3-k) (two's complement). N by a magic-number add
+// (rint, ties to even; the low word of t + 1.5 2^52 is N's two's complement for |t| < 2^31); then the balanced
+// digits are the bytes of N + 0x80808080 (each d + 128 in [0, 255], no carry out) with their top bits flipped.
+__device__ inline unsigned i8_digits_r8(double v, int e) {
+#pragma clang fp contract(off)
+    constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
+    const unsigned n = (unsigned)__double_as_longlong(ldexp(v, 31 - e) + kMagic);
+    return (n + 0x80808080u) ^ 0x80808080u;
+}
+
 // D digits of v under exponent e: t = 128 v 2^-e, d = rint(t), t = 128 (t - d), each step exact (in fp32
 // too: t never has more significant bits than v)
 template <int D, class T>
@@ -155,13 +174,14 @@ __device__ inline unsigned i8_quad_transpose(unsigned P, int lane) {
 // 32 channels goes to (((x * K/32 + kc) * slab_rows + r) * 4 + d) * 32 instead
 // -- the 4 digits of one row's chunk are one 128-byte line. NSEG = 2 (K = 512 only): one exponent per
 // 256-channel segment instead of per row (lanes 0-31 hold segment 0), at ex[(x * 2 + seg) * slab_rows + r].
-template <int K, class T, int D, bool RL = false, int NSEG = 1>
+template <int K, class T, int D, bool RL = false, int NSEG = 1, bool R8 = false>
 __global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict__ src, int n, int slab_rows,
                                                             int nslab, int8_t* __restrict__ dst,
                                                             int* __restrict__ ex) {
     static_assert(K == 256 || K == 512, "rows of 256 or 512 channels");
     static_assert(!RL || D == 4, "row lines hold 4 digits");
     static_assert(NSEG == 1 || (NSEG == 2 && K == 512), "segments of 256 channels");
+    static_assert(!R8 || (D == 4 && sizeof(T) == 8 && !RL && NSEG == 1), "radix 256: 4 digit planes of fp64 rows");
     constexpr int CPL = K / 64;  // 4 or 8 channels per lane
     const int lane = threadIdx.x & 63;
     const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -188,14 +208,20 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict_
         const unsigned t = (unsigned)__shfl_xor((int)m, o, 64);
         m = t > m ? t : m;
     }
-    const int e = sizeof(T) == 8 ? i8_row_exponent(m) : i8_row_exponent_f32(m);
+    const int e = R8 ? i8_row_exponent_r8(m) : sizeof(T) == 8 ? i8_row_exponent(m) : i8_row_exponent_f32(m);
     if (NSEG == 1 && lane == 0) ex[row] = e;
     if (NSEG == 2 && (lane & 31) == 0) ex[((size_t)x * 2 + (lane >> 5)) * slab_rows + r] = e;
     unsigned long long pk[D] = {};
 #pragma unroll
     for (int i = 0; i < CPL; ++i) {
         int dg[D];
-        i8_digits<D>(v[i], e, dg);
+        if constexpr (R8) {
+            const unsigned P = i8_digits_r8((double)v[i], e);
+#pragma unroll
+            for (int d = 0; d < D; ++d) dg[d] = (int)(signed char)(P >> (8 * (D - 1 - d)));
+        } else {
+            i8_digits<D>(v[i], e, dg);
+        }
 #pragma unroll
         for (int d = 0; d < D; ++d) pk[d] |= (unsigned long long)(unsigned char)(signed char)dg[d] << (8 * i);
     }
@@ -856,18 +882,22 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
 // B digits j >= LJ of a stage (their pairs i + j <= 4) run after the next barrier, under that stage's first
 // LDS reads; stage k + 2's copies (5 pieces per wave) go into stage k - 1's buffer right after barrier k.
 // Same products, same bits as wino88i_gemm_kernel<K, 5, ., double>.
-template <int K, int LJ = 3>
+// S = 4, RB = 8 (KV_PATH_WINO88_I8R): 4 radix-256 digit planes per operand (4 pieces per wave and stage), the
+// 13 pairs i + j <= 4 of 16 -- the same 5 levels, weighted 2^-8l -- combined in fp64 (the last two fma steps
+// may round: |level| <= 4 K 2^14 = 2^25, so the value has up to 57 significant bits; one fp64 rounding each).
+template <int K, int LJ = 3, int S = 5, int RB = 7>
 __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __restrict__ V8,
                                                                 const int* __restrict__ ev,
                                                                 const int8_t* __restrict__ U8,
                                                                 const int* __restrict__ eu, double* __restrict__ M,
                                                                 int rows, int cout, int stride) {
-    constexpr int S = 5, NBUF = 3;
+    constexpr int LEV = 5, NBUF = 3;  // levels: pairs i + j < LEV
     using T = Wino88iTile<S>;
     constexpr int NT = T::NT, WM = T::WM, WN = T::WN, GL = T::GL;
     constexpr int NK = K / 32;
-    constexpr int NA = S - LJ;
-    static_assert(GL == 5 && NK >= 3 && LJ >= 1 && LJ < S, "5 pieces per wave and stage");
+    constexpr int NA = S < LEV - LJ ? S : LEV - LJ;  // A digits the lagging half uses
+    static_assert(GL == S && NK >= 3 && LJ >= 1 && LJ < S && (S == 5 || (S == 4 && RB == 8)),
+                  "S pieces per wave and stage");
 
     extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8l5[];
     char* const L0 = (char*)lds_i8l5;
@@ -882,8 +912,8 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
     const int n_base = (idx % CT) * WN;
     const int r_base = ((idx / CT) % RT) * WM;
 
-    // copy pieces as wino88i_gemm_kernel's planes path: piece q = wave * 5 + g covers operand q / 20, digit
-    // (q % 20) / 4, rows 32 (q % 4) .. +31; lane l fills LDS row 32 (q % 4) + l / 2, half l & 1 (swapped on
+    // copy pieces as wino88i_gemm_kernel's planes path: piece q = wave * S + g covers operand q / 4S, digit
+    // (q % 4S) / 4, rows 32 (q % 4) .. +31; lane l fills LDS row 32 (q % 4) + l / 2, half l & 1 (swapped on
     // bit 3 of the row)
     const int op = (wave * GL) / (4 * S);
     const size_t rstride = op ? (size_t)cout : (size_t)stride;
@@ -910,9 +940,9 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
         boff[nt] = S * T::PLANE + bcol * 32 + i8_lds_half(bcol, lh);
     }
 
-    i32x16_t acc[S][NT];
+    i32x16_t acc[LEV][NT];
 #pragma unroll
-    for (int l = 0; l < S; ++l)
+    for (int l = 0; l < LEV; ++l)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[l][nt] = i32x16_t{};
     i8x16_t pa[NA] = {}, pb[S - LJ][NT] = {};
@@ -920,7 +950,7 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
 #pragma unroll
         for (int j = LJ; j < S; ++j)
 #pragma unroll
-            for (int i = 0; i + j < S; ++i)
+            for (int i = 0; i < S && i + j < LEV; ++i)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt)
                     acc[i + j][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(pa[i], pb[j - LJ][nt], acc[i + j][nt], 0, 0, 0);
@@ -956,7 +986,7 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
             }
             if (j < LJ) {
 #pragma unroll
-                for (int i = 0; i + j < S; ++i)
+                for (int i = 0; i < S && i + j < LEV; ++i)
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt)
                         acc[i + j][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[nt], acc[i + j][nt], 0, 0, 0);
@@ -965,9 +995,8 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
                 for (int nt = 0; nt < NT; ++nt) pb[j - LJ][nt] = b[nt];
             }
             if (j == 0 && kt + 2 < NK) {
-                issue1(2, kt + 2);
-                issue1(3, kt + 2);
-                issue1(4, kt + 2);
+#pragma unroll
+                for (int g = 2; g < GL; ++g) issue1(g, kt + 2);
             }
         }
 #pragma unroll
@@ -984,9 +1013,10 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
-            double m = (double)acc[S - 1][nt][r];
+            constexpr double w = RB == 8 ? 0.00390625 : 0.0078125;  // 2^-RB (radix 128: every step exact)
+            double m = (double)acc[LEV - 1][nt][r];
 #pragma unroll
-            for (int l = S - 2; l >= 0; --l) m = __builtin_fma(m, 0.0078125, (double)acc[l][nt][r]);  // exact
+            for (int l = LEV - 2; l >= 0; --l) m = __builtin_fma(m, w, (double)acc[l][nt][r]);
             M[((size_t)xi * stride + r_base + wm * 32 + row) * cout + col] = ldexp(m, evx[row] + ec);
         }
     }
@@ -1051,16 +1081,19 @@ __global__ __launch_bounds__(256) void wino88i_outmax_kernel(const double* __res
 // whole 128-byte line -- of each digit plane (xi, kc, d): 32-byte pieces from different workgroups made
 // the plane writes 2.8x slower (421 us per layer at 2,048 boards, profiles/r04_i8_fused_out.log).
 // X the fp32 activation [board][64][512]; writes the row exponents ex[xi][board] (from evmax) too.
+// R8 (KV_PATH_WINO88_I8R): 4 radix-256 digit planes (i8_digits_r8) instead of 5 radix-128 ones.
+template <bool R8 = false>
 __global__ __launch_bounds__(256) void wino88i_in_kernel(const float* __restrict__ X, int rows,
                                                          const unsigned* __restrict__ evmax,
                                                          int8_t* __restrict__ V8n, int* __restrict__ ex) {
-    constexpr int C = 512;
+    constexpr int C = 512, D = R8 ? 4 : kI8Digits;
     __shared__ int exs[4][100];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
     const int kc = blockIdx.x, c = kc * 32 + (lane & 31), b = blockIdx.y * 4 + w;
     for (int i = threadIdx.x; i < 400; i += 256) {
         const int bw = i / 100, xi = i % 100, bb = blockIdx.y * 4 + bw;
-        const int e = i8_row_exponent(evmax[(size_t)xi * rows + bb]);
+        const unsigned m = evmax[(size_t)xi * rows + bb];
+        const int e = R8 ? i8_row_exponent_r8(m) : i8_row_exponent(m);
         exs[bw][xi] = e;
         if (kc == 0) ex[(size_t)xi * rows + bb] = e;
     }
@@ -1074,8 +1107,8 @@ __global__ __launch_bounds__(256) void wino88i_in_kernel(const float* __restrict
     __syncthreads();
     // 32-bit byte offsets (the digit planes of 100 x rows x 512 values, 5 digits: < 2^32 bytes): one base
     // register + a 32-bit offset per store
-    const unsigned off0 = ((unsigned)kc * kI8Digits * rows + b) * 32 + (lane & 31);
-    const unsigned dstride = (unsigned)rows * 32, xstride = (C / 32) * kI8Digits * dstride;
+    const unsigned off0 = ((unsigned)kc * D * rows + b) * 32 + (lane & 31);
+    const unsigned dstride = (unsigned)rows * 32, xstride = (C / 32) * D * dstride;
     // (one byte store per digit: a lane-quad transpose into dword stores measured 3 % slower here,
     // profiles/r05_i8x5_ab.log -- the kernel is bound by its fp64 transform and digit arithmetic; the digits
     // by magic-number adds: profiles/r05_i8x5_magic_ab.log; non-temporal byte stores -- 32-byte pieces of
@@ -1088,10 +1121,16 @@ __global__ __launch_bounds__(256) void wino88i_in_kernel(const float* __restrict
 #pragma unroll
         for (int bb = 0; bb < 10; ++bb) {
             const int xi = a * 10 + bb;
-            unsigned dg[kI8Digits];
-            i8_digits_magic<kI8Digits>(o[bb], exs[w][xi], dg);
+            unsigned dg[D];
+            if constexpr (R8) {
+                const unsigned P = i8_digits_r8(o[bb], exs[w][xi]);
 #pragma unroll
-            for (int d = 0; d < kI8Digits; ++d) V8n[off0 + (unsigned)xi * xstride + (unsigned)d * dstride] = (int8_t)dg[d];
+                for (int d = 0; d < D; ++d) dg[d] = P >> (8 * (D - 1 - d));
+            } else {
+                i8_digits_magic<D>(o[bb], exs[w][xi], dg);
+            }
+#pragma unroll
+            for (int d = 0; d < D; ++d) V8n[off0 + (unsigned)xi * xstride + (unsigned)d * dstride] = (int8_t)dg[d];
         }
     }
 }

@@ -83,3 +83,42 @@ def gemm(V, U, digits=DIGITS):
     if digits == 4:
         M = M.astype(np.float32).astype(np.float64)
     return M, dv, ev
+
+
+def row_exponents_r8(a):
+    """KV_PREC_I8R4's rule (i8_row_exponent_r8): as row_exponents, plus one when the max's top 7 fraction bits
+    are >= 126 (max >= 127/128 2^e), so every rint(a 2^(31 - e)) stays below 127/128 2^31."""
+    hi = (a.view(np.uint64) >> np.uint64(32)).astype(np.uint32) & np.uint32(0x7FFFFFFF)
+    m = hi.max(axis=-1)
+    bump = ((m & np.uint32(0xFE000)) >= np.uint32(0xFC000)).astype(np.int64)
+    return np.where(m > 0, (m >> np.uint32(20)).astype(np.int64) - 1022 + bump, 0)
+
+
+def split_r8(a, e):
+    """a [..., K], e [...] -> the 4 radix-256 digits [4][..., K] int8, d_0 most significant: N = rint(a
+    2^(31 - e)), N = sum_i d_i 2^(8 (3 - i)) with every d_i in [-128, 127] (the bytes of N + 0x80808080, each
+    minus 128)."""
+    N = np.rint(np.ldexp(a, (31 - e[..., None]).astype(np.int32))).astype(np.int64)
+    u = (N + 0x80808080) & 0xFFFFFFFF
+    return np.stack([(((u >> (8 * (3 - i))) & 255) - 128).astype(np.int8) for i in range(4)])
+
+
+def gemm_r8(V, U):
+    """KV_PREC_I8R4's GEMM (wino88i_gemm_lag5_kernel<K, 2, 4, 8>): V [X][R][K], U [X][C][K] fp64 -> (M fp64,
+    V digits [4][X][R][K], V exponents [X][R]); the 13 pairs i + j <= 4 as 5 exact integer levels, combined
+    m = L4, m = m 2^-8 + L_l (each step one fp64 rounding, as the kernel's fma with an exact product), scaled
+    by 2^(ev + eu - 14)."""
+    ev, eu = row_exponents_r8(V), row_exponents_r8(U)
+    dv, du = split_r8(V, ev), split_r8(U, eu)
+    fv, fu = dv.astype(np.float64), du.astype(np.float64)
+    lev = []
+    for l in range(5):
+        acc = np.zeros((V.shape[0], V.shape[1], U.shape[1]))
+        for i in range(4):
+            if 0 <= l - i < 4:
+                acc += np.matmul(fv[i], np.swapaxes(fu[l - i], 1, 2))
+        lev.append(acc)
+    m = lev[4]
+    for l in range(3, -1, -1):
+        m = m * 0.00390625 + lev[l]
+    return np.ldexp(m, (ev[:, :, None] + eu[:, None, :] - 14).astype(np.int32)), dv, ev

@@ -140,6 +140,7 @@ GROUPS = {"pg_init_mm80": ("init", 80, 16), "pg_peaked_mm80": ("peaked", 80, 16)
 
 
 @pytest.mark.parametrize("precision,algo", [("fp32", "auto"), ("f16x3", "auto"), ("f64w", "auto"), ("i8x5", "auto"),
+                                            ("i8r4", "auto"),
                                             ("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "winograd88i8"),
                                             ("fp32", "winograd88i8v")])
 @pytest.mark.parametrize("group", list(GROUPS))
@@ -174,7 +175,7 @@ def test_engine_games_match_reference(golden_dir, group, precision, algo):
     # fp32 towers: every golden game identical (0 near-tie divergences measured on every run, the kernels are
     # deterministic and the fixtures fixed); the split precisions keep the near-tie allowance (a divergence
     # only where the reference's own decision margin is < MARGIN_TOL, see _compare)
-    assert len(ties) <= (0 if precision in ("fp32", "f64w", "i8x5") else max(1, n // 8))
+    assert len(ties) <= (0 if precision in ("fp32", "f64w", "i8x5", "i8r4") else max(1, n // 8))
 
 
 def test_sequential_self_play_api_matches_reference(golden_dir):

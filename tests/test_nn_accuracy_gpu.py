@@ -27,7 +27,7 @@ def _planes(n, seed=5):
 
 def _net(sd, algo):
     from knightvision_amd.model import ChessNet
-    m = ChessNet(precision=algo) if algo in ("f64w", "i8x5") else ChessNet(algo=algo)
+    m = ChessNet(precision=algo) if algo in ("f64w", "i8x5", "i8r4") else ChessNet(algo=algo)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
     return m.eval()
 
@@ -39,8 +39,8 @@ def _f64(sd, planes):
     return p.numpy(), v.numpy()
 
 
-def accuracy_table(sd, planes, algos=("direct", "winograd48", "winograd88", "winograd88i8", "winograd88i8v", "i8x5", "f64w",
-                                      "auto")):
+def accuracy_table(sd, planes, algos=("direct", "winograd48", "winograd88", "winograd88i8", "winograd88i8v", "i8r4", "i8x5",
+                                      "f64w", "auto")):
     """{name: (max |dlogit|, max |dvalue|) vs float64} for the reference's fp32
     forward ("ref32") and each HIP algorithm, plus each algorithm against ref32."""
     from oracle import torch_ref
@@ -80,13 +80,13 @@ def test_auto_within_tolerance_of_reference(variant):
     planes = _planes(N_BOARDS)
     tab, pmax, calib = accuracy_table(sd, planes)
     _report(variant, tab, pmax, N_BOARDS, calib)
-    for k in ("auto", "auto<=16", "f64w", "i8x5"):
+    for k in ("auto", "auto<=16", "f64w", "i8x5", "i8r4"):
         _, _, dpr, dvr = tab[k]
         assert dpr <= TOL_P and dvr <= TOL_V, (k, dpr, dvr)
     if variant in ("bn",):  # random-init magnitudes: the fp32 F(8x8) tower on int8 digits passes and is chosen
         assert calib["path_large"] == "winograd88_i8f32" and calib["path_small"] == "direct"
-    if variant == "stress":  # trained magnitudes: no fp32 Winograd tower passes; the int8-digit one does
-        assert calib["path_large"] == "winograd88_i8"
+    if variant == "stress":  # trained magnitudes: no fp32 Winograd tower passes; the fp64 domain on digits does
+        assert calib["path_large"] in ("winograd88_i8r", "winograd88_i8")
 
 
 def _bn_summary(sd):
@@ -121,7 +121,7 @@ def test_trained_weights_table():
     nb = int(os.environ.get("KV_TRAINED_BOARDS", str(N_BOARDS)))
     tab, pmax, calib = accuracy_table(sd, _planes(nb))
     _report(f"trained-{iters}x{games}", tab, pmax, nb, calib)
-    for k in ("auto", "auto<=16", "f64w", "i8x5"):
+    for k in ("auto", "auto<=16", "f64w", "i8x5", "i8r4"):
         _, _, dpr, dvr = tab[k]
         assert dpr <= TOL_P and dvr <= TOL_V, (k, dpr, dvr)
 
@@ -136,7 +136,7 @@ def test_calibration_choice_is_consistent(variant):
     sd = synthetic_state_dict(42, variant)
     c = _net(sd, "auto").kv_net(0).calibration()
     assert c["calibrated"] and c["n_boards"] == 64
-    order = ["winograd88_i8f32", "winograd88_i8f32v", "winograd88_i8", "winograd88_f64"]
+    order = ["winograd88_i8f32", "winograd88_i8f32v", "winograd88_i8r", "winograd88_i8", "winograd88_f64"]
     ok = {k: c["err_logit"][k] <= c["tol_logit"] and c["err_value"][k] <= c["tol_value"] for k in c["err_logit"]}
     first = next(k for k in order if k == "winograd88_f64" or ok.get(k))
     assert c["path_large"] == first, c

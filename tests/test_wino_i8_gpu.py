@@ -21,7 +21,7 @@ def _run(V, U, digits=D.DIGITS, seg=0):
     X, R, K = V.shape
     M = np.zeros((X, R, 512))
     dg = np.zeros((X, K // 32, digits, R, 32), dtype=np.int8)
-    ex = np.zeros((X, 2, R) if seg else (X, R), dtype=np.int32)
+    ex = np.zeros((X, 2, R) if seg == 1 else (X, R), dtype=np.int32)
     P = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
     _lib.check(L.kv_dev_wino88i(0, P(np.ascontiguousarray(V), C.c_double), R, P(np.ascontiguousarray(U), C.c_double),
                                 K, digits, seg, P(M, C.c_double), P(dg, C.c_int8), P(ex, C.c_int32)), "kv_dev_wino88i")
@@ -47,6 +47,30 @@ def test_i8_gemm_bit_exact(K, rows, digits):
     if digits == 4:  # row lines
         want = want.transpose(0, 1, 3, 2, 4)
     assert np.array_equal(dg.reshape(want.shape), want)
+    assert np.array_equal(M.view(np.uint64), Mr.view(np.uint64)), float(np.abs(M - Mr).max())
+
+
+@pytest.mark.parametrize("K,rows", [(256, 128), (512, 128), (512, 256)])
+def test_i8r_gemm_bit_exact(K, rows):
+    """KV_PREC_I8R4: the radix-256 slice kernel (4 balanced byte digits of rint(a 2^(31 - e)), the exponent
+    bumped at 127/128 of a power of two) and the 13-pair lag GEMM, bit for bit against tests/_i8_digits
+    (split_r8, gemm_r8): digits, exponents, fp64 M. Rows at the exponent rule's edges: a max just under
+    127/128 2^3 (no bump), exactly 127/128 2^3 (bump), an all-zero row, subnormals, +-2^-40."""
+    rng = np.random.default_rng(K + rows + 3)
+    V = rng.standard_normal((100, rows, K)) * np.exp2(rng.integers(-20, 20, size=(100, rows, 1)))
+    V[0, 0] = 0.0
+    V[1, 1] = np.nextafter(8.0 * 127 / 128, 0.0) * np.where(rng.random(K) < 0.5, -1.0, 1.0)
+    V[1, 2] = 8.0 * 127 / 128
+    V[1, 3] = -8.0 * 255 / 256
+    V[2, 2, ::3] = 1e-310
+    V[3, 3] = np.where(rng.random(K) < 0.5, -1.0, 1.0) * np.exp2(-40.0)
+    U = rng.standard_normal((100, 512, K)) * 0.05
+    U[5, 7] = 0.0
+    M, dg, ex = _run(V, U, 4, seg=2)
+    Mr, dv, evr = D.gemm_r8(V, U)
+    assert np.array_equal(ex, evr.astype(np.int32))
+    assert ex[1, 1] == 3 and ex[1, 2] == 4 and ex[1, 3] == 4
+    assert np.array_equal(dg.reshape(100, K // 32, 4, rows, 32), D.pack(dv))
     assert np.array_equal(M.view(np.uint64), Mr.view(np.uint64)), float(np.abs(M - Mr).max())
 
 
@@ -173,14 +197,32 @@ def _error_bound(V, U, digits, M):
     return b + np.abs(M) * (2.0 ** -24 if digits == 4 else 2.0 ** -53)
 
 
-@pytest.mark.parametrize("digits", [4, 5])
+def _error_bound_r8(V, U, M):
+    """_error_bound for KV_PREC_I8R4: a 2^-e = 2^-7 sum_i d_i 2^-8i + rho, |rho| <= 2^-32 (half a unit of the
+    31-bit block), the 13 pairs i + j <= 4 of the 4 radix-256 digits kept, the combine's fp64 roundings."""
+    K = V.shape[-1]
+    ev, eu = D.row_exponents_r8(V), D.row_exponents_r8(U)
+    dv, du = np.abs(D.split_r8(V, ev).astype(np.float64)), np.abs(D.split_r8(U, eu).astype(np.float64))
+    rho = 2.0 ** -32
+    an = np.abs(np.ldexp(V, (-ev[..., None]).astype(np.int32))).sum(-1)
+    bn = np.abs(np.ldexp(U, (-eu[..., None]).astype(np.int32))).sum(-1)
+    b = rho * (an[:, :, None] + bn[:, None, :]) + K * rho * rho
+    for i in range(4):
+        for j in range(4):
+            if i + j > 4:
+                b = b + np.matmul(dv[i], np.swapaxes(du[j], 1, 2)) * 2.0 ** (-14 - 8 * (i + j))
+    b = np.ldexp(b, (ev[:, :, None] + eu[:, None, :]).astype(np.int32))
+    return b + np.abs(M) * 2.0 ** -51
+
+
+@pytest.mark.parametrize("digits", [4, 5, "r8"])
 def test_i8_gemm_within_derived_bound_of_fp64_product(digits):
     """M of the int8-digit GEMM against an fp64 matmul of the UNSPLIT operands, on adversarial rows:
     channels spread over 2^-30 .. 1 of their row's max (so most values keep far fewer than the block's 28 /
     35 bits), all-equal rows, rows with one large channel, and sign-alternating rows. Every element must be
     within the bound derived from the arithmetic (_error_bound): per-row block fixed point of 7 x digits
     bits, digit pairs i + j < digits, exact int32 levels, one rounding."""
-    rng = np.random.default_rng(40 + digits)
+    rng = np.random.default_rng(40 + (6 if digits == "r8" else digits))
     X, R, K = 100, 128, 512
     V = np.where(rng.random((X, R, K)) < 0.5, -1.0, 1.0) * np.exp2(-30.0 * rng.random((X, R, K)))
     V *= np.exp2(rng.integers(-12, 12, size=(X, R, 1)))
@@ -192,9 +234,9 @@ def test_i8_gemm_within_derived_bound_of_fp64_product(digits):
     U[:, 3] = -0.3                        # an all-equal weight row
     if digits == 4:
         V, U = V.astype(np.float32).astype(np.float64), U.astype(np.float32).astype(np.float64)
-    M, _, _ = _run(V, U, digits)
+    M, _, _ = _run(V, U, 4, seg=2) if digits == "r8" else _run(V, U, digits)
     M64 = np.matmul(V, np.swapaxes(U, 1, 2))
-    bound = _error_bound(V, U, digits, M)
+    bound = _error_bound_r8(V, U, M) if digits == "r8" else _error_bound(V, U, digits, M)
     err = np.abs(M - M64)
     ratio = err / np.maximum(bound, 1e-300)
     print(f"digits {digits}: max |M - VU^T| / bound = {ratio.max():.3f}, max |err| / |M| (|M| > 0) = "

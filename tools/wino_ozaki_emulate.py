@@ -54,6 +54,38 @@ def split(a, e, s):
     return out
 
 
+def split8(a, e, s):
+    """radix-256 digits: N = rint(a 2^(31 - e)) (|a| 2^-e < 0.9921875 by the exponent rule), split into s signed
+    bytes by the sign-extended low byte of what remains (d_{s-1} first), so N = sum_i d_i 2^(8 (s - 1 - i)) with
+    every d_i in [-128, 127]; bits below 2^(e - 8 s + 1) are rounded away (s = 4: 31-bit block fixed point)."""
+    N = np.rint(a * np.exp2(8 * s - 1 - e)).astype(np.int64)
+    out = []
+    for i in range(s):
+        d = ((N + 128) & 255) - 128
+        out.append(d.astype(np.float64))
+        N = (N - d) >> 8
+    assert np.abs(N).max() == 0 if N.size else True
+    return out[::-1]
+
+
+def exps8(a):
+    m = np.abs(a).max(axis=-1, keepdims=True)
+    m = np.maximum(m, 1e-300)
+    fr, ex = np.frexp(m)  # m = fr 2^ex, fr in [0.5, 1)
+    return ex + (fr >= 0.9921875)
+
+
+def ozaki_gemm8(V, U, s, pairs):
+    ev, eu = exps8(V), exps8(U)
+    dv, du = split8(V, ev, s), split8(U, eu, s)
+    M = np.zeros((V.shape[0], V.shape[1], U.shape[1]))
+    for i in range(s):
+        for j in range(s):
+            if (i, j) in pairs:
+                M += np.einsum("bxk,xok->bxo", dv[i], du[j]) * 2.0 ** (-8 * (i + j))
+    return M * np.exp2(ev - 7) * np.exp2(eu[..., 0] - 7)[None]  # a = 2^(e - 7) sum_i d_i 2^(-8 i)
+
+
 def exps(a, mode, gain=None, ymax=None):
     if mode == "row":
         m = np.abs(a).max(axis=-1, keepdims=True)
@@ -67,6 +99,11 @@ def ozaki_gemm(V, U, s, mode, gain, ymax):
     """V [B,100,K], U [100,Cout,K] -> M [B,100,Cout]"""
     if mode == "f64":
         return np.einsum("bxk,xok->bxo", V, U)
+    if mode.startswith("r8"):  # r8:4 the 10 pairs i + j <= 3 of radix-256 digits; r8p:4 also (1,3),(2,2),(3,1)
+        pairs = {(i, j) for i in range(s) for j in range(s) if i + j <= s - 1}
+        if mode == "r8p":
+            pairs |= {(i, j) for i in range(s) for j in range(s) if i + j == s and 0 < i < s}
+        return ozaki_gemm8(V, U, s, pairs)
     if mode.startswith("group"):
         B, X, K = V.shape
         gs = int(mode[5:])
@@ -75,6 +112,12 @@ def ozaki_gemm(V, U, s, mode, gain, ymax):
             sl = slice(gs * g, gs * (g + 1))
             M += ozaki_gemm(V[..., sl], U[..., sl], s, "row", gain, ymax)
         return M
+    # "rowNN" variants of 5 digits: row12 drops the interior top-level pairs (1,3), (2,2), (3,1); row11v keeps only
+    # (4,0) (V's 5th digit) of them, row11u only (0,4) (U's)
+    drop = {"row12": {(1, 3), (2, 2), (3, 1)}, "row11v": {(0, 4), (1, 3), (2, 2), (3, 1)},
+            "row11u": {(4, 0), (1, 3), (2, 2), (3, 1)}}.get(mode, set())
+    if mode in ("row12", "row11v", "row11u"):
+        mode = "row"
     ev = exps(V, mode, gain, ymax)
     eu = exps(U, "row")
     dv, du = split(V, ev, s), split(U, eu, s)
@@ -82,6 +125,8 @@ def ozaki_gemm(V, U, s, mode, gain, ymax):
     for lev in range(s):
         acc = np.zeros_like(M)
         for i in range(lev + 1):
+            if (i, lev - i) in drop:
+                continue
             acc += np.einsum("bxk,xok->bxo", dv[i], du[lev - i])  # exact: |acc| < 2^53
         M += acc * 2.0 ** (-7 * (lev + 2))
     return M * np.exp2(ev + HEADROOM) * np.exp2(eu[..., 0] + HEADROOM)[None]
