@@ -331,12 +331,13 @@ def gemm_label(path: int, rows: int, split: int, cus: int = 256):
             "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 tiles, "
             "each stage's last 6 MFMAs per wave under the next stage's first LDS reads)")
     if path == 8:
-        return "wino88i_gemm_lag5_kernel<512,2,4,8>", (
-            " (residual-tower Winograd F(8x8,3x3) GEMMs in the fp64 domain from 4 radix-256 int8 digits per value: "
-            "the 13 pairs i + j <= 4, v_mfma_i32_32x32x32_i8 chains with exact int32 accumulation, 128x128 tiles, "
-            "each stage's last B digits under the next stage's first LDS reads)")
+        return "wino88i_gemm_lag5_kernel<512,3,4,8,true>", (
+            " (residual-tower Winograd F(8x8,3x3) GEMMs in the fp64 domain from 4 radix-256 int8 digits per value in "
+            "row lines: the 13 pairs i + j <= 4, v_mfma_i32_32x32x32_i8 chains with exact int32 accumulation, "
+            "128x128 tiles, each stage's last B digit under the next stage's first LDS reads; the operands' digits "
+            "come from the previous output kernel, wino88i64r_out_kernel)")
     if path == 5:
-        return "wino88i_gemm_lag5_kernel<512,3,5,7>", (
+        return "wino88i_gemm_lag5_kernel<512,3,5,7,false>", (
             " (residual-tower Winograd F(8x8,3x3) GEMMs in the fp64 domain from 5 int8 digits per value: 15 "
             "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, 128x128 tiles, each stage's last "
             "MFMAs under the next stage's first LDS reads)")

@@ -322,7 +322,7 @@ int kv_dev_py_random(int device, const uint64_t* seeds, int n, int count, double
  * [100][K/32][5][rows][32]; 4 digits: row lines [100][K/32][rows][4][32]) and
  * v_exp [100][rows] (either may be NULL) return V's digits and row exponents. seg 1 (4 digits, K 512):
  * V's exponents per 256-channel segment (v_exp [100][2][rows]), the fp32 tower's A/B form. seg 2 (4 digits):
- * KV_PREC_I8R4's 4 radix-256 digit planes [100][K/32][4][rows][32], its GEMM and fp64 M. */
+ * KV_PREC_I8R4's 4 radix-256 digits in row lines [100][K/32][rows][4][32], its GEMM and fp64 M. */
 int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, int digits, int seg, double* M,
                    int8_t* v_digits, int* v_exp);
 /* The fp32 tower's residual output kernel on int8 digits (KV_ALGO_WINOGRAD88_I8): M [100][rows][512] fp32
@@ -335,6 +335,12 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
  * wino88d_in_kernel's fp64 V and the slice kernel (bit-identical). */
 int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scale, const float* shift,
                          const float* resid, int fused, float* Y, int8_t* v_digits, int* v_exp);
+/* KV_PREC_I8R4's output step: M [100][rows][512] fp64 (rows a multiple of 128), folded BN scale / shift,
+ * resid or NULL -> Y [rows][64][512] and the next conv's V as 4 radix-256 digits in row lines
+ * [100][16][rows][4][32] with row exponents [100][rows]. fused 1: the product's wino88i64r_out_kernel; 0:
+ * wino88d_out_half_kernel's Y, wino88d_in_kernel's fp64 V, the radix-256 slice kernel (bit-identical). */
+int kv_dev_wino88r_out(int device, const double* M, int rows, const float* scale, const float* shift,
+                       const float* resid, int fused, float* Y, int8_t* v_digits, int* v_exp);
 /* Timing / A-B harness of the fp32 tower's int8-digit GEMM on seeded random digits (rows boards, K 256 or
  * 512): variant 0 the round-4 kernel, 1.. round-5 forms (persistent / per-tile, k per stage, ring depth);
  * avg_us = mean HIP-event time of `iters` launches; M_out [100][rows][512] (optional) for a bit-for-bit

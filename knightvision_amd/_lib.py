@@ -116,6 +116,8 @@ def _declare(L):
         "kv_dev_i8gemm_bench": ([i, i, i, i, i, P(C.c_float), P(C.c_float)], i),
         "kv_dev_wino88i32_out": ([i, P(C.c_float), i, P(C.c_float), P(C.c_float), P(C.c_float), i, P(C.c_float),
                                   P(C.c_int8), P(i)], i),
+        "kv_dev_wino88r_out": ([i, P(C.c_double), i, P(C.c_float), P(C.c_float), P(C.c_float), i, P(C.c_float),
+                                P(C.c_int8), P(i)], i),
         "kv_pgn_extract": ([C.c_char_p, sz, P(PgnRecord), sz, P(sz), P(sz), P(i64)], i),
         "kv_fen_codes": ([C.c_char_p, sz, i, P(C.c_int8)], i),
         "kv_san_move_index": ([C.c_char_p, sz, C.c_char_p, sz, i, P(C.c_int32)], i),
@@ -152,7 +154,7 @@ EXPORTED = ["kv_last_error", "kv_version", "kv_net_packed_size", "kv_net_create"
             "kv_create",
             "kv_load_weights", "kv_run", "kv_set_max_moves", "kv_records", "kv_games", "kv_stats_get", "kv_root_visits", "kv_root_visits_device", "kv_records_device", "kv_sync", "kv_reset_records", "kv_destroy",
             "kv_dev_valid_moves", "kv_dev_make_move", "kv_dev_attacks", "kv_dev_dirichlet", "kv_dev_py_random", "kv_host_libm",
-            "kv_dev_wino88i", "kv_dev_wino88i32_out", "kv_dev_i8gemm_bench",
+            "kv_dev_wino88i", "kv_dev_wino88i32_out", "kv_dev_wino88r_out", "kv_dev_i8gemm_bench",
             "kv_pgn_extract", "kv_fen_codes", "kv_san_move_index", "kv_chess_perft", "kv_chess_san", "kv_chess_fen",
             "kv_tr_conv3x3_f16", "kv_tr_conv3x3_add_f16", "kv_tr_conv_weights_f16", "kv_tr_wgrad_workspace", "kv_tr_conv3x3_wgrad_f16",
             "kv_tr_bn_workspace", "kv_tr_bn_stats_f16", "kv_tr_bn_apply_f16", "kv_tr_bn_backward_f16",

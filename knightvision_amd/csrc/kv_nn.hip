@@ -1103,12 +1103,12 @@ static int wino88d_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 // before each GEMM ----
 // (4 digits: the fp32 domain's row-line layout)
 // (NSEG 2: V's exponents per 256-channel segment, K 512 only)
-// (R8: KV_PATH_WINO88_I8R's 4 radix-256 digit planes of fp64 rows)
+// (R8: KV_PATH_WINO88_I8R's 4 radix-256 digits of fp64 rows, row lines)
 template <int K, int D = kv::kI8Digits, class T, int NSEG = 1, bool R8 = false>
 static int launch_wino88i_slice(const T* src, int n, int slab_rows, int nslab, int8_t* dst, int* ex,
                                 hipStream_t st) {
     const int waves = n * nslab;
-    hipLaunchKernelGGL((kv::wino88i_slice_kernel<K, T, D, D == kv::kI8DigitsF32 && !R8, NSEG, R8>),
+    hipLaunchKernelGGL((kv::wino88i_slice_kernel<K, T, D, D == kv::kI8DigitsF32, NSEG, R8>),
                        dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, src, n, slab_rows, nslab, dst, ex);
     KV_HIP(hipGetLastError());
     return KV_OK;
@@ -1156,17 +1156,17 @@ static int launch_wino88i32_gemm_mid(const int8_t* V8, const int* ev, const int8
 }
 
 // KV_PREC_I8X5's GEMM with the lagging half (wino88i_gemm_lag5_kernel); S = 4, RB = 8: KV_PATH_WINO88_I8R's
-template <int K, int LJ = 3, int S = kv::kI8Digits, int RB = 7>
+template <int K, int LJ = 3, int S = kv::kI8Digits, int RB = 7, bool RL = false>
 static int launch_wino88i_gemm_lag5(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, double* M,
                                     int rows, int stride, hipStream_t st) {
     using T = kv::Wino88iTile<S>;
     constexpr int bytes = 3 * T::STAGE;
-    KV_HIP(lds_opt_in((const void*)kv::wino88i_gemm_lag5_kernel<K, LJ, S, RB>, bytes));
+    KV_HIP(lds_opt_in((const void*)kv::wino88i_gemm_lag5_kernel<K, LJ, S, RB, RL>, bytes));
     const int nwg = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
     KV_REQUIRE(rows % T::WM == 0 && stride % T::WM == 0 && nwg % 8 == 0, KV_EINVAL,
                "wino gemm i8x5 (lag): rows %d / stride %d vs tile %d", rows, stride, T::WM);
-    hipLaunchKernelGGL((kv::wino88i_gemm_lag5_kernel<K, LJ, S, RB>), dim3(nwg), dim3(T::THREADS), bytes, st, V8, ev, U8,
-                       eu, M, rows, 512, stride);
+    hipLaunchKernelGGL((kv::wino88i_gemm_lag5_kernel<K, LJ, S, RB, RL>), dim3(nwg), dim3(T::THREADS), bytes, st, V8, ev,
+                       U8, eu, M, rows, 512, stride);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -1281,12 +1281,29 @@ static int i8x5_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const in
     return launch_wino88i_gemm_lag5<K>(V8, ev, U8, eu, M, rows, stride, st);
 }
 
-// KV_PATH_WINO88_I8R's GEMM: the lag kernel on 4 radix-256 digit planes, 13 pairs (B digits 2-3 lag)
-constexpr int kI8rLJ = 2;
+// KV_PATH_WINO88_I8R's GEMM: the lag kernel on 4 radix-256 digits in row lines, 13 pairs; the last B digit's
+// 2 MFMA pairs lag (KV_I8R_LJ 3: forward 10.07-10.13 vs 10.17-10.28 ms with digits 2-3 lagging, bit-identical,
+// profiles/r05_i8r4_fused_ab.log)
+#ifndef KV_I8R_LJ
+#define KV_I8R_LJ 3
+#endif
+constexpr int kI8rLJ = KV_I8R_LJ;
 template <int K>
 static int i8r_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, double* M, int rows, int stride,
                     hipStream_t st) {
-    return launch_wino88i_gemm_lag5<K, kI8rLJ, 4, 8>(V8, ev, U8, eu, M, rows, stride, st);
+    return launch_wino88i_gemm_lag5<K, kI8rLJ, 4, 8, true>(V8, ev, U8, eu, M, rows, stride, st);
+}
+
+// KV_PATH_WINO88_I8R's output step: wino88i64r_out_kernel (one 1,024-thread workgroup per board) writes Y (when
+// asked) and the next conv's radix-256 digits in row lines
+template <bool RESID, bool WRITE_Y>
+static int launch_wino88i64r_out(kv_net* net, int l, const double* M, int nb, int stride, const float* resid,
+                                 float* Y, hipStream_t st) {
+    const float* W = net->w;
+    hipLaunchKernelGGL((kv::wino88i64r_out_kernel<RESID, WRITE_Y>), dim3(1, nb), dim3(1024), 0, st, M, stride,
+                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, net->V8, net->ev8);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
 }
 
 // the fp64 domain on int8 digits; r8: KV_PATH_WINO88_I8R (4 radix-256 digits) instead of 5 radix-128 ones
@@ -1312,7 +1329,9 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, bool r8, hipStream_t s
             : launch_wino88i_slice<256>((const double*)net->V256, rows, stride, kv::W88_XI, net->V8, net->ev8, st);
     if (rc) return rc;
     if ((rc = gemm(1, true))) return rc;
-    if ((rc = launch_wino88i_out<false>(net, 1, M, nb, stride, nullptr, net->X, r8, st))) return rc;
+    rc = r8 ? launch_wino88i64r_out<false, true>(net, 1, M, nb, stride, nullptr, net->X, st)
+            : launch_wino88i_out<false>(net, 1, M, nb, stride, nullptr, net->X, false, st);
+    if (rc) return rc;
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
     for (int r = 0; r < 5; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
@@ -1320,10 +1339,13 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, bool r8, hipStream_t s
         if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
         if ((rc = gemm(l1, false))) return rc;
         if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
-        if ((rc = launch_wino88i_out<false>(net, l1, M, nb, stride, nullptr, net->T, r8, st))) return rc;
+        rc = r8 ? launch_wino88i64r_out<false, false>(net, l1, M, nb, stride, nullptr, nullptr, st)
+                : launch_wino88i_out<false>(net, l1, M, nb, stride, nullptr, net->T, false, st);
+        if (rc) return rc;
         if ((rc = gemm(l2, false))) return rc;
-        rc = r < 4 ? launch_wino88i_out<true>(net, l2, M, nb, stride, net->X, net->X, r8, st)
-                   : launch_wino88d_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
+        rc = r == 4 ? launch_wino88d_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st)
+             : r8   ? launch_wino88i64r_out<true, true>(net, l2, M, nb, stride, net->X, net->X, st)
+                    : launch_wino88i_out<true>(net, l2, M, nb, stride, net->X, net->X, false, st);
         if (rc) return rc;
     }
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
@@ -2311,6 +2333,58 @@ int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scal
     KV_HIP(hipMemcpy(Y, dy.p, ny * sizeof(float), hipMemcpyDeviceToHost));
     KV_HIP(hipMemcpy(v_digits, v8.p, nm * kv::kI8DigitsF32, hipMemcpyDeviceToHost));
     KV_HIP(hipMemcpy(v_exp, ev.p, (size_t)kv::W88_XI * rows * (seg ? 2 : 1) * sizeof(int), hipMemcpyDeviceToHost));
+    return KV_OK;
+}
+
+int kv_dev_wino88r_out(int device, const double* M, int rows, const float* scale, const float* shift,
+                       const float* resid, int fused, float* Y, int8_t* v_digits, int* v_exp) {
+    KV_REQUIRE(M && scale && shift && Y && v_digits && v_exp && rows > 0 && rows % 128 == 0, KV_EINVAL,
+               "kv_dev_wino88r_out: bad arguments (rows %d must be a multiple of 128)", rows);
+    KV_HIP(hipSetDevice(device));
+    const size_t nm = (size_t)kv::W88_XI * rows * 512, ny = (size_t)rows * 64 * 512;
+    kv::DevBuf<double> dm, dv;
+    kv::DevBuf<float> dsc, dsh, dy;
+    kv::DevBuf<int8_t> v8;
+    kv::DevBuf<int> ev;
+    KV_HIP(dm.alloc(nm));
+    KV_HIP(dsc.alloc(512));
+    KV_HIP(dsh.alloc(512));
+    KV_HIP(dy.alloc(ny));
+    KV_HIP(v8.alloc(nm * 4));
+    KV_HIP(ev.alloc((size_t)kv::W88_XI * rows));
+    KV_HIP(hipMemcpy(dm.p, M, nm * sizeof(double), hipMemcpyHostToDevice));
+    KV_HIP(hipMemcpy(dsc.p, scale, 512 * sizeof(float), hipMemcpyHostToDevice));
+    KV_HIP(hipMemcpy(dsh.p, shift, 512 * sizeof(float), hipMemcpyHostToDevice));
+    if (resid)
+        KV_HIP(hipMemcpy(dy.p, resid, ny * sizeof(float), hipMemcpyHostToDevice));
+    else
+        KV_HIP(hipMemset(dy.p, 0, ny * sizeof(float)));
+    const float* rs = resid ? dy.p : nullptr;  // Y doubles as the residual (in place, as the tower runs it)
+    if (fused) {
+        if (resid)
+            hipLaunchKernelGGL((kv::wino88i64r_out_kernel<true, true>), dim3(1, rows), dim3(1024), 0, 0, dm.p, rows,
+                               dsc.p, dsh.p, rs, dy.p, v8.p, ev.p);
+        else
+            hipLaunchKernelGGL((kv::wino88i64r_out_kernel<false, true>), dim3(1, rows), dim3(1024), 0, 0, dm.p, rows,
+                               dsc.p, dsh.p, rs, dy.p, v8.p, ev.p);
+        KV_HIP(hipGetLastError());
+    } else {  // wino88d_out_half_kernel's Y, wino88d_in_kernel's fp64 V, the radix-256 slice kernel
+        if (resid)
+            hipLaunchKernelGGL((kv::wino88d_out_half_kernel<true, true, false>), dim3(512 / 128, rows), dim3(256), 0, 0,
+                               dm.p, rows, dsc.p, dsh.p, rs, dy.p, nullptr);
+        else
+            hipLaunchKernelGGL((kv::wino88d_out_half_kernel<false, true, false>), dim3(512 / 128, rows), dim3(256), 0,
+                               0, dm.p, rows, dsc.p, dsh.p, rs, dy.p, nullptr);
+        KV_HIP(dv.alloc(nm));
+        hipLaunchKernelGGL(kv::wino88d_in_kernel<512>, dim3(512 / 256, rows), dim3(256), 0, 0, dy.p, rows, dv.p);
+        KV_HIP(hipGetLastError());
+        const int rc = launch_wino88i_slice<512, 4, double, 1, true>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
+        if (rc) return rc;
+    }
+    KV_HIP(hipDeviceSynchronize());
+    KV_HIP(hipMemcpy(Y, dy.p, ny * sizeof(float), hipMemcpyDeviceToHost));
+    KV_HIP(hipMemcpy(v_digits, v8.p, nm * 4, hipMemcpyDeviceToHost));
+    KV_HIP(hipMemcpy(v_exp, ev.p, (size_t)kv::W88_XI * rows * sizeof(int), hipMemcpyDeviceToHost));
     return KV_OK;
 }
 

@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict_
     static_assert(K == 256 || K == 512, "rows of 256 or 512 channels");
     static_assert(!RL || D == 4, "row lines hold 4 digits");
     static_assert(NSEG == 1 || (NSEG == 2 && K == 512), "segments of 256 channels");
-    static_assert(!R8 || (D == 4 && sizeof(T) == 8 && !RL && NSEG == 1), "radix 256: 4 digit planes of fp64 rows");
+    static_assert(!R8 || (D == 4 && sizeof(T) == 8 && NSEG == 1), "radix 256: 4 digits of fp64 rows");
     constexpr int CPL = K / 64;  // 4 or 8 channels per lane
     const int lane = threadIdx.x & 63;
     const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -885,7 +885,10 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
 // S = 4, RB = 8 (KV_PATH_WINO88_I8R): 4 radix-256 digit planes per operand (4 pieces per wave and stage), the
 // 13 pairs i + j <= 4 of 16 -- the same 5 levels, weighted 2^-8l -- combined in fp64 (the last two fma steps
 // may round: |level| <= 4 K 2^14 = 2^25, so the value has up to 57 significant bits; one fp64 rounding each).
-template <int K, int LJ = 3, int S = 5, int RB = 7>
+// RL (S = 4): the operands in row lines [xi][K/32][row][4][32] (the fp32 tower's layout and LDS image: a
+// stage of a tile is one contiguous 16 KiB block per operand), so the fused output kernel of one board writes
+// whole 128-byte lines.
+template <int K, int LJ = 3, int S = 5, int RB = 7, bool RL = false>
 __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __restrict__ V8,
                                                                 const int* __restrict__ ev,
                                                                 const int8_t* __restrict__ U8,
@@ -896,8 +899,8 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
     constexpr int NT = T::NT, WM = T::WM, WN = T::WN, GL = T::GL;
     constexpr int NK = K / 32;
     constexpr int NA = S < LEV - LJ ? S : LEV - LJ;  // A digits the lagging half uses
-    static_assert(GL == S && NK >= 3 && LJ >= 1 && LJ < S && (S == 5 || (S == 4 && RB == 8)),
-                  "S pieces per wave and stage");
+    static_assert(GL == S && NK >= 3 && LJ >= 1 && LJ < S && (S == 5 || (S == 4 && RB == 8)) && (!RL || S == 4),
+                  "S pieces per wave and stage; row lines hold 4 digits");
 
     extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8l5[];
     char* const L0 = (char*)lds_i8l5;
@@ -917,27 +920,46 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
     // bit 3 of the row)
     const int op = (wave * GL) / (4 * S);
     const size_t rstride = op ? (size_t)cout : (size_t)stride;
-    const int8_t* gbase = op ? U8 + (((size_t)xi * NK) * S * cout + (size_t)n_base) * 32
-                             : V8 + (((size_t)xi * NK) * S * stride + (size_t)r_base) * 32;
+    // (a tile's rows start at row * 32 in a plane, row * 128 in row lines; a stage is S * 32 B per row in both)
+    const int8_t* gbase = op ? U8 + ((size_t)xi * NK) * S * cout * 32 + (size_t)n_base * (RL ? 128 : 32)
+                             : V8 + ((size_t)xi * NK) * S * stride * 32 + (size_t)r_base * (RL ? 128 : 32);
     const size_t sstep = (size_t)S * rstride * 32;
     const int lane_off = (lane >> 1) * 32 + 16 * ((lane & 1) ^ ((lane >> 4) & 1));
+    // RL: piece q = wave * 4 + g is 8 row lines (1 KiB) of operand q / 16, rows 8 (q % 16) .. +7, copied as
+    // wino88i32_gemm_lag_kernel's (the 16-byte chunks swizzled by i8_rl_off on the global side)
+    const int rl_off0 = (lane >> 3) * 128 + 16 * ((lane & 7) ^ (lane >> 4));
+    const int rl_off1 = (lane >> 3) * 128 + 16 * ((lane & 7) ^ (lane >> 4) ^ 4);
     auto issue1 = [&](int g, int kt) {
-        const int q = wave * GL + g, d = (q % (4 * S)) / 4, rg = q % 4;
-        __builtin_amdgcn_global_load_lds(
-            (const void*)(gbase + kt * sstep + ((size_t)d * rstride + rg * 32) * 32 + lane_off),
-            (__attribute__((address_space(3))) void*)(L0 + (kt % NBUF) * T::STAGE + op * S * T::PLANE + d * T::PLANE +
-                                                      rg * 1024),
-            16, 0, 0);
+        const int q = wave * GL + g;
+        if constexpr (RL) {
+            const int rg8 = q % 16;
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(gbase + kt * sstep + (size_t)rg8 * 1024 + ((rg8 & 1) ? rl_off1 : rl_off0)),
+                (__attribute__((address_space(3))) void*)(L0 + (kt % NBUF) * T::STAGE + op * S * T::PLANE + rg8 * 1024),
+                16, 0, 0);
+        } else {
+            const int d = (q % (4 * S)) / 4, rg = q % 4;
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(gbase + kt * sstep + ((size_t)d * rstride + rg * 32) * 32 + lane_off),
+                (__attribute__((address_space(3))) void*)(L0 + (kt % NBUF) * T::STAGE + op * S * T::PLANE +
+                                                          d * T::PLANE + rg * 1024),
+                16, 0, 0);
+        }
     };
 
     const int lr = lane & 31, lh = lane >> 5;
     const int arow = wm * 32 + lr;
-    const int aoff = arow * 32 + i8_lds_half(arow, lh);
-    int boff[NT];
+    // LDS offsets of digit d's fragments: planes (d * PLANE + a fixed offset) or row lines (i8_rl_off per digit)
+    int aoffd[S], boffd[NT][S];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-        const int bcol = wn * NT * 32 + nt * 32 + lr;
-        boff[nt] = S * T::PLANE + bcol * 32 + i8_lds_half(bcol, lh);
+    for (int d = 0; d < S; ++d) {
+        aoffd[d] = RL ? i8_rl_off(arow, 2 * d + lh) : d * T::PLANE + arow * 32 + i8_lds_half(arow, lh);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int bcol = wn * NT * 32 + nt * 32 + lr;
+            boffd[nt][d] = S * T::PLANE + (RL ? i8_rl_off(bcol, 2 * d + lh) : d * T::PLANE + bcol * 32 +
+                                                                               i8_lds_half(bcol, lh));
+        }
     }
 
     i32x16_t acc[LEV][NT];
@@ -970,9 +992,9 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
         const char* buf = L0 + (kt % NBUF) * T::STAGE;
         i8x16_t a[S], b[NT];
 #pragma unroll
-        for (int i = 0; i < S; ++i) a[i] = *(const i8x16_t*)(buf + aoff + i * T::PLANE);
+        for (int i = 0; i < S; ++i) a[i] = *(const i8x16_t*)(buf + aoffd[i]);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) b[nt] = *(const i8x16_t*)(buf + boff[nt]);
+        for (int nt = 0; nt < NT; ++nt) b[nt] = *(const i8x16_t*)(buf + boffd[nt][0]);
         if (kt > 0) h2();  // the previous stage's lagging half, under the reads above
         if (kt + 2 < NK) {
             issue1(0, kt + 2);
@@ -982,7 +1004,7 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
         for (int j = 0; j < S; ++j) {
             if (j > 0) {
 #pragma unroll
-                for (int nt = 0; nt < NT; ++nt) b[nt] = *(const i8x16_t*)(buf + boff[nt] + j * T::PLANE);
+                for (int nt = 0; nt < NT; ++nt) b[nt] = *(const i8x16_t*)(buf + boffd[nt][j]);
             }
             if (j < LJ) {
 #pragma unroll
@@ -1553,11 +1575,15 @@ __device__ inline void wino88d_input_row_of_cols(float (&xc)[4][8], int aa, doub
 // true> give, bit for bit). 50 fp64 V values per lane do not fit beside the rest at 1,024 threads, so the
 // lane keeps its 32 fp32 activations across the exponent barrier instead and transforms them twice: once
 // for the row maxima (the high words of |V|), once for the digits (magic-number fp64 rint).
-template <bool RESID, bool WRITE_Y>
-__global__ __launch_bounds__(1024) void wino88i32v_out_kernel(const float* __restrict__ M, int rows,
-                                                              const float* __restrict__ scale,
-                                                              const float* __restrict__ shift, const float* resid,
-                                                              float* Y, int8_t* __restrict__ V8, int* __restrict__ ex) {
+// wino88i64r_out_kernel (KV_PATH_WINO88_I8R): the same from an fp64 M with the fp64 output transform
+// (wino88d_out_plane, as wino88d_out_half_kernel) and the 4 radix-256 digits (i8_digits_r8 under
+// i8_row_exponent_r8) -- what wino88d_out_half_kernel's Y + wino88d_in_kernel + the radix-256 slice kernel
+// give, bit for bit -- replacing the outmax + in kernel pair of the planes layout.
+template <bool RESID, bool WRITE_Y, class MT>
+__device__ inline void wino88v_out_body(const MT* __restrict__ M, int rows, const float* __restrict__ scale,
+                                        const float* __restrict__ shift, const float* resid, float* Y,
+                                        int8_t* __restrict__ V8, int* __restrict__ ex) {
+    constexpr bool R8 = sizeof(MT) == 8;
     constexpr int NK = 512 / 32, NW = 16;
     __shared__ __attribute__((aligned(16))) unsigned red[NW][2][5][16];
     __shared__ int exs[100];
@@ -1566,7 +1592,10 @@ __global__ __launch_bounds__(1024) void wino88i32v_out_kernel(const float* __res
     float xc[4][8];  // the half's columns 4h .. 4h+3, all 8 rows (after the half exchange)
     {
         float x2[4][8];
-        wino88_out_plane_half<RESID, WRITE_Y>(M, rows, b, c, h, scale[c], shift[c], resid, Y, x2);
+        if constexpr (R8)
+            wino88d_out_plane<RESID, WRITE_Y>(M, rows, b, c, h, (double)scale[c], (double)shift[c], resid, Y, x2);
+        else
+            wino88_out_plane_half<RESID, WRITE_Y>(M, rows, b, c, h, scale[c], shift[c], resid, Y, x2);
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
@@ -1599,7 +1628,7 @@ __global__ __launch_bounds__(1024) void wino88i32v_out_kernel(const float* __res
         unsigned m = 0;
 #pragma unroll
         for (int ww = 0; ww < NW; ++ww) m = red[ww][hh][aa][bb] > m ? red[ww][hh][aa][bb] : m;
-        const int e = i8_row_exponent(m);
+        const int e = R8 ? i8_row_exponent_r8(m) : i8_row_exponent(m);
         exs[xi] = e;
         ex[(size_t)xi * rows + b] = e;
     }
@@ -1615,13 +1644,33 @@ __global__ __launch_bounds__(1024) void wino88i32v_out_kernel(const float* __res
 #pragma unroll
         for (int bb = 0; bb < 10; ++bb) {
             const int xi = a * 10 + bb;
-            unsigned dq[4];
-            i8_digits_magic<4>(o[bb], exs[xi], dq);
-            const unsigned P = __builtin_amdgcn_perm(dq[1], dq[0], 0x0c0c0400u) |
-                               __builtin_amdgcn_perm(dq[3], dq[2], 0x0c0c0400u) << 16;
+            unsigned P;  // byte d = digit d (the most significant first)
+            if constexpr (R8) {
+                P = __builtin_bswap32(i8_digits_r8(o[bb], exs[xi]));
+            } else {
+                unsigned dq[4];
+                i8_digits_magic<4>(o[bb], exs[xi], dq);
+                P = __builtin_amdgcn_perm(dq[1], dq[0], 0x0c0c0400u) | __builtin_amdgcn_perm(dq[3], dq[2], 0x0c0c0400u) << 16;
+            }
             __builtin_nontemporal_store(i8_quad_transpose(P, lane), &dst[(off0 + (unsigned)xi * xstride) >> 2]);
         }
     }
+}
+
+template <bool RESID, bool WRITE_Y>
+__global__ __launch_bounds__(1024) void wino88i32v_out_kernel(const float* __restrict__ M, int rows,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift, const float* resid,
+                                                              float* Y, int8_t* __restrict__ V8, int* __restrict__ ex) {
+    wino88v_out_body<RESID, WRITE_Y>(M, rows, scale, shift, resid, Y, V8, ex);
+}
+
+template <bool RESID, bool WRITE_Y>
+__global__ __launch_bounds__(1024) void wino88i64r_out_kernel(const double* __restrict__ M, int rows,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift, const float* resid,
+                                                              float* Y, int8_t* __restrict__ V8, int* __restrict__ ex) {
+    wino88v_out_body<RESID, WRITE_Y>(M, rows, scale, shift, resid, Y, V8, ex);
 }
 
 }  // namespace kv

@@ -49,7 +49,7 @@ def test_gemm_traffic_summary_present():
     (2, 96, 100, "wino_gemm_kernel<512,1,2,1,2,16,100>"), (3, 2048, 0, "wino88d_gemm_kernel<512,2,4,4,2>"),
     (3, 64, 0, "wino88d_gemm_kernel<512,1,4,4,2>"), (3, 32, 0, "wino88d_gemm_kernel<512,1,4,2,2>"),
     (1, 4096, 0, "wino_gemm_kernel<512,4,2,1,2,32,60>"), (0, 2048, 0, "conv3x3_kernel<512,32>"),
-    (5, 2048, 0, "wino88i_gemm_lag5_kernel<512,3,5,7>"), (8, 2048, 0, "wino88i_gemm_lag5_kernel<512,2,4,8>"),
+    (5, 2048, 0, "wino88i_gemm_lag5_kernel<512,3,5,7,false>"), (8, 2048, 0, "wino88i_gemm_lag5_kernel<512,3,4,8,true>"),
     (6, 2048, 0, "wino88i32_gemm_lagt_kernel<512,5>"),
     (6, 256, 0, "wino88i32_gemm_lagt_kernel<512,4>"), (6, 128, 0, "wino88i32_gemm_lag_kernel<512,false>"),
     (6, 1024, 0, "wino88i32_gemm_lag_kernel<512,false>")])

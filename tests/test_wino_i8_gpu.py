@@ -70,8 +70,53 @@ def test_i8r_gemm_bit_exact(K, rows):
     Mr, dv, evr = D.gemm_r8(V, U)
     assert np.array_equal(ex, evr.astype(np.int32))
     assert ex[1, 1] == 3 and ex[1, 2] == 4 and ex[1, 3] == 4
-    assert np.array_equal(dg.reshape(100, K // 32, 4, rows, 32), D.pack(dv))
+    assert np.array_equal(dg.reshape(100, K // 32, rows, 4, 32), D.pack(dv).transpose(0, 1, 3, 2, 4))  # row lines
     assert np.array_equal(M.view(np.uint64), Mr.view(np.uint64)), float(np.abs(M - Mr).max())
+
+
+@pytest.mark.parametrize("rows,resid", [(128, False), (128, True), (256, True)])
+def test_i8r_out_kernel_writes_the_two_kernel_forms_digits(rows, resid):
+    """wino88i64r_out_kernel (KV_PREC_I8R4's output step: fp64 output transform + BN (+ residual) + ReLU, then
+    the next V as the fp64 input transform of that activation, cut to 4 radix-256 digits in row lines, one
+    workgroup per board) == wino88d_out_half_kernel's Y + wino88d_in_kernel's fp64 V + the radix-256 slice
+    kernel, bit for bit; and its digits decode to numpy's fp64 transform of Y within half a unit of the 31-bit
+    block (2^(e-32)) plus fp64 rounding, with the radix-256 exponent rule on numpy's row max."""
+    from knightvision_amd import _lib
+    from tests._wino_emul import input_transform_f64
+    L = _lib.lib()
+    rng = np.random.default_rng(rows + 17 * resid)
+    M = rng.standard_normal((100, rows, 512)) * 0.3
+    M[:, 5, :] = 0.0
+    scale = (0.5 + rng.random(512)).astype(np.float32)
+    scale[::7] *= np.float32(2.0 ** -12)
+    shift = -np.abs(rng.standard_normal(512) * 0.1).astype(np.float32)
+    R = (np.abs(rng.standard_normal((rows, 64, 512))) * 0.5).astype(np.float32) if resid else None
+    if resid:
+        R[5] = 0.0
+    P = lambda a, t: a.ctypes.data_as(C.POINTER(t))  # noqa: E731
+    out = []
+    for fused in (1, 0):
+        Y = np.zeros((rows, 64, 512), dtype=np.float32)
+        dg = np.zeros((100, 16, rows, 4, 32), dtype=np.int8)
+        ex = np.zeros((100, rows), dtype=np.int32)
+        rp = P(np.ascontiguousarray(R), C.c_float) if resid else None
+        _lib.check(L.kv_dev_wino88r_out(0, P(np.ascontiguousarray(M), C.c_double), rows, P(scale, C.c_float),
+                                        P(shift, C.c_float), rp, fused, P(Y, C.c_float), P(dg, C.c_int8),
+                                        P(ex, C.c_int32)), "kv_dev_wino88r_out")
+        out.append((Y, dg, ex))
+    (Yf, df, ef), (Ys, ds, es) = out
+    assert np.array_equal(Yf.view(np.uint32), Ys.view(np.uint32))
+    assert np.array_equal(ef, es) and np.array_equal(df, ds)
+    assert (ef[:, 5] == 0).all() and not df[:, :, 5].any()
+    V = input_transform_f64(Yf.astype(np.float64))
+    assert np.array_equal(ef, D.row_exponents_r8(V).astype(np.int32))
+    dec = np.zeros_like(V)
+    dgt = df.astype(np.float64).transpose(0, 2, 1, 4, 3)           # [100][rows][16][32][4]
+    for d in range(4):
+        dec += dgt[..., d].reshape(100, rows, 512) * 2.0 ** (-8 * d)
+    dec = np.ldexp(dec, (ef - 7)[:, :, None])
+    tol = np.ldexp(1.0, ef - 32)[:, :, None] + 1e-12 * np.abs(V).max(-1)[:, :, None]
+    assert (np.abs(dec - V) <= tol).all(), float((np.abs(dec - V) / tol).max())
 
 
 @pytest.mark.parametrize("rows", [128, 256])
