@@ -659,7 +659,7 @@ def main():
         out["calibration"] = dict(m["calibration"], note=(
             "the network's conv paths for these weights: fp32 + AUTO measures its candidates at load time against an "
             "fp64 forward on 64 seeded boards and keeps the fastest within max |dlogit| 4e-5 / |dvalue| 4e-6 "
-            "(F(8x8) fp32 with int8-digit GEMMs, the fp64 Winograd domain on int8 digits, else on fp64 MFMA); "
+            "(F(8x8) fp32 with int8-digit GEMMs, the same with fp64 input transforms, the fp64 Winograd domain on 4 radix-256 then 5 radix-128 int8 digits, else on fp64 MFMA); "
             "errors are max |x - fp64|"))
         out["conv_path"] = PATH_NAMES.get(path)
         out["conv_arithmetic"] = {
