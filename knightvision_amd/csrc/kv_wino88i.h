@@ -829,6 +829,12 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
             for (int i = 0; i < S; ++i) a[i] = *(const i8x16_t*)(buf + aoffr[i]);
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) b[0][nt] = *(const i8x16_t*)(buf + boffr[nt][0]);
+            // the stage's reads issue before the lagging MFMAs (hipcc otherwise hoists those MFMAs above the reads,
+            // so the reads start ~14 MFMA issues after the barrier): forward -2.3 % at 2,048 boards, -3.4 % at 256,
+            // bit-identical; with the same barrier after each B digit's reads below, -5 % / -6 %
+            // (profiles/r05_reads_first_ab.log; the 13-pair fp64-domain GEMM and the one-tile lag kernel came out
+            // 1-2 % slower with it, so only here)
+            __builtin_amdgcn_sched_barrier(0);
             if (kt > 0) h2();
             if (s + 2 < NS) {
                 issue1(0, s + 2);
@@ -840,6 +846,7 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt) b[jb + 1][nt] = *(const i8x16_t*)(buf + boffr[nt][jb + 1]);
                 }
+                __builtin_amdgcn_sched_barrier(0);  // likewise each next B digit's reads before this one's MFMAs
                 if (jb < LJ) {
 #pragma unroll
                     for (int i = 0; i + jb < S; ++i)
