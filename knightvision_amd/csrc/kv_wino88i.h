@@ -731,7 +731,10 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* _
 // profiles/r05_i8gemm_tpw_runtime_ab.log). Tile j of workgroup w is virtual
 // block w + j * gridDim in the XCD-aware order (the same XCD). At the first stage of a later tile a wave waits
 // for that stage's pieces with the previous tile's 32 M stores still allowed in flight. Same products, same bits.
-template <int K, int TPW, int LJ = 2>
+#ifndef KV_I8F32_LJ
+#define KV_I8F32_LJ 2
+#endif
+template <int K, int TPW, int LJ = KV_I8F32_LJ>
 __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* __restrict__ V8,
                                                                   const int* __restrict__ ev,
                                                                   const int8_t* __restrict__ U8,
