@@ -50,13 +50,13 @@ FP64_MFMA_PEAK_TFLOPS = 78.6          # AMD's MI355X FP64 matrix spec figure (th
                                       # measured here)
 PATH_NAMES = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3",
               5: "winograd88_i8", 6: "winograd88_i8f32", 7: "winograd88_i8f32v",
-              8: "winograd88_i8r"}  # KV_PATH_*
+              8: "winograd88_i8r", 9: "winograd88_i8f32r3"}  # KV_PATH_*
 BF16_MFMA_PEAK_TFLOPS = 2500.0        # dense bf16 MFMA
 I8_MFMA_PEAK_TOPS = 5000.0            # dense int8 MFMA: 2x the bf16 rate (cdna_hip_programming.md, MFMA rate per dtype);
                                       # v_mfma_i32_32x32x32_i8 back to back measured 4.1 POPS at the clock the chip
                                       # holds under it (profiles/r04_mfma_rate.log)
 I8_MFMA_MEASURED_TOPS = 4098.0
-I8_DIGIT_PRODUCTS = {5: 15, 6: 10, 7: 10, 8: 13}    # int8 GEMMs per Winograd GEMM: digit pairs i + j < 5 (KV_PREC_I8X5, fp64
+I8_DIGIT_PRODUCTS = {5: 15, 6: 10, 7: 10, 8: 13, 9: 6}    # int8 GEMMs per Winograd GEMM: digit pairs i + j < 5 (KV_PREC_I8X5, fp64
                                       # domain) / < 4 (KV_ALGO_WINOGRAD88_I8, fp32 domain)
 
 
@@ -69,7 +69,9 @@ def parse():
     ap.add_argument("--slots", type=int, default=2048)
     ap.add_argument("--sims", type=int, default=800)
     ap.add_argument("--precision", choices=["fp32", "f16x3", "f64w", "i8x5", "i8r4"], default="fp32")
-    ap.add_argument("--algo", choices=["auto", "direct", "winograd48", "winograd88", "winograd88i8"], default="auto",
+    ap.add_argument("--algo", choices=["auto", "direct", "winograd48", "winograd88", "winograd88i8", "winograd88i8v",
+                                       "winograd88i8r3"],
+                    default="auto",
                     help="conv algorithm of the fp32 tower (auto: the library's calibrated choice per weight load -- "
                          "Winograd F(8x8,3x3) fp32 for the random-init weights)")
     ap.add_argument("--compare-direct", type=int, default=0,
@@ -106,6 +108,9 @@ def parse():
                     help="MCTS edge pool per slot (0: KV_MAXM x (sims+1), which cannot overflow; an overflow "
                          "fails the run). Profiling runs under rocprofv3 --pmc use a smaller pool")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--clock-seconds", type=float, default=2.0,
+                    help="after the timed region: the headline GEMM back to back for this long, then one stamped "
+                         "launch of it -- the in-kernel clock the chip held (roofline.sclk_mhz); 0 to skip")
     ap.add_argument("--cpu-seconds", type=float, default=60.0,
                     help="duration of the MCTS CPU-baseline legs: 2/3 leaf-batched, 1/3 one leaf per call (the "
                          "reference-selection leg runs <= 10 s)")
@@ -299,59 +304,78 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def gemm_label(path: int, rows: int, split: int, cus: int = 256):
-    """(kernel name, description) of the dominant Winograd GEMM launch at `rows` rows per point, as
-    knightvision_amd/csrc/kv_nn.hip launches it; `split` = the engine's kv_stats.dom_split (F(8x8) fp32:
-    points in the 128x128-tile launch); `cus` = the device's CUs (the fp32 tower's GEMM runs 4 tiles per
-    workgroup when its grid is 3-4 rounds of single tiles: kv_nn.hip i8f32_four_tiles)."""
-    if path == 2:
-        if rows % 128 == 0:
-            name = "wino_gemm_kernel<512,4,2,1,2,32,100>"
-        elif rows % 64 == 0:
-            name = "wino_gemm_kernel<512,2,2,1,2,16,100>"
-        else:
-            name = "wino_gemm_kernel<512,1,2,1,2,32,100>" if rows == 32 else "wino_gemm_kernel<512,1,2,1,2,16,100>"
-        desc = " (residual-tower Winograd F(8x8,3x3) GEMMs, 100 points)"
-        if 0 < split < 100:
-            desc = (f" points 0-{split - 1} + wino_gemm_kernel<512,2,2,1,2,16,100> points {split}-99 (residual-tower "
-                    "Winograd F(8x8,3x3) GEMM layer: two launches, both inside the timed events)")
-        return name, desc
-    if path in (6, 7):  # 7: the same GEMM (fp64 input transforms)
-        tiles = 100 * (rows // 128) * 4
-        single = -(-tiles // cus)
-        for t in (5, 4):  # kv_nn.hip i8f32_tiles_per_wg
-            if tiles % (8 * t) == 0 and -(-(tiles // t) // cus) * t <= single:
-                return f"wino88i32_gemm_lagt_kernel<512,{t}>", (
-                    " (residual-tower Winograd F(8x8,3x3) GEMMs of the fp32 tower from 4 int8 digits per value: 10 "
-                    "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 "
-                    f"tiles, {t} per workgroup with the copy ring across them, each stage's last 6 MFMAs per wave "
-                    "under the next stage's first LDS reads)")
-        return "wino88i32_gemm_lag_kernel<512,false>", (
+def gemm_label(path: int, kernel: str):
+    """(kernel name, description) of the dominant Winograd GEMM launch: `kernel` is the name the library
+    reports for the launch it made (kv_stats.dom_kernel, set by the launcher in knightvision_amd/csrc/kv_nn.hip
+    that chose it), so a form switch (KV_I8F32_TPW=1, another CU count) relabels the line by itself; the
+    description is looked up from the name's kernel family."""
+    name = kernel or "?"
+    fam = name.split("<")[0]
+    targs = name[len(fam) + 1:-1].split(",") if "<" in name else []
+    if fam == "wino_gemm_kernel" and name.endswith(",100>") or "+" in name:
+        first, _, second = name.partition("+")
+        if second:
+            return first, (f" + {second} (residual-tower Winograd F(8x8,3x3) GEMM layer: the first points as "
+                           "128x128 tiles, the rest as 64x128 tiles in a second launch, both inside the timed events)")
+        return name, " (residual-tower Winograd F(8x8,3x3) GEMMs, 100 points)"
+    if fam == "wino88i32_gemm_lagt_kernel" and len(targs) > 2 and targs[2] == "3":
+        tpw = int(targs[1])
+        return name, (
+            " (residual-tower Winograd F(8x8,3x3) GEMMs of the fp32 tower from 3 radix-256 int8 digits per value: the "
+            "6 pairs i + j <= 2, v_mfma_i32_32x32x32_i8 chains, exact int32 accumulation, one rounding to fp32, "
+            "128x128 tiles, " + (f"{tpw} per workgroup with the copy ring across them, " if tpw > 1 else "") +
+            "each stage's last B digits per wave under the next stage's first LDS reads)")
+    if fam in ("wino88i32_gemm_lagt_kernel", "wino88i32_gemm_lag_kernel"):
+        tpw = int(targs[1]) if fam == "wino88i32_gemm_lagt_kernel" else 1
+        return name, (
             " (residual-tower Winograd F(8x8,3x3) GEMMs of the fp32 tower from 4 int8 digits per value: 10 "
-            "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 tiles, "
+            "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, one rounding to fp32, 128x128 "
+            "tiles, " + (f"{tpw} per workgroup with the copy ring across them, " if tpw > 1 else "") +
             "each stage's last 6 MFMAs per wave under the next stage's first LDS reads)")
-    if path == 8:
-        return "wino88i_gemm_lag5_kernel<512,3,4,8,true>", (
+    if fam == "wino88i_gemm_lag5_kernel" and targs[-1] == "true":
+        return name, (
             " (residual-tower Winograd F(8x8,3x3) GEMMs in the fp64 domain from 4 radix-256 int8 digits per value in "
             "row lines: the 13 pairs i + j <= 4, v_mfma_i32_32x32x32_i8 chains with exact int32 accumulation, "
             "128x128 tiles, each stage's last B digit under the next stage's first LDS reads; the operands' digits "
             "come from the previous output kernel, wino88i64r_out_kernel)")
-    if path == 5:
-        return "wino88i_gemm_lag5_kernel<512,3,5,7,false>", (
-            " (residual-tower Winograd F(8x8,3x3) GEMMs in the fp64 domain from 5 int8 digits per value: 15 "
-            "v_mfma_i32_32x32x32_i8 chains per point, exact int32 accumulation, 128x128 tiles, each stage's last "
-            "MFMAs under the next stage's first LDS reads)")
-    if path == 3:
-        name = ("wino88d_gemm_kernel<512,2,4,4,2>" if rows % 128 == 0 else
-                "wino88d_gemm_kernel<512,1,4,4,2>" if rows % 64 == 0 else "wino88d_gemm_kernel<512,1,4,2,2>")
+    if fam in ("wino88i_gemm_lag5_kernel", "wino88i_gemm_kernel"):
+        return name, (
+            " (residual-tower Winograd F(8x8,3x3) GEMMs from int8 digits per value, v_mfma_i32_32x32x32_i8 chains, "
+            "exact int32 accumulation, 128x128 tiles)")
+    if fam == "wino88i32_gemm_kernel":
+        return name, " (residual-tower Winograd F(8x8,3x3) GEMMs of the fp32 tower from 4 int8 digits, A/B form)"
+    if fam == "wino88d_gemm_kernel":
         return name, " (residual-tower Winograd F(8x8,3x3) GEMMs in fp64, 100 points, v_mfma_f64_16x16x4_f64)"
-    if path in (1, 4):
-        if path == 4:
-            return ("wino_gemm_h3_kernel<512,2,60,1>" if rows % 128 == 0 else "wino_gemm_h3_kernel<512,1,60,1>",
-                    " (residual-tower Winograd F(4x8,3x3) GEMMs, f16x3 split)")
-        return ("wino_gemm_kernel<512,4,2,1,2,32,60>" if rows % 128 == 0 else "wino_gemm_kernel<512,2,2,1,2,16,60>",
-                " (residual-tower Winograd F(4x8,3x3) GEMMs, 60 points)")
-    return "conv3x3_kernel<512,32>", " (residual-tower 3x3 conv, implicit GEMM)"
+    if fam == "wino_gemm_h3_kernel":
+        return name, " (residual-tower Winograd F(4x8,3x3) GEMMs, f16x3 split)"
+    if fam == "wino_gemm_kernel":
+        return name, " (residual-tower Winograd F(4x8,3x3) GEMMs, 60 points)"
+    if fam == "conv3x3_kernel":
+        return name, " (residual-tower 3x3 conv, implicit GEMM)"
+    return name, ""
+
+
+def baseline_config_tag(mcts: bool, G: int, sims: int, world: int) -> str:
+    """Which BASELINE.json config the run is: C3 (2,048 games x 800 sims on one GPU), C4 (the same per GPU on 8
+    GPUs, RCCL gather), C2 (256 x 400 on one GPU); other shapes name none."""
+    if mcts and G == 2048 and sims == 800:
+        return " (BASELINE configs[2], C3)" if world == 1 else (
+            " (BASELINE configs[3], C4)" if world == 8 else f" (BASELINE configs[3]'s per-GPU shape, C4 at {world} GPUs)")
+    if mcts and G == 256 and sims == 400 and world == 1:
+        return " (BASELINE configs[1], C2)"
+    return ""
+
+
+def dom_units(path: int, dom_flop: float, G: int):
+    """(algorithmic FLOP per board of the dominant launch, boards per launch, rows per Winograd point) for the
+    conv path the library ran: every F(8x8) path (2, 3, 5-8) has 100 points of [rows x 512] x [512 x 512],
+    F(4x8) (1, 4) 60 points at 2 rows per board, the direct conv 10 launches' worth per board."""
+    f88 = path in (2, 3, 5, 6, 7, 8, 9)
+    per_board = (FLOP_WINO88_GEMM_PER_BOARD if f88 else FLOP_WINO48_GEMM_PER_BOARD if path in (1, 4)
+                 else FLOP_RES_CONV_PER_BOARD)
+    bpl = min(G, int(round(dom_flop / per_board))) if dom_flop else G
+    rows = int(round(dom_flop / (2 * 512 * 512 * (100 if f88 else 60)))) if (path and dom_flop) else bpl
+    return per_board, bpl, rows
 
 
 def _pmc_traffic(kname: str, bpl: int):
@@ -367,6 +391,21 @@ def _pmc_traffic(kname: str, bpl: int):
                 pj.get("kernel", "").replace(" ", "") == kname and "hbm_bytes_per_launch" in pj):
             return pj["hbm_bytes_per_launch"], f
     return None, None
+
+
+def gemm_clock(device: int, rows: int, seconds: float):
+    """The clock this GPU holds under the headline GEMM (kv_dev_gemm_clock: the product's fp32-tower GEMM back to
+    back for `seconds` on seeded digits, then one launch of its stamped build; MI355X_MICROARCH.md DVFS item 6),
+    so a box-to-box spread of the line can be attributed."""
+    import ctypes as C
+    from knightvision_amd import _lib
+    out = (C.c_double * 4)()
+    _lib.check(_lib.lib().kv_dev_gemm_clock(device, rows, seconds, out), "kv_dev_gemm_clock")
+    return {"sclk_mhz": out[0], "gemm_us_back_to_back": out[1], "launches": int(out[2]),
+            "tiles_per_workgroup": int(out[3]),
+            "method": f"median over workgroups of s_memtime delta / s_memrealtime delta x 100 MHz in a stamped build "
+                      f"of the headline GEMM, launched right after {int(out[2])} back-to-back launches "
+                      f"({seconds:.1f} s) on seeded random digits at {rows} boards; after the timed region"}
 
 
 def _tree_pmc(G: int):
@@ -463,6 +502,7 @@ def main():
                    nn_rows_evaluated=float(d["nn_rows_lazy"]) if eval_mode == "lazy" else nn_rows,
                    conv_ms=d["res_conv_ms"] / max(d["res_conv_launches"], 1), dom_flop=s1["dom_flop"],
                    dom_algo=s1["dom_algo"], dom_path=s1["dom_path"], dom_split=s1["dom_split"],
+                   dom_kernel=s1["dom_kernel"],
                    tree_overflows=s1["tree_overflows"], steps=steps, warmup=warmup)
         if tag in ("main", "trained"):
             out["calibration"] = eng.calibration()
@@ -538,20 +578,21 @@ def main():
     # Winograd GEMM layer per forward (fp32 F(8x8) by default; [boards x 512] x [512 x 512] per point) or, for
     # the direct algorithm, the residual convs
     path = m["dom_path"]  # KV_PATH_*: 0 direct, 1 F(4x8), 2 F(8x8) fp32 (the fp32 default), 3 F(8x8) fp64, 4 f16x3
-    per_board = {1: FLOP_WINO48_GEMM_PER_BOARD, 2: FLOP_WINO88_GEMM_PER_BOARD, 3: FLOP_WINO88_GEMM_PER_BOARD,
-                 4: FLOP_WINO48_GEMM_PER_BOARD, 5: FLOP_WINO88_GEMM_PER_BOARD,
-                 6: FLOP_WINO88_GEMM_PER_BOARD}.get(path, FLOP_RES_CONV_PER_BOARD)
-    bpl = min(G, int(round(m["dom_flop"] / per_board))) if m["dom_flop"] else G
+    per_board, bpl, rows = dom_units(path, m["dom_flop"], G)
     flop_alg = per_board * bpl
     achieved = flop_alg / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
-    rows = int(round(m["dom_flop"] / (2 * 512 * 512 * (100 if path in (2, 3, 5, 6) else 60)))) if path else bpl
-    kname, kdesc = gemm_label(path, rows, m["dom_split"], torch.cuda.get_device_properties(0).multi_processor_count)
+    kname, kdesc = gemm_label(path, m["dom_kernel"])
     peak = FP64_MFMA_PEAK_TFLOPS if path == 3 else FP32_MFMA_PEAK_TFLOPS
     if path in I8_DIGIT_PRODUCTS:  # int8 operations of the digit products against the int8 peak
         achieved = achieved * I8_DIGIT_PRODUCTS[path] if achieved else None
         flop_alg *= I8_DIGIT_PRODUCTS[path]
         peak = I8_MFMA_PEAK_TOPS
     traffic, traffic_src = _pmc_traffic(kname, bpl)
+    clock = gemm_clock(local, bpl, args.clock_seconds) if (path in (6, 7, 9) and args.clock_seconds > 0) else None
+    clock_ranks = None
+    if world > 1 and clock is not None:
+        clock_ranks = [None] * world
+        dist.all_gather_object(clock_ranks, {"rank": rank, "sclk_mhz": clock["sclk_mhz"]})
 
     # HBM side of the search (north_star: tree kernels as a fraction of the HBM roofline), from the
     # rocprofv3 PMC + kernel-trace summary committed for this slot count (tools/tree_hbm.py)
@@ -585,7 +626,7 @@ def main():
             "dtype": args.precision,
             "data": (f"synthetic ({'random-init' if args.weights == 'init' else 'trained-magnitude (stress)'} weights "
                      "seed 42, self-play from the start position, per-game seeds)"),
-            "config": {"workload": wl + (" (BASELINE configs[2], C3)" if (mcts and G == 2048 and sims == 800) else ""),
+            "config": {"workload": wl + baseline_config_tag(mcts, G, sims, world),
                        "slots_per_gpu": G, "sims_per_move": sims, "nn_batch": G, "parallelism": f"games sharded x{world}",
                        "step": "one move of every slot (the whole search + the committed move)" if mcts else
                                "one ply of every slot"},
@@ -631,7 +672,9 @@ def main():
                              "kernel)" if path == 6 else
                              "; GEMM only: the operands' int8 digits come from the previous output kernel "
                              "(wino88i32v_out_kernel: the fp64 input transform of the fp32 activation, cut to 4 digits; "
-                             "conv2's from a slice kernel)" if path == 7 else ""),
+                             "conv2's from a slice kernel)" if path == 7 else
+                             "; GEMM only: the operands' 3 radix-256 int8 digits come from the previous output kernel "
+                             "(wino88i32_out2_kernel<., ., true>; conv2's from a slice kernel)" if path == 9 else ""),
                          "measured_peak_note": (f"v_mfma_i32_32x32x32_i8 back to back: {I8_MFMA_MEASURED_TOPS:.0f} "
                                                 "TOPS at the clock held (profiles/r04_mfma_rate.log)"
                                                 if path in I8_DIGIT_PRODUCTS else None),
@@ -643,6 +686,8 @@ def main():
                          "traffic": traffic, "traffic_source": ("profiles/" + traffic_src) if traffic_src else None,
                          "avg_launch_ms": conv_ms, "boards_per_launch": bpl,
                          "flop_per_launch": flop_alg, "mfma_flop_per_launch_incl_padding": m["dom_flop"],
+                         "sclk_mhz": clock["sclk_mhz"] if clock else None, "clock": clock,
+                         "clock_ranks": clock_ranks,
                          "direct_conv_equiv_tflops": (FLOP_RES_CONV_PER_BOARD * bpl / (conv_ms * 1e-3) / 1e12
                                                       if conv_ms > 0 else None)},
         }
@@ -675,6 +720,10 @@ def main():
             8: "fp32 activations, fp64 Winograd domain, GEMMs on 4 radix-256 int8 digits per value (per-row 31-bit "
                "block fixed point, 13 of 16 digit pairs, exact int32 levels, fp64 combine)",
             7: "fp32 network with fp64 input transforms (V cut to 4 int8 digits from fp64); GEMMs as path 6",
+            9: "fp32 network (fp32 activations, fp32 Winograd transforms, U, V and M); each Winograd GEMM on 3 "
+               "radix-256 int8 digits per value: per-row 24-bit block fixed point (N = rint(a 2^(23-e)) as balanced "
+               "bytes), the 6 digit pairs i + j <= 2 of 9 as v_mfma_i32_32x32x32_i8 chains, exact int32 levels, "
+               "exact combine, one rounding to fp32 (calibration errors above)",
             3: "fp32 activations, fp64 Winograd domain on v_mfma_f64",
             0: "fp32 direct implicit-GEMM convs"}.get(path)
         if pg_info is not None:
@@ -698,7 +747,7 @@ def main():
                 "value": (trained["sims"] if mcts else trained["plies"]) / trained["dt"], "unit": unit,
                 "steps": trained["steps"], "warmup": trained["warmup"],
                 "ms_per_step": trained["dt"] * 1e3 / trained["steps"],
-                "dominant_kernel": gemm_label(tp, G, 0)[0], "res_gemm_avg_launch_ms": trained["conv_ms"],
+                "dominant_kernel": trained["dom_kernel"], "res_gemm_avg_launch_ms": trained["conv_ms"],
                 "res_gemm_fp64_equiv_tflops": t_ach if tp == 5 else None,
                 "res_gemm_i8_tops": (t_ach * I8_DIGIT_PRODUCTS[tp]) if (t_ach and tp in I8_DIGIT_PRODUCTS) else None,
                 "peak_i8_tops": I8_MFMA_PEAK_TOPS,
@@ -712,7 +761,7 @@ def main():
                 "note": "the fp64 Winograd domain on v_mfma_f64 (KV_PREC_F64W)",
                 "value": (f64w["sims"] if mcts else f64w["plies"]) / f64w["dt"], "unit": unit,
                 "steps": f64w["steps"], "warmup": f64w["warmup"], "ms_per_step": f64w["dt"] * 1e3 / f64w["steps"],
-                "dominant_kernel": gemm_label(3, G, 0)[0], "res_gemm_avg_launch_ms": f64w["conv_ms"],
+                "dominant_kernel": f64w["dom_kernel"], "res_gemm_avg_launch_ms": f64w["conv_ms"],
                 "res_gemm_tflops": f_ach, "peak": FP64_MFMA_PEAK_TFLOPS,
                 "res_gemm_frac_fp64": (f_ach / FP64_MFMA_PEAK_TFLOPS) if f_ach else None}
         if alt_algo is not None:
@@ -749,7 +798,7 @@ def main():
                 "steps": alt["steps"], "warmup": alt["warmup"],
                 "ms_per_step": alt["dt"] * 1e3 / alt["steps"], "plies_per_s": alt["plies"] / alt["dt"],
                 "nn_tflops_fp32_equiv": alt["nn_rows"] * FLOP_PER_EVAL / alt["dt"] / 1e12,
-                "dominant_kernel": gemm_label(alt["dom_path"], 2 * G, alt["dom_split"])[0],
+                "dominant_kernel": alt["dom_kernel"],
                 "dominant_avg_launch_ms": alt["conv_ms"], "dominant_tflops_fp32_equiv": a_ach,
                 "dominant_bf16_mfma_frac": (a_ach * a_prod / BF16_MFMA_PEAK_TFLOPS) if (a_ach and a_prod) else None}
         if refsel is not None:

@@ -48,7 +48,10 @@ size_t kv_net_packed_size(void);
 int kv_net_create(int device, kv_net** out);
 int kv_net_load(kv_net* net, const float* packed, size_t n_floats);
 /* planes_dev: [B][12][8][8] fp32 (encode_board layout, ai/ai.py:17-30);
- * policy_dev: [B][4096] logits; value_dev: [B] tanh value. */
+ * policy_dev: [B][4096] logits; value_dev: [B] tanh value. Any B >= 1: a batch of more than 16,384
+ * boards (the tower's 32-bit workspace offsets) runs as equal slices of at most 16,384, each in the same
+ * size class (> 16 boards) as the whole batch, so every output is the one a single pass would give. The same
+ * holds for the two board-code forwards below. */
 int kv_net_forward(kv_net* net, const float* planes_dev, int B, float* policy_dev, float* value_dev, void* stream);
 /* boards_dev: [B][64] int8 piece codes (0 empty, 1..6 wK wQ wR wB wN wp,
  * 7..12 bK bQ bR bB bN bp; square r*8+c, row 0 = rank 8). */
@@ -105,7 +108,8 @@ int kv_net_set_precision(kv_net* net, int precision);
  *                   within 4e-5 / 4e-6 of an fp64 forward on 64 calibration
  *                   boards (the initial position, 16 positions of reference
  *                   self-play, 47 seeded random ones): > 16 boards F(8x8) fp32
- *                   with int8-digit GEMMs (KV_ALGO_WINOGRAD88_I8), else the
+ *                   on 3 radix-256 int8 digits (KV_ALGO_WINOGRAD88_I8R3),
+ *                   else on 4 radix-128 ones (KV_ALGO_WINOGRAD88_I8), else the
  *                   same with fp64 input transforms (KV_ALGO_WINOGRAD88_I8V),
  *                   else the fp64 Winograd domain on 4 radix-256 int8
  *                   digits (KV_PREC_I8R4), else on 5 radix-128 ones
@@ -125,6 +129,12 @@ int kv_net_set_precision(kv_net* net, int precision);
  * KV_ALGO_WINOGRAD88_I8V the same tower with each conv's V the fp64 input
  *                   transform of its fp32 input, cut to 4 digits from fp64
  *                   (M, the output transform and the activations stay fp32)
+ * KV_ALGO_WINOGRAD88_I8R3 the fp32 tower of KV_ALGO_WINOGRAD88_I8 with each
+ *                   GEMM on 3 radix-256 int8 digits per value: per-row 24-bit
+ *                   block fixed point (N = rint(a 2^(23-e)) as balanced
+ *                   bytes), the 6 digit pairs i + j <= 2 of 9, exact int32
+ *                   levels, one rounding to fp32 -- 6 int8 GEMMs per point
+ *                   instead of 10 (AUTO's first candidate)
  * Value 2 (F(4x4)) was retired in round 4: KV_EINVAL. Setting the precision or
  * the algorithm of a loaded net re-prepares it (synchronous).
  * Results are batch-invariant inside a class (<= 16 boards, > 16 boards). */
@@ -134,6 +144,7 @@ int kv_net_set_precision(kv_net* net, int precision);
 #define KV_ALGO_WINOGRAD88 4
 #define KV_ALGO_WINOGRAD88_I8 5
 #define KV_ALGO_WINOGRAD88_I8V 6
+#define KV_ALGO_WINOGRAD88_I8R3 7
 int kv_net_set_algo(kv_net* net, int algo);
 /* conv paths (what a forward runs) */
 #define KV_PATH_DIRECT 0
@@ -145,7 +156,8 @@ int kv_net_set_algo(kv_net* net, int algo);
 #define KV_PATH_WINO88_I8F32 6
 #define KV_PATH_WINO88_I8F32V 7
 #define KV_PATH_WINO88_I8R 8
-#define KV_NPATH 9
+#define KV_PATH_WINO88_I8F32R3 9
+#define KV_NPATH 10
 typedef struct {
     int calibrated;      /* 1: the last load / setting ran the fp32 AUTO calibration */
     int path_large;      /* KV_PATH_* of batches > 16 boards (also without calibration) */
@@ -247,6 +259,8 @@ typedef struct {
     int64_t dom_path;       /* KV_PATH_* of those launches (F(8x8) fp32 or fp64 for KV_ALGO_WINOGRAD88) */
     int64_t dom_split;      /* fp32 F(8x8): points of the GEMM layer run as 128x128 tiles in its first launch
                                (the rest as 64x128 tiles in a second one; 100: one launch); 0 otherwise */
+    char dom_kernel[96];    /* the name of the kernel those launches ran, as the library chose it (template
+                               arguments included, e.g. "wino88i32_gemm_lagt_kernel<512,5>") */
 } kv_stats;
 
 typedef struct kv_engine kv_engine;
@@ -329,7 +343,8 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
  * (rows a multiple of 128), folded BN scale / shift [512], resid [rows][64][512] or NULL -> Y
  * [rows][64][512] (= ReLU(A^T M A * scale + shift (+ resid))) and the next conv's V as row-line digits
  * [100][16][rows][4][32] with row exponents [100][rows]. fused bit 0 set: the product's one-kernel form
- * (wino88i32_out_kernel), clear: wino88_out_kernel's fp32 V then the slice kernel (bit-identical); bit 1:
+ * (wino88i32_out2_kernel; with bit 3 also set the held-V form wino88i32_out_kernel), clear:
+ * wino88_out_kernel's fp32 V then the slice kernel (bit-identical); bit 1:
  * exponents per 256-channel segment ([100][2][rows]) instead of per row; bit 2 (KV_ALGO_WINOGRAD88_I8V's V,
  * per row): with bit 0 the one-kernel wino88i32v_out_kernel, without it wino88_out_kernel's Y, then
  * wino88d_in_kernel's fp64 V and the slice kernel (bit-identical). */
@@ -346,6 +361,12 @@ int kv_dev_wino88r_out(int device, const double* M, int rows, const float* scale
  * avg_us = mean HIP-event time of `iters` launches; M_out [100][rows][512] (optional) for a bit-for-bit
  * comparison of the variants. */
 int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, float* avg_us, float* M_out);
+/* The clock the chip holds under the headline GEMM (a diagnostic; MI355X_MICROARCH.md "DVFS give-back" item 6):
+ * the product's fp32-tower GEMM (K 512, `rows` boards, seeded random digits) back to back for `seconds`, then
+ * one launch of its stamped build: out[0] = median over workgroups of (s_memtime delta / s_memrealtime delta)
+ * x 100 MHz, out[1] = the back-to-back launches' mean time (us), out[2] = their count, out[3] = tiles per
+ * workgroup of the stamped kernel. */
+int kv_dev_gemm_clock(int device, int rows, double seconds, double* out);
 
 /* ------------------------------------------------------- data pipeline ---
  * Full-rules chess (python-chess 1.999 semantics, csrc/kv_chess.cpp) for the

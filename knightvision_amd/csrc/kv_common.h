@@ -20,6 +20,15 @@ struct DevBuf {
     hipError_t alloc(size_t n) { return hipMalloc(&p, n * sizeof(T) + 16); }
 };
 
+// a HIP event destroyed on every return path
+struct DevEvent {
+    hipEvent_t e = nullptr;
+    ~DevEvent() {
+        if (e) (void)hipEventDestroy(e);
+    }
+    hipError_t create() { return hipEventCreate(&e); }
+};
+
 }  // namespace kv
 
 #define KV_HIP(call)                                                                                  \

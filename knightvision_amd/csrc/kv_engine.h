@@ -18,7 +18,8 @@ int net_forward_boards_internal(kv_net* net, const int8_t* boards_dev, int B, fl
 int net_forward_boards_legal_internal(kv_net* net, const int8_t* boards_dev, int B, const uint16_t* moves,
                                       const int* n_moves, int maxm, float* legal, float* value, hipStream_t st);
 int net_set_res_events(kv_net* net, hipEvent_t a, hipEvent_t b);
-void net_dom_info(const kv_net* net, int* algo, int* launches, double* flop, int* path, int* split);
+void net_dom_info(const kv_net* net, int* algo, int* launches, double* flop, int* path, int* split,
+                  const char** kernel);
 
 enum : int { ST_IDLE = 0, ST_ACTIVE = 1, ST_FINISHED = 2 };
 enum : int { END_NONE = 0, END_NOMOVES = 1, END_DRAW = 2, END_RESIGN = 3, END_MAXED = 4 };

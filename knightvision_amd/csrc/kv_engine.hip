@@ -17,6 +17,7 @@
 // The host only launches and, every few steps, reads one counter.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -452,6 +453,7 @@ struct kv_engine {
     int dom_algo = KV_ALGO_DIRECT, dom_launches = 10;  // what each event pair brackets
     int dom_path = KV_PATH_DIRECT, dom_split = 0;
     double dom_flop = 0;
+    const char* dom_kernel = "";
     bool loaded = false;
     // MCTS (sims > 0)
     kv::Tree tree;
@@ -733,7 +735,8 @@ static int eng_eval(kv_engine* e, const int8_t* boards, int rows, bool leaf = fa
                                                                 values, st)
                         : kv::net_forward_boards_internal(net, boards, rows, logits, values, st);
     kv::net_set_res_events(net, nullptr, nullptr);
-    kv::net_dom_info(net, &e->dom_algo, &e->dom_launches, &e->dom_flop, &e->dom_path, &e->dom_split);
+    kv::net_dom_info(net, &e->dom_algo, &e->dom_launches, &e->dom_flop, &e->dom_path, &e->dom_split,
+                     &e->dom_kernel);
     return rc;
 }
 
@@ -914,6 +917,7 @@ int kv_stats_get(kv_engine* e, kv_stats* out) {
     out->dom_algo = e->dom_algo;
     out->dom_path = e->dom_path;
     out->dom_split = e->dom_split;
+    snprintf(out->dom_kernel, sizeof(out->dom_kernel), "%s", e->dom_kernel ? e->dom_kernel : "");
     out->tree_overflows = (int64_t)e->ctr_host->tree_overflows;
     out->nn_rows_lazy = e->lazy_rows;
     return KV_OK;

@@ -613,6 +613,7 @@ __global__ void planes_to_nhwc16_kernel(const float* __restrict__ planes, int nb
 //   KV_PATH_WINO88_I8F32 F(8x8), fp32 Winograd domain, GEMMs on int8 digits (kv_wino88i.h)
 //   KV_PATH_WINO88_I8F32V the same with fp64 input transforms (V cut to digits from fp64)
 //   KV_PATH_WINO88_I8R F(8x8), fp64 Winograd domain, GEMMs on 4 radix-256 digits (13 of 16 pairs)
+//   KV_PATH_WINO88_I8F32R3 F(8x8), fp32 Winograd domain, GEMMs on 3 radix-256 digits (6 of 9 pairs)
 // fp32 + KV_ALGO_AUTO picks its paths per weight load (kv_net_calibration).
 constexpr int kNPath = KV_NPATH;
 
@@ -644,6 +645,8 @@ struct kv_net {
     int* eu88i = nullptr;   // their row exponents [100][Cout]
     int8_t* U88i32 = nullptr;  // the same with 4 digits (KV_PATH_WINO88_I8F32 and _I8F32V)
     int* eu88i32 = nullptr;
+    int8_t* U88r3 = nullptr;   // 3 radix-256 digits in row lines (KV_PATH_WINO88_I8F32R3; slot 3 zero)
+    int* eu88r3 = nullptr;
     int8_t* U88r = nullptr;    // 4 radix-256 digit planes [100][Cin/32][4][Cout][32] (KV_PATH_WINO88_I8R)
     int* eu88r = nullptr;
     size_t euoff[12] = {};
@@ -676,7 +679,16 @@ struct kv_net {
     int dom_launches = 10;
     int dom_split = 0;  // F(8x8) fp32: points run as 128x128 tiles in the first launch (100: one launch)
     double dom_flop = 0;
+    const char* dom_kernel = "conv3x3_kernel<512,32>";  // the launched kernel's name (kv_stats.dom_kernel)
 };
+
+// The residual (K 512) GEMM kernel the launchers below chose last on this thread: each launcher names what it
+// launches, so the engine's kv_stats.dom_kernel is the library's own record, not a rule re-derived by a caller.
+static thread_local const char* t_dom_kernel = nullptr;
+template <int K>
+static inline void note_dom(const char* name) {
+    if constexpr (K == 512) t_dom_kernel = name;
+}
 
 // Small batches (<= 16 boards: the sequential reference path, batch-16
 // schedules) have far fewer output tiles than CUs: split K into groups of 3
@@ -694,6 +706,7 @@ static int path_for(const kv_net* net, int B) {
     if (net->precision == KV_PREC_I8R4) return KV_PATH_WINO88_I8R;
     if (net->precision == KV_PREC_FP32 && net->algo == KV_ALGO_WINOGRAD88_I8) return KV_PATH_WINO88_I8F32;
     if (net->precision == KV_PREC_FP32 && net->algo == KV_ALGO_WINOGRAD88_I8V) return KV_PATH_WINO88_I8F32V;
+    if (net->precision == KV_PREC_FP32 && net->algo == KV_ALGO_WINOGRAD88_I8R3) return KV_PATH_WINO88_I8F32R3;
     if (net->precision == KV_PREC_F16X3) {
         if (net->algo == KV_ALGO_DIRECT || (net->algo == KV_ALGO_AUTO && small)) return KV_PATH_DIRECT;
         return KV_PATH_WINO48_F16X3;
@@ -783,14 +796,29 @@ static int net_pad(const kv_net* net, int B) {
         case KV_PATH_WINO88_I8:
         case KV_PATH_WINO88_I8R:
         case KV_PATH_WINO88_I8F32:
+        case KV_PATH_WINO88_I8F32R3:
         case KV_PATH_WINO88_I8F32V: return (B + 127) & ~127;  // the int8 GEMM's 128-row tiles
         default: return (B + 31) & ~31;
     }
 }
 
-// boards per forward: the output / input kernels index the Winograd workspaces with 32-bit offsets (the
-// 5-digit planes of 100 x boards x 512 values: 256,000 bytes per board)
+// boards per tower pass: the output / input kernels index the Winograd workspaces with 32-bit offsets (the
+// 5-digit planes of 100 x boards x 512 values: 256,000 bytes per board). The public forwards run a larger
+// batch as equal slices of at most kMaxBoards (for_slices), so no caller sees the limit.
 constexpr int kMaxBoards = 16384;
+
+// f(first, count) over slices of [0, B): one slice when B <= kMaxBoards, else ceil(B / kMaxBoards) equal ones
+// (each > 16 boards, so in the same size class as the whole batch: the same path and the same bits)
+template <class F>
+static int for_slices(int B, F&& f) {
+    if (B <= kMaxBoards) return f(0, B);
+    const int n = (B + kMaxBoards - 1) / kMaxBoards, per = (B + n - 1) / n;
+    for (int s0 = 0; s0 < B; s0 += per) {
+        const int rc = f(s0, per < B - s0 ? per : B - s0);
+        if (rc) return rc;
+    }
+    return KV_OK;
+}
 
 static int net_reserve(kv_net* net, int nb_pad) {
     KV_REQUIRE(nb_pad <= kMaxBoards, KV_EINVAL, "kv_net: %d boards per forward (at most %d)", nb_pad, kMaxBoards);
@@ -846,7 +874,11 @@ static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows
 // 128x256 the same way 1.73 / 12.89; 256x128 k-tile 32 (1 per CU) 1.78 / 13.35 -- against 1.65 / 12.22
 template <int K>
 static int launch_wino48_gemm(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
-    if (rows % 128 == 0) return launch_wino_gemm_t<K, 4, 2, 1, 2, 32, 0, kv::W48_XI>(V, U, M, rows, stride, st);
+    if (rows % 128 == 0) {
+        note_dom<K>("wino_gemm_kernel<512,4,2,1,2,32,60>");
+        return launch_wino_gemm_t<K, 4, 2, 1, 2, 32, 0, kv::W48_XI>(V, U, M, rows, stride, st);
+    }
+    note_dom<K>("wino_gemm_kernel<512,2,2,1,2,16,60>");
     return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720, kv::W48_XI>(V, U, M, rows, stride, st);
 }
 
@@ -869,7 +901,11 @@ static int launch_wino_gemm_h3_t(const float* V, const uint16_t* Uh, const uint1
 template <int K>
 static int launch_wino48_gemm_h3(const float* V, const uint16_t* Uh, const uint16_t* Ul, const unsigned* vmax, float* M,
                                  int rows, int stride, hipStream_t st) {
-    if (rows % 128) return launch_wino_gemm_h3_t<K, 1, kv::W48_XI, 1>(V, Uh, Ul, vmax, M, rows, stride, st);
+    if (rows % 128) {
+        note_dom<K>("wino_gemm_h3_kernel<512,1,60,1>");
+        return launch_wino_gemm_h3_t<K, 1, kv::W48_XI, 1>(V, Uh, Ul, vmax, M, rows, stride, st);
+    }
+    note_dom<K>("wino_gemm_h3_kernel<512,2,60,1>");
     return launch_wino_gemm_h3_t<K, 2, kv::W48_XI, 1>(V, Uh, Ul, vmax, M, rows, stride, st);
 }
 
@@ -984,13 +1020,18 @@ template <int K>
 static int launch_wino88_gemm(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
     if (rows % 128 == 0) {
         const int xa = wino88_split_points(rows);
+        note_dom<K>(xa == kv::W88_XI ? "wino_gemm_kernel<512,4,2,1,2,32,100>"
+                                     : "wino_gemm_kernel<512,4,2,1,2,32,100>+wino_gemm_kernel<512,2,2,1,2,16,100>");
         int rc = launch_wino_gemm_t<K, 4, 2, 1, 2, 32, 0, kv::W88_XI>(V, U, M, rows, stride, st, 0, xa);
         if (rc || xa == kv::W88_XI) return rc;
         return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720, kv::W88_XI>(V, U, M, rows, stride, st, xa,
                                                                                    kv::W88_XI - xa);
     }
-    if (rows % 64 == 0)
+    if (rows % 64 == 0) {
+        note_dom<K>("wino_gemm_kernel<512,2,2,1,2,16,100>");
         return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720, kv::W88_XI>(V, U, M, rows, stride, st);
+    }
+    note_dom<K>(rows == 32 ? "wino_gemm_kernel<512,1,2,1,2,32,100>" : "wino_gemm_kernel<512,1,2,1,2,16,100>");
     // 32-row tiles (2 waves of 32x64): batches of <= 32 and 65-96 boards (net_pad), below one round of
     // tiles, where the time is the padded work per CU; k-tiles of 32 at 32 rows (forward 0.537 -> 0.522
     // ms), of 16 at 96 (0.783 vs 0.915 ms; profiles/r03_w88_rows32_ck_ab.log)
@@ -1058,6 +1099,8 @@ static int launch_wino88d_gemm_t(const double* V, const double* U, double* M, in
 // 2,048 boards, bit-identical; profiles/r04_w88d_out_ab.log)
 template <int K>
 static int launch_wino88d_gemm(const double* V, const double* U, double* M, int rows, int stride, hipStream_t st) {
+    note_dom<K>(rows % 128 == 0 ? "wino88d_gemm_kernel<512,2,4,4,2>"
+                : rows % 64 == 0 ? "wino88d_gemm_kernel<512,1,4,4,2>" : "wino88d_gemm_kernel<512,1,4,2,2>");
     if (rows % 128 == 0) return launch_wino88d_gemm_t<K, 2, 4, 4, 2>(V, U, M, rows, stride, st);
     if (rows % 64 == 0) return launch_wino88d_gemm_t<K, 1, 4, 4, 2>(V, U, M, rows, stride, st);
     return launch_wino88d_gemm_t<K, 1, 4, 2, 2>(V, U, M, rows, stride, st);
@@ -1104,11 +1147,12 @@ static int wino88d_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 // (4 digits: the fp32 domain's row-line layout)
 // (NSEG 2: V's exponents per 256-channel segment, K 512 only)
 // (R8: KV_PATH_WINO88_I8R's 4 radix-256 digits of fp64 rows, row lines)
-template <int K, int D = kv::kI8Digits, class T, int NSEG = 1, bool R8 = false>
+// (R3: KV_PATH_WINO88_I8F32R3's 3 radix-256 digits in the 4 slots of row lines)
+template <int K, int D = kv::kI8Digits, class T, int NSEG = 1, bool R8 = false, bool R3 = false>
 static int launch_wino88i_slice(const T* src, int n, int slab_rows, int nslab, int8_t* dst, int* ex,
                                 hipStream_t st) {
     const int waves = n * nslab;
-    hipLaunchKernelGGL((kv::wino88i_slice_kernel<K, T, D, D == kv::kI8DigitsF32, NSEG, R8>),
+    hipLaunchKernelGGL((kv::wino88i_slice_kernel<K, T, D, D == kv::kI8DigitsF32, NSEG, R8, R3>),
                        dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, src, n, slab_rows, nslab, dst, ex);
     KV_HIP(hipGetLastError());
     return KV_OK;
@@ -1188,17 +1232,22 @@ static int launch_wino88i32_gemm_lag(const int8_t* V8, const int* ev, const int8
 }
 
 // TPW tiles per workgroup, the ring across tiles (kv_wino88i.h wino88i32_gemm_lagt_kernel)
-template <int K, int TPW>
+// ND 3: KV_PATH_WINO88_I8F32R3's 3 radix-256 digits (6 pairs), its B digits LJ.. lagging
+#ifndef KV_I8R3_LJ
+#define KV_I8R3_LJ 1
+#endif
+template <int K, int TPW, int ND = 4, int LJ = (ND == 4 ? KV_I8F32_LJ : KV_I8R3_LJ)>
 static int launch_wino88i32_gemm_lagt(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
                                       int rows, int stride, hipStream_t st) {
     using T = kv::Wino88iTile<kv::kI8DigitsF32>;
     constexpr int bytes = 3 * T::STAGE;
-    KV_HIP(lds_opt_in((const void*)kv::wino88i32_gemm_lagt_kernel<K, TPW>, bytes));
+    auto kern = kv::wino88i32_gemm_lagt_kernel<K, TPW, LJ, false, ND>;
+    KV_HIP(lds_opt_in((const void*)kern, bytes));
     const int tiles = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
     KV_REQUIRE(rows % T::WM == 0 && stride % T::WM == 0 && tiles % (8 * TPW) == 0, KV_EINVAL,
                "wino gemm i8 (lagt): rows %d / stride %d vs tile %d", rows, stride, T::WM);
-    hipLaunchKernelGGL((kv::wino88i32_gemm_lagt_kernel<K, TPW>), dim3(tiles / TPW), dim3(T::THREADS), bytes, st, V8,
-                       ev, U8, eu, M, rows, 512, stride);
+    hipLaunchKernelGGL(kern, dim3(tiles / TPW), dim3(T::THREADS), bytes, st, V8, ev, U8, eu, M, rows, 512, stride,
+                       nullptr);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -1277,6 +1326,7 @@ static int i8x5_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const in
         const char* e = getenv("KV_I8X5_GEMM");
         return e && !strcmp(e, "r4");
     }();
+    note_dom<K>(r4 ? "wino88i_gemm_kernel<512,5>" : "wino88i_gemm_lag5_kernel<512,3,5,7,false>");
     if (r4) return launch_wino88i_gemm<K>(V8, ev, U8, eu, M, rows, stride, st);
     return launch_wino88i_gemm_lag5<K>(V8, ev, U8, eu, M, rows, stride, st);
 }
@@ -1288,9 +1338,12 @@ static int i8x5_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const in
 #define KV_I8R_LJ 3
 #endif
 constexpr int kI8rLJ = KV_I8R_LJ;
+#define KV_STR2(x) #x
+#define KV_STR(x) KV_STR2(x)
 template <int K>
 static int i8r_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, double* M, int rows, int stride,
                     hipStream_t st) {
+    note_dom<K>("wino88i_gemm_lag5_kernel<512," KV_STR(KV_I8R_LJ) ",4,8,true>");
     return launch_wino88i_gemm_lag5<K, kI8rLJ, 4, 8, true>(V8, ev, U8, eu, M, rows, stride, st);
 }
 
@@ -1365,8 +1418,11 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, bool r8, hipStream_t s
 //                  kernel, bit-identical, profiles/r05_i8gemm_lag_ab.log); r4: the round-4
 //                  wino88i_gemm_kernel; p: the persistent wino88i32_gemm_kernel (5 % slower than r4,
 //                  profiles/r05_i8gemm_variants.log). The segment form always runs wino88i32_gemm_kernel ----
+//   KV_I8F32_OUT   hold: the output kernel that holds the next V's 50 values per lane across the exponent barrier
+//                  (wino88i32_out_kernel, one board per CU); default: wino88i32_out2_kernel (the 32 activations
+//                  held, the transform run twice, two boards per CU; the same bits)
 struct I8f32Form {
-    bool seg = false, slice = false, r4 = false, persist = false;
+    bool seg = false, slice = false, r4 = false, persist = false, out_hold = false;
 };
 static const I8f32Form& i8f32_form() {
     static const I8f32Form f = [] {
@@ -1378,21 +1434,45 @@ static const I8f32Form& i8f32_form() {
         e = getenv("KV_I8F32_GEMM");
         x.r4 = e && !strcmp(e, "r4") && !x.seg;
         x.persist = e && !strcmp(e, "p");
+        e = getenv("KV_I8F32_OUT");
+        x.out_hold = e && !strcmp(e, "hold");
         return x;
     }();
     return f;
 }
 
+// KV_OUT_STAG: the output kernels' phase stagger (kv_wino88i.h out_stagger), in units of s_sleep 127
+static int out_stag() {
+    static const int v = [] {
+        const char* e = getenv("KV_OUT_STAG");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
+// r3: KV_PATH_WINO88_I8F32R3's digits (3 radix-256, per-row exponents)
 template <bool RESID, bool WRITE_Y>
 static int launch_wino88i32_out(kv_net* net, int l, const float* M, int nb, int stride, const float* resid,
-                                float* Y, int8_t* V8, int* ev, bool seg, hipStream_t st) {
+                                float* Y, int8_t* V8, int* ev, bool seg, hipStream_t st, bool r3 = false) {
     const float* W = net->w;
+    const int cus = device_cus(), stag = out_stag();
+    const float* sc = W + net->off.scale[l];
+    const float* sh = W + net->off.shift[l];
     if (seg)
         hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y, 256>), dim3(2, nb), dim3(512), 0, st, M, stride,
-                           W + net->off.scale[l], W + net->off.shift[l], resid, Y, V8, ev);
-    else
+                           sc, sh, resid, Y, V8, ev, 0, 0);
+    else if (i8f32_form().out_hold && r3)
+        hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y, 512, true>), dim3(1, nb), dim3(1024), 0, st, M,
+                           stride, sc, sh, resid, Y, V8, ev, stag, cus);
+    else if (i8f32_form().out_hold)
         hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y, 512>), dim3(1, nb), dim3(1024), 0, st, M, stride,
-                           W + net->off.scale[l], W + net->off.shift[l], resid, Y, V8, ev);
+                           sc, sh, resid, Y, V8, ev, stag, cus);
+    else if (r3)
+        hipLaunchKernelGGL((kv::wino88i32_out2_kernel<RESID, WRITE_Y, true>), dim3(1, nb), dim3(1024), 0, st, M,
+                           stride, sc, sh, resid, Y, V8, ev, stag, 2 * cus);
+    else
+        hipLaunchKernelGGL((kv::wino88i32_out2_kernel<RESID, WRITE_Y>), dim3(1, nb), dim3(1024), 0, st, M, stride,
+                           sc, sh, resid, Y, V8, ev, stag, 2 * cus);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -1411,29 +1491,64 @@ static int launch_wino88i32v_out(kv_net* net, int l, const float* M, int nb, int
 // the fp32 tower's int8-digit GEMM of one conv (K 256: one segment, per-row exponents)
 template <int K>
 static int i8f32_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M, int rows, int stride,
-                      bool seg, hipStream_t st) {
+                      bool seg, hipStream_t st, bool r3 = false) {
     constexpr int D = kv::kI8DigitsF32;
     const I8f32Form& f = i8f32_form();
+    if (r3) {  // KV_PATH_WINO88_I8F32R3: the lagt kernel on 3 digit levels, tile count as the 4-digit one's
+        const int tpw = i8f32_tiles_per_wg(rows);
+        if (tpw == 5) {
+            note_dom<K>("wino88i32_gemm_lagt_kernel<512,5,3>");
+            return launch_wino88i32_gemm_lagt<K, 5, 3>(V8, ev, U8, eu, M, rows, stride, st);
+        }
+        if (tpw == 4) {
+            note_dom<K>("wino88i32_gemm_lagt_kernel<512,4,3>");
+            return launch_wino88i32_gemm_lagt<K, 4, 3>(V8, ev, U8, eu, M, rows, stride, st);
+        }
+        note_dom<K>("wino88i32_gemm_lagt_kernel<512,1,3>");
+        return launch_wino88i32_gemm_lagt<K, 1, 3>(V8, ev, U8, eu, M, rows, stride, st);
+    }
     if constexpr (K == 512)
-        if (seg) return launch_wino88i32_gemm<K, 32, 3, 2>(V8, ev, U8, eu, M, rows, stride, true, st);
-    if (f.r4) return launch_wino88i_gemm<K, D>(V8, ev, U8, eu, M, rows, stride, st);
-    if (f.persist) return launch_wino88i32_gemm<K, 32, 3, 1>(V8, ev, U8, eu, M, rows, stride, true, st);
+        if (seg) {
+            note_dom<K>("wino88i32_gemm_kernel<512,32,3,2>");
+            return launch_wino88i32_gemm<K, 32, 3, 2>(V8, ev, U8, eu, M, rows, stride, true, st);
+        }
+    if (f.r4) {
+        note_dom<K>("wino88i_gemm_kernel<512,4>");
+        return launch_wino88i_gemm<K, D>(V8, ev, U8, eu, M, rows, stride, st);
+    }
+    if (f.persist) {
+        note_dom<K>("wino88i32_gemm_kernel<512,32,3,1>");
+        return launch_wino88i32_gemm<K, 32, 3, 1>(V8, ev, U8, eu, M, rows, stride, true, st);
+    }
     const int tpw = i8f32_tiles_per_wg(rows);
-    if (tpw == 5) return launch_wino88i32_gemm_lagt<K, 5>(V8, ev, U8, eu, M, rows, stride, st);
-    if (tpw == 4) return launch_wino88i32_gemm_lagt<K, 4>(V8, ev, U8, eu, M, rows, stride, st);
+    if (tpw == 5) {
+        note_dom<K>("wino88i32_gemm_lagt_kernel<512,5>");
+        return launch_wino88i32_gemm_lagt<K, 5>(V8, ev, U8, eu, M, rows, stride, st);
+    }
+    if (tpw == 4) {
+        note_dom<K>("wino88i32_gemm_lagt_kernel<512,4>");
+        return launch_wino88i32_gemm_lagt<K, 4>(V8, ev, U8, eu, M, rows, stride, st);
+    }
+    note_dom<K>("wino88i32_gemm_lag_kernel<512,false>");
     return launch_wino88i32_gemm_lag<K, false>(V8, ev, U8, eu, M, rows, stride, st);
 }
 
 // conv l's GEMM; slice: V (fp32; v64: conv2's fp64 V256) -> digits first. (mark: the engine's timing hook
 // brackets the slice, when there is one, and the GEMM)
+// r3 (KV_PATH_WINO88_I8F32R3): 3 radix-256 digits -- conv2's slice, the weights' digits and the 6-pair GEMM
 static int wino88i32_gemm_layer(kv_net* net, int l, int K, int rows, int stride, bool slice, bool mark, bool v64,
-                                hipStream_t st) {
+                                hipStream_t st, bool r3 = false) {
     constexpr int D = kv::kI8DigitsF32;
-    const bool seg = K == 512 && i8f32_form().seg && !v64;
+    const bool seg = K == 512 && i8f32_form().seg && !v64 && !r3;
     float* M = (float*)net->Mw;
     int rc;
     if (mark && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-    if (slice && v64) {
+    if (slice && r3) {
+        KV_REQUIRE(K == 256, KV_EINVAL, "wino88i32r3: the output kernels write the digits of K 512");
+        if ((rc = launch_wino88i_slice<256, D, float, 1, false, true>((const float*)net->V256, rows, stride,
+                                                                      kv::W88_XI, net->V8, net->ev8, st)))
+            return rc;
+    } else if (slice && v64) {
         KV_REQUIRE(K == 256, KV_EINVAL, "wino88i32v: the output kernels write the digits of K 512");
         if ((rc = launch_wino88i_slice<256, D>((const double*)net->V256, rows, stride, kv::W88_XI, net->V8, net->ev8,
                                                st)))
@@ -1445,10 +1560,10 @@ static int wino88i32_gemm_layer(kv_net* net, int l, int K, int rows, int stride,
                       : launch_wino88i_slice<512, D>(Vsrc, rows, stride, kv::W88_XI, net->V8, net->ev8, st);
         if (rc) return rc;
     }
-    const int8_t* U = net->U88i32 + net->uoff88[l] * D;
-    const int* eu = net->eu88i32 + net->euoff[l];
-    rc = K == 256 ? i8f32_gemm<256>(net->V8, net->ev8, U, eu, M, rows, stride, false, st)
-                  : i8f32_gemm<512>(net->V8, net->ev8, U, eu, M, rows, stride, seg, st);
+    const int8_t* U = (r3 ? net->U88r3 : net->U88i32) + net->uoff88[l] * D;
+    const int* eu = (r3 ? net->eu88r3 : net->eu88i32) + net->euoff[l];
+    rc = K == 256 ? i8f32_gemm<256>(net->V8, net->ev8, U, eu, M, rows, stride, false, st, r3)
+                  : i8f32_gemm<512>(net->V8, net->ev8, U, eu, M, rows, stride, seg, st, r3);
     if (rc) return rc;
     if (mark && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
     return KV_OK;
@@ -1456,35 +1571,35 @@ static int wino88i32_gemm_layer(kv_net* net, int l, int K, int rows, int stride,
 
 // v64 (KV_PATH_WINO88_I8F32V): conv2's V256 is fp64 (the stem's / wino88d_in_kernel's) and every output
 // kernel is wino88i32v_out_kernel (the slice and segment forms do not apply)
-static int wino88i32_blocks(kv_net* net, int nb, bool mark, bool v64, hipStream_t st) {
+static int wino88i32_blocks(kv_net* net, int nb, bool mark, bool v64, hipStream_t st, bool r3 = false) {
     const int rows = nb, stride = rows;
     float* V = (float*)net->V;
     const float* M = (const float*)net->Mw;
-    const bool sf = i8f32_form().slice && !v64, seg = i8f32_form().seg && !v64;
+    const bool sf = i8f32_form().slice && !v64 && !r3, seg = i8f32_form().seg && !v64 && !r3;
     int8_t* V8 = net->V8;
     int* ev = net->ev8;
     int rc;
-    if ((rc = wino88i32_gemm_layer(net, 1, 256, rows, stride, true, false, v64, st))) return rc;
+    if ((rc = wino88i32_gemm_layer(net, 1, 256, rows, stride, true, false, v64, st, r3))) return rc;
     rc = v64  ? launch_wino88i32v_out<false, true>(net, 1, M, nb, stride, nullptr, net->X, V8, ev, st)
          : sf ? launch_wino88_out<false, true, true>(net, 1, M, nb, stride, nullptr, net->X, V, st)
-              : launch_wino88i32_out<false, true>(net, 1, M, nb, stride, nullptr, net->X, V8, ev, seg, st);
+              : launch_wino88i32_out<false, true>(net, 1, M, nb, stride, nullptr, net->X, V8, ev, seg, st, r3);
     if (rc) return rc;
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
     for (int r = 0; r < 5; ++r) {
         const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
         const bool m = mark && r == 2;
-        if ((rc = wino88i32_gemm_layer(net, l1, 512, rows, stride, sf, m, v64, st))) return rc;
+        if ((rc = wino88i32_gemm_layer(net, l1, 512, rows, stride, sf, m, v64, st, r3))) return rc;
         rc = v64  ? launch_wino88i32v_out<false, false>(net, l1, M, nb, stride, nullptr, nullptr, V8, ev, st)
              : sf ? launch_wino88_out<false, false, true>(net, l1, M, nb, stride, nullptr, nullptr, V, st)
-                  : launch_wino88i32_out<false, false>(net, l1, M, nb, stride, nullptr, nullptr, V8, ev, seg, st);
+                  : launch_wino88i32_out<false, false>(net, l1, M, nb, stride, nullptr, nullptr, V8, ev, seg, st, r3);
         if (rc) return rc;
-        if ((rc = wino88i32_gemm_layer(net, l2, 512, rows, stride, sf, false, v64, st))) return rc;
+        if ((rc = wino88i32_gemm_layer(net, l2, 512, rows, stride, sf, false, v64, st, r3))) return rc;
         if (r == 4)
             rc = launch_wino88_out<true, true, false>(net, l2, M, nb, stride, net->X, net->X, nullptr, st);
         else
             rc = v64  ? launch_wino88i32v_out<true, true>(net, l2, M, nb, stride, net->X, net->X, V8, ev, st)
                  : sf ? launch_wino88_out<true, true, true>(net, l2, M, nb, stride, net->X, net->X, V, st)
-                      : launch_wino88i32_out<true, true>(net, l2, M, nb, stride, net->X, net->X, V8, ev, seg, st);
+                      : launch_wino88i32_out<true, true>(net, l2, M, nb, stride, net->X, net->X, V8, ev, seg, st, r3);
         if (rc) return rc;
     }
     if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
@@ -1511,6 +1626,7 @@ static WsNeed ws_need(int path) {
             return {{i8f32_form().slice ? P88 * 512 * f : 0, P88 * 512 * f, P88 * 256 * f,
                      P88 * 512 * kv::kI8DigitsF32}};
         case KV_PATH_WINO88_I8F32V: return {{0, P88 * 512 * f, P88 * 256 * d, P88 * 512 * kv::kI8DigitsF32}};
+        case KV_PATH_WINO88_I8F32R3: return {{0, P88 * 512 * f, P88 * 256 * f, P88 * 512 * kv::kI8DigitsF32}};
         default: return {{0, 0, 0, 0}};  // direct: the split-K slab only
     }
 }
@@ -1538,8 +1654,10 @@ static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hi
     int rc;
     net->dom_path = path;
     net->dom_launches = 1;
+    t_dom_kernel = nullptr;
     if (path == KV_PATH_WINO88 || path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8 ||
-        path == KV_PATH_WINO88_I8R || path == KV_PATH_WINO88_I8F32 || path == KV_PATH_WINO88_I8F32V) {
+        path == KV_PATH_WINO88_I8R || path == KV_PATH_WINO88_I8F32 || path == KV_PATH_WINO88_I8F32V ||
+        path == KV_PATH_WINO88_I8F32R3) {
         const bool f64 = path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8 || path == KV_PATH_WINO88_I8R ||
                          path == KV_PATH_WINO88_I8F32V;
         if (!v256_ready) {
@@ -1552,6 +1670,7 @@ static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hi
             KV_HIP(hipGetLastError());
         }
         if ((rc = path == KV_PATH_WINO88_I8F32    ? wino88i32_blocks(net, nb_pad, true, false, st)
+                  : path == KV_PATH_WINO88_I8F32R3 ? wino88i32_blocks(net, nb_pad, true, false, st, true)
                   : path == KV_PATH_WINO88_I8F32V ? wino88i32_blocks(net, nb_pad, true, true, st)
                   : path == KV_PATH_WINO88_I8  ? wino88i_blocks(net, nb_pad, true, false, st)
                   : path == KV_PATH_WINO88_I8R ? wino88i_blocks(net, nb_pad, true, true, st)
@@ -1559,6 +1678,7 @@ static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hi
                                                : wino88_blocks(net, nb_pad, true, st)))
             return rc;
         net->dom_flop = 2.0 * kv::W88_XI * nb_pad * 512.0 * 512.0;
+        net->dom_kernel = t_dom_kernel ? t_dom_kernel : "?";
         net->dom_algo = KV_ALGO_WINOGRAD88;
         net->dom_split = path != KV_PATH_WINO88 ? 0 : (nb_pad % 128 == 0 ? wino88_split_points(nb_pad) : kv::W88_XI);
         return KV_OK;
@@ -1571,6 +1691,7 @@ static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hi
     }
     if ((rc = wino48_blocks(net, nb_pad, path, true, st))) return rc;
     net->dom_flop = 2.0 * kv::W48_XI * rows48 * 512.0 * 512.0;
+    net->dom_kernel = t_dom_kernel ? t_dom_kernel : "?";
     net->dom_algo = KV_ALGO_WINOGRAD48;
     net->dom_split = 0;
     return KV_OK;
@@ -1595,7 +1716,7 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     // Winograd paths: the stem builds conv2's V itself
     bool v256_ready = false;
     if (boards) {
-        if (path == KV_PATH_WINO88 || path == KV_PATH_WINO88_I8F32)
+        if (path == KV_PATH_WINO88 || path == KV_PATH_WINO88_I8F32 || path == KV_PATH_WINO88_I8F32R3)
             hipLaunchKernelGGL(kv::stem_kernel<4>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], (float*)net->V256, nb_pad, nullptr);
         else if (path == KV_PATH_WINO88_F64 || path == KV_PATH_WINO88_I8 || path == KV_PATH_WINO88_I8R ||
@@ -1638,6 +1759,7 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     net->dom_algo = KV_ALGO_DIRECT;
     net->dom_path = KV_PATH_DIRECT;
     net->dom_split = 0;
+    net->dom_kernel = "conv3x3_kernel<512,32>";
     net->dom_launches = 10;
     net->dom_flop = (double)nb_pad * 64 * 512 * 4608 * 2;
     return net_heads(net, nb, policy, value, st);
@@ -1759,13 +1881,16 @@ static int ensure_path(kv_net* net, int path) {
         }
         case KV_PATH_WINO88_I8:
         case KV_PATH_WINO88_I8R:
+        case KV_PATH_WINO88_I8F32R3:
         case KV_PATH_WINO88_I8F32: {
             // U64 per layer (from the fp64 set when it is built, else into a one-layer scratch), then its digits
-            // (5 for the fp64 domain, 4 radix-256 ones for its I8R form, 4 row-line ones for the fp32 tower)
+            // (5 for the fp64 domain, 4 radix-256 ones for its I8R form, 4 row-line ones for the fp32 tower, 3
+            // radix-256 ones in row lines for its R3 form)
             const bool f32 = path == KV_PATH_WINO88_I8F32, r8 = path == KV_PATH_WINO88_I8R;
-            const int D = f32 || r8 ? 4 : kv::kI8Digits;
-            int8_t*& Ud = f32 ? net->U88i32 : r8 ? net->U88r : net->U88i;
-            int*& Ue = f32 ? net->eu88i32 : r8 ? net->eu88r : net->eu88i;
+            const bool r3 = path == KV_PATH_WINO88_I8F32R3;
+            const int D = f32 || r8 || r3 ? 4 : kv::kI8Digits;
+            int8_t*& Ud = f32 ? net->U88i32 : r8 ? net->U88r : r3 ? net->U88r3 : net->U88i;
+            int*& Ue = f32 ? net->eu88i32 : r8 ? net->eu88r : r3 ? net->eu88r3 : net->eu88i;
             const size_t tot = wino_offsets(net->uoff88, kv::W88_XI);
             size_t tot_co = 0;
             for (int l = 1; l < 12; ++l) {
@@ -1792,6 +1917,10 @@ static int ensure_path(kv_net* net, int path) {
                 else if (r8)
                     rc = ci == 256 ? launch_wino88i_slice<256, 4, double, 1, true>(U64, co, co, kv::W88_XI, dst, ex, 0)
                                    : launch_wino88i_slice<512, 4, double, 1, true>(U64, co, co, kv::W88_XI, dst, ex, 0);
+                else if (r3)
+                    rc = ci == 256
+                             ? launch_wino88i_slice<256, 4, double, 1, false, true>(U64, co, co, kv::W88_XI, dst, ex, 0)
+                             : launch_wino88i_slice<512, 4, double, 1, false, true>(U64, co, co, kv::W88_XI, dst, ex, 0);
                 else
                     rc = ci == 256 ? launch_wino88i_slice<256>(U64, co, co, kv::W88_XI, dst, ex, 0)
                                    : launch_wino88i_slice<512>(U64, co, co, kv::W88_XI, dst, ex, 0);
@@ -1848,6 +1977,13 @@ static void release_unused(kv_net* net) {
         net->U88r = nullptr;
         net->eu88r = nullptr;
         net->built[KV_PATH_WINO88_I8R] = false;
+    }
+    if (!keep[KV_PATH_WINO88_I8F32R3]) {
+        (void)hipFree(net->U88r3);
+        (void)hipFree(net->eu88r3);
+        net->U88r3 = nullptr;
+        net->eu88r3 = nullptr;
+        net->built[KV_PATH_WINO88_I8F32R3] = false;
     }
     if (!keep[KV_PATH_WINO88_I8F32V]) net->built[KV_PATH_WINO88_I8F32V] = false;
     if (!keep[KV_PATH_WINO88_I8F32] && !keep[KV_PATH_WINO88_I8F32V]) {
@@ -1999,10 +2135,10 @@ static int net_calibrate(kv_net* net) {
     // > 16 boards
     // (F(8x8) and F(4x8) on fp32 MFMA are never within the budget when the int8-digit fp32 tower is not:
     // on every weight set measured they are further from fp64 -- DESIGN.md; they stay explicit algos)
-    const int cands[5] = {KV_PATH_WINO88_I8F32, KV_PATH_WINO88_I8F32V, KV_PATH_WINO88_I8R, KV_PATH_WINO88_I8,
-                          KV_PATH_WINO88_F64};
+    const int cands[6] = {KV_PATH_WINO88_I8F32R3, KV_PATH_WINO88_I8F32, KV_PATH_WINO88_I8F32V, KV_PATH_WINO88_I8R,
+                          KV_PATH_WINO88_I8, KV_PATH_WINO88_F64};
     net->auto_small = KV_PATH_DIRECT;
-    for (int i = 0; i < 5; ++i) {
+    for (int i = 0; i < 6; ++i) {
         const int p = cands[i];
         if ((rc = ensure_path(net, p))) return fail(rc);
         net->auto_large = p;
@@ -2096,7 +2232,8 @@ int kv_net_set_algo(kv_net* net, int algo) {
     KV_REQUIRE(algo != 2, KV_EINVAL, "kv_net_set_algo: KV_ALGO 2 (Winograd F(4x4)) was retired; use "
                                      "KV_ALGO_WINOGRAD48 or KV_ALGO_WINOGRAD88");
     KV_REQUIRE(algo == KV_ALGO_AUTO || algo == KV_ALGO_DIRECT || algo == KV_ALGO_WINOGRAD48 ||
-                   algo == KV_ALGO_WINOGRAD88 || algo == KV_ALGO_WINOGRAD88_I8 || algo == KV_ALGO_WINOGRAD88_I8V,
+                   algo == KV_ALGO_WINOGRAD88 || algo == KV_ALGO_WINOGRAD88_I8 || algo == KV_ALGO_WINOGRAD88_I8V ||
+                   algo == KV_ALGO_WINOGRAD88_I8R3,
                KV_EINVAL, "kv_net_set_algo: unknown algo %d", algo);
     if (net->algo == algo && (!net->loaded || net->built[path_for(net, 1024)])) return KV_OK;
     const int prev = net->algo;
@@ -2141,13 +2278,15 @@ int kv_net_forward(kv_net* net, const float* planes_dev, int B, float* policy_de
     KV_REQUIRE(net && net->loaded, KV_EINVAL, "kv_net_forward: net not loaded");
     KV_REQUIRE(B > 0 && planes_dev && policy_dev && value_dev, KV_EINVAL, "kv_net_forward: bad arguments (B=%d)", B);
     hipStream_t st = (hipStream_t)stream;
-    const int nb_pad = net_pad(net, B);
-    int rc = net_reserve(net, nb_pad);
-    if (rc) return rc;
-    hipLaunchKernelGGL(kv::planes_to_nhwc16_kernel, dim3((nb_pad * 64 + 255) / 256), dim3(256), 0, st, planes_dev, B,
-                       nb_pad, net->x16);
-    KV_HIP(hipGetLastError());
-    return net_tower(net, B, nb_pad, nullptr, policy_dev, value_dev, st);
+    return for_slices(B, [&](int s0, int b) {
+        const int nb_pad = net_pad(net, b);
+        int rc = net_reserve(net, nb_pad);
+        if (rc) return rc;
+        hipLaunchKernelGGL(kv::planes_to_nhwc16_kernel, dim3((nb_pad * 64 + 255) / 256), dim3(256), 0, st,
+                           planes_dev + (size_t)s0 * 12 * 64, b, nb_pad, net->x16);
+        KV_HIP(hipGetLastError());
+        return net_tower(net, b, nb_pad, nullptr, policy_dev + (size_t)s0 * 4096, value_dev + s0, st);
+    });
 }
 
 int kv_net_forward_boards(kv_net* net, const int8_t* boards_dev, int B, float* policy_dev, float* value_dev,
@@ -2155,10 +2294,14 @@ int kv_net_forward_boards(kv_net* net, const int8_t* boards_dev, int B, float* p
     KV_REQUIRE(net && net->loaded, KV_EINVAL, "kv_net_forward_boards: net not loaded");
     KV_REQUIRE(B > 0 && boards_dev && policy_dev && value_dev, KV_EINVAL, "kv_net_forward_boards: bad arguments");
     hipStream_t st = (hipStream_t)stream;
-    const int nb_pad = net_pad(net, B);
-    int rc = net_reserve(net, nb_pad);
-    if (rc) return rc;
-    return net_tower(net, B, nb_pad, boards_dev, policy_dev, value_dev, st);  // stem_kernel encodes on the fly
+    return for_slices(B, [&](int s0, int b) {
+        const int nb_pad = net_pad(net, b);
+        int rc = net_reserve(net, nb_pad);
+        if (rc) return rc;
+        // stem_kernel encodes on the fly
+        return net_tower(net, b, nb_pad, boards_dev + (size_t)s0 * 64, policy_dev + (size_t)s0 * 4096, value_dev + s0,
+                         st);
+    });
 }
 
 int kv_net_forward_boards_legal(kv_net* net, const int8_t* boards_dev, int B, const uint16_t* moves_dev,
@@ -2167,26 +2310,30 @@ int kv_net_forward_boards_legal(kv_net* net, const int8_t* boards_dev, int B, co
     KV_REQUIRE(B > 0 && boards_dev && moves_dev && n_moves_dev && legal_dev && value_dev && maxm > 0, KV_EINVAL,
                "kv_net_forward_boards_legal: bad arguments");
     hipStream_t st = (hipStream_t)stream;
-    const int nb_pad = net_pad(net, B);
-    int rc = net_reserve(net, nb_pad);
-    if (rc) return rc;
-    net->legal.moves = moves_dev;
-    net->legal.n = n_moves_dev;
-    net->legal.maxm = maxm;
-    net->legal.out = legal_dev;
-    rc = net_tower(net, B, nb_pad, boards_dev, nullptr, value_dev, st);
-    net->legal.out = nullptr;
-    return rc;
+    return for_slices(B, [&](int s0, int b) {
+        const int nb_pad = net_pad(net, b);
+        int rc = net_reserve(net, nb_pad);
+        if (rc) return rc;
+        net->legal.moves = moves_dev + (size_t)s0 * maxm;
+        net->legal.n = n_moves_dev + s0;
+        net->legal.maxm = maxm;
+        net->legal.out = legal_dev + (size_t)s0 * maxm;
+        rc = net_tower(net, b, nb_pad, boards_dev + (size_t)s0 * 64, nullptr, value_dev + s0, st);
+        net->legal.out = nullptr;
+        return rc;
+    });
 }
 
 int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, int digits, int seg, double* M,
                    int8_t* v_digits, int* v_exp) {
-    KV_REQUIRE(V && U && M && rows > 0 && rows % 128 == 0 && (K == 256 || K == 512) && (digits == 4 || digits == 5) &&
-                   (!seg || (seg == 1 && digits == 4 && K == 512) || (seg == 2 && digits == 4)),
+    KV_REQUIRE(V && U && M && rows > 0 && rows % 128 == 0 && rows <= kMaxBoards && (K == 256 || K == 512) &&
+                   (digits == 4 || digits == 5) &&
+                   (!seg || (seg == 1 && digits == 4 && K == 512) || (seg == 2 && digits == 4) ||
+                    (seg == 3 && digits == 4)),
                KV_EINVAL, "kv_dev_wino88i: bad arguments (rows %d must be a multiple of 128, K %d 256 or 512, "
-               "digits %d 4 or 5, seg %d: 1 only with 4 digits and K 512, 2 (radix 256) only with 4 digits)", rows,
-               K, digits, seg);
-    const bool r8 = seg == 2;
+               "digits %d 4 or 5, seg %d: 1 only with 4 digits and K 512, 2 (radix 256) and 3 (3 radix-256 digits "
+               "in 4 slots) only with 4 digits)", rows, K, digits, seg);
+    const bool r8 = seg == 2, r3 = seg == 3;
     const int nseg = seg == 1 ? 2 : 1;
     KV_HIP(hipSetDevice(device));
     const size_t nv = (size_t)kv::W88_XI * rows * K, nu = (size_t)kv::W88_XI * 512 * K;
@@ -2224,6 +2371,17 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
         if (!rc)
             rc = K == 256 ? launch_wino88i_gemm<256>(v8.p, ev.p, u8.p, eu.p, dm.p, rows, rows, 0)
                           : launch_wino88i_gemm<512>(v8.p, ev.p, u8.p, eu.p, dm.p, rows, rows, 0);
+    } else if (r3) {  // KV_PATH_WINO88_I8F32R3: 3 radix-256 digits in row lines, 6 pairs, M rounded to fp32
+        constexpr int D = kv::kI8DigitsF32;
+        rc = K == 256 ? launch_wino88i_slice<256, D, double, 1, false, true>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0)
+                      : launch_wino88i_slice<512, D, double, 1, false, true>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0);
+        if (!rc)
+            rc = K == 256
+                     ? launch_wino88i_slice<256, D, double, 1, false, true>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0)
+                     : launch_wino88i_slice<512, D, double, 1, false, true>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
+        if (!rc)
+            rc = K == 256 ? i8f32_gemm<256>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, false, 0, true)
+                          : i8f32_gemm<512>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, false, 0, true);
     } else {  // the fp32 domain: 4 digits, M rounded to fp32 (returned widened)
         constexpr int D = kv::kI8DigitsF32;
         rc = K == 256 ? launch_wino88i_slice<256, D>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0)
@@ -2250,10 +2408,28 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
     return KV_OK;
 }
 
+}  // extern "C"
+
+// the per-row fused output kernel of kv_dev_wino88i32_out: the held-V form (hold) or the product's default
+template <bool RESID, bool R3>
+static void dev_out_rowform(bool hold, const float* M, int rows, const float* sc, const float* sh, float* y,
+                            int8_t* v8, int* ev) {
+    const float* rs = RESID ? y : nullptr;  // Y doubles as the residual (in place, as the tower runs it)
+    if (hold)
+        hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, true, 512, R3>), dim3(1, rows), dim3(1024), 0, 0, M, rows,
+                           sc, sh, rs, y, v8, ev, 0, 0);
+    else
+        hipLaunchKernelGGL((kv::wino88i32_out2_kernel<RESID, true, R3>), dim3(1, rows), dim3(1024), 0, 0, M, rows, sc,
+                           sh, rs, y, v8, ev, 0, 0);
+}
+
+extern "C" {
+
 int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scale, const float* shift,
                          const float* resid, int fused, float* Y, int8_t* v_digits, int* v_exp) {
-    KV_REQUIRE(M && scale && shift && Y && v_digits && v_exp && rows > 0 && rows % 128 == 0, KV_EINVAL,
-               "kv_dev_wino88i32_out: bad arguments (rows %d must be a multiple of 128)", rows);
+    KV_REQUIRE(M && scale && shift && Y && v_digits && v_exp && rows > 0 && rows % 128 == 0 && rows <= kMaxBoards,
+               KV_EINVAL, "kv_dev_wino88i32_out: bad arguments (rows %d: a multiple of 128, at most %d)", rows,
+               kMaxBoards);
     KV_HIP(hipSetDevice(device));
     const size_t nm = (size_t)kv::W88_XI * rows * 512, ny = (size_t)rows * 64 * 512;
     kv::DevBuf<float> dm, dsc, dsh, dy, dv;
@@ -2265,8 +2441,12 @@ int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scal
     KV_HIP(dy.alloc(ny));
     KV_HIP(dv.alloc(nm));
     KV_HIP(v8.alloc(nm * kv::kI8DigitsF32));
-    const bool seg = (fused & 2) != 0, v64 = (fused & 4) != 0;
+    const bool seg = (fused & 2) != 0, v64 = (fused & 4) != 0, hold = (fused & 8) != 0, r3 = (fused & 16) != 0;
     KV_REQUIRE(!(seg && v64), KV_EINVAL, "kv_dev_wino88i32_out: fp64 V (bit 2) has per-row exponents only");
+    KV_REQUIRE(!r3 || (!seg && !v64), KV_EINVAL, "kv_dev_wino88i32_out: bit 4 (3 radix-256 digits) has per-row "
+               "fp32 V only");
+    KV_REQUIRE(!hold || ((fused & 1) && !seg && !v64), KV_EINVAL,
+               "kv_dev_wino88i32_out: bit 3 (the held form) is a form of the fused per-row kernel (bit 0 alone)");
     KV_HIP(ev.alloc((size_t)kv::W88_XI * rows * 2));
     KV_HIP(hipMemcpy(dm.p, M, nm * sizeof(float), hipMemcpyHostToDevice));
     KV_HIP(hipMemcpy(dsc.p, scale, 512 * sizeof(float), hipMemcpyHostToDevice));
@@ -2301,20 +2481,19 @@ int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scal
         if (rc) return rc;
         KV_HIP(hipDeviceSynchronize());
     } else if (fused & 1) {
-        if (resid) {
-            if (seg)
+        if (seg) {
+            if (resid)
                 hipLaunchKernelGGL((kv::wino88i32_out_kernel<true, true, 256>), dim3(2, rows), dim3(512), 0, 0, dm.p,
-                                   rows, sc, sh, dy.p, dy.p, v8.p, ev.p);
+                                   rows, sc, sh, dy.p, dy.p, v8.p, ev.p, 0, 0);
             else
-                hipLaunchKernelGGL((kv::wino88i32_out_kernel<true, true, 512>), dim3(1, rows), dim3(1024), 0, 0, dm.p,
-                                   rows, sc, sh, dy.p, dy.p, v8.p, ev.p);
-        } else {
-            if (seg)
                 hipLaunchKernelGGL((kv::wino88i32_out_kernel<false, true, 256>), dim3(2, rows), dim3(512), 0, 0, dm.p,
-                                   rows, sc, sh, nullptr, dy.p, v8.p, ev.p);
-            else
-                hipLaunchKernelGGL((kv::wino88i32_out_kernel<false, true, 512>), dim3(1, rows), dim3(1024), 0, 0,
-                                   dm.p, rows, sc, sh, nullptr, dy.p, v8.p, ev.p);
+                                   rows, sc, sh, nullptr, dy.p, v8.p, ev.p, 0, 0);
+        } else if (resid) {
+            if (r3) dev_out_rowform<true, true>(hold, dm.p, rows, sc, sh, dy.p, v8.p, ev.p);
+            else dev_out_rowform<true, false>(hold, dm.p, rows, sc, sh, dy.p, v8.p, ev.p);
+        } else {
+            if (r3) dev_out_rowform<false, true>(hold, dm.p, rows, sc, sh, dy.p, v8.p, ev.p);
+            else dev_out_rowform<false, false>(hold, dm.p, rows, sc, sh, dy.p, v8.p, ev.p);
         }
         KV_HIP(hipGetLastError());
     } else {
@@ -2325,8 +2504,10 @@ int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scal
             hipLaunchKernelGGL((kv::wino88_out_kernel<false, true, true>), dim3(512 / 256, rows), dim3(256), 0, 0,
                                dm.p, rows, sc, sh, nullptr, dy.p, dv.p);
         KV_HIP(hipGetLastError());
-        int rc = seg ? launch_wino88i_slice<512, kv::kI8DigitsF32, float, 2>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0)
-                     : launch_wino88i_slice<512, kv::kI8DigitsF32>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
+        int rc = seg  ? launch_wino88i_slice<512, kv::kI8DigitsF32, float, 2>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0)
+                 : r3 ? launch_wino88i_slice<512, kv::kI8DigitsF32, float, 1, false, true>(dv.p, rows, rows, kv::W88_XI,
+                                                                                           v8.p, ev.p, 0)
+                      : launch_wino88i_slice<512, kv::kI8DigitsF32>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
         if (rc) return rc;
     }
     KV_HIP(hipDeviceSynchronize());
@@ -2338,8 +2519,9 @@ int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scal
 
 int kv_dev_wino88r_out(int device, const double* M, int rows, const float* scale, const float* shift,
                        const float* resid, int fused, float* Y, int8_t* v_digits, int* v_exp) {
-    KV_REQUIRE(M && scale && shift && Y && v_digits && v_exp && rows > 0 && rows % 128 == 0, KV_EINVAL,
-               "kv_dev_wino88r_out: bad arguments (rows %d must be a multiple of 128)", rows);
+    KV_REQUIRE(M && scale && shift && Y && v_digits && v_exp && rows > 0 && rows % 128 == 0 && rows <= kMaxBoards,
+               KV_EINVAL, "kv_dev_wino88r_out: bad arguments (rows %d: a multiple of 128, at most %d)", rows,
+               kMaxBoards);
     KV_HIP(hipSetDevice(device));
     const size_t nm = (size_t)kv::W88_XI * rows * 512, ny = (size_t)rows * 64 * 512;
     kv::DevBuf<double> dm, dv;
@@ -2400,8 +2582,8 @@ __global__ void i8_fill_kernel(int8_t* d, size_t n_lines, int* e, size_t ne, uns
 }
 
 int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, float* avg_us, float* M_out) {
-    KV_REQUIRE(rows > 0 && rows % 128 == 0 && (K == 256 || K == 512) && iters > 0 && avg_us, KV_EINVAL,
-               "kv_dev_i8gemm_bench: bad arguments");
+    KV_REQUIRE(rows > 0 && rows % 128 == 0 && rows <= kMaxBoards && (K == 256 || K == 512) && iters > 0 && avg_us,
+               KV_EINVAL, "kv_dev_i8gemm_bench: bad arguments");
     KV_HIP(hipSetDevice(device));
     const size_t lv = (size_t)kv::W88_XI * (K / 32) * rows, lu = (size_t)kv::W88_XI * (K / 32) * 512;
     const size_t nm = (size_t)kv::W88_XI * rows * 512;
@@ -2482,20 +2664,97 @@ int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, flo
     int rc;
     for (int w = 0; w < 2; ++w)
         if ((rc = run())) return rc;
-    hipEvent_t e0, e1;
-    KV_HIP(hipEventCreate(&e0));
-    KV_HIP(hipEventCreate(&e1));
-    KV_HIP(hipEventRecord(e0, 0));
+    kv::DevEvent e0, e1;  // destroyed on every return path
+    KV_HIP(e0.create());
+    KV_HIP(e1.create());
+    KV_HIP(hipEventRecord(e0.e, 0));
     for (int it = 0; it < iters; ++it)
         if ((rc = run())) return rc;
-    KV_HIP(hipEventRecord(e1, 0));
-    KV_HIP(hipEventSynchronize(e1));
+    KV_HIP(hipEventRecord(e1.e, 0));
+    KV_HIP(hipEventSynchronize(e1.e));
     float ms = 0.f;
-    KV_HIP(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
+    KV_HIP(hipEventElapsedTime(&ms, e0.e, e1.e));
     *avg_us = 1000.f * ms / iters;
     if (M_out) KV_HIP(hipMemcpy(M_out, m.p, nm * sizeof(float), hipMemcpyDeviceToHost));
+    return KV_OK;
+}
+
+// The in-kernel clock of the headline GEMM (MI355X_MICROARCH.md, DVFS give-back item 6): the product's fp32-tower
+// GEMM (i8f32_gemm<512>, the kernel and tile count it picks for `rows`) back to back on seeded random digits
+// for `seconds`, then ONE launch of the stamped build of the same kernel (wino88i32_gemm_lagt_kernel<., TPW, .,
+// true>; TPW 1 where the product runs single tiles): per workgroup (s_memtime delta) / (s_memrealtime delta)
+// x 100 MHz, the median over workgroups. out[0] = that clock in MHz, out[1] = the back-to-back launches'
+// mean time in us (HIP events), out[2] = launches timed, out[3] = tiles per workgroup of the stamped build.
+int kv_dev_gemm_clock(int device, int rows, double seconds, double* out) {
+    KV_REQUIRE(rows > 0 && rows % 128 == 0 && rows <= kMaxBoards && seconds > 0 && out, KV_EINVAL,
+               "kv_dev_gemm_clock: bad arguments (rows %d: a multiple of 128, at most %d)", rows, kMaxBoards);
+    KV_HIP(hipSetDevice(device));
+    constexpr int K = 512;
+    const size_t lv = (size_t)kv::W88_XI * (K / 32) * rows, lu = (size_t)kv::W88_XI * (K / 32) * 512;
+    const size_t nm = (size_t)kv::W88_XI * rows * 512;
+    kv::DevBuf<int8_t> v8, u8;
+    kv::DevBuf<int> ev, eu;
+    kv::DevBuf<float> m;
+    kv::DevBuf<unsigned long long> stamps;
+    KV_HIP(v8.alloc(lv * 128));
+    KV_HIP(u8.alloc(lu * 128));
+    KV_HIP(ev.alloc((size_t)kv::W88_XI * rows * 2));
+    KV_HIP(eu.alloc((size_t)kv::W88_XI * 512));
+    KV_HIP(m.alloc(nm));
+    hipLaunchKernelGGL(i8_fill_kernel, dim3((unsigned)((lv * 128 + 255) / 256)), dim3(256), 0, 0, v8.p, lv, ev.p,
+                       (size_t)kv::W88_XI * rows * 2, 1234u);
+    hipLaunchKernelGGL(i8_fill_kernel, dim3((unsigned)((lu * 128 + 255) / 256)), dim3(256), 0, 0, u8.p, lu, eu.p,
+                       (size_t)kv::W88_XI * 512, 99u);
+    KV_HIP(hipGetLastError());
+    int rc;
+    for (int w = 0; w < 3; ++w)
+        if ((rc = i8f32_gemm<K>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, false, 0))) return rc;
+    KV_HIP(hipDeviceSynchronize());
+    kv::DevEvent e0, e1;
+    KV_HIP(e0.create());
+    KV_HIP(e1.create());
+    int launches = 0;
+    const auto t_start = std::chrono::steady_clock::now();
+    KV_HIP(hipEventRecord(e0.e, 0));
+    while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() < seconds) {
+        for (int i = 0; i < 50; ++i)  // 50 launches queued per check (~25 ms at C3)
+            if ((rc = i8f32_gemm<K>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, false, 0))) return rc;
+        launches += 50;
+        KV_HIP(hipStreamSynchronize(0));
+    }
+    KV_HIP(hipEventRecord(e1.e, 0));
+    KV_HIP(hipEventSynchronize(e1.e));
+    float ms = 0.f;
+    KV_HIP(hipEventElapsedTime(&ms, e0.e, e1.e));
+    // the stamped build, right after the loop (the chip still at the clock the loop held)
+    using T = kv::Wino88iTile<kv::kI8DigitsF32>;
+    const int tpw = i8f32_tiles_per_wg(rows) >= 4 ? i8f32_tiles_per_wg(rows) : 1;
+    const int tiles = kv::W88_XI * (rows / T::WM) * (512 / T::WN), nwg = tiles / tpw;
+    KV_REQUIRE(tiles % (8 * tpw) == 0, KV_EINVAL, "kv_dev_gemm_clock: %d tiles, %d per workgroup", tiles, tpw);
+    KV_HIP(stamps.alloc((size_t)nwg * 4));
+    constexpr int bytes = 3 * T::STAGE;
+    auto kern = tpw == 5   ? kv::wino88i32_gemm_lagt_kernel<K, 5, KV_I8F32_LJ, true>
+                : tpw == 4 ? kv::wino88i32_gemm_lagt_kernel<K, 4, KV_I8F32_LJ, true>
+                           : kv::wino88i32_gemm_lagt_kernel<K, 1, KV_I8F32_LJ, true>;
+    KV_HIP(lds_opt_in((const void*)kern, bytes));
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(T::THREADS), bytes, 0, v8.p, ev.p, u8.p, eu.p, m.p, rows, 512, rows,
+                       stamps.p);
+    KV_HIP(hipGetLastError());
+    KV_HIP(hipDeviceSynchronize());
+    std::vector<unsigned long long> h((size_t)nwg * 4);
+    KV_HIP(hipMemcpy(h.data(), stamps.p, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    std::vector<double> mhz;
+    mhz.reserve(nwg);
+    for (int b = 0; b < nwg; ++b) {
+        const double dt = (double)(h[4 * b + 1] - h[4 * b]), dr = (double)(h[4 * b + 3] - h[4 * b + 2]);
+        if (dr > 0) mhz.push_back(dt / dr * 100.0);
+    }
+    KV_REQUIRE(!mhz.empty(), KV_EHIP, "kv_dev_gemm_clock: no stamp pair advanced");
+    std::nth_element(mhz.begin(), mhz.begin() + mhz.size() / 2, mhz.end());
+    out[0] = mhz[mhz.size() / 2];
+    out[1] = 1000.0 * ms / launches;
+    out[2] = launches;
+    out[3] = tpw;
     return KV_OK;
 }
 
@@ -2533,6 +2792,8 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->eu88i32);
     (void)hipFree(net->U88r);
     (void)hipFree(net->eu88r);
+    (void)hipFree(net->U88r3);
+    (void)hipFree(net->eu88r3);
     (void)hipFree(net->V8);
     (void)hipFree(net->ev8);
     (void)hipFree(net->evmax8);
@@ -2564,7 +2825,9 @@ int net_set_res_events(kv_net* net, hipEvent_t a, hipEvent_t b) {
     net->res_b = b;
     return KV_OK;
 }
-void net_dom_info(const kv_net* net, int* algo, int* launches, double* flop, int* path, int* split) {
+void net_dom_info(const kv_net* net, int* algo, int* launches, double* flop, int* path, int* split,
+                  const char** kernel) {
+    *kernel = net->dom_kernel;
     *split = net->dom_split;
     *algo = net->dom_algo;
     *launches = net->dom_launches;

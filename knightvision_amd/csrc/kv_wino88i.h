@@ -72,6 +72,25 @@ __device__ inline int i8_row_exponent_r8(unsigned m) {
     return (int)(m >> 20) - 1022 + ((m & 0xFE000u) >= 0xFC000u ? 1 : 0);
 }
 
+// fp32 form of the radix-256 rule (KV_PATH_WINO88_I8F32R3): m = the bits of the row's largest |float|; one more
+// when its top 6 fraction bits are all ones (max >= 127/128 2^e)
+__device__ inline int i8_row_exponent_f32r(unsigned m) {
+    if (!m) return 0;
+    return (int)(m >> 23) - 126 + ((m & 0x7E0000u) == 0x7E0000u ? 1 : 0);
+}
+
+// The 3 radix-256 digits of v under e (KV_PATH_WINO88_I8F32R3: the fp32 tower's 24-bit block fixed point), in
+// the row lines' 4 digit slots: N = rint(v 2^(23-e)) by an fp64 magic-number add (ties to even; exact for
+// |N| < 2^31 -- the fp32 magic add would round at |t| >= 2^22), |N| < 127/128 2^23 under the radix-256 rule, so
+// the balanced digits d_0 (most significant) .. d_2, N = d_0 2^16 + d_1 2^8 + d_2, are the bytes of
+// N + 0x808080 with their top bits flipped; packed byte d = d_d (slot 3 zero): v ~ 2^(e-7) sum_d d_d 2^(-8 d).
+__device__ inline unsigned i8_digits_r3(double v, int e) {
+#pragma clang fp contract(off)
+    constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
+    const unsigned n = (unsigned)__double_as_longlong(ldexp(v, 23 - e) + kMagic);
+    return __builtin_amdgcn_perm(0u, (n + 0x808080u) ^ 0x808080u, 0x0c000102u);
+}
+
 // the 4 radix-256 digits of v under e, packed: byte k = d_(3-k) (two's complement). N by a magic-number add
 // (rint, ties to even; the low word of t + 1.5 2^52 is N's two's complement for |t| < 2^31); then the balanced
 // digits are the bytes of N + 0x80808080 (each d + 128 in [0, 255], no carry out) with their top bits flipped.
@@ -174,7 +193,9 @@ __device__ inline unsigned i8_quad_transpose(unsigned P, int lane) {
 // 32 channels goes to (((x * K/32 + kc) * slab_rows + r) * 4 + d) * 32 instead
 // -- the 4 digits of one row's chunk are one 128-byte line. NSEG = 2 (K = 512 only): one exponent per
 // 256-channel segment instead of per row (lanes 0-31 hold segment 0), at ex[(x * 2 + seg) * slab_rows + r].
-template <int K, class T, int D, bool RL = false, int NSEG = 1, bool R8 = false>
+// R3 (KV_PATH_WINO88_I8F32R3; row lines, D = 4 slots): 3 radix-256 digits (i8_digits_r3) under the radix-256
+// exponent rule of the fp32 or fp64 rows, slot 3 zero
+template <int K, class T, int D, bool RL = false, int NSEG = 1, bool R8 = false, bool R3 = false>
 __global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict__ src, int n, int slab_rows,
                                                             int nslab, int8_t* __restrict__ dst,
                                                             int* __restrict__ ex) {
@@ -182,6 +203,7 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict_
     static_assert(!RL || D == 4, "row lines hold 4 digits");
     static_assert(NSEG == 1 || (NSEG == 2 && K == 512), "segments of 256 channels");
     static_assert(!R8 || (D == 4 && sizeof(T) == 8 && NSEG == 1), "radix 256: 4 digits of fp64 rows");
+    static_assert(!R3 || (D == 4 && RL && NSEG == 1 && !R8), "3 radix-256 digits in the 4 slots of row lines");
     constexpr int CPL = K / 64;  // 4 or 8 channels per lane
     const int lane = threadIdx.x & 63;
     const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -208,7 +230,10 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict_
         const unsigned t = (unsigned)__shfl_xor((int)m, o, 64);
         m = t > m ? t : m;
     }
-    const int e = R8 ? i8_row_exponent_r8(m) : sizeof(T) == 8 ? i8_row_exponent(m) : i8_row_exponent_f32(m);
+    const int e = (R8 || (R3 && sizeof(T) == 8)) ? i8_row_exponent_r8(m)
+                  : R3                              ? i8_row_exponent_f32r(m)
+                  : sizeof(T) == 8                  ? i8_row_exponent(m)
+                                                    : i8_row_exponent_f32(m);
     if (NSEG == 1 && lane == 0) ex[row] = e;
     if (NSEG == 2 && (lane & 31) == 0) ex[((size_t)x * 2 + (lane >> 5)) * slab_rows + r] = e;
     unsigned long long pk[D] = {};
@@ -219,6 +244,10 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict_
             const unsigned P = i8_digits_r8((double)v[i], e);
 #pragma unroll
             for (int d = 0; d < D; ++d) dg[d] = (int)(signed char)(P >> (8 * (D - 1 - d)));
+        } else if constexpr (R3) {
+            const unsigned P = i8_digits_r3((double)v[i], e);  // byte d = digit d, slot 3 zero
+#pragma unroll
+            for (int d = 0; d < D; ++d) dg[d] = (int)(signed char)(P >> (8 * d));
         } else {
             i8_digits<D>(v[i], e, dg);
         }
@@ -658,11 +687,13 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* _
     issue1(0, 0); issue1(1, 0); issue1(2, 0); issue1(3, 0);
     issue1(0, 1); issue1(1, 1); issue1(2, 1); issue1(3, 1);
     for (int kt = 0; kt < NK; ++kt) {
-        // stage kt landed: only stage kt + 1's copies may still be in flight
+        // stage kt landed: only stage kt + 1's copies may still be in flight; lgkmcnt(0): the lagging B digits
+        // of stage kt - 1 were read from the buffer stage kt + 2's copies overwrite once every wave passes this
+        // barrier, and their reads are only waited for at the MFMAs after it (a formal WAR race)
         if (kt + 1 < NK)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
         else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         const char* buf = L0 + (kt % NBUF) * T::STAGE;
@@ -734,18 +765,30 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* _
 #ifndef KV_I8F32_LJ
 #define KV_I8F32_LJ 2
 #endif
-template <int K, int TPW, int LJ = KV_I8F32_LJ>
+// STAMP (a diagnostic build, never the product's): wave 0 of each workgroup records the shader clock
+// (s_memtime) and the 100 MHz constant clock (s_memrealtime) at its start and end into stamps[4 * block] -- a
+// buffer of its own that no other code reads; kv_dev_gemm_clock turns them into the clock the chip held.
+// ND = 3 (KV_PATH_WINO88_I8F32R3): the same row lines (4 digit slots per 32-channel chunk), of which digits 0-2
+// hold 3 radix-256 digits (slot 3 zero, never read): the 6 pairs i + j <= 2, 3 exact int32 levels weighted 2^-8l.
+template <int K, int TPW, int LJ = KV_I8F32_LJ, bool STAMP = false, int ND = 4>
 __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* __restrict__ V8,
                                                                   const int* __restrict__ ev,
                                                                   const int8_t* __restrict__ U8,
                                                                   const int* __restrict__ eu, float* __restrict__ M,
-                                                                  int rows, int cout, int stride) {
+                                                                  int rows, int cout, int stride,
+                                                                  unsigned long long* __restrict__ stamps) {
+    unsigned long long t0 = 0, r0 = 0;
+    if constexpr (STAMP) {
+        t0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
     constexpr int S = 4, NBUF = 3;
     using T = Wino88iTile<S>;
     constexpr int NT = T::NT, WM = T::WM, WN = T::WN, GL = T::GL;
     constexpr int NK = K / 32, NS = TPW * NK;
-    constexpr int NA = S - LJ;
-    static_assert(GL == 4 && NK >= 3 && LJ >= 1 && LJ <= 3, "4 pieces per wave and stage");
+    constexpr int NA = ND - LJ;
+    static_assert(GL == 4 && NK >= 3 && LJ >= 1 && LJ < ND && (ND == 4 || ND == 3), "4 pieces per wave and stage");
+    constexpr double kStep = ND == 4 ? 0.0078125 : 0.00390625;  // level weight: radix 128 / 256
 
     extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8t[];
     char* const L0 = (char*)lds_i8t;
@@ -789,9 +832,9 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
 
     const int lr = lane & 31, lh = lane >> 5;
     const int arow = wm * 32 + lr;
-    int aoffr[S], boffr[NT][S];
+    int aoffr[ND], boffr[NT][ND];
 #pragma unroll
-    for (int i = 0; i < S; ++i) {
+    for (int i = 0; i < ND; ++i) {
         aoffr[i] = i8_rl_off(arow, 2 * i + lh);
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) boffr[nt][i] = S * T::PLANE + i8_rl_off(wn * NT * 32 + nt * 32 + lr, 2 * i + lh);
@@ -801,17 +844,17 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
     issue1(0, 1); issue1(1, 1); issue1(2, 1); issue1(3, 1);
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
-        i32x16_t acc[S][NT];
+        i32x16_t acc[ND][NT];
 #pragma unroll
-        for (int l = 0; l < S; ++l)
+        for (int l = 0; l < ND; ++l)
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) acc[l][nt] = i32x16_t{};
-        i8x16_t pa[NA] = {}, pb[S - LJ][NT] = {};
+        i8x16_t pa[NA] = {}, pb[ND - LJ][NT] = {};
         auto h2 = [&]() {
 #pragma unroll
-            for (int jb = LJ; jb < S; ++jb)
+            for (int jb = LJ; jb < ND; ++jb)
 #pragma unroll
-                for (int i = 0; i + jb < S; ++i)
+                for (int i = 0; i + jb < ND; ++i)
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt)
                         acc[i + jb][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(pa[i], pb[jb - LJ][nt], acc[i + jb][nt], 0, 0, 0);
@@ -819,17 +862,17 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
         for (int kt = 0; kt < NK; ++kt) {
             const int s = j * NK + kt;
             if (s + 1 >= NS)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             else if (kt == 0 && j > 0)
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL + 32) : "memory");
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL + 32) : "memory");
             else
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             const char* buf = L0 + (s % NBUF) * T::STAGE;
-            i8x16_t a[S], b[S][NT];
+            i8x16_t a[ND], b[ND][NT];
 #pragma unroll
-            for (int i = 0; i < S; ++i) a[i] = *(const i8x16_t*)(buf + aoffr[i]);
+            for (int i = 0; i < ND; ++i) a[i] = *(const i8x16_t*)(buf + aoffr[i]);
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) b[0][nt] = *(const i8x16_t*)(buf + boffr[nt][0]);
             // the stage's reads issue before the lagging MFMAs (hipcc otherwise hoists those MFMAs above the reads,
@@ -844,15 +887,15 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
                 issue1(1, s + 2);
             }
 #pragma unroll
-            for (int jb = 0; jb < S; ++jb) {
-                if (jb + 1 < S) {
+            for (int jb = 0; jb < ND; ++jb) {
+                if (jb + 1 < ND) {
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt) b[jb + 1][nt] = *(const i8x16_t*)(buf + boffr[nt][jb + 1]);
                 }
                 __builtin_amdgcn_sched_barrier(0);  // likewise each next B digit's reads before this one's MFMAs
                 if (jb < LJ) {
 #pragma unroll
-                    for (int i = 0; i + jb < S; ++i)
+                    for (int i = 0; i + jb < ND; ++i)
 #pragma unroll
                         for (int nt = 0; nt < NT; ++nt)
                             acc[i + jb][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[jb][nt], acc[i + jb][nt], 0, 0, 0);
@@ -865,7 +908,7 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
 #pragma unroll
             for (int i = 0; i < NA; ++i) pa[i] = a[i];
 #pragma unroll
-            for (int jb = LJ; jb < S; ++jb)
+            for (int jb = LJ; jb < ND; ++jb)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) pb[jb - LJ][nt] = b[jb][nt];
         }
@@ -879,11 +922,18 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
-                double m = (double)acc[S - 1][nt][r];
+                double m = (double)acc[ND - 1][nt][r];
 #pragma unroll
-                for (int l = S - 2; l >= 0; --l) m = __builtin_fma(m, 0.0078125, (double)acc[l][nt][r]);  // exact
+                for (int l = ND - 2; l >= 0; --l) m = __builtin_fma(m, kStep, (double)acc[l][nt][r]);  // exact
                 M[((size_t)xi * stride + r_base + wm * 32 + row) * cout + col] = (float)ldexp(m, evx[row] + ec);
             }
+        }
+    }
+    if constexpr (STAMP) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x < 4) {  // one vector store per value, lanes 0-3
+            const unsigned long long v = threadIdx.x == 0 ? t0 : threadIdx.x == 1 ? t1 : threadIdx.x == 2 ? r0 : r1;
+            stamps[(size_t)blockIdx.x * 4 + threadIdx.x] = v;
         }
     }
 }
@@ -994,9 +1044,9 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
     for (int g = 0; g < GL; ++g) issue1(g, 1);
     for (int kt = 0; kt < NK; ++kt) {
         if (kt + 1 < NK)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
         else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         const char* buf = L0 + (kt % NBUF) * T::STAGE;
@@ -1471,12 +1521,142 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_kernel(const int8_t* __res
 // profiles/r04_i8f32_fused_out.log; and an output kernel computing only the row maxima plus a second
 // input-transform pass, 294-356 + 220 us, profiles/r04_i8f32_outmax_form.log.)
 
-template <bool RESID, bool WRITE_Y, int CW>
+// fp32 transform row 5h + aa of a plane split over lanes l, l ^ 32 (half h), from the half's 4 columns after the
+// half exchange (xc[kk][i] = pixel (i, 4h + kk)): the fmaf chains of wino88_input_cols + wino88_input_row on the
+// same inputs -- each column's w88_bt taken for rows aa and 5 + aa only -- so the same bits, and no 10x4
+// intermediate is live. The asm makes xc opaque per row: otherwise the compiler merges the two passes of
+// wino88i32_out2_kernel (the same chains on the same values) and keeps the 50 results across the barrier.
+__device__ inline void wino88_input_row_of_cols(float (&xc)[4][8], int aa, float (&o)[10]) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(xc[kk][i]));
+    float row[10];
+    row[0] = 0.f;
+    row[9] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+        float col[10], t[10];
+        col[0] = 0.f;
+        col[9] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) col[1 + i] = xc[kk][i];
+        w88_bt(col, t);
+        float lo = t[aa], hi = t[5 + aa];
+        half_swap(lo, hi);
+        row[1 + kk] = lo;
+        row[5 + kk] = hi;
+    }
+    w88_bt(row, o);
+}
+
+// R3 (KV_PATH_WINO88_I8F32R3): the next V's 3 radix-256 digits (i8_digits_r3 under i8_row_exponent_f32r) in
+// the same lines, slot 3 zero
+template <bool R3>
+__device__ inline int i8f32_row_exponent(unsigned m) {
+    return R3 ? i8_row_exponent_f32r(m) : i8_row_exponent_f32(m);
+}
+template <bool R3>
+__device__ inline unsigned i8f32_digits(float v, int e) {
+    if constexpr (R3)
+        return i8_digits_r3((double)v, e);
+    else
+        return i8_digits4_packed(v, e);
+}
+
+// Phase stagger of the one-board-per-workgroup output kernels: every board runs load M -> transforms -> store
+// digits, and boards that start together on every CU put the whole chip in the same phase (HBM saturated in the
+// load and store phases, idle in the transforms). The first-round workgroups of half the CUs (first: the
+// resident workgroup count; (b >> 3) & 1 picks half the workgroups of each XCD) wait `stag` x 8,128 cycles
+// before starting, and the slots they occupy keep that offset for the rest of the grid. Timing only: no
+// output depends on it.
+__device__ inline void out_stagger(int b, int stag, int first) {
+    if (b < first && ((b >> 3) & 1))
+        for (int i = 0; i < stag; ++i) __builtin_amdgcn_s_sleep(127);
+}
+
+// wino88i32_out2_kernel: wino88i32_out_kernel<RESID, WRITE_Y, 512>'s result, bit for bit, in a register budget
+// that lets two boards (two 1,024-thread workgroups) share a CU, so one board's digit stores drain under the
+// other's transforms: a lane keeps its 32 fp32 activations (xc) across the exponent barrier instead of 50 V
+// values and runs the input transform twice -- once for the row maxima, once for the digits. The transform is
+// partitioned by row, not repeated within a pass (each pass computes each V value once), so the VALU work is
+// twice the held form's input transform; at 8 waves per SIMD that is ~20 us of issue over 2,048 boards.
+template <bool RESID, bool WRITE_Y, bool R3 = false>
+__global__ __launch_bounds__(1024, 8) void wino88i32_out2_kernel(const float* __restrict__ M, int rows,
+                                                                 const float* __restrict__ scale,
+                                                                 const float* __restrict__ shift, const float* resid,
+                                                                 float* Y, int8_t* __restrict__ V8,
+                                                                 int* __restrict__ ex, int stag, int first) {
+#pragma clang fp contract(off)
+    constexpr int NK = 512 / 32, NW = 16;
+    __shared__ __attribute__((aligned(16))) unsigned red[NW][2][5][16];
+    __shared__ int exs[100];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+    const int c = w * 32 + (lane & 31), b = blockIdx.y;
+    out_stagger(b, stag, first);
+    float xc[4][8];  // the half's columns 4h .. 4h+3, all 8 rows (after the half exchange)
+    {
+        float x2[4][8];
+        wino88_out_plane_half<RESID, WRITE_Y, true>(M, rows, b, c, h, scale[c], shift[c], resid, Y, x2);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+            for (int ii = 0; ii < 4; ++ii) {
+                float lo = x2[ii][kk], hi = x2[ii][4 + kk];
+                half_swap(lo, hi);
+                xc[kk][ii] = lo;
+                xc[kk][4 + ii] = hi;
+            }
+    }
+#pragma unroll
+    for (int aa = 0; aa < 5; ++aa) {
+        float o[10];
+        wino88_input_row_of_cols(xc, aa, o);
+        unsigned m[10];
+#pragma unroll
+        for (int bb = 0; bb < 10; ++bb) m[bb] = i8_half_max_dpp(__float_as_uint(o[bb]) & 0x7fffffffu);
+        if ((lane & 31) == 16) {  // this half's 10 maxima, written by one lane
+            uint4* rr = (uint4*)&red[w][h][aa][0];
+            rr[0] = make_uint4(m[0], m[1], m[2], m[3]);
+            rr[1] = make_uint4(m[4], m[5], m[6], m[7]);
+            *(uint2*)&red[w][h][aa][8] = make_uint2(m[8], m[9]);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 100) {
+        const int xi = threadIdx.x, a = xi / 10, bb = xi % 10, hh = a / 5, aa = a % 5;
+        unsigned m = 0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) m = red[ww][hh][aa][bb] > m ? red[ww][hh][aa][bb] : m;
+        const int e = i8f32_row_exponent<R3>(m);
+        exs[xi] = e;
+        ex[(size_t)xi * rows + b] = e;
+    }
+    __syncthreads();
+    const int q = lane & 3;
+    const unsigned off0 = ((unsigned)(c >> 5) * rows + b) * 128 + q * 32 + (c & 28), xstride = NK * rows * 128;
+    unsigned* const dst = (unsigned*)V8;
+#pragma unroll
+    for (int aa = 0; aa < 5; ++aa) {
+        float o[10];
+        wino88_input_row_of_cols(xc, aa, o);
+        const int a = 5 * h + aa;
+#pragma unroll
+        for (int bb = 0; bb < 10; ++bb) {
+            const int xi = a * 10 + bb;
+            const unsigned P = i8f32_digits<R3>(o[bb], exs[xi]);
+            __builtin_nontemporal_store(i8_quad_transpose(P, lane), &dst[(off0 + (unsigned)xi * xstride) >> 2]);
+        }
+    }
+}
+
+template <bool RESID, bool WRITE_Y, int CW, bool R3 = false>
 __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __restrict__ M, int rows,
                                                                const float* __restrict__ scale,
                                                                const float* __restrict__ shift, const float* resid,
                                                                float* Y, int8_t* __restrict__ V8,
-                                                               int* __restrict__ ex) {
+                                                               int* __restrict__ ex, int stag, int first) {
 #pragma clang fp contract(off)
     static_assert(CW == 512 || CW == 256, "a row or a 256-channel segment per workgroup");
     constexpr int NK = 512 / 32, NW = CW / 32, NSEG = 512 / CW;
@@ -1484,6 +1664,7 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
     __shared__ int exs[100];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
     const int seg = blockIdx.x, c = seg * CW + w * 32 + (lane & 31), b = blockIdx.y;
+    out_stagger(b, stag, first);
     float vk[5][10];  // this half's 50 V values (rows 5h .. 5h+4), kept across the exponent barrier
     {
         float t2[10][4];  // B10^T of the plane's columns 4h .. 4h+3
@@ -1514,7 +1695,7 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
         unsigned m = 0;
 #pragma unroll
         for (int ww = 0; ww < NW; ++ww) m = red[ww][hh][aa][bb] > m ? red[ww][hh][aa][bb] : m;
-        const int e = i8_row_exponent_f32(m);
+        const int e = i8f32_row_exponent<R3>(m);
         exs[xi] = e;
         ex[((size_t)xi * NSEG + seg) * rows + b] = e;
     }
@@ -1530,7 +1711,7 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
 #pragma unroll
         for (int bb = 0; bb < 10; ++bb) {
             const int xi = a * 10 + bb;
-            const unsigned P = i8_digits4_packed(vk[aa][bb], exs[xi]);
+            const unsigned P = i8f32_digits<R3>(vk[aa][bb], exs[xi]);
             // non-temporal: the digits are read once, by the next GEMM (forward -1.2 % at 2,048 boards against
             // plain stores, bit-identical; the GEMM's M stored non-temporal instead slowed the output kernel that
             // reads it: profiles/r05_out_nt_ab.log)

@@ -144,7 +144,9 @@ class SelfPlayEngine:
     def stats(self) -> dict:
         st = _lib.Stats()
         _lib.check(_lib.lib().kv_stats_get(self.h, C.byref(st)), "kv_stats_get")
-        return {k: getattr(st, k) for k, _ in _lib.Stats._fields_}
+        out = {k: getattr(st, k) for k, _ in _lib.Stats._fields_}
+        out["dom_kernel"] = out["dom_kernel"].decode()
+        return out
 
     def close(self):
         if getattr(self, "h", None):

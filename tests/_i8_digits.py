@@ -122,3 +122,55 @@ def gemm_r8(V, U):
     for l in range(3, -1, -1):
         m = m * 0.00390625 + lev[l]
     return np.ldexp(m, (ev[:, :, None] + eu[:, None, :] - 14).astype(np.int32)), dv, ev
+
+
+def row_exponents_r3(a):
+    """KV_PATH_WINO88_I8F32R3's rule: the radix-256 one (row_exponents_r8) on fp64 rows; on fp32 rows (a is
+    fp32-representable, widened) the same rule read from the fp32 bits (i8_row_exponent_f32r: biased exponent
+    - 126, plus one when the top 6 fraction bits are all ones) -- both give the e with max < 127/128 2^e."""
+    return row_exponents_r8(a)
+
+
+def row_exponents_r3_f32(a):
+    """i8_row_exponent_f32r on fp32 rows a [..., K] (float32)."""
+    b = np.abs(a.astype(np.float32)).view(np.uint32)
+    m = b.max(axis=-1)
+    bump = ((m & np.uint32(0x7E0000)) == np.uint32(0x7E0000)).astype(np.int64)
+    return np.where(m > 0, (m >> np.uint32(23)).astype(np.int64) - 126 + bump, 0)
+
+
+def split_r3(a, e):
+    """a [..., K], e [...] -> the 3 radix-256 digits [3][..., K] int8, d_0 most significant: N = rint(a 2^(23 - e))
+    (ties to even), N = d_0 2^16 + d_1 2^8 + d_2 with every d_i in [-128, 127] (the bytes of N + 0x808080, each
+    minus 128)."""
+    N = np.rint(np.ldexp(np.asarray(a, dtype=np.float64), (23 - e[..., None]).astype(np.int32))).astype(np.int64)
+    u = (N + 0x808080) & 0xFFFFFF
+    return np.stack([(((u >> (8 * (2 - i))) & 255) - 128).astype(np.int8) for i in range(3)])
+
+
+def slots_r3(d):
+    """3 digits [3][...] -> the row lines' 4 slots [4][...] (slot 3 zero)."""
+    return np.concatenate([d, np.zeros_like(d[:1])])
+
+
+def gemm_r3(V, U, f32_rows=False):
+    """KV_PATH_WINO88_I8F32R3's GEMM (wino88i32_gemm_lagt_kernel<K, TPW, LJ, false, 3>): V [X][R][K], U [X][C][K]
+    -> (M [X][R][C] rounded to fp32 once, returned widened; V digits [4][X][R][K] with slot 3 zero; V exponents
+    [X][R]). The 6 pairs i + j <= 2 as 3 exact integer levels, combined m = L2, m = m 2^-8 + L_l (exact), scaled
+    by 2^(ev + eu - 14). f32_rows: V's exponents by the fp32-bit rule (the output kernel's and conv2's slice of
+    fp32 V), U's always from fp64."""
+    ev = row_exponents_r3_f32(V) if f32_rows else row_exponents_r3(V)
+    eu = row_exponents_r3(U)
+    dv, du = split_r3(V, ev), split_r3(U, eu)
+    fv, fu = dv.astype(np.float64), du.astype(np.float64)
+    lev = []
+    for l in range(3):
+        acc = np.zeros((V.shape[0], V.shape[1], U.shape[1]))
+        for i in range(l + 1):
+            acc += np.matmul(fv[i], np.swapaxes(fu[l - i], 1, 2))
+        lev.append(acc)
+    m = lev[2]
+    for l in (1, 0):
+        m = m * 0.00390625 + lev[l]  # exact, as the kernel's fma
+    M = np.ldexp(m, (ev[:, :, None] + eu[:, None, :] - 14).astype(np.int32)).astype(np.float32).astype(np.float64)
+    return M, slots_r3(dv), ev

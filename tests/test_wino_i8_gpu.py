@@ -74,6 +74,31 @@ def test_i8r_gemm_bit_exact(K, rows):
     assert np.array_equal(M.view(np.uint64), Mr.view(np.uint64)), float(np.abs(M - Mr).max())
 
 
+@pytest.mark.parametrize("K,rows", [(256, 128), (512, 128), (512, 256)])
+def test_i8r3_gemm_bit_exact(K, rows):
+    """KV_PATH_WINO88_I8F32R3: the slice kernel's 3 radix-256 digits (balanced bytes of rint(a 2^(23 - e)), the
+    exponent bumped at 127/128 of a power of two; slot 3 of each row line zero) and the 6-pair GEMM (3 digit
+    levels, lagt kernel), bit for bit against tests/_i8_digits (split_r3, gemm_r3): digits, exponents, M rounded
+    to fp32. Rows at the exponent rule's edges, an all-zero row, subnormals, +-2^-40."""
+    rng = np.random.default_rng(K + rows + 5)
+    V = rng.standard_normal((100, rows, K)) * np.exp2(rng.integers(-20, 20, size=(100, rows, 1)))
+    V[0, 0] = 0.0
+    V[1, 1] = np.nextafter(8.0 * 127 / 128, 0.0) * np.where(rng.random(K) < 0.5, -1.0, 1.0)
+    V[1, 2] = 8.0 * 127 / 128
+    V[1, 3] = -8.0 * 255 / 256
+    V[2, 2, ::3] = 1e-310
+    V[3, 3] = np.where(rng.random(K) < 0.5, -1.0, 1.0) * np.exp2(-40.0)
+    U = rng.standard_normal((100, 512, K)) * 0.05
+    U[5, 7] = 0.0
+    M, dg, ex = _run(V, U, 4, seg=3)
+    Mr, dv, evr = D.gemm_r3(V, U)
+    assert np.array_equal(ex, evr.astype(np.int32))
+    assert ex[1, 1] == 3 and ex[1, 2] == 4 and ex[1, 3] == 4
+    assert not dg.reshape(100, K // 32, rows, 4, 32)[:, :, :, 3].any()  # slot 3 unused
+    assert np.array_equal(dg.reshape(100, K // 32, rows, 4, 32), D.pack(dv).transpose(0, 1, 3, 2, 4))  # row lines
+    assert np.array_equal(M.view(np.uint64), Mr.view(np.uint64)), float(np.abs(M - Mr).max())
+
+
 @pytest.mark.parametrize("rows,resid", [(128, False), (128, True), (256, True)])
 def test_i8r_out_kernel_writes_the_two_kernel_forms_digits(rows, resid):
     """wino88i64r_out_kernel (KV_PREC_I8R4's output step: fp64 output transform + BN (+ residual) + ReLU, then
@@ -154,12 +179,14 @@ def _out(M, scale, shift, resid, flags):
 
 
 @pytest.mark.parametrize("rows,resid,seg", [(128, False, 0), (128, True, 0), (256, True, 0), (128, True, 2),
-                                            (256, False, 2)])
+                                            (256, False, 2), (128, False, 8), (256, True, 8), (128, False, 16),
+                                            (256, True, 16), (128, True, 24)])
 def test_i8f32_out_kernel_writes_the_slice_kernels_digits(rows, resid, seg):
-    """wino88i32_out_kernel (output transform + BN (+ residual) + ReLU, then the next V's row-line digits in
-    one kernel) == wino88_out_kernel's fp32 V + wino88i_slice_kernel, bit for bit: Y, every digit and every
-    exponent (per row, or per 256-channel segment: seg 2). Board 5 is all zero after the ReLU (its V rows:
-    exponent 0, digits 0); every 7th channel sits 2^-12 below the others."""
+    """wino88i32_out2_kernel (output transform + BN (+ residual) + ReLU, then the next V's row-line digits in
+    one kernel, the input transform run twice) == wino88_out_kernel's fp32 V + wino88i_slice_kernel, bit for
+    bit: Y, every digit and every exponent (per row, or per 256-channel segment: seg 2; seg 8: the held-V form
+    wino88i32_out_kernel). Board 5 is all zero after the ReLU (its V rows: exponent 0, digits 0); every 7th
+    channel sits 2^-12 below the others."""
     rng = np.random.default_rng(rows + resid + seg)
     M = (rng.standard_normal((100, rows, 512)) * 0.3).astype(np.float32)
     M[:, 5, :] = 0.0
@@ -172,12 +199,14 @@ def test_i8f32_out_kernel_writes_the_slice_kernels_digits(rows, resid, seg):
     if resid:
         R[5] = 0.0
     Yf, df, ef = _out(M, scale, shift, R, 1 | seg)
-    Ys, ds, es = _out(M, scale, shift, R, seg)
+    Ys, ds, es = _out(M, scale, shift, R, seg & 18)  # the slice-kernel form of the same exponents / digits
     assert np.array_equal(Yf.view(np.uint32), Ys.view(np.uint32))
     assert np.array_equal(ef, es)
     assert np.array_equal(df, ds)
     assert (ef[..., 5] == 0).all() and not df[:, :, 5].any()
     assert len(np.unique(ef)) > 3  # exponents actually vary across rows
+    if seg & 16:  # 3 radix-256 digits (KV_PATH_WINO88_I8F32R3): slot 3 of every row line zero
+        assert not df[:, :, :, 3].any()
 
 
 @pytest.mark.parametrize("rows,resid", [(128, False), (128, True), (256, True)])
