@@ -393,16 +393,16 @@ def _pmc_traffic(kname: str, bpl: int):
     return None, None
 
 
-def gemm_clock(device: int, rows: int, seconds: float):
+def gemm_clock(device: int, rows: int, seconds: float, digits: int = 4):
     """The clock this GPU holds under the headline GEMM (kv_dev_gemm_clock: the product's fp32-tower GEMM back to
     back for `seconds` on seeded digits, then one launch of its stamped build; MI355X_MICROARCH.md DVFS item 6),
     so a box-to-box spread of the line can be attributed."""
     import ctypes as C
     from knightvision_amd import _lib
     out = (C.c_double * 4)()
-    _lib.check(_lib.lib().kv_dev_gemm_clock(device, rows, seconds, out), "kv_dev_gemm_clock")
+    _lib.check(_lib.lib().kv_dev_gemm_clock(device, rows, digits, seconds, out), "kv_dev_gemm_clock")
     return {"sclk_mhz": out[0], "gemm_us_back_to_back": out[1], "launches": int(out[2]),
-            "tiles_per_workgroup": int(out[3]),
+            "tiles_per_workgroup": int(out[3]), "digits": digits,
             "method": f"median over workgroups of s_memtime delta / s_memrealtime delta x 100 MHz in a stamped build "
                       f"of the headline GEMM, launched right after {int(out[2])} back-to-back launches "
                       f"({seconds:.1f} s) on seeded random digits at {rows} boards; after the timed region"}
@@ -588,7 +588,9 @@ def main():
         flop_alg *= I8_DIGIT_PRODUCTS[path]
         peak = I8_MFMA_PEAK_TOPS
     traffic, traffic_src = _pmc_traffic(kname, bpl)
-    clock = gemm_clock(local, bpl, args.clock_seconds) if (path in (6, 7, 9) and args.clock_seconds > 0) else None
+    # (rows: the launch's padded rows per point, a multiple of the GEMM's 128-row tile)
+    clock = (gemm_clock(local, rows, args.clock_seconds, 3 if path == 9 else 4)
+             if (path in (6, 7, 9) and args.clock_seconds > 0) else None)
     clock_ranks = None
     if world > 1 and clock is not None:
         clock_ranks = [None] * world

@@ -343,7 +343,8 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
  * (rows a multiple of 128), folded BN scale / shift [512], resid [rows][64][512] or NULL -> Y
  * [rows][64][512] (= ReLU(A^T M A * scale + shift (+ resid))) and the next conv's V as row-line digits
  * [100][16][rows][4][32] with row exponents [100][rows]. fused bit 0 set: the product's one-kernel form
- * (wino88i32_out2_kernel; with bit 3 also set the held-V form wino88i32_out_kernel), clear:
+ * (KV_I8F32_OUT's choice; with bit 3 also set the 64-register wino88i32_out2_kernel, with bit 5 the
+ * persistent LDS-DMA wino88i32_outp_kernel; bit 4: 3 radix-256 digits, KV_ALGO_WINOGRAD88_I8R3's), clear:
  * wino88_out_kernel's fp32 V then the slice kernel (bit-identical); bit 1:
  * exponents per 256-channel segment ([100][2][rows]) instead of per row; bit 2 (KV_ALGO_WINOGRAD88_I8V's V,
  * per row): with bit 0 the one-kernel wino88i32v_out_kernel, without it wino88_out_kernel's Y, then
@@ -362,11 +363,12 @@ int kv_dev_wino88r_out(int device, const double* M, int rows, const float* scale
  * comparison of the variants. */
 int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, float* avg_us, float* M_out);
 /* The clock the chip holds under the headline GEMM (a diagnostic; MI355X_MICROARCH.md "DVFS give-back" item 6):
- * the product's fp32-tower GEMM (K 512, `rows` boards, seeded random digits) back to back for `seconds`, then
+ * the product's fp32-tower GEMM (K 512, `rows` boards, `digits` 4 or 3 (KV_ALGO_WINOGRAD88_I8R3), seeded random
+ * digits) back to back for `seconds`, then
  * one launch of its stamped build: out[0] = median over workgroups of (s_memtime delta / s_memrealtime delta)
  * x 100 MHz, out[1] = the back-to-back launches' mean time (us), out[2] = their count, out[3] = tiles per
  * workgroup of the stamped kernel. */
-int kv_dev_gemm_clock(int device, int rows, double seconds, double* out);
+int kv_dev_gemm_clock(int device, int rows, int digits, double seconds, double* out);
 
 /* ------------------------------------------------------- data pipeline ---
  * Full-rules chess (python-chess 1.999 semantics, csrc/kv_chess.cpp) for the

@@ -114,7 +114,7 @@ def _declare(L):
         "kv_host_libm": ([i, P(C.c_double), P(C.c_double), i, P(C.c_double)], i),
         "kv_dev_wino88i": ([i, P(C.c_double), i, P(C.c_double), i, i, i, P(C.c_double), P(C.c_int8), P(i)], i),
         "kv_dev_i8gemm_bench": ([i, i, i, i, i, P(C.c_float), P(C.c_float)], i),
-        "kv_dev_gemm_clock": ([i, i, C.c_double, P(C.c_double)], i),
+        "kv_dev_gemm_clock": ([i, i, i, C.c_double, P(C.c_double)], i),
         "kv_dev_wino88i32_out": ([i, P(C.c_float), i, P(C.c_float), P(C.c_float), P(C.c_float), i, P(C.c_float),
                                   P(C.c_int8), P(i)], i),
         "kv_dev_wino88r_out": ([i, P(C.c_double), i, P(C.c_float), P(C.c_float), P(C.c_float), i, P(C.c_float),

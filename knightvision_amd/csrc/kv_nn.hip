@@ -748,6 +748,15 @@ static hipError_t lds_opt_in(const void* fn, int bytes) {
 }
 
 // CUs of the current device, cached per device (the F(8x8) point split reads it per launch)
+// KV_OUT_STAG: the output kernels' phase stagger (kv_wino88i.h out_stagger), in units of s_sleep 127
+static int out_stag() {
+    static const int v = [] {
+        const char* e = getenv("KV_OUT_STAG");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 static int device_cus() {
     static std::mutex mu;
     static int cus[64] = {};
@@ -1354,7 +1363,8 @@ static int launch_wino88i64r_out(kv_net* net, int l, const double* M, int nb, in
                                  float* Y, hipStream_t st) {
     const float* W = net->w;
     hipLaunchKernelGGL((kv::wino88i64r_out_kernel<RESID, WRITE_Y>), dim3(1, nb), dim3(1024), 0, st, M, stride,
-                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, net->V8, net->ev8);
+                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, net->V8, net->ev8, out_stag(),
+                       device_cus());
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -1418,11 +1428,14 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, bool r8, hipStream_t s
 //                  kernel, bit-identical, profiles/r05_i8gemm_lag_ab.log); r4: the round-4
 //                  wino88i_gemm_kernel; p: the persistent wino88i32_gemm_kernel (5 % slower than r4,
 //                  profiles/r05_i8gemm_variants.log). The segment form always runs wino88i32_gemm_kernel ----
-//   KV_I8F32_OUT   hold: the output kernel that holds the next V's 50 values per lane across the exponent barrier
-//                  (wino88i32_out_kernel, one board per CU); default: wino88i32_out2_kernel (the 32 activations
-//                  held, the transform run twice, two boards per CU; the same bits)
+//   KV_I8F32_OUT   the output kernel (the same bits in every form): default the held-V one (wino88i32_out_kernel:
+//                  the next V's 50 values per lane held across the exponent barrier, one board per CU); r64:
+//                  wino88i32_out2_kernel (the 32 activations held, the transform run twice, 64 registers: two boards
+//                  per CU; 2-3 % slower forward, profiles/r06_out2_ab.log); p: wino88i32_outp_kernel (persistent,
+//                  M streamed through LDS by DMA two column steps ahead, across boards)
 struct I8f32Form {
-    bool seg = false, slice = false, r4 = false, persist = false, out_hold = false;
+    bool seg = false, slice = false, r4 = false, persist = false;
+    int out = 0;  // 0 held, 1 r64, 2 persistent
 };
 static const I8f32Form& i8f32_form() {
     static const I8f32Form f = [] {
@@ -1435,19 +1448,25 @@ static const I8f32Form& i8f32_form() {
         x.r4 = e && !strcmp(e, "r4") && !x.seg;
         x.persist = e && !strcmp(e, "p");
         e = getenv("KV_I8F32_OUT");
-        x.out_hold = e && !strcmp(e, "hold");
+        x.out = !e ? 0 : !strcmp(e, "r64") ? 1 : !strcmp(e, "p") ? 2 : 0;
         return x;
     }();
     return f;
 }
 
-// KV_OUT_STAG: the output kernels' phase stagger (kv_wino88i.h out_stagger), in units of s_sleep 127
-static int out_stag() {
-    static const int v = [] {
-        const char* e = getenv("KV_OUT_STAG");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
+// the persistent output kernel (kv_wino88i.h wino88i32_outp_kernel): one workgroup per CU (at most one per
+// board), each looping over boards blockIdx.x + k gridDim.x; M's stride must be the board count (rows)
+template <bool RESID, bool WRITE_Y>
+static int launch_wino88i32_outp(const float* M, int nb, int stride, const float* sc, const float* sh,
+                                 const float* resid, float* Y, int8_t* V8, int* ev, hipStream_t st, bool r3) {
+    KV_REQUIRE(stride == nb, KV_EINVAL, "wino88i32_outp: M stride %d != boards %d", stride, nb);
+    const int cus = device_cus();
+    const int grid = cus > 0 && cus < nb ? cus : nb;
+    auto kern = r3 ? kv::wino88i32_outp_kernel<RESID, WRITE_Y, true> : kv::wino88i32_outp_kernel<RESID, WRITE_Y, false>;
+    KV_HIP(lds_opt_in((const void*)kern, kv::kOutpLds));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), kv::kOutpLds, st, M, nb, sc, sh, resid, Y, V8, ev);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
 }
 
 // r3: KV_PATH_WINO88_I8F32R3's digits (3 radix-256, per-row exponents)
@@ -1458,13 +1477,16 @@ static int launch_wino88i32_out(kv_net* net, int l, const float* M, int nb, int 
     const int cus = device_cus(), stag = out_stag();
     const float* sc = W + net->off.scale[l];
     const float* sh = W + net->off.shift[l];
+    const int form = i8f32_form().out;
     if (seg)
         hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y, 256>), dim3(2, nb), dim3(512), 0, st, M, stride,
                            sc, sh, resid, Y, V8, ev, 0, 0);
-    else if (i8f32_form().out_hold && r3)
+    else if (form == 2)
+        return launch_wino88i32_outp<RESID, WRITE_Y>(M, nb, stride, sc, sh, resid, Y, V8, ev, st, r3);
+    else if (form == 0 && r3)
         hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y, 512, true>), dim3(1, nb), dim3(1024), 0, st, M,
                            stride, sc, sh, resid, Y, V8, ev, stag, cus);
-    else if (i8f32_form().out_hold)
+    else if (form == 0)
         hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y, 512>), dim3(1, nb), dim3(1024), 0, st, M, stride,
                            sc, sh, resid, Y, V8, ev, stag, cus);
     else if (r3)
@@ -1483,7 +1505,7 @@ static int launch_wino88i32v_out(kv_net* net, int l, const float* M, int nb, int
                                  float* Y, int8_t* V8, int* ev, hipStream_t st) {
     const float* W = net->w;
     hipLaunchKernelGGL((kv::wino88i32v_out_kernel<RESID, WRITE_Y>), dim3(1, nb), dim3(1024), 0, st, M, stride,
-                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, V8, ev);
+                       W + net->off.scale[l], W + net->off.shift[l], resid, Y, V8, ev, out_stag(), device_cus());
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -2412,10 +2434,12 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
 
 // the per-row fused output kernel of kv_dev_wino88i32_out: the held-V form (hold) or the product's default
 template <bool RESID, bool R3>
-static void dev_out_rowform(bool hold, const float* M, int rows, const float* sc, const float* sh, float* y,
+static void dev_out_rowform(int form, const float* M, int rows, const float* sc, const float* sh, float* y,
                             int8_t* v8, int* ev) {
     const float* rs = RESID ? y : nullptr;  // Y doubles as the residual (in place, as the tower runs it)
-    if (hold)
+    if (form == 2)
+        (void)launch_wino88i32_outp<RESID, true>(M, rows, rows, sc, sh, rs, y, v8, ev, 0, R3);
+    else if (form == 0)
         hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, true, 512, R3>), dim3(1, rows), dim3(1024), 0, 0, M, rows,
                            sc, sh, rs, y, v8, ev, 0, 0);
     else
@@ -2441,12 +2465,17 @@ int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scal
     KV_HIP(dy.alloc(ny));
     KV_HIP(dv.alloc(nm));
     KV_HIP(v8.alloc(nm * kv::kI8DigitsF32));
-    const bool seg = (fused & 2) != 0, v64 = (fused & 4) != 0, hold = (fused & 8) != 0, r3 = (fused & 16) != 0;
+    // the per-row fused form: bit 3 the 64-register kernel, bit 5 the persistent one, neither the product's
+    // default (KV_I8F32_OUT)
+    const bool seg = (fused & 2) != 0, v64 = (fused & 4) != 0, r64 = (fused & 8) != 0, r3 = (fused & 16) != 0;
+    const bool pers = (fused & 32) != 0;
+    const int form = pers ? 2 : r64 ? 1 : i8f32_form().out;
     KV_REQUIRE(!(seg && v64), KV_EINVAL, "kv_dev_wino88i32_out: fp64 V (bit 2) has per-row exponents only");
     KV_REQUIRE(!r3 || (!seg && !v64), KV_EINVAL, "kv_dev_wino88i32_out: bit 4 (3 radix-256 digits) has per-row "
                "fp32 V only");
-    KV_REQUIRE(!hold || ((fused & 1) && !seg && !v64), KV_EINVAL,
-               "kv_dev_wino88i32_out: bit 3 (the held form) is a form of the fused per-row kernel (bit 0 alone)");
+    KV_REQUIRE(!(r64 || pers) || ((fused & 1) && !seg && !v64 && !(r64 && pers)), KV_EINVAL,
+               "kv_dev_wino88i32_out: bits 3 / 5 (the 64-register / persistent form) are forms of the fused per-row "
+               "kernel");
     KV_HIP(ev.alloc((size_t)kv::W88_XI * rows * 2));
     KV_HIP(hipMemcpy(dm.p, M, nm * sizeof(float), hipMemcpyHostToDevice));
     KV_HIP(hipMemcpy(dsc.p, scale, 512 * sizeof(float), hipMemcpyHostToDevice));
@@ -2461,10 +2490,10 @@ int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scal
     if (v64 && (fused & 1)) {
         if (resid)
             hipLaunchKernelGGL((kv::wino88i32v_out_kernel<true, true>), dim3(1, rows), dim3(1024), 0, 0, dm.p, rows, sc,
-                               sh, dy.p, dy.p, v8.p, ev.p);
+                               sh, dy.p, dy.p, v8.p, ev.p, 0, 0);
         else
             hipLaunchKernelGGL((kv::wino88i32v_out_kernel<false, true>), dim3(1, rows), dim3(1024), 0, 0, dm.p, rows,
-                               sc, sh, nullptr, dy.p, v8.p, ev.p);
+                               sc, sh, nullptr, dy.p, v8.p, ev.p, 0, 0);
         KV_HIP(hipGetLastError());
     } else if (v64) {  // Y, then fp64 V from Y, then its digits
         if (resid)
@@ -2489,11 +2518,11 @@ int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scal
                 hipLaunchKernelGGL((kv::wino88i32_out_kernel<false, true, 256>), dim3(2, rows), dim3(512), 0, 0, dm.p,
                                    rows, sc, sh, nullptr, dy.p, v8.p, ev.p, 0, 0);
         } else if (resid) {
-            if (r3) dev_out_rowform<true, true>(hold, dm.p, rows, sc, sh, dy.p, v8.p, ev.p);
-            else dev_out_rowform<true, false>(hold, dm.p, rows, sc, sh, dy.p, v8.p, ev.p);
+            if (r3) dev_out_rowform<true, true>(form, dm.p, rows, sc, sh, dy.p, v8.p, ev.p);
+            else dev_out_rowform<true, false>(form, dm.p, rows, sc, sh, dy.p, v8.p, ev.p);
         } else {
-            if (r3) dev_out_rowform<false, true>(hold, dm.p, rows, sc, sh, dy.p, v8.p, ev.p);
-            else dev_out_rowform<false, false>(hold, dm.p, rows, sc, sh, dy.p, v8.p, ev.p);
+            if (r3) dev_out_rowform<false, true>(form, dm.p, rows, sc, sh, dy.p, v8.p, ev.p);
+            else dev_out_rowform<false, false>(form, dm.p, rows, sc, sh, dy.p, v8.p, ev.p);
         }
         KV_HIP(hipGetLastError());
     } else {
@@ -2545,10 +2574,10 @@ int kv_dev_wino88r_out(int device, const double* M, int rows, const float* scale
     if (fused) {
         if (resid)
             hipLaunchKernelGGL((kv::wino88i64r_out_kernel<true, true>), dim3(1, rows), dim3(1024), 0, 0, dm.p, rows,
-                               dsc.p, dsh.p, rs, dy.p, v8.p, ev.p);
+                               dsc.p, dsh.p, rs, dy.p, v8.p, ev.p, 0, 0);
         else
             hipLaunchKernelGGL((kv::wino88i64r_out_kernel<false, true>), dim3(1, rows), dim3(1024), 0, 0, dm.p, rows,
-                               dsc.p, dsh.p, rs, dy.p, v8.p, ev.p);
+                               dsc.p, dsh.p, rs, dy.p, v8.p, ev.p, 0, 0);
         KV_HIP(hipGetLastError());
     } else {  // wino88d_out_half_kernel's Y, wino88d_in_kernel's fp64 V, the radix-256 slice kernel
         if (resid)
@@ -2680,14 +2709,17 @@ int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, flo
 }
 
 // The in-kernel clock of the headline GEMM (MI355X_MICROARCH.md, DVFS give-back item 6): the product's fp32-tower
-// GEMM (i8f32_gemm<512>, the kernel and tile count it picks for `rows`) back to back on seeded random digits
+// GEMM (i8f32_gemm<512> on 4 digits or, digits 3, on 3 radix-256 ones; the kernel and tile count it picks for
+// `rows`) back to back on seeded random digits
 // for `seconds`, then ONE launch of the stamped build of the same kernel (wino88i32_gemm_lagt_kernel<., TPW, .,
 // true>; TPW 1 where the product runs single tiles): per workgroup (s_memtime delta) / (s_memrealtime delta)
 // x 100 MHz, the median over workgroups. out[0] = that clock in MHz, out[1] = the back-to-back launches'
 // mean time in us (HIP events), out[2] = launches timed, out[3] = tiles per workgroup of the stamped build.
-int kv_dev_gemm_clock(int device, int rows, double seconds, double* out) {
-    KV_REQUIRE(rows > 0 && rows % 128 == 0 && rows <= kMaxBoards && seconds > 0 && out, KV_EINVAL,
-               "kv_dev_gemm_clock: bad arguments (rows %d: a multiple of 128, at most %d)", rows, kMaxBoards);
+int kv_dev_gemm_clock(int device, int rows, int digits, double seconds, double* out) {
+    KV_REQUIRE(rows > 0 && rows % 128 == 0 && rows <= kMaxBoards && (digits == 3 || digits == 4) && seconds > 0 && out,
+               KV_EINVAL, "kv_dev_gemm_clock: bad arguments (rows %d: a multiple of 128, at most %d; digits %d: 3 or 4)",
+               rows, kMaxBoards, digits);
+    const bool r3 = digits == 3;
     KV_HIP(hipSetDevice(device));
     constexpr int K = 512;
     const size_t lv = (size_t)kv::W88_XI * (K / 32) * rows, lu = (size_t)kv::W88_XI * (K / 32) * 512;
@@ -2708,7 +2740,7 @@ int kv_dev_gemm_clock(int device, int rows, double seconds, double* out) {
     KV_HIP(hipGetLastError());
     int rc;
     for (int w = 0; w < 3; ++w)
-        if ((rc = i8f32_gemm<K>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, false, 0))) return rc;
+        if ((rc = i8f32_gemm<K>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, false, 0, r3))) return rc;
     KV_HIP(hipDeviceSynchronize());
     kv::DevEvent e0, e1;
     KV_HIP(e0.create());
@@ -2718,7 +2750,7 @@ int kv_dev_gemm_clock(int device, int rows, double seconds, double* out) {
     KV_HIP(hipEventRecord(e0.e, 0));
     while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count() < seconds) {
         for (int i = 0; i < 50; ++i)  // 50 launches queued per check (~25 ms at C3)
-            if ((rc = i8f32_gemm<K>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, false, 0))) return rc;
+            if ((rc = i8f32_gemm<K>(v8.p, ev.p, u8.p, eu.p, m.p, rows, rows, false, 0, r3))) return rc;
         launches += 50;
         KV_HIP(hipStreamSynchronize(0));
     }
@@ -2733,9 +2765,12 @@ int kv_dev_gemm_clock(int device, int rows, double seconds, double* out) {
     KV_REQUIRE(tiles % (8 * tpw) == 0, KV_EINVAL, "kv_dev_gemm_clock: %d tiles, %d per workgroup", tiles, tpw);
     KV_HIP(stamps.alloc((size_t)nwg * 4));
     constexpr int bytes = 3 * T::STAGE;
-    auto kern = tpw == 5   ? kv::wino88i32_gemm_lagt_kernel<K, 5, KV_I8F32_LJ, true>
-                : tpw == 4 ? kv::wino88i32_gemm_lagt_kernel<K, 4, KV_I8F32_LJ, true>
-                           : kv::wino88i32_gemm_lagt_kernel<K, 1, KV_I8F32_LJ, true>;
+    auto kern = r3 ? (tpw == 5   ? kv::wino88i32_gemm_lagt_kernel<K, 5, KV_I8R3_LJ, true, 3>
+                      : tpw == 4 ? kv::wino88i32_gemm_lagt_kernel<K, 4, KV_I8R3_LJ, true, 3>
+                                 : kv::wino88i32_gemm_lagt_kernel<K, 1, KV_I8R3_LJ, true, 3>)
+                   : (tpw == 5   ? kv::wino88i32_gemm_lagt_kernel<K, 5, KV_I8F32_LJ, true>
+                      : tpw == 4 ? kv::wino88i32_gemm_lagt_kernel<K, 4, KV_I8F32_LJ, true>
+                                 : kv::wino88i32_gemm_lagt_kernel<K, 1, KV_I8F32_LJ, true>);
     KV_HIP(lds_opt_in((const void*)kern, bytes));
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(T::THREADS), bytes, 0, v8.p, ev.p, u8.p, eu.p, m.p, rows, 512, rows,
                        stamps.p);

@@ -1720,6 +1720,164 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
     }
 }
 
+// wino88i32_outp_kernel: wino88i32_out_kernel<RESID, WRITE_Y, 512, R3>'s result, bit for bit, as a persistent
+// kernel that streams M through LDS by DMA. One 1,024-thread workgroup per CU loops over its boards (blockIdx.x,
+// + gridDim.x, ...); a board's output transform runs in 5 column steps, step jj reading M's points i*10 + jj and
+// i*10 + 5 + jj (the two plane halves' columns, 20 points x 512 channels = 40 KiB: a "slot"). Slots are copied
+// global -> LDS by global_load_lds_dwordx4 (1 KiB per wave-instruction, 40 per slot, dealt over the 16 waves)
+// into a ring of 3 LDS buffers, two steps ahead -- across the board boundary, so the next board's first two
+// slots land while this board reduces its row maxima and stores its digits. The M loads then hold no VGPRs (the
+// held kernel keeps 50 loads per lane in flight at the board's start, the 64-register one only 10), and a board's
+// load latency hides under its predecessor's back half. Same fmaf chains on the same values as the held kernel.
+// Waits: before step t the wave waits for its own pieces of slot t (vmcnt = its pieces of slot t + 1, the only
+// VMEM issued since) and lgkmcnt(0) (its reads of slot t - 1, whose buffer slot t + 2's copies overwrite once
+// every wave passes this barrier); the first two slots of a later board were drained by the vmcnt(0) before the
+// previous board's digit stores.
+template <bool RESID, bool WRITE_Y, bool R3 = false>
+__global__ __launch_bounds__(1024) void wino88i32_outp_kernel(const float* __restrict__ M, int rows,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift, const float* resid,
+                                                              float* Y, int8_t* __restrict__ V8,
+                                                              int* __restrict__ ex) {
+#pragma clang fp contract(off)
+    constexpr int NK = 512 / 32, NW = 16, NSLOT = 3, SLOT = 20 * 2048;
+    extern __shared__ __attribute__((aligned(16))) char lds_outp[];  // NSLOT slots, then red, exs
+    unsigned(*red)[2][5][16] = (unsigned(*)[2][5][16])(lds_outp + NSLOT * SLOT);
+    int* exs = (int*)(lds_outp + NSLOT * SLOT + NW * 2 * 5 * 16 * 4);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const int c = w * 32 + (lane & 31);
+    const int G = (int)gridDim.x;
+    const int nbw = ((int)rows - (int)blockIdx.x + G - 1) / G;  // boards of this workgroup
+    const int nsteps = 5 * nbw;
+    const int npieces = wu < 8 ? 3 : 2;  // this wave's pieces of a slot (40 = 16 + 16 + 8)
+    const float sc = scale[c], sh = shift[c];
+    const unsigned xs = (unsigned)rows * 512;
+    // slot of step t: board blockIdx.x + (t / 5) G, column step t % 5; LDS row r = hh * 10 + i holds point
+    // i * 10 + 5 hh + jj; piece q = row q / 2, channels 256 (q & 1) ..
+    auto issue = [&](int t) {
+        if (t >= nsteps) return;
+        const int b = (int)blockIdx.x + (t / 5) * G, jj = t % 5;
+        char* dst = lds_outp + (t % NSLOT) * SLOT;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int q = wu + 16 * k;
+            if (q < 40) {
+                const int r = q >> 1, hh = r / 10, i = r - 10 * hh;
+                const float* src = M + (unsigned)(i * 10 + 5 * hh + jj) * xs + (unsigned)b * 512 + (q & 1) * 256 +
+                                   lane * 4;
+                __builtin_amdgcn_global_load_lds((const void*)src,
+                                                 (__attribute__((address_space(3))) void*)(dst + q * 1024), 16, 0, 0);
+            }
+        }
+    };
+    issue(0);
+    issue(1);
+    int t = 0;
+    for (int k = 0; k < nbw; ++k) {
+        const int b = (int)blockIdx.x + k * G;
+        float tt[8][5];  // A8^T m of this half's columns 5h + jj
+#pragma unroll
+        for (int jj = 0; jj < 5; ++jj, ++t) {
+            if (k > 0 && jj < 2) {  // drained before the previous board's digit stores
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            } else {
+                const int younger = t + 1 < nsteps ? npieces : 0;  // slot t + 1's pieces, issued after slot t's
+                if (younger == 3)
+                    asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+                else if (younger == 2)
+                    asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            }
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            issue(t + 2);  // into slot t - 1's buffer: every wave has read it (lgkmcnt(0) before this barrier)
+            const float* sl = (const float*)(lds_outp + (t % NSLOT) * SLOT) + h * 10 * 512 + c;
+            float col[10], o[8];
+#pragma unroll
+            for (int i = 0; i < 10; ++i) col[i] = sl[i * 512];
+            w88_at(col, o);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) tt[i][jj] = o[i];
+        }
+        // the row pass, BN (+ residual) + ReLU (+ Y) -- wino88_out_plane_half's
+        float x2[4][8];
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+            float row[10];
+#pragma unroll
+            for (int jj = 0; jj < 5; ++jj) {
+                float lo = tt[ii][jj], hi = tt[4 + ii][jj];
+                half_swap(lo, hi);
+                row[jj] = lo;
+                row[5 + jj] = hi;
+            }
+            float o[8];
+            w88_at(row, o);
+            const int i = 4 * h + ii;
+            float res[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) res[j] = RESID ? resid[((unsigned)b * 64 + i * 8 + j) * 512 + c] : 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float v = o[j] * sc + sh;
+                if (RESID) v += res[j];
+                v = v > 0.f ? v : 0.f;
+                if (WRITE_Y) Y[((unsigned)b * 64 + i * 8 + j) * 512 + c] = v;
+                x2[ii][j] = v;
+            }
+        }
+        // the next V (held: 50 values per lane), its row maxima, exponents, digits -- wino88i32_out_kernel's
+        float vk[5][10];
+        {
+            float t2[10][4];
+            wino88_input_cols(x2, h, t2);
+#pragma unroll
+            for (int aa = 0; aa < 5; ++aa) wino88_input_row(t2, h, aa, vk[aa]);
+        }
+#pragma unroll
+        for (int aa = 0; aa < 5; ++aa) {
+            unsigned m[10];
+#pragma unroll
+            for (int bb = 0; bb < 10; ++bb) m[bb] = i8_half_max_dpp(__float_as_uint(vk[aa][bb]) & 0x7fffffffu);
+            if ((lane & 31) == 16) {
+                uint4* rr = (uint4*)&red[w][h][aa][0];
+                rr[0] = make_uint4(m[0], m[1], m[2], m[3]);
+                rr[1] = make_uint4(m[4], m[5], m[6], m[7]);
+                *(uint2*)&red[w][h][aa][8] = make_uint2(m[8], m[9]);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 100) {
+            const int xi = threadIdx.x, a = xi / 10, bb = xi % 10, hh = a / 5, aa = a % 5;
+            unsigned m = 0;
+#pragma unroll
+            for (int ww = 0; ww < NW; ++ww) m = red[ww][hh][aa][bb] > m ? red[ww][hh][aa][bb] : m;
+            const int e = i8f32_row_exponent<R3>(m);
+            exs[xi] = e;
+            ex[(size_t)xi * rows + b] = e;
+        }
+        __syncthreads();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next board's first two slots (and Y) landed
+        const int q = lane & 3;
+        const unsigned off0 = ((unsigned)(c >> 5) * rows + b) * 128 + q * 32 + (c & 28), xstride = NK * rows * 128;
+        unsigned* const dst = (unsigned*)V8;
+#pragma unroll
+        for (int aa = 0; aa < 5; ++aa) {
+            const int a = 5 * h + aa;
+#pragma unroll
+            for (int bb = 0; bb < 10; ++bb) {
+                const int xi = a * 10 + bb;
+                const unsigned P = i8f32_digits<R3>(vk[aa][bb], exs[xi]);
+                __builtin_nontemporal_store(i8_quad_transpose(P, lane), &dst[(off0 + (unsigned)xi * xstride) >> 2]);
+            }
+        }
+    }
+}
+
+constexpr int kOutpLds = 3 * 20 * 2048 + 16 * 2 * 5 * 16 * 4 + 100 * 4;  // wino88i32_outp_kernel's dynamic LDS
+
 // ---- the fp32 tower with fp64 input transforms (KV_PATH_WINO88_I8F32V) ----
 // The same tower as KV_PATH_WINO88_I8F32 (fp32 M, output transform and activations, the 4-digit GEMM)
 // except that every conv's V is the fp64 input transform of its fp32 input, cut to 4 digits from fp64:
@@ -1773,13 +1931,14 @@ __device__ inline void wino88d_input_row_of_cols(float (&xc)[4][8], int aa, doub
 template <bool RESID, bool WRITE_Y, class MT>
 __device__ inline void wino88v_out_body(const MT* __restrict__ M, int rows, const float* __restrict__ scale,
                                         const float* __restrict__ shift, const float* resid, float* Y,
-                                        int8_t* __restrict__ V8, int* __restrict__ ex) {
+                                        int8_t* __restrict__ V8, int* __restrict__ ex, int stag, int first) {
     constexpr bool R8 = sizeof(MT) == 8;
     constexpr int NK = 512 / 32, NW = 16;
     __shared__ __attribute__((aligned(16))) unsigned red[NW][2][5][16];
     __shared__ int exs[100];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
     const int c = w * 32 + (lane & 31), b = blockIdx.y;
+    out_stagger(b, stag, first);
     float xc[4][8];  // the half's columns 4h .. 4h+3, all 8 rows (after the half exchange)
     {
         float x2[4][8];
@@ -1852,16 +2011,18 @@ template <bool RESID, bool WRITE_Y>
 __global__ __launch_bounds__(1024) void wino88i32v_out_kernel(const float* __restrict__ M, int rows,
                                                               const float* __restrict__ scale,
                                                               const float* __restrict__ shift, const float* resid,
-                                                              float* Y, int8_t* __restrict__ V8, int* __restrict__ ex) {
-    wino88v_out_body<RESID, WRITE_Y>(M, rows, scale, shift, resid, Y, V8, ex);
+                                                              float* Y, int8_t* __restrict__ V8, int* __restrict__ ex,
+                                                              int stag, int first) {
+    wino88v_out_body<RESID, WRITE_Y>(M, rows, scale, shift, resid, Y, V8, ex, stag, first);
 }
 
 template <bool RESID, bool WRITE_Y>
 __global__ __launch_bounds__(1024) void wino88i64r_out_kernel(const double* __restrict__ M, int rows,
                                                               const float* __restrict__ scale,
                                                               const float* __restrict__ shift, const float* resid,
-                                                              float* Y, int8_t* __restrict__ V8, int* __restrict__ ex) {
-    wino88v_out_body<RESID, WRITE_Y>(M, rows, scale, shift, resid, Y, V8, ex);
+                                                              float* Y, int8_t* __restrict__ V8, int* __restrict__ ex,
+                                                              int stag, int first) {
+    wino88v_out_body<RESID, WRITE_Y>(M, rows, scale, shift, resid, Y, V8, ex, stag, first);
 }
 
 }  // namespace kv

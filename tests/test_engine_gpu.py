@@ -142,7 +142,7 @@ GROUPS = {"pg_init_mm80": ("init", 80, 16), "pg_peaked_mm80": ("peaked", 80, 16)
 @pytest.mark.parametrize("precision,algo", [("fp32", "auto"), ("f16x3", "auto"), ("f64w", "auto"), ("i8x5", "auto"),
                                             ("i8r4", "auto"),
                                             ("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "winograd88i8"),
-                                            ("fp32", "winograd88i8v")])
+                                            ("fp32", "winograd88i8v"), ("fp32", "winograd88i8r3")])
 @pytest.mark.parametrize("group", list(GROUPS))
 def test_engine_games_match_reference(golden_dir, group, precision, algo):
     """Complete games vs the reference's golden games. The slot counts here put

@@ -18,12 +18,16 @@ TOL_P, TOL_V = 1e-4, 1e-5
 # on fp64 MFMA / the same domain with the GEMMs on int8 digits; ("fp32", "winograd88i8") the fp32 F(8x8) tower with
 # its GEMMs on int8 digits, ("fp32", "winograd88i8v") the same with fp64 input transforms
 MODES = [("fp32", "direct"), ("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "winograd88i8"),
-         ("fp32", "winograd88i8v"), ("fp32", "auto"), ("f16x3", "winograd48"), ("f64w", "auto"), ("i8x5", "auto"),
-         ("i8r4", "auto")]
+         ("fp32", "winograd88i8v"), ("fp32", "winograd88i8r3"), ("fp32", "auto"), ("f16x3", "winograd48"),
+         ("f64w", "auto"), ("i8x5", "auto"), ("i8r4", "auto")]
 # the explicit fp32 / f16x3 Winograd towers are outside the tolerance at trained magnitudes ("stress": 1.2e-3 to
 # 3.6e-3); AUTO measures that at load time and runs the fp64 Winograd domain instead (test_nn_accuracy_gpu.py)
 UNGUARDED = {("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "winograd88i8"), ("fp32", "winograd88i8v"),
-             ("f16x3", "winograd48")}
+             ("fp32", "winograd88i8r3"), ("f16x3", "winograd48")}
+# the 24-bit tower (3 radix-256 digits) is also outside at the peaked set's logit magnitudes (|logit| up to 8.2:
+# 1.03e-4, a relative 1.3e-5); AUTO measures that too and takes it only where it holds the budget (random-init
+# weights: 2.4e-6 on the calibration boards)
+UNGUARDED_PEAKED = {("fp32", "winograd88i8r3")}
 
 
 def _net(variant, precision="fp32", algo="auto"):
@@ -39,6 +43,8 @@ def _net(variant, precision="fp32", algo="auto"):
 def test_forward_matches_reference_golden(golden_dir, variant, precision, algo):
     if variant == "stress" and (precision, algo) in UNGUARDED:
         pytest.skip("explicit Winograd fp32 / f16x3: outside the tolerance at trained magnitudes by design")
+    if variant == "peaked" and (precision, algo) in UNGUARDED_PEAKED:
+        pytest.skip("explicit 24-bit tower: outside the tolerance at peaked-logit magnitudes; AUTO guards it")
     g = np.load(os.path.join(golden_dir, "nn.npz"))
     m = _net(variant, precision, algo)
     p, v = m(torch.from_numpy(g["planes"]).cuda())
@@ -96,7 +102,7 @@ def test_batch_invariance(precision):
     assert float((p_16 - p_all[:16]).abs().max()) < 1e-4
 
 
-@pytest.mark.parametrize("precision", ["fp32", "f64w", "i8x5", "i8r4", "fp32-i8"])
+@pytest.mark.parametrize("precision", ["fp32", "f64w", "i8x5", "i8r4", "fp32-i8", "fp32-r3"])
 def test_wino88_batch_invariance(precision):
     """F(8x8) (one row per board): a board's outputs are the same bits at 20
     boards (padded to 32: 32-row GEMM tiles, k-tiles of 32), 80 / 96 (padded to
@@ -109,7 +115,8 @@ def test_wino88_batch_invariance(precision):
     codes = rng.integers(0, 13, size=(512, 64)) * (rng.random((512, 64)) < 0.4)
     planes = torch.from_numpy(codes_to_planes(codes)).cuda()
     m = (_net("peaked", "fp32", "winograd88") if precision == "fp32" else
-         _net("peaked", "fp32", "winograd88i8") if precision == "fp32-i8" else _net("peaked", precision, "auto"))
+         _net("peaked", "fp32", "winograd88i8") if precision == "fp32-i8" else
+         _net("peaked", "fp32", "winograd88i8r3") if precision == "fp32-r3" else _net("peaked", precision, "auto"))
     p_l, v_l = m(planes)
     for lo, hi in ((0, 40), (20, 40), (0, 300), (0, 96), (16, 96)) + (((0, 1), (5, 8)) if precision != "fp32" else ()):
         p, v = m(planes[lo:hi])

@@ -188,9 +188,11 @@ def test_bench_json_line_contract():
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in d["cpu_baseline"], k
     c = d["calibration"]  # the conv paths the run used, chosen by the load-time calibration (random-init: the
-    # fp32 F(8x8) tower on int8-digit GEMMs)
-    assert c["calibrated"] and c["path_large"] == "winograd88_i8f32" and c["path_small"] == "direct"
-    assert d["conv_path"] == "winograd88_i8f32" and d["roofline"]["peak"] == 5000.0  # int8 operations vs the int8 peak
+    # fp32 F(8x8) tower on 3 radix-256 int8 digits)
+    assert c["calibrated"] and c["path_large"] == "winograd88_i8f32r3" and c["path_small"] == "direct"
+    assert d["conv_path"] == "winograd88_i8f32r3" and d["roofline"]["peak"] == 5000.0  # int8 operations vs the peak
+    assert d["roofline"]["kernel"].startswith("wino88i32_gemm_lagt_kernel<512,")  # the name the library reported
+    assert d["roofline"]["sclk_mhz"] is None or 500 < d["roofline"]["sclk_mhz"] < 2600
     assert d["trained_weights_path"]["value"] > 0
 
 

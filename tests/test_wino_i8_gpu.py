@@ -180,13 +180,15 @@ def _out(M, scale, shift, resid, flags):
 
 @pytest.mark.parametrize("rows,resid,seg", [(128, False, 0), (128, True, 0), (256, True, 0), (128, True, 2),
                                             (256, False, 2), (128, False, 8), (256, True, 8), (128, False, 16),
-                                            (256, True, 16), (128, True, 24)])
+                                            (256, True, 16), (128, True, 24), (128, False, 32), (384, True, 32),
+                                            (256, True, 48)])
 def test_i8f32_out_kernel_writes_the_slice_kernels_digits(rows, resid, seg):
-    """wino88i32_out2_kernel (output transform + BN (+ residual) + ReLU, then the next V's row-line digits in
-    one kernel, the input transform run twice) == wino88_out_kernel's fp32 V + wino88i_slice_kernel, bit for
-    bit: Y, every digit and every exponent (per row, or per 256-channel segment: seg 2; seg 8: the held-V form
-    wino88i32_out_kernel). Board 5 is all zero after the ReLU (its V rows: exponent 0, digits 0); every 7th
-    channel sits 2^-12 below the others."""
+    """The fused output kernel (output transform + BN (+ residual) + ReLU, then the next V's row-line digits in
+    one kernel; the product's form, KV_I8F32_OUT) == wino88_out_kernel's fp32 V + wino88i_slice_kernel, bit for
+    bit: Y, every digit and every exponent (per row, or per 256-channel segment: seg 2; seg 8: the 64-register
+    form wino88i32_out2_kernel; seg 32: the persistent LDS-DMA form wino88i32_outp_kernel, 384 rows = 1.5 boards
+    per CU, so workgroups loop over different board counts; seg 16: 3 radix-256 digits). Board 5 is all zero
+    after the ReLU (its V rows: exponent 0, digits 0); every 7th channel sits 2^-12 below the others."""
     rng = np.random.default_rng(rows + resid + seg)
     M = (rng.standard_normal((100, rows, 512)) * 0.3).astype(np.float32)
     M[:, 5, :] = 0.0

@@ -51,6 +51,7 @@ def main():
                 break
         games = eng.games()
         st = eng.stats()
+        cal = eng.calibration()
     plies = np.sort(games["plies"]).tolist()
     reasons = {REASONS.get(int(r), "?"): int((games["reason"] == r).sum()) for r in np.unique(games["reason"])}
     n = len(plies)
@@ -58,14 +59,16 @@ def main():
     sd = float(np.std(plies, ddof=1)) if n > 1 else None
     se = sd / np.sqrt(n) if sd is not None else None
     res = {"what": "complete MCTS games at the C3 settings (game ids 0..n-1 of the C3 run: 800 sims/move, "
-                   "uncapped, per-game seeds 42+id, random-init weights seed 42, c_puct 1.5)",
+                   "uncapped, per-game seeds 42+id, random-init weights seed 42, c_puct 1.5) on the conv path the "
+                   "AUTO calibration chose (conv_path): the games the headline plays",
            "sims": a.sims, "games": a.games, "finished": n, "still_running": a.games - n,
            "plies_played_by_running_games": ply if n < a.games else None,
            "mean_plies_finished": mean, "median_plies_finished": float(np.median(plies)) if plies else None,
            "sd_plies": sd, "se_mean_plies": se, "se_frac": (se / mean) if se else None,
            "ci95_mean_plies": [mean - 1.96 * se, mean + 1.96 * se] if se else None,
            "plies": plies, "reasons": reasons, "wall_s": time.perf_counter() - t0,
-           "total_sims": int(st["sims"])}
+           "total_sims": int(st["sims"]), "conv_path": cal["path_large"], "conv_path_small": cal["path_small"],
+           "dom_kernel": st["dom_kernel"]}
     line = json.dumps(res)
     print(line, flush=True)
     if a.out:
