@@ -48,7 +48,8 @@ FLOP_WINO88_GEMM_PER_BOARD = 52428800  # the fp32 default, F(8x8,3x3) GEMMs: 2 *
 FP32_MFMA_PEAK_TFLOPS = 157.3         # MI355X_MICROARCH.md, f32-input MFMA (dense)
 FP64_MFMA_PEAK_TFLOPS = 78.6          # AMD's MI355X FP64 matrix spec figure (the guides give no f64 row; not
                                       # measured here)
-PATH_NAMES = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3",
+PATH_NAMES = {0: "direct", 1: "winograd48 (retired)", 2: "winograd88", 3: "winograd88_f64",
+              4: "winograd48_f16x3 (retired)",
               5: "winograd88_i8", 6: "winograd88_i8f32", 7: "winograd88_i8f32v",
               8: "winograd88_i8r", 9: "winograd88_i8f32r3"}  # KV_PATH_*
 BF16_MFMA_PEAK_TFLOPS = 2500.0        # dense bf16 MFMA
@@ -68,8 +69,8 @@ def parse():
     ap.add_argument("--mode", choices=["mcts", "ref"], default=os.environ.get("KV_BENCH_MODE", "mcts"))
     ap.add_argument("--slots", type=int, default=2048)
     ap.add_argument("--sims", type=int, default=800)
-    ap.add_argument("--precision", choices=["fp32", "f16x3", "f64w", "i8x5", "i8r4"], default="fp32")
-    ap.add_argument("--algo", choices=["auto", "direct", "winograd48", "winograd88", "winograd88i8", "winograd88i8v",
+    ap.add_argument("--precision", choices=["fp32", "f64w", "i8x5", "i8r4"], default="fp32")
+    ap.add_argument("--algo", choices=["auto", "direct", "winograd88", "winograd88i8", "winograd88i8v",
                                        "winograd88i8r3"],
                     default="auto",
                     help="conv algorithm of the fp32 tower (auto: the library's calibrated choice per weight load -- "
@@ -86,7 +87,7 @@ def parse():
     ap.add_argument("--f64w-steps", type=int, default=0,
                     help="also time this many moves with the fp64 Winograd domain on fp64 MFMA (KV_PREC_F64W), "
                          "reported under 'f64w_path'")
-    ap.add_argument("--alt-precision", default="f16x3",
+    ap.add_argument("--alt-precision", default="",
                     help="also measure this network precision (reported under 'alt_precision'; '' to skip)")
     ap.add_argument("--alt-algo", default="winograd88",
                     help="fp32 only: also time this conv algorithm for --alt-steps moves beside the headline's own "
@@ -119,18 +120,23 @@ def parse():
     return ap.parse_args()
 
 
-def _mcts_game_length(sims: int):
+def _mcts_game_length(sims: int, conv_path: str = None):
     """The newest committed game-length run at these search settings (tools/mcts_game_length.py: complete
-    MCTS games at C3's settings, game ids 0..n-1 of the C3 run played to the end), or (None, None)."""
+    MCTS games at C3's settings, game ids 0..n-1 of the C3 run played to the end), preferring one played on
+    `conv_path` (the conv path the run's AUTO chose: those are the games it plays), or (None, None)."""
     d = os.path.join(HERE, "profiles")
+    found = []
     for f in sorted((x for x in os.listdir(d) if "mcts_game_length" in x and x.endswith(".json")), reverse=True):
         try:
             gl = json.loads(open(os.path.join(d, f)).read().splitlines()[-1])
         except (OSError, ValueError, IndexError):
             continue
         if gl.get("sims") == sims and gl.get("still_running") == 0 and gl.get("finished", 0) >= 2:
+            found.append((gl, f))
+    for gl, f in found:
+        if conv_path is not None and gl.get("conv_path") == conv_path:
             return gl, f
-    return None, None
+    return found[0] if found else (None, None)
 
 
 def _free_port() -> int:
@@ -347,7 +353,7 @@ def gemm_label(path: int, kernel: str):
     if fam == "wino88d_gemm_kernel":
         return name, " (residual-tower Winograd F(8x8,3x3) GEMMs in fp64, 100 points, v_mfma_f64_16x16x4_f64)"
     if fam == "wino_gemm_h3_kernel":
-        return name, " (residual-tower Winograd F(4x8,3x3) GEMMs, f16x3 split)"
+        return name, " (residual-tower Winograd F(4x8,3x3) GEMMs, f16x3 split; retired)"
     if fam == "wino_gemm_kernel":
         return name, " (residual-tower Winograd F(4x8,3x3) GEMMs, 60 points)"
     if fam == "conv3x3_kernel":
@@ -549,7 +555,7 @@ def main():
         alt = measure(args.alt_precision, steps=args.alt_steps, warmup=args.alt_warmup, tag="alt " + args.alt_precision)
     alt_algo = None
     if args.alt_algo and args.precision == "fp32" and PATH_NAMES.get(m["dom_path"]) != {
-            "winograd88": "winograd88", "winograd48": "winograd48", "direct": "direct",
+            "winograd88": "winograd88", "direct": "direct",
             "winograd88i8": "winograd88_i8f32"}.get(args.alt_algo):
         alt_algo = measure("fp32", args.alt_algo, steps=args.alt_steps, warmup=args.alt_warmup,
                            tag="alt " + args.alt_algo)
@@ -577,7 +583,7 @@ def main():
     # roofline of the dominant kernel, timed with HIP events on the engine stream: one residual-tower
     # Winograd GEMM layer per forward (fp32 F(8x8) by default; [boards x 512] x [512 x 512] per point) or, for
     # the direct algorithm, the residual convs
-    path = m["dom_path"]  # KV_PATH_*: 0 direct, 1 F(4x8), 2 F(8x8) fp32 (the fp32 default), 3 F(8x8) fp64, 4 f16x3
+    path = m["dom_path"]  # KV_PATH_* (include/kv.h): 0 direct, 2 F(8x8) fp32, 3 F(8x8) fp64, 5-9 int8-digit towers
     per_board, bpl, rows = dom_units(path, m["dom_flop"], G)
     flop_alg = per_board * bpl
     achieved = flop_alg / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else None
@@ -608,7 +614,7 @@ def main():
                     "note": "latency-bound: one wave per game (select descent + leaf getValidMoves, backup)"}
 
     # complete-game length at these search settings (per-game seeds: the same distribution at any slot count)
-    gl, gl_file = _mcts_game_length(sims) if mcts else (None, None)
+    gl, gl_file = _mcts_game_length(sims, PATH_NAMES.get(path)) if mcts else (None, None)
     steady = bool(gl) and warmup >= 2 * gl["mean_plies_finished"]  # slots have cycled through whole games
     if rank == 0:
         if mcts:
@@ -651,7 +657,8 @@ def main():
                                            if gl is not None and gl.get("ci95_mean_plies") else None),
             "games_per_hour_steady_note": (
                 f"this run's measured plies/s x 3600 / the mean length of complete games at these settings, "
-                f"{gl['mean_plies_finished']:.1f} plies (game ids 0-{gl['games'] - 1} played to the end: "
+                f"{gl['mean_plies_finished']:.1f} plies (game ids 0-{gl['games'] - 1} played to the end on "
+                f"{gl.get('conv_path', 'winograd88 (round 3)')}: "
                 f"{gl['reasons']}; median {gl['median_plies_finished']:.0f}, range {gl['plies'][0]}-"
                 f"{gl['plies'][-1]}, standard error {100 * gl['se_frac']:.1f} %; the 95 % interval of the mean "
                 f"gives games_per_hour_steady_ci95) -- profiles/{gl_file}, tools/mcts_game_length.py"
@@ -785,15 +792,11 @@ def main():
         if alt is not None:
             # dominant launch of the alternate run (Winograd GEMM or direct residual conv), fp32-equivalent FLOPs
             a_ach = (alt["dom_flop"] / (alt["conv_ms"] * 1e-3) / 1e12) if alt["conv_ms"] > 0 else None
-            a_prod = {"f16x3": 3}.get(args.alt_precision)
+            a_prod = None  # bf16-class MFMA products per fp32 product (none of the remaining precisions)
             notes = {
-                "f16x3": "fp32-accurate split: every fp32 operand scaled by an exact power of two (per layer for "
-                         "the weights, per board for the activations) and split into 2 fp16 pieces (22 significant "
-                         "bits), the 3 piece products of weight >= 2^-22 on f16 MFMA, fp32 accumulation, Winograd "
-                         "F(4x8) tower; batch-invariant; logits within the fp32 tolerance (tests/test_nn_gpu.py); "
-                         "narrower operands than the reference's fp32, so never the headline",
-                "f64w": "the fp64 Winograd domain (KV_PREC_F64W)",
-                "fp32": "exact f32 MFMA"}
+                "f64w": "the fp64 Winograd domain on v_mfma_f64 (KV_PREC_F64W)",
+                "i8r4": "the fp64 Winograd domain on 4 radix-256 int8 digits (KV_PREC_I8R4)",
+                "i8x5": "the fp64 Winograd domain on 5 radix-128 int8 digits (KV_PREC_I8X5)"}
             out["alt_precision"] = {
                 "precision": args.alt_precision, "note": notes.get(args.alt_precision, ""),
                 "value": (alt["sims"] if mcts else alt["plies"]) / alt["dt"], "unit": unit,

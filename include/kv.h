@@ -73,12 +73,6 @@ int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv);
  * KV_PREC_FP32   fp32 (default; the parity mode). Under KV_ALGO_AUTO the net
  *                picks its conv path per weight load by measuring the
  *                candidates against an fp64 forward (kv_net_calibration).
- * KV_PREC_F16X3  F(4x8) Winograd GEMMs on fp16 MFMA: both operands split into
- *                two fp16 pieces (22 significant bits) after exact power-of-two
- *                scaling (per layer for the weights, per board for the
- *                activations), the three products of weight >= 2^-22 with fp32
- *                accumulation (> 16 boards; fp32 direct below). Batch-invariant;
- *                reported beside the fp32 headline, not a parity mode.
  * KV_PREC_F64W   Winograd F(8x8) with every Winograd-domain quantity (U, V, M,
  *                transforms) in fp64, on v_mfma_f64_16x16x4_f64, at every batch
  *                size: logits within ~3e-6 of an fp64 forward on every weight set
@@ -96,9 +90,9 @@ int kv_net_last_timing(kv_net* net, float* conv_ms, int* n_conv);
  *                balanced bytes) and the 13 digit pairs i + j <= 4 of 16:
  *                13 int8 GEMMs instead of 15 over 4 digit planes instead of
  *                5 (AUTO's candidate before KV_PREC_I8X5).
- * Values 1 and 2 (bf16x3 / bf16x6) were retired in round 4: KV_EINVAL. */
+ * Values 1 and 2 (bf16x3 / bf16x6) were retired in round 4, 3 (f16x3: F(4x8) GEMMs on fp16 MFMA with both
+ * operands split in two fp16 pieces) in round 6 -- no configuration chose them: KV_EINVAL. */
 #define KV_PREC_FP32 0
-#define KV_PREC_F16X3 3
 #define KV_PREC_F64W 4
 #define KV_PREC_I8X5 5
 #define KV_PREC_I8R4 6
@@ -117,10 +111,8 @@ int kv_net_set_precision(kv_net* net, int precision);
  *                   on fp64 MFMA; <= 16 boards direct (split-K), else F(8x8)
  *                   fp64 (kv_net_calibration reports it)
  * KV_ALGO_DIRECT    implicit GEMM over the 9 taps (exact fp32 products)
- * KV_ALGO_WINOGRAD48 F(4x8,3x3): 60 GEMMs of 2 tiles x Cin x Cout per board,
- *                   4.8x fewer FLOPs than direct (fp32 and f16x3)
  * KV_ALGO_WINOGRAD88 F(8x8,3x3): 100 GEMMs of 1 tile x Cin x Cout per board,
- *                   5.76x fewer FLOPs than direct (fp32; f16x3 runs F(4x8))
+ *                   5.76x fewer FLOPs than direct (fp32 MFMA)
  * KV_ALGO_WINOGRAD88_I8 the F(8x8) fp32 tower (fp32 U, V, M, transforms) with
  *                   each GEMM on 4 int8 digits per value: per-row 28-bit
  *                   block fixed point, the 10 digit pairs i + j <= 3, exact
@@ -135,12 +127,11 @@ int kv_net_set_precision(kv_net* net, int precision);
  *                   bytes), the 6 digit pairs i + j <= 2 of 9, exact int32
  *                   levels, one rounding to fp32 -- 6 int8 GEMMs per point
  *                   instead of 10 (AUTO's first candidate)
- * Value 2 (F(4x4)) was retired in round 4: KV_EINVAL. Setting the precision or
+ * Values 2 (F(4x4)) and 3 (F(4x8)) were retired in rounds 4 and 6: KV_EINVAL. Setting the precision or
  * the algorithm of a loaded net re-prepares it (synchronous).
  * Results are batch-invariant inside a class (<= 16 boards, > 16 boards). */
 #define KV_ALGO_AUTO 0
 #define KV_ALGO_DIRECT 1
-#define KV_ALGO_WINOGRAD48 3
 #define KV_ALGO_WINOGRAD88 4
 #define KV_ALGO_WINOGRAD88_I8 5
 #define KV_ALGO_WINOGRAD88_I8V 6
@@ -148,11 +139,9 @@ int kv_net_set_precision(kv_net* net, int precision);
 int kv_net_set_algo(kv_net* net, int algo);
 /* conv paths (what a forward runs) */
 #define KV_PATH_DIRECT 0
-#define KV_PATH_WINO48 1
 #define KV_PATH_WINO88 2
 #define KV_PATH_WINO88_F64 3
-#define KV_PATH_WINO48_F16X3 4
-#define KV_PATH_WINO88_I8 5
+#define KV_PATH_WINO88_I8 5     /* (1 and 4, the retired F(4x8) towers, stay unused indices) */
 #define KV_PATH_WINO88_I8F32 6
 #define KV_PATH_WINO88_I8F32V 7
 #define KV_PATH_WINO88_I8R 8
@@ -252,7 +241,7 @@ typedef struct {
     int64_t res_conv_launches;
     double step_ms;       /* wall time inside kv_run */
     double dom_flop;      /* MFMA FLOPs of one measured launch (padded rows included) */
-    int64_t dom_algo;     /* KV_ALGO_DIRECT, _WINOGRAD48 or _WINOGRAD88 for those launches */
+    int64_t dom_algo;     /* KV_ALGO_DIRECT or _WINOGRAD88 for those launches */
     int64_t tree_overflows; /* MCTS expansions dropped for a full edge pool (each also fails kv_run) */
     int64_t nn_rows_lazy;   /* KV_EVAL_LAZY above 16 slots: rows the compact batches sent through the
                                network (nn_rows counts the rows the reference's schedule evaluates) */
@@ -369,6 +358,11 @@ int kv_dev_i8gemm_bench(int device, int rows, int K, int variant, int iters, flo
  * x 100 MHz, out[1] = the back-to-back launches' mean time (us), out[2] = their count, out[3] = tiles per
  * workgroup of the stamped kernel. */
 int kv_dev_gemm_clock(int device, int rows, int digits, double seconds, double* out);
+/* Phase timing of the fp32 tower's output kernel (a diagnostic build of wino88i32_out_kernel with shader-clock
+ * stamps) at `rows` boards on seeded M (resid: the residual + Y variant; r3: 3 radix-256 digits): stamps
+ * [min(rows, 4096)][2][6] = s_memtime of waves 0 and 15 of each board's workgroup at start, V ready, after the
+ * maxima barrier, after the exponent barrier, digit stores issued, stores drained; us = that launch's time. */
+int kv_dev_out_phases(int device, int rows, int resid, int r3, unsigned long long* stamps, float* us);
 
 /* ------------------------------------------------------- data pipeline ---
  * Full-rules chess (python-chess 1.999 semantics, csrc/kv_chess.cpp) for the

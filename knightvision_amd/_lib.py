@@ -43,7 +43,7 @@ class Stats(C.Structure):
 
 
 NPATH = 10  # KV_NPATH
-PATHS = {0: "direct", 1: "winograd48", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3",
+PATHS = {0: "direct", 1: "winograd48 (retired)", 2: "winograd88", 3: "winograd88_f64", 4: "winograd48_f16x3 (retired)",
          5: "winograd88_i8", 6: "winograd88_i8f32", 7: "winograd88_i8f32v",
          8: "winograd88_i8r", 9: "winograd88_i8f32r3"}  # KV_PATH_*
 
@@ -115,6 +115,7 @@ def _declare(L):
         "kv_dev_wino88i": ([i, P(C.c_double), i, P(C.c_double), i, i, i, P(C.c_double), P(C.c_int8), P(i)], i),
         "kv_dev_i8gemm_bench": ([i, i, i, i, i, P(C.c_float), P(C.c_float)], i),
         "kv_dev_gemm_clock": ([i, i, i, C.c_double, P(C.c_double)], i),
+        "kv_dev_out_phases": ([i, i, i, i, P(C.c_uint64), P(C.c_float)], i),
         "kv_dev_wino88i32_out": ([i, P(C.c_float), i, P(C.c_float), P(C.c_float), P(C.c_float), i, P(C.c_float),
                                   P(C.c_int8), P(i)], i),
         "kv_dev_wino88r_out": ([i, P(C.c_double), i, P(C.c_float), P(C.c_float), P(C.c_float), i, P(C.c_float),
@@ -156,7 +157,7 @@ EXPORTED = ["kv_last_error", "kv_version", "kv_net_packed_size", "kv_net_create"
             "kv_load_weights", "kv_run", "kv_set_max_moves", "kv_records", "kv_games", "kv_stats_get", "kv_root_visits", "kv_root_visits_device", "kv_records_device", "kv_sync", "kv_reset_records", "kv_destroy",
             "kv_dev_valid_moves", "kv_dev_make_move", "kv_dev_attacks", "kv_dev_dirichlet", "kv_dev_py_random", "kv_host_libm",
             "kv_dev_wino88i", "kv_dev_wino88i32_out", "kv_dev_wino88r_out", "kv_dev_i8gemm_bench",
-            "kv_dev_gemm_clock",
+            "kv_dev_gemm_clock", "kv_dev_out_phases",
             "kv_pgn_extract", "kv_fen_codes", "kv_san_move_index", "kv_chess_perft", "kv_chess_san", "kv_chess_fen",
             "kv_tr_conv3x3_f16", "kv_tr_conv3x3_add_f16", "kv_tr_conv_weights_f16", "kv_tr_wgrad_workspace", "kv_tr_conv3x3_wgrad_f16",
             "kv_tr_bn_workspace", "kv_tr_bn_stats_f16", "kv_tr_bn_apply_f16", "kv_tr_bn_backward_f16",

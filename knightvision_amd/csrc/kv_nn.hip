@@ -27,7 +27,6 @@
 
 #include "kv_common.h"
 #include "kv_wino.h"
-#include "kv_wino48.h"
 #include "kv_wino88.h"
 #include "kv_wino88d.h"
 #include "kv_wino88i.h"
@@ -457,7 +456,7 @@ __global__ void encode_boards_kernel(const int8_t* __restrict__ boards, int nb, 
 // V [points][rows][256]. WINO 4: F(8x8) by lane swaps (below), the same bits
 // as wino88_in_kernel over T; WINO 5 the same into the fp64 V64
 // (wino88d_in_kernel's bits).
-template <int WINO>  // 0: NHWC out, 2: F(4x8) V of conv2, 4: F(8x8) V of conv2, 5: its fp64 V64
+template <int WINO>  // 0: NHWC out, 4: F(8x8) V of conv2, 5: its fp64 V64
 __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ boards, int nb,
                                                    const float* __restrict__ wT, const float* __restrict__ scale,
                                                    const float* __restrict__ shift, float* __restrict__ out,
@@ -509,48 +508,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const int8_t* __restrict__ bo
     } else {
     const float sc = scale[c], sh = shift[c];
     const int bb = w >> 1, b = b0 + bb;
-    if constexpr (WINO == 2) {
-        // no plane exchange: wave w computes the conv1 outputs of its own tile's 6x10 patch (the
-        // 40 on-board pixels; rows 3-4 are computed by both tiles' waves, same sums, same bits).
-        // 25 % more LDS reads than sharing the 64 pixels through a plane, but no 32 KB plane:
-        // 4 workgroups per CU instead of 2 (VGPR-bound at 106), so one workgroup's V stores
-        // overlap another's sums (forward 12.40 -> 12.35 ms at 2,048 boards), bit-identical
-        const int tile = w & 1;
-        float d48[60];
-        // the tile as a compile-time constant: every patch position's on-board test and LDS
-        // offset are then static
-        auto patch = [&](auto T) {
-            constexpr int TILE = decltype(T)::value;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                const int py = TILE * 4 - 1 + i;
-#pragma unroll
-                for (int j = 0; j < 10; ++j) {
-                    const int px = j - 1;
-                    float y = 0.f;
-                    if (py >= 0 && py < 8 && px >= 0 && px < 8) {
-                        float acc = 0.f;
-#pragma unroll
-                        for (int t = 0; t < 9; ++t)
-                            acc += wl[t * 13 + codes[bb][(py + t / 3) * 10 + px + t % 3]][cl];
-                        const float v = acc * sc + sh;
-                        y = v > 0.f ? v : 0.f;
-                    }
-                    d48[i * 10 + j] = y;
-                }
-            }
-        };
-        if (tile == 0)
-            patch(std::integral_constant<int, 0>{});
-        else
-            patch(std::integral_constant<int, 1>{});
-        float mx = wino48_input_tile(d48, out, ((size_t)b * 2 + tile) * 256 + c, (size_t)rows * 256);
-        if (vmax) {
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-            if (cl == 0) atomicMax(vmax + b, __float_as_uint(mx));
-        }
-    } else {
+    {
     // branch-free: an empty or off-board neighbour adds +0 (exact, acc starts at +0),
     // so every pixel issues its 9 independent LDS reads back to back
 #pragma unroll 4
@@ -605,10 +563,9 @@ __global__ void planes_to_nhwc16_kernel(const float* __restrict__ planes, int nb
 // Conv paths of the 11 3x3 convs with Cin 256 / 512 (the stem conv, the heads
 // and the activations between layers are fp32 on every path):
 //   KV_PATH_DIRECT     implicit GEMM over the 9 taps (split-K at <= 16 boards)
-//   KV_PATH_WINO48     fp32 Winograd F(4x8)
 //   KV_PATH_WINO88     fp32 Winograd F(8x8)
 //   KV_PATH_WINO88_F64 Winograd F(8x8) with an fp64 Winograd domain
-//   KV_PATH_WINO48_F16X3 F(4x8) with the f16x3 split GEMM
+//   (KV_PATH 1 / 4, the F(4x8) towers in fp32 and on the f16x3 split, were retired in round 6)
 //   KV_PATH_WINO88_I8  F(8x8), fp64 Winograd domain, GEMMs on int8 digits (kv_wino88i.h)
 //   KV_PATH_WINO88_I8F32 F(8x8), fp32 Winograd domain, GEMMs on int8 digits (kv_wino88i.h)
 //   KV_PATH_WINO88_I8F32V the same with fp64 input transforms (V cut to digits from fp64)
@@ -634,10 +591,6 @@ struct kv_net {
     int algo = KV_ALGO_AUTO;
     float* slab = nullptr;  // split-K partial sums (small batches)
     // Winograd weights of convs 1..11, built when a path needs them (ensure_path)
-    float* U48 = nullptr;   // F(4x8) [60][Cout][Cin]
-    size_t uoff48[12] = {};
-    uint16_t* Uf48[2] = {};  // fp16 pieces of U48 * 2^ut48[l] (KV_PREC_F16X3)
-    int ut48[12] = {};
     float* U88 = nullptr;   // F(8x8) [100][Cout][Cin]
     size_t uoff88[12] = {};
     double* U88d = nullptr; // F(8x8), fp64 [100][Cout][Cin] (KV_PATH_WINO88_F64)
@@ -651,7 +604,6 @@ struct kv_net {
     int* eu88r = nullptr;
     size_t euoff[12] = {};
     bool built[kNPath] = {};
-    unsigned* vmax = nullptr;  // f16x3: per-board max |V| of each conv's input, [12][cap]
     float* stemT = nullptr; // conv1 as [tap][piece][cout] (stem_kernel)
     float* v1wT = nullptr;  // value_fc1 weight as [k][o] (heads_kernel)
     // Winograd workspaces, shared by the paths; each sized by net_reserve_ws for the paths this net has run
@@ -707,13 +659,8 @@ static int path_for(const kv_net* net, int B) {
     if (net->precision == KV_PREC_FP32 && net->algo == KV_ALGO_WINOGRAD88_I8) return KV_PATH_WINO88_I8F32;
     if (net->precision == KV_PREC_FP32 && net->algo == KV_ALGO_WINOGRAD88_I8V) return KV_PATH_WINO88_I8F32V;
     if (net->precision == KV_PREC_FP32 && net->algo == KV_ALGO_WINOGRAD88_I8R3) return KV_PATH_WINO88_I8F32R3;
-    if (net->precision == KV_PREC_F16X3) {
-        if (net->algo == KV_ALGO_DIRECT || (net->algo == KV_ALGO_AUTO && small)) return KV_PATH_DIRECT;
-        return KV_PATH_WINO48_F16X3;
-    }
     switch (net->algo) {
         case KV_ALGO_DIRECT: return KV_PATH_DIRECT;
-        case KV_ALGO_WINOGRAD48: return KV_PATH_WINO48;
         case KV_ALGO_WINOGRAD88: return KV_PATH_WINO88;
         default: return small ? net->auto_small : net->auto_large;
     }
@@ -790,8 +737,8 @@ static int launch_conv(const float* in, const float* w, const float* sc, const f
     return KV_OK;
 }
 
-// padded batch: a multiple of 4 boards (direct tiles), 32 (F(4x8): 128-row GEMM tiles of 2 rows per
-// board; F(8x8) in fp64: 32 / 64 / 128-row tiles) or F(8x8)'s one row per board: 32 / 96 boards
+// padded batch: a multiple of 4 boards (direct tiles), 32 (F(8x8) in fp64: 32 / 64 / 128-row tiles) or
+// F(8x8)'s one row per board: 32 / 96 boards
 // (32-row tiles: forward 0.556 -> 0.522 ms at <= 32 boards, 0.895 -> 0.783 at 65-96) else a multiple of
 // 64 (at 160 boards the 32-row tiles were 1.26 -> 1.38 ms slower than padding to 192;
 // profiles/r03_w88_rows32_ab.log)
@@ -834,17 +781,15 @@ static int net_reserve(kv_net* net, int nb_pad) {
     if (nb_pad <= net->cap) return KV_OK;
     int cap = nb_pad < 64 ? 64 : nb_pad;
     (void)hipFree(net->x16); (void)hipFree(net->X); (void)hipFree(net->T); (void)hipFree(net->pfeat);
-    (void)hipFree(net->vmax); (void)hipFree(net->ev8); (void)hipFree(net->evmax8);
+    (void)hipFree(net->ev8); (void)hipFree(net->evmax8);
     net->x16 = net->X = net->T = net->pfeat = nullptr;
     net->ev8 = nullptr;
     net->evmax8 = nullptr;
-    net->vmax = nullptr;
     net->cap = 0;
     KV_HIP(hipMalloc(&net->x16, (size_t)cap * 64 * 16 * 4));
     KV_HIP(hipMalloc(&net->X, (size_t)cap * 64 * 512 * 4));
     KV_HIP(hipMalloc(&net->T, (size_t)cap * 64 * 512 * 4));
     KV_HIP(hipMalloc(&net->pfeat, (size_t)cap * 128 * 4));
-    KV_HIP(hipMalloc(&net->vmax, (size_t)12 * cap * sizeof(unsigned)));
     KV_HIP(hipMalloc(&net->ev8, (size_t)cap * kv::W88_XI * 2 * sizeof(int)));  // 2: segment exponents
     KV_HIP(hipMalloc(&net->evmax8, (size_t)cap * kv::W88_XI * sizeof(unsigned)));
     if (!net->slab)  // 48 splits x 16 boards x 64 px x 512 channels
@@ -871,80 +816,6 @@ static int launch_wino_gemm_t(const float* V, const float* U, float* M, int rows
     return KV_OK;
 }
 
-// F(4x8) GEMMs (60 points, rows = 2 per board): 128x128 tiles (8 waves, 2 per CU) when
-// the rows allow, else 64x128 (3 per CU); same k order, same bits. Measured at 256 /
-// 2048 boards (forward ms): 128x128 k-tile 32 1.83 / 12.77; 128x128 k-tile 16 1.88 /
-// 12.88; 64x128 uncapped (5 per CU) 1.88 / 13.12; 64x128 capped at 3 per CU 1.95 / 13.26;
-// 64x64 (3,840 tiles: an equal share per CU) 1.87 / 13.49; 64x128 as 8 waves of 32x32 1.89 / 13.18;
-// 128x128 as 4 waves of 64x64 1.82 / 13.06 (k-tile 16: 1.85 / 13.20), as 8 waves of 64x32 1.79 / 12.60
-// (re-measured A/B on the final out kernels: 8 waves of 32x64 1.78 / 12.55, of 64x32 1.80 / 12.77,
-// 4 waves of 64x64 1.84 / 13.07); larger tiles, round 2 (bit-identical, two alternating runs on one box,
-// profiles/r02_gemm_tile_ab.log): 256x128 as 8 waves of 64x64, k-tile 16 (2 per CU) 1.74 / 12.83;
-// 128x256 the same way 1.73 / 12.89; 256x128 k-tile 32 (1 per CU) 1.78 / 13.35 -- against 1.65 / 12.22
-template <int K>
-static int launch_wino48_gemm(const float* V, const float* U, float* M, int rows, int stride, hipStream_t st) {
-    if (rows % 128 == 0) {
-        note_dom<K>("wino_gemm_kernel<512,4,2,1,2,32,60>");
-        return launch_wino_gemm_t<K, 4, 2, 1, 2, 32, 0, kv::W48_XI>(V, U, M, rows, stride, st);
-    }
-    note_dom<K>("wino_gemm_kernel<512,2,2,1,2,16,60>");
-    return launch_wino_gemm_t<K, 2, 2, 1, 2, 16, 48 * 1024 - 30720, kv::W48_XI>(V, U, M, rows, stride, st);
-}
-
-template <int K, int TM, int XI, int RSH>
-static int launch_wino_gemm_h3_t(const float* V, const uint16_t* Uh, const uint16_t* Ul, const unsigned* vmax,
-                                 float* M, int rows, int stride, hipStream_t st) {
-    using T = kv::WinoH3<TM>;
-    KV_HIP(lds_opt_in((const void*)kv::wino_gemm_h3_kernel<K, TM, XI, RSH>, (int)T::BYTES));
-    const int nwg = XI * (rows / T::WM) * (512 / T::WN);
-    KV_REQUIRE(rows % T::WM == 0 && nwg % 8 == 0, KV_EINVAL, "wino gemm f16x3: rows %d", rows);
-    hipLaunchKernelGGL((kv::wino_gemm_h3_kernel<K, TM, XI, RSH>), dim3(nwg), dim3(256), T::BYTES, st, V, Uh, Ul, vmax,
-                       M, rows, 512, stride);
-    KV_HIP(hipGetLastError());
-    return KV_OK;
-}
-
-// 128-row tiles (2 workgroups per CU) when the rows allow: at 1,024 rows 4 %
-// faster per forward than the 64-row tile's exact 3 rounds (operand traffic
-// into the CUs, not MFMA, bounds this kernel); same k order, same bits.
-template <int K>
-static int launch_wino48_gemm_h3(const float* V, const uint16_t* Uh, const uint16_t* Ul, const unsigned* vmax, float* M,
-                                 int rows, int stride, hipStream_t st) {
-    if (rows % 128) {
-        note_dom<K>("wino_gemm_h3_kernel<512,1,60,1>");
-        return launch_wino_gemm_h3_t<K, 1, kv::W48_XI, 1>(V, Uh, Ul, vmax, M, rows, stride, st);
-    }
-    note_dom<K>("wino_gemm_h3_kernel<512,2,60,1>");
-    return launch_wino_gemm_h3_t<K, 2, kv::W48_XI, 1>(V, Uh, Ul, vmax, M, rows, stride, st);
-}
-
-// f16x3: the per-board max |V| slot of conv layer l's input (nullptr otherwise)
-static unsigned* net_vmax(kv_net* net, int l, int path) {
-    return path == KV_PATH_WINO48_F16X3 ? net->vmax + (size_t)l * net->cap : nullptr;
-}
-
-template <bool RESID, bool WRITE_Y, bool NEXT_V>
-static int launch_wino48_out(kv_net* net, int l, int path, const float* M, int nb, int stride, const float* resid,
-                             float* Y, float* Vn, hipStream_t st) {
-    const float* W = net->w;
-    hipLaunchKernelGGL((kv::wino48_out_kernel<RESID, WRITE_Y, NEXT_V>), dim3(512 / 64, nb), dim3(128), 0, st, M,
-                       stride, W + net->off.scale[l], W + net->off.shift[l], resid, Y, Vn, net_vmax(net, l, path),
-                       net->ut48[l], NEXT_V ? net_vmax(net, l + 1, path) : nullptr);
-    KV_HIP(hipGetLastError());
-    return KV_OK;
-}
-
-// the F(4x8) GEMMs of conv layer l on the path (fp32 or f16x3)
-template <int K>
-static int wino48_gemm_layer(kv_net* net, int l, int path, const float* V, float* M, int rows, int stride,
-                             hipStream_t st) {
-    const size_t o = net->uoff48[l];
-    if (path == KV_PATH_WINO48_F16X3)
-        return launch_wino48_gemm_h3<K>(V, net->Uf48[0] + o, net->Uf48[1] + o, net_vmax(net, l, path), M, rows,
-                                        stride, st);
-    return launch_wino48_gemm<K>(V, net->U48 + o, M, rows, stride, st);
-}
-
 // KV_DEBUG_SKIP_TRANSFORMS=1: the Winograd towers' output/input transform launches are skipped (timing
 // probe only: the GEMM-only forward bounds what fusing the transforms away could gain; outputs invalid)
 static bool debug_skip_transforms() {
@@ -953,39 +824,6 @@ static bool debug_skip_transforms() {
         return e && e[0] == '1' ? 1 : 0;
     }();
     return v != 0;
-}
-
-// conv2 + the 5 residual blocks for boards [0, nb), F(4x8)
-static int wino48_blocks(kv_net* net, int nb, int path, bool mark, hipStream_t st) {
-    const int rows = nb * 2, stride = rows;
-    float* V = (float*)net->V;
-    float* M = (float*)net->Mw;
-    float* V256 = (float*)net->V256;
-    int rc;
-    if (debug_skip_transforms()) {
-        if ((rc = wino48_gemm_layer<256>(net, 1, path, V256, M, rows, stride, st))) return rc;
-        for (int l = 2; l < 12; ++l)
-            if ((rc = wino48_gemm_layer<512>(net, l, path, V, M, rows, stride, st))) return rc;
-        return KV_OK;
-    }
-    if ((rc = wino48_gemm_layer<256>(net, 1, path, V256, M, rows, stride, st))) return rc;
-    if ((rc = launch_wino48_out<false, true, true>(net, 1, path, M, nb, stride, nullptr, net->X, V, st))) return rc;
-    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[1], st));
-    for (int r = 0; r < 5; ++r) {
-        const int l1 = 2 + 2 * r, l2 = 3 + 2 * r;
-        const bool m = mark && r == 2;  // one representative residual GEMM for the engine's timing hook
-        if (m && net->res_a) KV_HIP(hipEventRecord(net->res_a, st));
-        if ((rc = wino48_gemm_layer<512>(net, l1, path, V, M, rows, stride, st))) return rc;
-        if (m && net->res_b) KV_HIP(hipEventRecord(net->res_b, st));
-        if ((rc = launch_wino48_out<false, false, true>(net, l1, path, M, nb, stride, nullptr, nullptr, V, st)))
-            return rc;
-        if ((rc = wino48_gemm_layer<512>(net, l2, path, V, M, rows, stride, st))) return rc;
-        rc = r < 4 ? launch_wino48_out<true, true, true>(net, l2, path, M, nb, stride, net->X, net->X, V, st)
-                   : launch_wino48_out<true, true, false>(net, l2, path, M, nb, stride, net->X, net->X, nullptr, st);
-        if (rc) return rc;
-    }
-    if (mark && net->timing) KV_HIP(hipEventRecord(net->ev[2], st));
-    return KV_OK;
 }
 
 // F(8x8) GEMMs (100 points, rows = 1 per board, a multiple of 64): 128x128 tiles when the
@@ -1629,17 +1467,15 @@ static int wino88i32_blocks(kv_net* net, int nb, bool mark, bool v64, hipStream_
 }
 
 // Winograd workspace bytes per board of a conv path: V (the residual convs' input transform), M (the GEMM
-// output), V256 (conv2's input transform), V8 (the digit planes). F(4x8): 2 rows per board of 60 points;
-// F(8x8): 1 row of 100 points; fp64 on the fp64 domains (the 5-digit one keeps no fp64 V: its output kernel
+// output), V256 (conv2's input transform), V8 (the digit planes). F(8x8): 1 row of 100 points per board; fp64
+// on the fp64 domains (the 5-digit one keeps no fp64 V: its output kernel
 // writes the digits)
 struct WsNeed {
     size_t b[4];
 };
 static WsNeed ws_need(int path) {
-    constexpr size_t f = 4, d = 8, R48 = 2 * kv::W48_XI, P88 = kv::W88_XI;
+    constexpr size_t f = 4, d = 8, P88 = kv::W88_XI;
     switch (path) {
-        case KV_PATH_WINO48:
-        case KV_PATH_WINO48_F16X3: return {{R48 * 512 * f, R48 * 512 * f, R48 * 256 * f, 0}};
         case KV_PATH_WINO88: return {{P88 * 512 * f, P88 * 512 * f, P88 * 256 * f, 0}};
         case KV_PATH_WINO88_F64: return {{P88 * 512 * d, P88 * 512 * d, P88 * 256 * d, 0}};
         case KV_PATH_WINO88_I8: return {{0, P88 * 512 * d, P88 * 256 * d, P88 * 512 * kv::kI8Digits}};
@@ -1705,18 +1541,7 @@ static int net_tower_wino(kv_net* net, int nb_pad, int path, bool v256_ready, hi
         net->dom_split = path != KV_PATH_WINO88 ? 0 : (nb_pad % 128 == 0 ? wino88_split_points(nb_pad) : kv::W88_XI);
         return KV_OK;
     }
-    const int rows48 = nb_pad * 2;
-    if (!v256_ready) {
-        hipLaunchKernelGGL(kv::wino48_in_kernel<256>, dim3(256 / 64, nb_pad), dim3(128), 0, st, net->T, rows48,
-                           (float*)net->V256, net_vmax(net, 1, path));
-        KV_HIP(hipGetLastError());
-    }
-    if ((rc = wino48_blocks(net, nb_pad, path, true, st))) return rc;
-    net->dom_flop = 2.0 * kv::W48_XI * rows48 * 512.0 * 512.0;
-    net->dom_kernel = t_dom_kernel ? t_dom_kernel : "?";
-    net->dom_algo = KV_ALGO_WINOGRAD48;
-    net->dom_split = 0;
-    return KV_OK;
+    KV_REQUIRE(false, KV_EINVAL, "kv_net: conv path %d is not a Winograd tower", path);
 }
 
 // the tower + heads; the stem reads net->x16 (encoded planes) or, when
@@ -1733,8 +1558,6 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
     KV_REQUIRE(nb_pad <= net->cap, KV_EINVAL, "kv_net: %d boards over the reserved %d", nb_pad, net->cap);
     if ((rc = net_reserve_ws(net, path))) return rc;
     if (tm) KV_HIP(hipEventRecord(net->ev[0], st));
-    if (path == KV_PATH_WINO48_F16X3)
-        KV_HIP(hipMemsetAsync(net->vmax, 0, (size_t)12 * net->cap * sizeof(unsigned), st));
     // Winograd paths: the stem builds conv2's V itself
     bool v256_ready = false;
     if (boards) {
@@ -1745,10 +1568,6 @@ static int net_tower(kv_net* net, int nb, int nb_pad, const int8_t* boards, floa
                  path == KV_PATH_WINO88_I8F32V)
             hipLaunchKernelGGL(kv::stem_kernel<5>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], (float*)net->V256, nb_pad, nullptr);
-        else if (path == KV_PATH_WINO48 || path == KV_PATH_WINO48_F16X3)
-            hipLaunchKernelGGL(kv::stem_kernel<2>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
-                               W + o.scale[0], W + o.shift[0], (float*)net->V256, nb_pad * 2,
-                               net_vmax(net, 1, path));
         else
             hipLaunchKernelGGL(kv::stem_kernel<0>, dim3(4, nb_pad / 2), dim3(256), 0, st, boards, nb, net->stemT,
                                W + o.scale[0], W + o.shift[0], net->T, nb_pad * 4, nullptr);
@@ -1805,35 +1624,6 @@ static int net_heads(kv_net* net, int nb, float* policy, float* value, hipStream
 }
 
 // ------------------------------------------------ path weights (lazy) --
-// f16x3 weights of one Winograd set: per-layer scale 2^ut putting max |U| in
-// [2^14, 2^15), then the two fp16 pieces in the GEMM's B-image layout
-static int split_f16_set(const float* U, const size_t* uoff, int nxi, uint16_t* const* Uf, int* ut) {
-    unsigned* umax = nullptr;
-    KV_HIP(hipMalloc(&umax, 12 * sizeof(unsigned)));
-    KV_HIP(hipMemset(umax, 0, 12 * sizeof(unsigned)));
-    for (int l = 1; l < 12; ++l) {
-        const size_t n = (size_t)nxi * kv::kConv[l].cout * kv::kConv[l].cin;
-        hipLaunchKernelGGL(kv::absmax_kernel, dim3(1024), dim3(256), 0, 0, U + uoff[l], n, umax + l);
-        KV_HIP(hipGetLastError());
-    }
-    unsigned hmax[12];
-    const hipError_t e = hipMemcpy(hmax, umax, sizeof(hmax), hipMemcpyDeviceToHost);
-    (void)hipFree(umax);
-    KV_HIP(e);
-    for (int l = 1; l < 12; ++l) {
-        const size_t n = (size_t)nxi * kv::kConv[l].cout * kv::kConv[l].cin;
-        int ex = 0;
-        float mf;
-        memcpy(&mf, &hmax[l], sizeof mf);
-        (void)frexp(hmax[l] ? (double)mf : 1.0, &ex);  // max in [2^(ex-1), 2^ex)
-        ut[l] = 15 - ex;
-        hipLaunchKernelGGL(kv::split_f16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, U + uoff[l],
-                           kv::kConv[l].cout, kv::kConv[l].cin, ut[l], Uf[0] + uoff[l], Uf[1] + uoff[l], nxi);
-        KV_HIP(hipGetLastError());
-    }
-    return KV_OK;
-}
-
 static size_t wino_offsets(size_t* uoff, int nxi) {
     size_t tot = 0;
     for (int l = 1; l < 12; ++l) {
@@ -1861,26 +1651,6 @@ static int ensure_path(kv_net* net, int path) {
     int rc = KV_OK;
     switch (path) {
         case KV_PATH_DIRECT: break;
-        case KV_PATH_WINO48:
-        case KV_PATH_WINO48_F16X3: {
-            if (!net->built[KV_PATH_WINO48]) {
-                const size_t tot = wino_offsets(net->uoff48, kv::W48_XI);
-                if (!net->U48) KV_HIP(hipMalloc(&net->U48, tot * sizeof(float)));
-                each_conv([&](int l, dim3 g) {
-                    hipLaunchKernelGGL(kv::wino48_weights_kernel, g, dim3(256), 0, 0, net->w + net->off.w[l],
-                                       kv::kConv[l].cout, kv::kConv[l].cin, net->U48 + net->uoff48[l]);
-                });
-                KV_HIP(hipGetLastError());
-                net->built[KV_PATH_WINO48] = true;
-            }
-            if (path == KV_PATH_WINO48_F16X3) {
-                const size_t tot = wino_offsets(net->uoff48, kv::W48_XI);
-                for (int p = 0; p < 2; ++p)
-                    if (!net->Uf48[p]) KV_HIP(hipMalloc(&net->Uf48[p], tot * sizeof(uint16_t)));
-                if ((rc = split_f16_set(net->U48, net->uoff48, kv::W48_XI, net->Uf48, net->ut48))) return rc;
-            }
-            break;
-        }
         case KV_PATH_WINO88: {
             const size_t tot = wino_offsets(net->uoff88, kv::W88_XI);
             if (!net->U88) KV_HIP(hipMalloc(&net->U88, tot * sizeof(float)));
@@ -1964,18 +1734,6 @@ static int ensure_path(kv_net* net, int path) {
 static void release_unused(kv_net* net) {
     bool keep[kNPath] = {};
     keep[path_for(net, 1)] = keep[path_for(net, 1024)] = true;
-    if (!keep[KV_PATH_WINO48] && !keep[KV_PATH_WINO48_F16X3]) {
-        (void)hipFree(net->U48);
-        net->U48 = nullptr;
-        net->built[KV_PATH_WINO48] = false;
-    }
-    if (!keep[KV_PATH_WINO48_F16X3]) {
-        for (int p = 0; p < 2; ++p) {
-            (void)hipFree(net->Uf48[p]);
-            net->Uf48[p] = nullptr;
-        }
-        net->built[KV_PATH_WINO48_F16X3] = false;
-    }
     if (!keep[KV_PATH_WINO88]) {
         (void)hipFree(net->U88);
         net->U88 = nullptr;
@@ -2251,9 +2009,9 @@ int kv_net_load(kv_net* net, const float* packed, size_t n_floats) {
 
 int kv_net_set_algo(kv_net* net, int algo) {
     KV_REQUIRE(net, KV_EINVAL, "kv_net_set_algo: NULL");
-    KV_REQUIRE(algo != 2, KV_EINVAL, "kv_net_set_algo: KV_ALGO 2 (Winograd F(4x4)) was retired; use "
-                                     "KV_ALGO_WINOGRAD48 or KV_ALGO_WINOGRAD88");
-    KV_REQUIRE(algo == KV_ALGO_AUTO || algo == KV_ALGO_DIRECT || algo == KV_ALGO_WINOGRAD48 ||
+    KV_REQUIRE(algo != 2 && algo != 3, KV_EINVAL, "kv_net_set_algo: KV_ALGO %d (Winograd F(4x4) / F(4x8)) was "
+                                                  "retired; use KV_ALGO_AUTO or KV_ALGO_WINOGRAD88", algo);
+    KV_REQUIRE(algo == KV_ALGO_AUTO || algo == KV_ALGO_DIRECT ||
                    algo == KV_ALGO_WINOGRAD88 || algo == KV_ALGO_WINOGRAD88_I8 || algo == KV_ALGO_WINOGRAD88_I8V ||
                    algo == KV_ALGO_WINOGRAD88_I8R3,
                KV_EINVAL, "kv_net_set_algo: unknown algo %d", algo);
@@ -2270,11 +2028,11 @@ int kv_net_set_algo(kv_net* net, int algo) {
 
 int kv_net_set_precision(kv_net* net, int precision) {
     KV_REQUIRE(net, KV_EINVAL, "kv_net_set_precision: NULL");
-    KV_REQUIRE(precision != 1 && precision != 2, KV_EINVAL,
-               "kv_net_set_precision: precision %d (bf16x3 / bf16x6) was retired; use KV_PREC_FP32, KV_PREC_F16X3 "
-               "or KV_PREC_F64W", precision);
-    KV_REQUIRE(precision == KV_PREC_FP32 || precision == KV_PREC_F16X3 || precision == KV_PREC_F64W ||
-                   precision == KV_PREC_I8X5 || precision == KV_PREC_I8R4,
+    KV_REQUIRE(precision != 1 && precision != 2 && precision != 3, KV_EINVAL,
+               "kv_net_set_precision: precision %d (bf16x3 / bf16x6 / f16x3) was retired; use KV_PREC_FP32, "
+               "KV_PREC_F64W, KV_PREC_I8R4 or KV_PREC_I8X5", precision);
+    KV_REQUIRE(precision == KV_PREC_FP32 || precision == KV_PREC_F64W || precision == KV_PREC_I8X5 ||
+                   precision == KV_PREC_I8R4,
                KV_EINVAL,
                "kv_net_set_precision: unknown precision %d", precision);
     if (net->precision == precision && (!net->loaded || net->built[path_for(net, 1024)])) return KV_OK;
@@ -2793,6 +2551,77 @@ int kv_dev_gemm_clock(int device, int rows, int digits, double seconds, double* 
     return KV_OK;
 }
 
+// Phase timing of the fp32 tower's held-V output kernel (a diagnostic build: wino88i32_out_kernel<., ., 512, R3,
+// true>) at `rows` boards on seeded M: stamps [min(rows, 4096)][2][6] = shader clocks of waves 0 and 15 of each
+// board's workgroup at start, V ready, after the maxima barrier, after the exponent barrier, digit stores issued,
+// stores drained (kv_wino88i.h kOutStamps); us = the stamped launch's HIP-event time. The 4th launch is the one
+// read (after three warm ones).
+__global__ void out_phase_fill_kernel(float* M, size_t n, float* sc, float* sh) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        uint32_t z = (uint32_t)(i * 2654435761u) ^ 0x9e3779b9u;
+        z ^= z >> 15;
+        z *= 0x2c1b3c6du;
+        z ^= z >> 12;
+        M[i] = ((float)(z & 0xffffff) / 16777216.0f - 0.5f) * 0.6f;
+    }
+    if (i < 512) {
+        sc[i] = 0.5f + (float)(i % 7) * 0.1f;
+        sh[i] = -0.01f * (float)(i % 5);
+    }
+}
+
+int kv_dev_out_phases(int device, int rows, int resid, int r3, unsigned long long* stamps, float* us) {
+    KV_REQUIRE(rows > 0 && rows % 128 == 0 && rows <= kMaxBoards && stamps && us, KV_EINVAL,
+               "kv_dev_out_phases: bad arguments (rows %d)", rows);
+    KV_HIP(hipSetDevice(device));
+    const size_t nm = (size_t)kv::W88_XI * rows * 512, ny = (size_t)rows * 64 * 512;
+    kv::DevBuf<float> dm, dsc, dsh, dy;
+    kv::DevBuf<int8_t> v8;
+    kv::DevBuf<int> ev;
+    KV_HIP(dm.alloc(nm));
+    KV_HIP(dsc.alloc(512));
+    KV_HIP(dsh.alloc(512));
+    KV_HIP(dy.alloc(ny));
+    KV_HIP(v8.alloc(nm * 4));
+    KV_HIP(ev.alloc((size_t)kv::W88_XI * rows));
+    hipLaunchKernelGGL(out_phase_fill_kernel, dim3((unsigned)((nm + 255) / 256)), dim3(256), 0, 0, dm.p, nm, dsc.p,
+                       dsh.p);
+    KV_HIP(hipMemset(dy.p, 0, ny * sizeof(float)));
+    KV_HIP(hipGetLastError());
+    kv::DevEvent e0, e1;
+    KV_HIP(e0.create());
+    KV_HIP(e1.create());
+    for (int it = 0; it < 4; ++it) {
+        if (it == 3) KV_HIP(hipEventRecord(e0.e, 0));
+        if (resid && r3)
+            hipLaunchKernelGGL((kv::wino88i32_out_kernel<true, true, 512, true, true>), dim3(1, rows), dim3(1024), 0, 0,
+                               dm.p, rows, dsc.p, dsh.p, dy.p, dy.p, v8.p, ev.p, 0, 0);
+        else if (resid)
+            hipLaunchKernelGGL((kv::wino88i32_out_kernel<true, true, 512, false, true>), dim3(1, rows), dim3(1024), 0,
+                               0, dm.p, rows, dsc.p, dsh.p, dy.p, dy.p, v8.p, ev.p, 0, 0);
+        else if (r3)
+            hipLaunchKernelGGL((kv::wino88i32_out_kernel<false, false, 512, true, true>), dim3(1, rows), dim3(1024), 0,
+                               0, dm.p, rows, dsc.p, dsh.p, nullptr, nullptr, v8.p, ev.p, 0, 0);
+        else
+            hipLaunchKernelGGL((kv::wino88i32_out_kernel<false, false, 512, false, true>), dim3(1, rows), dim3(1024), 0,
+                               0, dm.p, rows, dsc.p, dsh.p, nullptr, nullptr, v8.p, ev.p, 0, 0);
+        KV_HIP(hipGetLastError());
+    }
+    KV_HIP(hipEventRecord(e1.e, 0));
+    KV_HIP(hipEventSynchronize(e1.e));
+    float ms = 0.f;
+    KV_HIP(hipEventElapsedTime(&ms, e0.e, e1.e));
+    *us = 1000.f * ms;
+    const int nb = rows < kv::kOutStampBoards ? rows : kv::kOutStampBoards;
+    std::vector<unsigned long long> h((size_t)kv::kOutStampBoards * 16);
+    KV_HIP(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(kv::kOutStamps), h.size() * sizeof(unsigned long long)));
+    for (int b = 0; b < nb; ++b)
+        for (int w = 0; w < 2; ++w)
+            for (int k = 0; k < 6; ++k) stamps[((size_t)b * 2 + w) * 6 + k] = h[((size_t)b * 2 + w) * 8 + k];
+    return KV_OK;
+}
+
 int kv_net_set_timing(kv_net* net, int enable) {
     KV_REQUIRE(net, KV_EINVAL, "kv_net_set_timing: NULL");
     net->timing = enable != 0;
@@ -2818,7 +2647,6 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->X);
     (void)hipFree(net->T);
     (void)hipFree(net->pfeat);
-    (void)hipFree(net->U48);
     (void)hipFree(net->U88);
     (void)hipFree(net->U88d);
     (void)hipFree(net->U88i);
@@ -2834,8 +2662,6 @@ void kv_net_destroy(kv_net* net) {
     (void)hipFree(net->evmax8);
     (void)hipFree(net->stemT);
     (void)hipFree(net->v1wT);
-    for (int p = 0; p < 2; ++p) (void)hipFree(net->Uf48[p]);
-    (void)hipFree(net->vmax);
     (void)hipFree(net->V);
     (void)hipFree(net->Mw);
     (void)hipFree(net->V256);

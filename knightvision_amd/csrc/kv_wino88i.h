@@ -615,6 +615,9 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_mid_kernel(const int8_t* _
 // 4-7 do not -- the two waves of a SIMD then reach each barrier at different points of their MFMA streams
 // (one finishing a stage, one mid-stage), so one issues MFMAs while the other waits on its LDS reads; else
 // every wave lags. Same products, same bits.
+#ifndef KV_LAG_OPAQUE
+#define KV_LAG_OPAQUE 1  // 0: A/B probe of the lag kernels without the opaque lagging operands
+#endif
 template <int K, bool STAG, int LJ = 2>
 __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* __restrict__ V8,
                                                                  const int* __restrict__ ev,
@@ -694,6 +697,14 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* _
             asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
         else
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#if KV_LAG_OPAQUE  // the lagging operands are in registers (wino88i32_gemm_lagt_kernel)
+#pragma unroll
+        for (int i = 0; i < NA; ++i) asm volatile("" : "+v"(pa[i]));
+#pragma unroll
+        for (int jb = 0; jb < S - LJ; ++jb)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(pb[jb][nt]));
+#endif
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         const char* buf = L0 + (kt % NBUF) * T::STAGE;
@@ -867,6 +878,17 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
                 asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL + 32) : "memory");
             else
                 asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
+            // the lagging operands are in registers now (lgkmcnt(0) above); an opaque definition tells the
+            // compiler so, or its waitcnt pass waits for every LDS read of the new stage before the first
+            // lagging MFMA (lgkmcnt(0) across the loop back-edge) and the lag hides nothing
+#if KV_LAG_OPAQUE
+#pragma unroll
+            for (int i = 0; i < NA; ++i) asm volatile("" : "+v"(pa[i]));
+#pragma unroll
+            for (int jb = 0; jb < ND - LJ; ++jb)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(pb[jb][nt]));
+#endif
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             const char* buf = L0 + (s % NBUF) * T::STAGE;
@@ -1047,6 +1069,14 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
             asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
         else
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#if KV_LAG_OPAQUE  // the lagging operands are in registers (wino88i32_gemm_lagt_kernel)
+#pragma unroll
+        for (int i = 0; i < NA; ++i) asm volatile("" : "+v"(pa[i]));
+#pragma unroll
+        for (int jb = 0; jb < S - LJ; ++jb)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(pb[jb][nt]));
+#endif
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         const char* buf = L0 + (kt % NBUF) * T::STAGE;
@@ -1651,7 +1681,14 @@ __global__ __launch_bounds__(1024, 8) void wino88i32_out2_kernel(const float* __
     }
 }
 
-template <bool RESID, bool WRITE_Y, int CW, bool R3 = false>
+// STAMP (a diagnostic build, never the product's; kv_dev_out_phases): waves 0 and 15 record the shader clock at the
+// kernel's phase boundaries into kOutStamps[board][wave 0/15][8] -- a buffer no other code reads: start, V ready
+// (M loaded, both transforms done), after the maxima barrier, after the exponent barrier, digit stores issued,
+// stores drained.
+constexpr int kOutStampBoards = 4096;
+__device__ unsigned long long kOutStamps[kOutStampBoards][2][8];
+
+template <bool RESID, bool WRITE_Y, int CW, bool R3 = false, bool STAMP = false>
 __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __restrict__ M, int rows,
                                                                const float* __restrict__ scale,
                                                                const float* __restrict__ shift, const float* resid,
@@ -1665,6 +1702,9 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
     const int seg = blockIdx.x, c = seg * CW + w * 32 + (lane & 31), b = blockIdx.y;
     out_stagger(b, stag, first);
+    unsigned long long st[6] = {};
+    const bool stamper = STAMP && (w == 0 || w == NW - 1) && lane == 0 && b < kOutStampBoards;
+    if constexpr (STAMP) st[0] = __builtin_amdgcn_s_memtime();
     float vk[5][10];  // this half's 50 V values (rows 5h .. 5h+4), kept across the exponent barrier
     {
         float t2[10][4];  // B10^T of the plane's columns 4h .. 4h+3
@@ -1675,6 +1715,13 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
         }
 #pragma unroll
         for (int aa = 0; aa < 5; ++aa) wino88_input_row(t2, h, aa, vk[aa]);
+    }
+    if constexpr (STAMP) {  // V ready: the transforms' results are consumed by an opaque use first
+#pragma unroll
+        for (int aa = 0; aa < 5; ++aa)
+#pragma unroll
+            for (int bb = 0; bb < 10; ++bb) asm volatile("" ::"v"(vk[aa][bb]));
+        st[1] = __builtin_amdgcn_s_memtime();
     }
 #pragma unroll
     for (int aa = 0; aa < 5; ++aa) {
@@ -1690,6 +1737,7 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
         }
     }
     __syncthreads();
+    if constexpr (STAMP) st[2] = __builtin_amdgcn_s_memtime();
     if (threadIdx.x < 100) {
         const int xi = threadIdx.x, a = xi / 10, bb = xi % 10, hh = a / 5, aa = a % 5;
         unsigned m = 0;
@@ -1700,6 +1748,7 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
         ex[((size_t)xi * NSEG + seg) * rows + b] = e;
     }
     __syncthreads();
+    if constexpr (STAMP) st[3] = __builtin_amdgcn_s_memtime();
     // row line (xi, kc = c / 32, b): 128 bytes, digit d of channel 32 kc + i at byte 32 d + i
     const int q = lane & 3;
     // 32-bit byte offsets (the digits of 100 x rows x 512 values < 2^32 bytes)
@@ -1716,6 +1765,16 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
             // plain stores, bit-identical; the GEMM's M stored non-temporal instead slowed the output kernel that
             // reads it: profiles/r05_out_nt_ab.log)
             __builtin_nontemporal_store(i8_quad_transpose(P, lane), &dst[(off0 + (unsigned)xi * xstride) >> 2]);
+        }
+    }
+    if constexpr (STAMP) {
+        st[4] = __builtin_amdgcn_s_memtime();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st[5] = __builtin_amdgcn_s_memtime();
+        if (stamper) {
+            unsigned long long* o = kOutStamps[b][w == 0 ? 0 : 1];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) o[k] = st[k];
         }
     }
 }

@@ -29,9 +29,9 @@ from .weights import pack_weights, state_dict_to_numpy
 
 # KV_PREC_* / KV_ALGO_* (include/kv.h). fp32 + auto: the conv path is chosen per weight load by the
 # library's calibration against an fp64 forward (KVNet.calibration()); f64w: the fp64 Winograd domain.
-PRECISIONS = {"fp32": 0, "f16x3": 3, "f64w": 4, "i8x5": 5, "i8r4": 6}
-ALGOS = {"auto": 0, "direct": 1, "winograd48": 3, "winograd88": 4, "winograd88i8": 5, "winograd88i8v": 6,
-         "winograd88i8r3": 7}
+PRECISIONS = {"fp32": 0, "f64w": 4, "i8x5": 5, "i8r4": 6}  # 3 (f16x3) retired in round 6
+ALGOS = {"auto": 0, "direct": 1, "winograd88": 4, "winograd88i8": 5, "winograd88i8v": 6,
+         "winograd88i8r3": 7}  # 3 (winograd48, F(4x8)) retired in round 6
 
 
 def batch_norm_rows(bn: nn.BatchNorm2d, x, n_real=None, explicit: bool = False):

@@ -139,16 +139,15 @@ GROUPS = {"pg_init_mm80": ("init", 80, 16), "pg_peaked_mm80": ("peaked", 80, 16)
           "pg_init_b1_mm60": ("init", 60, 1), "pg_init_full": ("init", None, 16)}
 
 
-@pytest.mark.parametrize("precision,algo", [("fp32", "auto"), ("f16x3", "auto"), ("f64w", "auto"), ("i8x5", "auto"),
-                                            ("i8r4", "auto"),
-                                            ("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "winograd88i8"),
+@pytest.mark.parametrize("precision,algo", [("fp32", "auto"), ("f64w", "auto"), ("i8x5", "auto"), ("i8r4", "auto"),
+                                            ("fp32", "winograd88"), ("fp32", "winograd88i8"),
                                             ("fp32", "winograd88i8v"), ("fp32", "winograd88i8r3")])
 @pytest.mark.parametrize("group", list(GROUPS))
 def test_engine_games_match_reference(golden_dir, group, precision, algo):
     """Complete games vs the reference's golden games. The slot counts here put
-    the network in the <= 16-board class; ("fp32", "winograd48") forces the
-    F(4x8) Winograd tower and ("fp32", "winograd88") the F(8x8) one (the
-    > 16-board class of C2 / C3) on the same games; ("f64w", "auto") the fp64
+    the network in the <= 16-board class; ("fp32", "winograd88") forces the fp32 MFMA F(8x8) tower and
+    ("fp32", "winograd88i8" / "winograd88i8r3") the F(8x8) towers on 4 / 3 int8 digits (the > 16-board class of
+    C2 / C3) on the same games; ("f64w", "auto") the fp64
     Winograd domain and ("i8x5", "auto") the same domain on int8 digits (AUTO's
     fallback for trained weights)."""
     from knightvision_amd.engine import SelfPlayEngine, records_by_game

@@ -76,7 +76,7 @@ def test_c3_2048x800_one_move():
         _replay(by[g][0], by[g][1], None)
 
 
-@pytest.mark.parametrize("algo", ["winograd88", "winograd48"])
+@pytest.mark.parametrize("algo", ["winograd88i8r3", "winograd88"])
 def test_c2_256x400_three_moves(algo):
     big = _run(256, 256, 400, 3, algo=algo)
     assert big[2]["sims"] == 256 * 3 * 400 and len(big[1]) == 256

@@ -39,7 +39,7 @@ def _f64(sd, planes):
     return p.numpy(), v.numpy()
 
 
-def accuracy_table(sd, planes, algos=("direct", "winograd48", "winograd88", "winograd88i8r3", "winograd88i8",
+def accuracy_table(sd, planes, algos=("direct", "winograd88", "winograd88i8r3", "winograd88i8",
                                       "winograd88i8v", "i8r4", "i8x5", "f64w", "auto")):
     """{name: (max |dlogit|, max |dvalue|) vs float64} for the reference's fp32
     forward ("ref32") and each HIP algorithm, plus each algorithm against ref32."""

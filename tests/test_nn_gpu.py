@@ -13,17 +13,17 @@ pytestmark = pytest.mark.gpu
 TOL_P, TOL_V = 1e-4, 1e-5
 
 
-# (precision, conv algorithm): fp32 direct / fp32 Winograd F(4x8,3x3) / fp32 Winograd F(8x8,3x3) / fp32 auto
-# (the calibrated choice every product caller runs) / f16x3 Winograd F(4x8) / F(8x8) with the fp64 Winograd domain
-# on fp64 MFMA / the same domain with the GEMMs on int8 digits; ("fp32", "winograd88i8") the fp32 F(8x8) tower with
-# its GEMMs on int8 digits, ("fp32", "winograd88i8v") the same with fp64 input transforms
-MODES = [("fp32", "direct"), ("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "winograd88i8"),
-         ("fp32", "winograd88i8v"), ("fp32", "winograd88i8r3"), ("fp32", "auto"), ("f16x3", "winograd48"),
-         ("f64w", "auto"), ("i8x5", "auto"), ("i8r4", "auto")]
-# the explicit fp32 / f16x3 Winograd towers are outside the tolerance at trained magnitudes ("stress": 1.2e-3 to
+# (precision, conv algorithm): fp32 direct / fp32 Winograd F(8x8,3x3) on fp32 MFMA / fp32 auto (the calibrated
+# choice every product caller runs) / F(8x8) with the fp64 Winograd domain on fp64 MFMA / the same domain with the
+# GEMMs on int8 digits; ("fp32", "winograd88i8") the fp32 F(8x8) tower with its GEMMs on 4 int8 digits,
+# ("fp32", "winograd88i8v") the same with fp64 input transforms, ("fp32", "winograd88i8r3") on 3 radix-256 digits.
+# (The F(4x8) towers in fp32 and on the f16x3 split were retired in round 6.)
+MODES = [("fp32", "direct"), ("fp32", "winograd88"), ("fp32", "winograd88i8"), ("fp32", "winograd88i8v"),
+         ("fp32", "winograd88i8r3"), ("fp32", "auto"), ("f64w", "auto"), ("i8x5", "auto"), ("i8r4", "auto")]
+# the explicit fp32 Winograd towers are outside the tolerance at trained magnitudes ("stress": 1.2e-3 to
 # 3.6e-3); AUTO measures that at load time and runs the fp64 Winograd domain instead (test_nn_accuracy_gpu.py)
-UNGUARDED = {("fp32", "winograd48"), ("fp32", "winograd88"), ("fp32", "winograd88i8"), ("fp32", "winograd88i8v"),
-             ("fp32", "winograd88i8r3"), ("f16x3", "winograd48")}
+UNGUARDED = {("fp32", "winograd88"), ("fp32", "winograd88i8"), ("fp32", "winograd88i8v"),
+             ("fp32", "winograd88i8r3")}
 # the 24-bit tower (3 radix-256 digits) is also outside at the peaked set's logit magnitudes (|logit| up to 8.2:
 # 1.03e-4, a relative 1.3e-5); AUTO measures that too and takes it only where it holds the budget (random-init
 # weights: 2.4e-6 on the calibration boards)
@@ -42,7 +42,7 @@ def _net(variant, precision="fp32", algo="auto"):
 @pytest.mark.parametrize("variant", ["init", "bn", "peaked", "stress"])
 def test_forward_matches_reference_golden(golden_dir, variant, precision, algo):
     if variant == "stress" and (precision, algo) in UNGUARDED:
-        pytest.skip("explicit Winograd fp32 / f16x3: outside the tolerance at trained magnitudes by design")
+        pytest.skip("explicit fp32 Winograd towers: outside the tolerance at trained magnitudes by design")
     if variant == "peaked" and (precision, algo) in UNGUARDED_PEAKED:
         pytest.skip("explicit 24-bit tower: outside the tolerance at peaked-logit magnitudes; AUTO guards it")
     g = np.load(os.path.join(golden_dir, "nn.npz"))
@@ -76,7 +76,7 @@ def test_forward_batch_sizes_vs_torch(B, precision, algo):
     assert np.abs(vb.cpu().numpy() - v.cpu().numpy()).max() == 0.0
 
 
-@pytest.mark.parametrize("precision", ["fp32", "f16x3", "f64w", "i8x5"])
+@pytest.mark.parametrize("precision", ["fp32", "f64w", "i8x5"])
 def test_batch_invariance(precision):
     """A board's outputs do not depend on the batch it is evaluated in, within a
     batch-size class (<= 16 boards: split-K direct kernels; > 16: whole-K
@@ -90,7 +90,7 @@ def test_batch_invariance(precision):
     p_all, v_all = m(planes)  # 40 boards: whole-K class
     p_20, v_20 = m(planes[20:])
     assert torch.equal(p_20, p_all[20:]) and torch.equal(v_20, v_all[20:])
-    if precision in ("fp32", "f16x3", "f64w", "i8x5"):  # 300 boards run the 128-row GEMM tiles, 40 the 64-row ones
+    if precision in ("fp32", "f64w", "i8x5"):  # 300 boards run the 128-row GEMM tiles, 40 the 64-row ones
         codes_l = rng.integers(0, 13, size=(300, 64)) * (rng.random((300, 64)) < 0.4)
         codes_l[:40] = codes
         p_l, v_l = m(torch.from_numpy(codes_to_planes(codes_l)).cuda())
