@@ -106,9 +106,8 @@ int kv_net_set_precision(kv_net* net, int precision);
  *                   else on 4 radix-128 ones (KV_ALGO_WINOGRAD88_I8), else the
  *                   same with fp64 input transforms (KV_ALGO_WINOGRAD88_I8V),
  *                   else the fp64 Winograd domain on 4 radix-256 int8
- *                   digits (KV_PREC_I8R4), else on 5 radix-128 ones
- *                   (KV_PREC_I8X5), else
- *                   on fp64 MFMA; <= 16 boards direct (split-K), else F(8x8)
+ *                   digits (KV_PREC_I8R4), else on fp64 MFMA; <= 16 boards
+ *                   direct (split-K), else F(8x8)
  *                   fp64 (kv_net_calibration reports it)
  * KV_ALGO_DIRECT    implicit GEMM over the 9 taps (exact fp32 products)
  * KV_ALGO_WINOGRAD88 F(8x8,3x3): 100 GEMMs of 1 tile x Cin x Cout per board,

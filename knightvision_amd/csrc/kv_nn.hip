@@ -1915,10 +1915,13 @@ static int net_calibrate(kv_net* net) {
     // > 16 boards
     // (F(8x8) and F(4x8) on fp32 MFMA are never within the budget when the int8-digit fp32 tower is not:
     // on every weight set measured they are further from fp64 -- DESIGN.md; they stay explicit algos)
-    const int cands[6] = {KV_PATH_WINO88_I8F32R3, KV_PATH_WINO88_I8F32, KV_PATH_WINO88_I8F32V, KV_PATH_WINO88_I8R,
-                          KV_PATH_WINO88_I8, KV_PATH_WINO88_F64};
+    // (the 5-digit fp64 domain, KV_PATH_WINO88_I8, left the chain in round 6: on no weight set measured was it
+    // chosen -- the 4-digit radix-256 one before it always held the budget where the fp32 towers did not; it
+    // stays as KV_PREC_I8X5)
+    const int cands[5] = {KV_PATH_WINO88_I8F32R3, KV_PATH_WINO88_I8F32, KV_PATH_WINO88_I8F32V, KV_PATH_WINO88_I8R,
+                          KV_PATH_WINO88_F64};
     net->auto_small = KV_PATH_DIRECT;
-    for (int i = 0; i < 6; ++i) {
+    for (int i = 0; i < 5; ++i) {
         const int p = cands[i];
         if ((rc = ensure_path(net, p))) return fail(rc);
         net->auto_large = p;
