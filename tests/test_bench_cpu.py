@@ -11,9 +11,11 @@ import bench
 
 
 def test_game_length_summary_is_complete_and_tight():
-    gl, f = bench._mcts_game_length(800)
-    assert gl is not None and f.startswith("r03_")
+    """VERDICT r5 #5: re-measured on the path the headline's AUTO chooses (round 6: R3), >= 256 games."""
+    gl, f = bench._mcts_game_length(800, "winograd88_i8f32r3")
+    assert gl is not None and f.startswith("r06_") and gl["conv_path"] == "winograd88_i8f32r3"
     assert gl["still_running"] == 0 and gl["finished"] == gl["games"] >= 256
+    assert bench._mcts_game_length(800)[1] == f  # the newest run is the default too
     assert gl["se_frac"] <= 0.05  # VERDICT r2 #4: SE <= 5 %
     lo, hi = gl["ci95_mean_plies"]
     assert lo < gl["mean_plies_finished"] < hi
