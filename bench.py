@@ -683,7 +683,7 @@ def main():
                              "(wino88i32v_out_kernel: the fp64 input transform of the fp32 activation, cut to 4 digits; "
                              "conv2's from a slice kernel)" if path == 7 else
                              "; GEMM only: the operands' 3 radix-256 int8 digits come from the previous output kernel "
-                             "(wino88i32_out2_kernel<., ., true>; conv2's from a slice kernel)" if path == 9 else ""),
+                             "(wino88i32_out_kernel<., ., 512, true>; conv2's from a slice kernel)" if path == 9 else ""),
                          "measured_peak_note": (f"v_mfma_i32_32x32x32_i8 back to back: {I8_MFMA_MEASURED_TOPS:.0f} "
                                                 "TOPS at the clock held (profiles/r04_mfma_rate.log)"
                                                 if path in I8_DIGIT_PRODUCTS else None),

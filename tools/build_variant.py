@@ -14,7 +14,7 @@ name, extra = sys.argv[1], sys.argv[2:]
 out = os.path.join(B.HERE, name)
 objs, procs = [], []
 for s in B.SRC:
-    o = os.path.join("/tmp", "kvvar_" + os.path.basename(s) + ".o")
+    o = os.path.join("/tmp", "kvvar_" + name + "_" + os.path.basename(s) + ".o")
     cmd = [B.HIPCC, *B.FLAGS, *extra, "-c", s, "-o", o]
     procs.append((subprocess.Popen(cmd), cmd))
     objs.append(o)
