@@ -324,6 +324,14 @@ def gemm_label(path: int, kernel: str):
             return first, (f" + {second} (residual-tower Winograd F(8x8,3x3) GEMM layer: the first points as "
                            "128x128 tiles, the rest as 64x128 tiles in a second launch, both inside the timed events)")
         return name, " (residual-tower Winograd F(8x8,3x3) GEMMs, 100 points)"
+    if fam == "wino88i32_gemm_r3k64_kernel":
+        tpw = int(targs[1])
+        return name, (
+            " (residual-tower Winograd F(8x8,3x3) GEMMs of the fp32 tower from 3 radix-256 int8 digits per value: the "
+            "6 pairs i + j <= 2, v_mfma_i32_32x32x32_i8 chains, exact int32 accumulation, one rounding to fp32, "
+            "128x128 tiles, " + (f"{tpw} per workgroup with the copy ring across them, " if tpw > 1 else "") +
+            "64-k stages of 96-byte row copies (24 MFMAs per wave per barrier), chunk 1's last B digits per wave "
+            "under the next stage's first LDS reads)")
     if fam == "wino88i32_gemm_lagt_kernel" and len(targs) > 2 and targs[2] == "3":
         tpw = int(targs[1])
         return name, (

@@ -1080,21 +1080,55 @@ static int launch_wino88i32_gemm_lag(const int8_t* V8, const int* ev, const int8
 
 // TPW tiles per workgroup, the ring across tiles (kv_wino88i.h wino88i32_gemm_lagt_kernel)
 // ND 3: KV_PATH_WINO88_I8F32R3's 3 radix-256 digits (6 pairs), its B digits LJ.. lagging
+// NB: stage buffers of the copy ring (NB - 1 stages in flight)
 #ifndef KV_I8R3_LJ
 #define KV_I8R3_LJ 1
 #endif
-template <int K, int TPW, int ND = 4, int LJ = (ND == 4 ? KV_I8F32_LJ : KV_I8R3_LJ)>
+#ifndef KV_I8F32_NB
+#define KV_I8F32_NB 3
+#endif
+#ifndef KV_I8R3_NB
+#define KV_I8R3_NB 3
+#endif
+template <int K, int TPW, int ND = 4, int LJ = (ND == 4 ? KV_I8F32_LJ : KV_I8R3_LJ),
+          int NB = (ND == 4 ? KV_I8F32_NB : KV_I8R3_NB)>
 static int launch_wino88i32_gemm_lagt(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
                                       int rows, int stride, hipStream_t st) {
     using T = kv::Wino88iTile<kv::kI8DigitsF32>;
-    constexpr int bytes = 3 * T::STAGE;
-    auto kern = kv::wino88i32_gemm_lagt_kernel<K, TPW, LJ, false, ND>;
+    constexpr int bytes = NB * T::STAGE;
+    auto kern = kv::wino88i32_gemm_lagt_kernel<K, TPW, LJ, false, ND, NB>;
     KV_HIP(lds_opt_in((const void*)kern, bytes));
     const int tiles = kv::W88_XI * (rows / T::WM) * (512 / T::WN);
     KV_REQUIRE(rows % T::WM == 0 && stride % T::WM == 0 && tiles % (8 * TPW) == 0, KV_EINVAL,
                "wino gemm i8 (lagt): rows %d / stride %d vs tile %d", rows, stride, T::WM);
     hipLaunchKernelGGL(kern, dim3(tiles / TPW), dim3(T::THREADS), bytes, st, V8, ev, U8, eu, M, rows, 512, stride,
                        nullptr);
+    KV_HIP(hipGetLastError());
+    return KV_OK;
+}
+
+// R3's GEMM with 64-k stages (kv_wino88i.h wino88i32_gemm_r3k64_kernel): 3 x 48 KiB of LDS
+template <int K, int TPW>
+static int launch_wino88i32_gemm_r3k64(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
+                                       int rows, int stride, hipStream_t st) {
+    constexpr int bytes = 3 * 4 * 128 * 96;
+    auto kern = kv::wino88i32_gemm_r3k64_kernel<K, TPW>;
+    if constexpr (K == 512 && TPW == 5) {  // KV_R3K64_ABL: timing ablations (outputs invalid; A/B tooling only)
+        static const int abl = [] {
+            const char* e = getenv("KV_R3K64_ABL");
+            return e ? atoi(e) : 0;
+        }();
+        if (abl == 1) kern = kv::wino88i32_gemm_r3k64_kernel<K, TPW, false, 1>;
+        if (abl == 2) kern = kv::wino88i32_gemm_r3k64_kernel<K, TPW, false, 2>;
+        if (abl == 3) kern = kv::wino88i32_gemm_r3k64_kernel<K, TPW, false, 3>;
+        if (abl == 4) kern = kv::wino88i32_gemm_r3k64_kernel<K, TPW, false, 4>;
+        if (abl == 7) kern = kv::wino88i32_gemm_r3k64_kernel<K, TPW, false, 7>;
+    }
+    KV_HIP(lds_opt_in((const void*)kern, bytes));
+    const int tiles = kv::W88_XI * (rows / 128) * (512 / 128);
+    KV_REQUIRE(rows % 128 == 0 && stride % 128 == 0 && tiles % (8 * TPW) == 0, KV_EINVAL,
+               "wino gemm i8 (r3k64): rows %d / stride %d vs tile 128", rows, stride);
+    hipLaunchKernelGGL(kern, dim3(tiles / TPW), dim3(512), bytes, st, V8, ev, U8, eu, M, rows, 512, stride, nullptr);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -1274,6 +1308,9 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, bool r8, hipStream_t s
 struct I8f32Form {
     bool seg = false, slice = false, r4 = false, persist = false;
     int out = 0;  // 0 held, 1 r64, 2 persistent
+    // R3's GEMM with 64-k stages (wino88i32_gemm_r3k64_kernel; KV_I8R3_K64=0: the 32-k lagt kernel): 357 vs
+    // 375 us back to back at 2,048 boards, forward -3-5 %, bit-identical (profiles/r06_saddr_ab.log)
+    bool r3k64 = true;
 };
 static const I8f32Form& i8f32_form() {
     static const I8f32Form f = [] {
@@ -1287,6 +1324,8 @@ static const I8f32Form& i8f32_form() {
         x.persist = e && !strcmp(e, "p");
         e = getenv("KV_I8F32_OUT");
         x.out = !e ? 0 : !strcmp(e, "r64") ? 1 : !strcmp(e, "p") ? 2 : 0;
+        e = getenv("KV_I8R3_K64");
+        x.r3k64 = !e || e[0] != '0';
         return x;
     }();
     return f;
@@ -1351,11 +1390,23 @@ static int launch_wino88i32v_out(kv_net* net, int l, const float* M, int nb, int
 // the fp32 tower's int8-digit GEMM of one conv (K 256: one segment, per-row exponents)
 template <int K>
 static int i8f32_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M, int rows, int stride,
-                      bool seg, hipStream_t st, bool r3 = false) {
+                      bool seg, hipStream_t st, bool r3 = false, int r3form = -1) {
     constexpr int D = kv::kI8DigitsF32;
     const I8f32Form& f = i8f32_form();
-    if (r3) {  // KV_PATH_WINO88_I8F32R3: the lagt kernel on 3 digit levels, tile count as the 4-digit one's
+    if (r3) {  // KV_PATH_WINO88_I8F32R3, tile count as the 4-digit one's; r3form 0 / 1: the 32-k / 64-k kernel
         const int tpw = i8f32_tiles_per_wg(rows);
+        if (r3form < 0 ? f.r3k64 : r3form == 1) {
+            if (tpw == 5) {
+                note_dom<K>("wino88i32_gemm_r3k64_kernel<512,5>");
+                return launch_wino88i32_gemm_r3k64<K, 5>(V8, ev, U8, eu, M, rows, stride, st);
+            }
+            if (tpw == 4) {
+                note_dom<K>("wino88i32_gemm_r3k64_kernel<512,4>");
+                return launch_wino88i32_gemm_r3k64<K, 4>(V8, ev, U8, eu, M, rows, stride, st);
+            }
+            note_dom<K>("wino88i32_gemm_r3k64_kernel<512,1>");
+            return launch_wino88i32_gemm_r3k64<K, 1>(V8, ev, U8, eu, M, rows, stride, st);
+        }
         if (tpw == 5) {
             note_dom<K>("wino88i32_gemm_lagt_kernel<512,5,3>");
             return launch_wino88i32_gemm_lagt<K, 5, 3>(V8, ev, U8, eu, M, rows, stride, st);
@@ -2112,11 +2163,13 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
     KV_REQUIRE(V && U && M && rows > 0 && rows % 128 == 0 && rows <= kMaxBoards && (K == 256 || K == 512) &&
                    (digits == 4 || digits == 5) &&
                    (!seg || (seg == 1 && digits == 4 && K == 512) || (seg == 2 && digits == 4) ||
-                    (seg == 3 && digits == 4)),
+                    (seg >= 3 && seg <= 5 && digits == 4)),
                KV_EINVAL, "kv_dev_wino88i: bad arguments (rows %d must be a multiple of 128, K %d 256 or 512, "
-               "digits %d 4 or 5, seg %d: 1 only with 4 digits and K 512, 2 (radix 256) and 3 (3 radix-256 digits "
-               "in 4 slots) only with 4 digits)", rows, K, digits, seg);
-    const bool r8 = seg == 2, r3 = seg == 3;
+               "digits %d 4 or 5, seg %d: 1 only with 4 digits and K 512, 2 (radix 256) and 3-5 (3 radix-256 "
+               "digits in 4 slots: the product's GEMM / the 32-k / the 64-k kernel) only with 4 digits)",
+               rows, K, digits, seg);
+    const bool r8 = seg == 2, r3 = seg >= 3;
+    const int r3form = seg == 4 ? 0 : seg == 5 ? 1 : -1;
     const int nseg = seg == 1 ? 2 : 1;
     KV_HIP(hipSetDevice(device));
     const size_t nv = (size_t)kv::W88_XI * rows * K, nu = (size_t)kv::W88_XI * 512 * K;
@@ -2163,8 +2216,8 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
                      ? launch_wino88i_slice<256, D, double, 1, false, true>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0)
                      : launch_wino88i_slice<512, D, double, 1, false, true>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
         if (!rc)
-            rc = K == 256 ? i8f32_gemm<256>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, false, 0, true)
-                          : i8f32_gemm<512>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, false, 0, true);
+            rc = K == 256 ? i8f32_gemm<256>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, false, 0, true, r3form)
+                          : i8f32_gemm<512>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, false, 0, true, r3form);
     } else {  // the fp32 domain: 4 digits, M rounded to fp32 (returned widened)
         constexpr int D = kv::kI8DigitsF32;
         rc = K == 256 ? launch_wino88i_slice<256, D>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0)
@@ -2525,13 +2578,17 @@ int kv_dev_gemm_clock(int device, int rows, int digits, double seconds, double* 
     const int tiles = kv::W88_XI * (rows / T::WM) * (512 / T::WN), nwg = tiles / tpw;
     KV_REQUIRE(tiles % (8 * tpw) == 0, KV_EINVAL, "kv_dev_gemm_clock: %d tiles, %d per workgroup", tiles, tpw);
     KV_HIP(stamps.alloc((size_t)nwg * 4));
-    constexpr int bytes = 3 * T::STAGE;
-    auto kern = r3 ? (tpw == 5   ? kv::wino88i32_gemm_lagt_kernel<K, 5, KV_I8R3_LJ, true, 3>
-                      : tpw == 4 ? kv::wino88i32_gemm_lagt_kernel<K, 4, KV_I8R3_LJ, true, 3>
-                                 : kv::wino88i32_gemm_lagt_kernel<K, 1, KV_I8R3_LJ, true, 3>)
-                   : (tpw == 5   ? kv::wino88i32_gemm_lagt_kernel<K, 5, KV_I8F32_LJ, true>
-                      : tpw == 4 ? kv::wino88i32_gemm_lagt_kernel<K, 4, KV_I8F32_LJ, true>
-                                 : kv::wino88i32_gemm_lagt_kernel<K, 1, KV_I8F32_LJ, true>);
+    const bool k64 = r3 && i8f32_form().r3k64;  // the stamped build of the form the product launches
+    const int bytes = k64 ? 3 * 4 * 128 * 96 : (r3 ? KV_I8R3_NB : KV_I8F32_NB) * T::STAGE;
+    auto kern = k64 ? (tpw == 5   ? kv::wino88i32_gemm_r3k64_kernel<K, 5, true>
+                       : tpw == 4 ? kv::wino88i32_gemm_r3k64_kernel<K, 4, true>
+                                  : kv::wino88i32_gemm_r3k64_kernel<K, 1, true>)
+               : r3 ? (tpw == 5   ? kv::wino88i32_gemm_lagt_kernel<K, 5, KV_I8R3_LJ, true, 3, KV_I8R3_NB>
+                      : tpw == 4 ? kv::wino88i32_gemm_lagt_kernel<K, 4, KV_I8R3_LJ, true, 3, KV_I8R3_NB>
+                                 : kv::wino88i32_gemm_lagt_kernel<K, 1, KV_I8R3_LJ, true, 3, KV_I8R3_NB>)
+                   : (tpw == 5   ? kv::wino88i32_gemm_lagt_kernel<K, 5, KV_I8F32_LJ, true, 4, KV_I8F32_NB>
+                      : tpw == 4 ? kv::wino88i32_gemm_lagt_kernel<K, 4, KV_I8F32_LJ, true, 4, KV_I8F32_NB>
+                                 : kv::wino88i32_gemm_lagt_kernel<K, 1, KV_I8F32_LJ, true, 4, KV_I8F32_NB>);
     KV_HIP(lds_opt_in((const void*)kern, bytes));
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(T::THREADS), bytes, 0, v8.p, ev.p, u8.p, eu.p, m.p, rows, 512, rows,
                        stamps.p);

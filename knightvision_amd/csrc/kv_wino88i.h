@@ -616,7 +616,10 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_mid_kernel(const int8_t* _
 // (one finishing a stage, one mid-stage), so one issues MFMAs while the other waits on its LDS reads; else
 // every wave lags. Same products, same bits.
 #ifndef KV_LAG_OPAQUE
-#define KV_LAG_OPAQUE 1  // 0: A/B probe of the lag kernels without the opaque lagging operands
+// 1: the lagging operands redefined opaquely after the pre-barrier lgkmcnt(0) (so the compiler's waitcnt pass
+// cannot make the first lagging MFMA wait for the new stage's LDS reads). Bit-identical either way; measured
+// (profiles/r06_gemm_opaque_lj_ab.log) neutral on the 4-digit tower and 0.6-1.5 % slower forward on R3: off.
+#define KV_LAG_OPAQUE 0
 #endif
 template <int K, bool STAG, int LJ = 2>
 __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* __restrict__ V8,
@@ -781,7 +784,18 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* _
 // buffer of its own that no other code reads; kv_dev_gemm_clock turns them into the clock the chip held.
 // ND = 3 (KV_PATH_WINO88_I8F32R3): the same row lines (4 digit slots per 32-channel chunk), of which digits 0-2
 // hold 3 radix-256 digits (slot 3 zero, never read): the 6 pairs i + j <= 2, 3 exact int32 levels weighted 2^-8l.
-template <int K, int TPW, int LJ = KV_I8F32_LJ, bool STAMP = false, int ND = 4>
+// KV_COPY_SADDR (1): the ring's copies address a wave-uniform 64-bit base plus an unsigned 32-bit lane offset,
+// so they issue in the scalar-base form (one address VGPR per lane); 0: a 64-bit VGPR address pair per lane.
+#ifndef KV_COPY_SADDR
+#define KV_COPY_SADDR 1
+#endif
+// NB: buffers of the copy ring (NB x 32 KiB of LDS), so NB - 1 stages are in flight past the one being read: the
+// copies of stage k + NB - 1 go into stage k - 1's buffer right after barrier k.
+template <int N>
+__device__ __forceinline__ void vm_lgkm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+template <int K, int TPW, int LJ = KV_I8F32_LJ, bool STAMP = false, int ND = 4, int NB = 3>
 __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* __restrict__ V8,
                                                                   const int* __restrict__ ev,
                                                                   const int8_t* __restrict__ U8,
@@ -793,12 +807,13 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
         t0 = __builtin_amdgcn_s_memtime();
         r0 = __builtin_amdgcn_s_memrealtime();
     }
-    constexpr int S = 4, NBUF = 3;
+    constexpr int S = 4, NBUF = NB, PD = NB - 1;  // PD: prefetch distance in stages
     using T = Wino88iTile<S>;
     constexpr int NT = T::NT, WM = T::WM, WN = T::WN, GL = T::GL;
     constexpr int NK = K / 32, NS = TPW * NK;
     constexpr int NA = ND - LJ;
     static_assert(GL == 4 && NK >= 3 && LJ >= 1 && LJ < ND && (ND == 4 || ND == 3), "4 pieces per wave and stage");
+    static_assert(NB >= 3 && NB <= 5 && PD < NK, "ring of 3-5 stage buffers (at most 160 KiB)");
     constexpr double kStep = ND == 4 ? 0.0078125 : 0.00390625;  // level weight: radix 128 / 256
 
     extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8t[];
@@ -835,9 +850,14 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
         const int8_t* base = gb[0];
 #pragma unroll
         for (int jj = 1; jj < TPW; ++jj) base = j == jj ? gb[jj] : base;
+        const int8_t* const sb = base + kt * sstep + (size_t)rg8 * 1024;  // wave-uniform
+#if KV_COPY_SADDR
+        const void* src = (const void*)(sb + (unsigned)((rg8 & 1) ? rl_off1 : rl_off0));
+#else
+        const void* src = (const void*)(sb + (size_t)((rg8 & 1) ? rl_off1 : rl_off0));
+#endif
         __builtin_amdgcn_global_load_lds(
-            (const void*)(base + kt * sstep + (size_t)rg8 * 1024 + ((rg8 & 1) ? rl_off1 : rl_off0)),
-            (__attribute__((address_space(3))) void*)(L0 + (s % NBUF) * T::STAGE + op * S * T::PLANE + rg8 * 1024),
+            src, (__attribute__((address_space(3))) void*)(L0 + (s % NBUF) * T::STAGE + op * S * T::PLANE + rg8 * 1024),
             16, 0, 0);
     };
 
@@ -851,8 +871,10 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
         for (int nt = 0; nt < NT; ++nt) boffr[nt][i] = S * T::PLANE + i8_rl_off(wn * NT * 32 + nt * 32 + lr, 2 * i + lh);
     }
 
-    issue1(0, 0); issue1(1, 0); issue1(2, 0); issue1(3, 0);
-    issue1(0, 1); issue1(1, 1); issue1(2, 1); issue1(3, 1);
+#pragma unroll
+    for (int p = 0; p < PD; ++p) {
+        issue1(0, p); issue1(1, p); issue1(2, p); issue1(3, p);
+    }
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
         i32x16_t acc[ND][NT];
@@ -872,15 +894,23 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
         };
         for (int kt = 0; kt < NK; ++kt) {
             const int s = j * NK + kt;
-            if (s + 1 >= NS)
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            else if (kt == 0 && j > 0)
-                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL + 32) : "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
-            // the lagging operands are in registers now (lgkmcnt(0) above); an opaque definition tells the
-            // compiler so, or its waitcnt pass waits for every LDS read of the new stage before the first
-            // lagging MFMA (lgkmcnt(0) across the loop back-edge) and the lag hides nothing
+            // stage s's pieces landed: vmcnt counts in issue order, so what may stay outstanding is the m later
+            // stages already issued and, for a tile's first PD stages, the previous tile's 32 M stores (issued
+            // after them). For NB = 3 and kt = 1 this is one wait less strict than round 5's vmcnt(GL)
+            const int m = NS - 1 - s < PD - 1 ? NS - 1 - s : PD - 1;
+            if (j > 0 && kt < PD) {
+                if (m == 0) vm_lgkm_wait<32>();
+                else if (m == 1) vm_lgkm_wait<GL + 32>();
+                else if (m == 2) vm_lgkm_wait<2 * GL + 32>();
+                else vm_lgkm_wait<3 * GL + 32>();
+            } else {
+                if (m == 0) vm_lgkm_wait<0>();
+                else if (m == 1) vm_lgkm_wait<GL>();
+                else if (m == 2) vm_lgkm_wait<2 * GL>();
+                else vm_lgkm_wait<3 * GL>();
+            }
+            // the lagging operands are in registers now (lgkmcnt(0) above); KV_LAG_OPAQUE tells the compiler
+            // so by an opaque redefinition (measured: no gain, see its definition)
 #if KV_LAG_OPAQUE
 #pragma unroll
             for (int i = 0; i < NA; ++i) asm volatile("" : "+v"(pa[i]));
@@ -904,9 +934,9 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
             // 1-2 % slower with it, so only here)
             __builtin_amdgcn_sched_barrier(0);
             if (kt > 0) h2();
-            if (s + 2 < NS) {
-                issue1(0, s + 2);
-                issue1(1, s + 2);
+            if (s + PD < NS) {
+                issue1(0, s + PD);
+                issue1(1, s + PD);
             }
 #pragma unroll
             for (int jb = 0; jb < ND; ++jb) {
@@ -922,9 +952,9 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
                         for (int nt = 0; nt < NT; ++nt)
                             acc[i + jb][nt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], b[jb][nt], acc[i + jb][nt], 0, 0, 0);
                 }
-                if (jb == 0 && s + 2 < NS) {
-                    issue1(2, s + 2);
-                    issue1(3, s + 2);
+                if (jb == 0 && s + PD < NS) {
+                    issue1(2, s + PD);
+                    issue1(3, s + PD);
                 }
             }
 #pragma unroll
@@ -948,6 +978,240 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
 #pragma unroll
                 for (int l = ND - 2; l >= 0; --l) m = __builtin_fma(m, kStep, (double)acc[l][nt][r]);  // exact
                 M[((size_t)xi * stride + r_base + wm * 32 + row) * cout + col] = (float)ldexp(m, evx[row] + ec);
+            }
+        }
+    }
+    if constexpr (STAMP) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x < 4) {  // one vector store per value, lanes 0-3
+            const unsigned long long v = threadIdx.x == 0 ? t0 : threadIdx.x == 1 ? t1 : threadIdx.x == 2 ? r0 : r1;
+            stamps[(size_t)blockIdx.x * 4 + threadIdx.x] = v;
+        }
+    }
+}
+
+template <int ABL>
+__device__ __forceinline__ i32x16_t r3mfma(i8x16_t a, i8x16_t b, i32x16_t c) {
+    if constexpr ((ABL & 2) != 0) {  // ablation: the fragments are consumed, no MFMA issues
+        asm volatile("" ::"v"(a), "v"(b));
+        return c;
+    } else {
+        return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
+    }
+}
+// R3's GEMM (KV_PATH_WINO88_I8F32R3) with 64-k stages: the 32-k lagt kernel gives a wave 12 MFMAs per stage
+// barrier at 3 digits (20 at 4), and its time did not move with 3, 4 or 5 ring buffers (370.6 / 371.3 / 371.6
+// us, profiles/r06_ring_depth_ab.log): the barrier's fixed cost, not the copies' latency, sets it. Here a stage is
+// two 32-channel chunks (24 MFMAs per wave per barrier), and only the 96 live bytes of each 128-byte row line
+// (digit slots 0-2; slot 3 is zero and never read) are copied, so a stage is 48 KiB and the ring keeps 3
+// buffers (144 KiB) with two stages in flight. LDS image per operand and chunk: 128 rows of 96 bytes, 16-byte
+// piece c = 2 d + half at position c ^ ((row >> 4) & 1) -- every ds_read_b128 lane group conflict-free
+// (rows 16-31 of a 32-row block land on the odd 16-byte bank groups, rows 0-15 on the even ones). Copies: wave
+// w fills 6 KiB pieces of plane (operand w >> 2, chunk (w >> 1) & 1), pieces 6 (w & 1) .. + 5; lane l of piece
+// pp carries unit u = 64 pp + l = (row u / 6, slot u % 6). Per stage a wave runs chunk 0's 12 MFMAs, chunk 1's
+// B digit 0 (6), and chunk 1's B digits 1-2 (6) after the next barrier under that stage's first reads. Same
+// products, same exact int32 levels, same bits as wino88i32_gemm_lagt_kernel<K, TPW, ., ., 3>.
+// ABL (timing ablations, outputs invalid; never the product's): 1 no copies after the prologue, 2 no MFMAs (the
+// fragments still read), 4 no M stores.
+template <int K, int TPW, bool STAMP = false, int ABL = 0>
+__global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t* __restrict__ V8,
+                                                                   const int* __restrict__ ev,
+                                                                   const int8_t* __restrict__ U8,
+                                                                   const int* __restrict__ eu, float* __restrict__ M,
+                                                                   int rows, int cout, int stride,
+                                                                   unsigned long long* __restrict__ stamps) {
+    unsigned long long t0 = 0, r0 = 0;
+    if constexpr (STAMP) {
+        t0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    constexpr int ND = 3, NB = 3, PD = NB - 1, GL = 6;
+    constexpr int NT = 2, WM = 128, WN = 128, WC = 2;
+    constexpr int NK = K / 32, NU = NK / 2, NS = TPW * NU;
+    constexpr int PLANE = 128 * 96, STAGE = 4 * PLANE;  // [operand][chunk] planes: 48 KiB
+    static_assert(NK % 2 == 0 && NU > PD && 8 * GL * 1024 == STAGE, "64-k stages, 6 pieces per wave");
+    constexpr double kStep = 0.00390625;  // level weight: radix 256
+
+    extern __shared__ __attribute__((aligned(16))) i8x16_t lds_i8k64[];
+    char* const L0 = (char*)lds_i8k64;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WC, wn = wave % WC;
+    const int CT = cout / WN, RT = rows / WM;
+    const int nwg = (int)gridDim.x, nv = nwg * TPW;  // nwg a multiple of 8
+    int xis[TPW], nbs[TPW], rbs[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+        const int vb = (int)blockIdx.x + j * nwg;
+        const int idx = (vb & 7) * (nv >> 3) + (vb >> 3);
+        xis[j] = idx / (CT * RT);
+        nbs[j] = (idx % CT) * WN;
+        rbs[j] = ((idx / CT) % RT) * WM;
+    }
+
+    const int wu = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the plane this wave copies
+    const int op = wu >> 2, chunk = (wu >> 1) & 1, pp0 = 6 * (wu & 1);
+    const size_t sstep = (op ? (size_t)cout : (size_t)stride) * 128;  // one 32-channel chunk of row lines
+    const int8_t* gb[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+        gb[j] = (op ? U8 + (((size_t)xis[j] * NK) * cout + (size_t)nbs[j]) * 128
+                    : V8 + (((size_t)xis[j] * NK) * stride + (size_t)rbs[j]) * 128) +
+                (size_t)chunk * sstep;
+    // this lane's source byte in a chunk's row-line block, per piece: unsigned 32-bit, so the copy takes the
+    // scalar-base + 32-bit-offset address form (one address VGPR per lane instead of a 64-bit pair)
+    unsigned goff[GL];
+#pragma unroll
+    for (int g = 0; g < GL; ++g) {
+        const int u = (pp0 + g) * 64 + lane, row = u / 6, slot = u - 6 * (u / 6);
+        goff[g] = (unsigned)(row * 128 + 16 * (slot ^ ((row >> 4) & 1)));
+    }
+    const int ldst = (op * 2 + chunk) * PLANE + pp0 * 1024;
+    auto issue1 = [&](int g, int s) {  // piece g of global stage s (tile s / NU, stage s % NU)
+        if constexpr ((ABL & 1) != 0)
+            if (s >= PD) return;
+        const int j = s / NU, ku = s - j * NU;
+        const int8_t* base = gb[0];
+#pragma unroll
+        for (int jj = 1; jj < TPW; ++jj) base = j == jj ? gb[jj] : base;
+        const int8_t* const sb = base + (size_t)(2 * ku) * sstep;  // wave-uniform
+#if KV_COPY_SADDR
+        const void* src = (const void*)(sb + goff[g]);
+#else
+        const void* src = (const void*)(sb + (size_t)(int)goff[g]);
+#endif
+        __builtin_amdgcn_global_load_lds(src,
+                                         (__attribute__((address_space(3))) void*)(L0 + (s % NB) * STAGE + ldst +
+                                                                                   g * 1024),
+                                         16, 0, 0);
+    };
+
+    const int lr = lane & 31, lh = lane >> 5;
+    const int arow = wm * 32 + lr;
+    int aoff[2][ND], boff[2][NT][ND];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+            aoff[h][d] = h * PLANE + arow * 96 + 16 * ((2 * d + lh) ^ ((arow >> 4) & 1));
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const int brow = wn * NT * 32 + nt * 32 + lr;
+                boff[h][nt][d] = (2 + h) * PLANE + brow * 96 + 16 * ((2 * d + lh) ^ ((brow >> 4) & 1));
+            }
+        }
+
+#pragma unroll
+    for (int p = 0; p < PD; ++p)
+#pragma unroll
+        for (int g = 0; g < GL; ++g) issue1(g, p);
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+        i32x16_t acc[ND][NT];
+#pragma unroll
+        for (int l = 0; l < ND; ++l)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc[l][nt] = i32x16_t{};
+        i8x16_t pa[2] = {}, pb[2][NT] = {};  // chunk 1's A digits 0-1 and B digits 1-2, lagging
+        auto h2 = [&]() {
+#pragma unroll
+            for (int jb = 1; jb < ND; ++jb)
+#pragma unroll
+                for (int i = 0; i + jb < ND; ++i)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+                        acc[i + jb][nt] = r3mfma<ABL>(pa[i], pb[jb - 1][nt], acc[i + jb][nt]);
+        };
+        for (int ku = 0; ku < NU; ++ku) {
+            const int s = j * NU + ku;
+            // stage s's pieces landed (vmcnt counts in issue order): what may stay outstanding is the m later
+            // stages already issued and, for a tile's first PD stages, the previous tile's 32 M stores
+            const int m = NS - 1 - s < PD - 1 ? NS - 1 - s : PD - 1;
+            if (j > 0 && ku < PD) {
+                if (m == 0) vm_lgkm_wait<32>();
+                else vm_lgkm_wait<GL + 32>();
+            } else {
+                if (m == 0) vm_lgkm_wait<0>();
+                else vm_lgkm_wait<GL>();
+            }
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            const char* buf = L0 + (s % NB) * STAGE;
+            i8x16_t a0[ND], b0[ND][NT], a1[ND], b1[ND][NT];
+#pragma unroll
+            for (int d = 0; d < ND; ++d) a0[d] = *(const i8x16_t*)(buf + aoff[0][d]);
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) b0[0][nt] = *(const i8x16_t*)(buf + boff[0][nt][0]);
+            __builtin_amdgcn_sched_barrier(0);
+            if (ku > 0) h2();
+            if (s + PD < NS) {
+                issue1(0, s + PD);
+                issue1(1, s + PD);
+                issue1(2, s + PD);
+            }
+            // chunk 0: all 6 pairs
+#pragma unroll
+            for (int jb = 0; jb < ND; ++jb) {
+                if (jb + 1 < ND) {
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) b0[jb + 1][nt] = *(const i8x16_t*)(buf + boff[0][nt][jb + 1]);
+                } else {
+#pragma unroll
+                    for (int d = 0; d < ND; ++d) a1[d] = *(const i8x16_t*)(buf + aoff[1][d]);
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) b1[0][nt] = *(const i8x16_t*)(buf + boff[1][nt][0]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i + jb < ND; ++i)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+                        acc[i + jb][nt] = r3mfma<ABL>(a0[i], b0[jb][nt], acc[i + jb][nt]);
+                if (jb == 0 && s + PD < NS) {
+                    issue1(3, s + PD);
+                    issue1(4, s + PD);
+                    issue1(5, s + PD);
+                }
+            }
+            // chunk 1: B digit 0 now, digits 1-2 after the next barrier
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                b1[1][nt] = *(const i8x16_t*)(buf + boff[1][nt][1]);
+                b1[2][nt] = *(const i8x16_t*)(buf + boff[1][nt][2]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < ND; ++i)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    acc[i][nt] = r3mfma<ABL>(a1[i], b1[0][nt], acc[i][nt]);
+            pa[0] = a1[0];
+            pa[1] = a1[1];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                pb[0][nt] = b1[1][nt];
+                pb[1][nt] = b1[2][nt];
+            }
+        }
+        h2();
+        const int xi = xis[j], n_base = nbs[j], r_base = rbs[j];
+        const int* evx = ev + (size_t)xi * stride + r_base + wm * 32;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+            const int col = n_base + wn * NT * 32 + nt * 32 + lr;
+            const int ec = eu[(size_t)xi * cout + col] - 14;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+                double mm = (double)acc[ND - 1][nt][r];
+#pragma unroll
+                for (int l = ND - 2; l >= 0; --l) mm = __builtin_fma(mm, kStep, (double)acc[l][nt][r]);  // exact
+                const float o = (float)ldexp(mm, evx[row] + ec);
+                if constexpr ((ABL & 4) != 0)
+                    asm volatile("" ::"v"(o));
+                else
+                    M[((size_t)xi * stride + r_base + wm * 32 + row) * cout + col] = o;
             }
         }
     }
@@ -1000,7 +1264,7 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
     // copy pieces as wino88i_gemm_kernel's planes path: piece q = wave * S + g covers operand q / 4S, digit
     // (q % 4S) / 4, rows 32 (q % 4) .. +31; lane l fills LDS row 32 (q % 4) + l / 2, half l & 1 (swapped on
     // bit 3 of the row)
-    const int op = (wave * GL) / (4 * S);
+    const int op = (__builtin_amdgcn_readfirstlane(wave) * GL) / (4 * S);  // wave-uniform
     const size_t rstride = op ? (size_t)cout : (size_t)stride;
     // (a tile's rows start at row * 32 in a plane, row * 128 in row lines; a stage is S * 32 B per row in both)
     const int8_t* gbase = op ? U8 + ((size_t)xi * NK) * S * cout * 32 + (size_t)n_base * (RL ? 128 : 32)
@@ -1014,10 +1278,15 @@ __global__ __launch_bounds__(512) void wino88i_gemm_lag5_kernel(const int8_t* __
     auto issue1 = [&](int g, int kt) {
         const int q = wave * GL + g;
         if constexpr (RL) {
-            const int rg8 = q % 16;
+            const int rg8 = __builtin_amdgcn_readfirstlane(q) % 16;  // wave-uniform: the scalar-base form
+            const int8_t* const sb = gbase + kt * sstep + (size_t)rg8 * 1024;
+#if KV_COPY_SADDR
+            const void* src = (const void*)(sb + (unsigned)((rg8 & 1) ? rl_off1 : rl_off0));
+#else
+            const void* src = (const void*)(sb + (size_t)((rg8 & 1) ? rl_off1 : rl_off0));
+#endif
             __builtin_amdgcn_global_load_lds(
-                (const void*)(gbase + kt * sstep + (size_t)rg8 * 1024 + ((rg8 & 1) ? rl_off1 : rl_off0)),
-                (__attribute__((address_space(3))) void*)(L0 + (kt % NBUF) * T::STAGE + op * S * T::PLANE + rg8 * 1024),
+                src, (__attribute__((address_space(3))) void*)(L0 + (kt % NBUF) * T::STAGE + op * S * T::PLANE + rg8 * 1024),
                 16, 0, 0);
         } else {
             const int d = (q % (4 * S)) / 4, rg = q % 4;

@@ -52,6 +52,8 @@ def test_gemm_traffic_summary_present():
     (0, "conv3x3_kernel<512,32>", 0), (5, "wino88i_gemm_lag5_kernel<512,3,5,7,false>", 0),
     (8, "wino88i_gemm_lag5_kernel<512,3,4,8,true>", 0), (6, "wino88i32_gemm_lagt_kernel<512,5>", 5),
     (6, "wino88i32_gemm_lagt_kernel<512,4>", 4), (7, "wino88i32_gemm_lagt_kernel<512,5>", 5),
+    (9, "wino88i32_gemm_r3k64_kernel<512,5>", 5), (9, "wino88i32_gemm_r3k64_kernel<512,4>", 4),
+    (9, "wino88i32_gemm_lagt_kernel<512,5,3>", 5),
     # KV_I8F32_TPW=1 (or a CU count where multi-tile workgroups do not pay): the library reports the
     # single-tile kernel, and the line follows it
     (6, "wino88i32_gemm_lag_kernel<512,false>", 1)])
@@ -69,7 +71,7 @@ def test_roofline_units_of_every_f88_path():
     """the F(8x8) int8-digit paths 7 (fp64 input transforms) and 8 (radix-256 fp64 domain) are
     costed as F(8x8) GEMMs (100 points x 512 x 512 per board), not as the direct conv or F(4x8)."""
     G = 2048
-    for path in (2, 3, 5, 6, 7, 8):
+    for path in (2, 3, 5, 6, 7, 8, 9):
         flop = 2.0 * 100 * G * 512 * 512
         per_board, bpl, rows = bench.dom_units(path, flop, G)
         assert per_board == bench.FLOP_WINO88_GEMM_PER_BOARD and bpl == G and rows == G, path

@@ -74,12 +74,15 @@ def test_i8r_gemm_bit_exact(K, rows):
     assert np.array_equal(M.view(np.uint64), Mr.view(np.uint64)), float(np.abs(M - Mr).max())
 
 
-@pytest.mark.parametrize("K,rows", [(256, 128), (512, 128), (512, 256)])
-def test_i8r3_gemm_bit_exact(K, rows):
+@pytest.mark.parametrize("K,rows,form", [(256, 128, 3), (512, 128, 3), (512, 256, 3), (256, 128, 4), (512, 256, 4),
+                                         (256, 128, 5), (512, 256, 5), (512, 2048, 5)])
+def test_i8r3_gemm_bit_exact(K, rows, form):
     """KV_PATH_WINO88_I8F32R3: the slice kernel's 3 radix-256 digits (balanced bytes of rint(a 2^(23 - e)), the
     exponent bumped at 127/128 of a power of two; slot 3 of each row line zero) and the 6-pair GEMM (3 digit
-    levels, lagt kernel), bit for bit against tests/_i8_digits (split_r3, gemm_r3): digits, exponents, M rounded
-    to fp32. Rows at the exponent rule's edges, an all-zero row, subnormals, +-2^-40."""
+    levels), bit for bit against tests/_i8_digits (split_r3, gemm_r3): digits, exponents, M rounded to fp32.
+    form 3: the product's GEMM; 4: the 32-k-stage lagt kernel; 5: the 64-k-stage kernel copying 96-byte rows
+    (at 2,048 rows: C3's grid, 5 tiles per workgroup). Rows at the exponent rule's edges, an all-zero row,
+    subnormals, +-2^-40."""
     rng = np.random.default_rng(K + rows + 5)
     V = rng.standard_normal((100, rows, K)) * np.exp2(rng.integers(-20, 20, size=(100, rows, 1)))
     V[0, 0] = 0.0
@@ -90,7 +93,7 @@ def test_i8r3_gemm_bit_exact(K, rows):
     V[3, 3] = np.where(rng.random(K) < 0.5, -1.0, 1.0) * np.exp2(-40.0)
     U = rng.standard_normal((100, 512, K)) * 0.05
     U[5, 7] = 0.0
-    M, dg, ex = _run(V, U, 4, seg=3)
+    M, dg, ex = _run(V, U, 4, seg=form)
     Mr, dv, evr = D.gemm_r3(V, U)
     assert np.array_equal(ex, evr.astype(np.int32))
     assert ex[1, 1] == 3 and ex[1, 2] == 4 and ex[1, 3] == 4
