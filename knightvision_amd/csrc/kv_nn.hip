@@ -696,6 +696,14 @@ static hipError_t lds_opt_in(const void* fn, int bytes) {
 
 // CUs of the current device, cached per device (the F(8x8) point split reads it per launch)
 // KV_OUT_STAG: the output kernels' phase stagger (kv_wino88i.h out_stagger), in units of s_sleep 127
+static int out_abl() {  // KV_OUT_ABL: output-kernel timing ablations (A/B tooling only; outputs invalid)
+    static const int v = [] {
+        const char* e = getenv("KV_OUT_ABL");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 static int out_stag() {
     static const int v = [] {
         const char* e = getenv("KV_OUT_STAG");
@@ -1360,6 +1368,9 @@ static int launch_wino88i32_out(kv_net* net, int l, const float* M, int nb, int 
                            sc, sh, resid, Y, V8, ev, 0, 0);
     else if (form == 2)
         return launch_wino88i32_outp<RESID, WRITE_Y>(M, nb, stride, sc, sh, resid, Y, V8, ev, st, r3);
+    else if (form == 0 && r3 && out_abl() == 1)  // KV_OUT_ABL=1: timing ablation (outputs invalid)
+        hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y, 512, true, false, 1>), dim3(1, nb), dim3(1024), 0,
+                           st, M, stride, sc, sh, resid, Y, V8, ev, stag, cus);
     else if (form == 0 && r3)
         hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y, 512, true>), dim3(1, nb), dim3(1024), 0, st, M,
                            stride, sc, sh, resid, Y, V8, ev, stag, cus);

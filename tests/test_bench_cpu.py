@@ -86,6 +86,9 @@ def test_pmc_traffic_follows_the_reported_kernel():
     assert t5 is not None and 0.94e9 <= t5 < 1.3e9
     t1, f1 = bench._pmc_traffic("wino88i32_gemm_lag_kernel<512,false>", 2048)
     assert f1 != f5
+    # the headline's kernel since round 6 (R3, 64-k stages): its own summary, 3-digit V read + fp32 M written
+    tk, fk = bench._pmc_traffic("wino88i32_gemm_r3k64_kernel<512,5>", 2048)
+    assert tk is not None and fk.startswith("r06_") and 0.81e9 <= tk < 1.2e9
 
 
 @pytest.mark.parametrize("G,sims,world,tag", [(2048, 800, 1, "configs[2], C3"), (2048, 800, 8, "configs[3], C4"),
