@@ -102,6 +102,22 @@ def test_batch_invariance(precision):
     assert float((p_16 - p_all[:16]).abs().max()) < 1e-4
 
 
+def test_forward_over_the_slice_limit():
+    """a forward of more boards than one pass holds (16,384: the int8 kernels' 32-bit offsets) runs as
+    equal slices (for_slices) -- 16,768 boards as 2 x 8,384 -- and every board's outputs are the bits it gets in a
+    small batch of the same size class (batch invariance), at both ends of the range."""
+    rng = np.random.default_rng(11)
+    B = 16768
+    codes = (rng.integers(0, 13, size=(B, 64)) * (rng.random((B, 64)) < 0.4)).astype(np.int8)
+    net = _net("init").kv_net(0)  # random-init weights: the headline's path
+    assert net.calibration()["path_large"] == "winograd88_i8f32r3"
+    cd = torch.from_numpy(codes).cuda()
+    p_all, v_all = net.forward_boards(cd)
+    for lo, hi in ((0, 300), (8300, 8500), (B - 300, B)):
+        p, v = net.forward_boards(cd[lo:hi])
+        assert torch.equal(p, p_all[lo:hi]) and torch.equal(v, v_all[lo:hi]), (lo, hi)
+
+
 @pytest.mark.parametrize("precision", ["fp32", "f64w", "i8x5", "i8r4", "fp32-i8", "fp32-r3"])
 def test_wino88_batch_invariance(precision):
     """F(8x8) (one row per board): a board's outputs are the same bits at 20
