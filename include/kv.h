@@ -325,8 +325,8 @@ int kv_dev_py_random(int device, const uint64_t* seeds, int n, int count, double
  * v_exp [100][rows] (either may be NULL) return V's digits and row exponents. seg 1 (4 digits, K 512):
  * V's exponents per 256-channel segment (v_exp [100][2][rows]), the fp32 tower's A/B form. seg 2 (4 digits):
  * KV_PREC_I8R4's 4 radix-256 digits in row lines [100][K/32][rows][4][32], its GEMM and fp64 M. seg 3
- * (4 digits): KV_ALGO_WINOGRAD88_I8R3's 3 radix-256 digits in row lines (slot 3 zero), the product's 6-pair
- * GEMM and fp32 M; seg 4 / 5: the same digits through the 32-k-stage / 64-k-stage GEMM kernel explicitly. */
+ * (4 digits): KV_ALGO_WINOGRAD88_I8R3's 3 radix-256 digits in 96-byte row lines [100][K/32][rows][3][32] (the
+ * first 3/4 of v_digits, the rest zero), the product's 6-pair GEMM and fp32 M. */
 int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K, int digits, int seg, double* M,
                    int8_t* v_digits, int* v_exp);
 /* The fp32 tower's residual output kernel on int8 digits (KV_ALGO_WINOGRAD88_I8): M [100][rows][512] fp32

@@ -1087,19 +1087,11 @@ static int launch_wino88i32_gemm_lag(const int8_t* V8, const int* ev, const int8
 }
 
 // TPW tiles per workgroup, the ring across tiles (kv_wino88i.h wino88i32_gemm_lagt_kernel)
-// ND 3: KV_PATH_WINO88_I8F32R3's 3 radix-256 digits (6 pairs), its B digits LJ.. lagging
-// NB: stage buffers of the copy ring (NB - 1 stages in flight)
-#ifndef KV_I8R3_LJ
-#define KV_I8R3_LJ 1
-#endif
+// NB: stage buffers of the copy ring (NB - 1 stages in flight; 3, 4 and 5 measured the same)
 #ifndef KV_I8F32_NB
 #define KV_I8F32_NB 3
 #endif
-#ifndef KV_I8R3_NB
-#define KV_I8R3_NB 3
-#endif
-template <int K, int TPW, int ND = 4, int LJ = (ND == 4 ? KV_I8F32_LJ : KV_I8R3_LJ),
-          int NB = (ND == 4 ? KV_I8F32_NB : KV_I8R3_NB)>
+template <int K, int TPW, int ND = 4, int LJ = KV_I8F32_LJ, int NB = KV_I8F32_NB>
 static int launch_wino88i32_gemm_lagt(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
                                       int rows, int stride, hipStream_t st) {
     using T = kv::Wino88iTile<kv::kI8DigitsF32>;
@@ -1316,9 +1308,6 @@ static int wino88i_blocks(kv_net* net, int nb, bool mark, bool r8, hipStream_t s
 struct I8f32Form {
     bool seg = false, slice = false, r4 = false, persist = false;
     int out = 0;  // 0 held, 1 r64, 2 persistent
-    // R3's GEMM with 64-k stages (wino88i32_gemm_r3k64_kernel; KV_I8R3_K64=0: the 32-k lagt kernel): 357 vs
-    // 375 us back to back at 2,048 boards, forward -3-5 %, bit-identical (profiles/r06_saddr_ab.log)
-    bool r3k64 = true;
 };
 static const I8f32Form& i8f32_form() {
     static const I8f32Form f = [] {
@@ -1332,8 +1321,6 @@ static const I8f32Form& i8f32_form() {
         x.persist = e && !strcmp(e, "p");
         e = getenv("KV_I8F32_OUT");
         x.out = !e ? 0 : !strcmp(e, "r64") ? 1 : !strcmp(e, "p") ? 2 : 0;
-        e = getenv("KV_I8R3_K64");
-        x.r3k64 = !e || e[0] != '0';
         return x;
     }();
     return f;
@@ -1363,6 +1350,7 @@ static int launch_wino88i32_out(kv_net* net, int l, const float* M, int nb, int 
     const float* sc = W + net->off.scale[l];
     const float* sh = W + net->off.shift[l];
     const int form = i8f32_form().out;
+    KV_REQUIRE(!r3 || nb % 32 == 0, KV_EINVAL, "R3 output kernel: %d boards (a multiple of 32: out_board)", nb);
     if (seg)
         hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y, 256>), dim3(2, nb), dim3(512), 0, st, M, stride,
                            sc, sh, resid, Y, V8, ev, 0, 0);
@@ -1401,33 +1389,22 @@ static int launch_wino88i32v_out(kv_net* net, int l, const float* M, int nb, int
 // the fp32 tower's int8-digit GEMM of one conv (K 256: one segment, per-row exponents)
 template <int K>
 static int i8f32_gemm(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M, int rows, int stride,
-                      bool seg, hipStream_t st, bool r3 = false, int r3form = -1) {
+                      bool seg, hipStream_t st, bool r3 = false) {
     constexpr int D = kv::kI8DigitsF32;
     const I8f32Form& f = i8f32_form();
-    if (r3) {  // KV_PATH_WINO88_I8F32R3, tile count as the 4-digit one's; r3form 0 / 1: the 32-k / 64-k kernel
+    if (r3) {  // KV_PATH_WINO88_I8F32R3 (96-byte row lines): the 64-k-stage kernel, tile count as the 4-digit one's
+        // (round 6: 357 vs 375 us for the 32-k form on 128-byte lines, forward -3-5 %, profiles/r06_saddr_ab.log)
         const int tpw = i8f32_tiles_per_wg(rows);
-        if (r3form < 0 ? f.r3k64 : r3form == 1) {
-            if (tpw == 5) {
-                note_dom<K>("wino88i32_gemm_r3k64_kernel<512,5>");
-                return launch_wino88i32_gemm_r3k64<K, 5>(V8, ev, U8, eu, M, rows, stride, st);
-            }
-            if (tpw == 4) {
-                note_dom<K>("wino88i32_gemm_r3k64_kernel<512,4>");
-                return launch_wino88i32_gemm_r3k64<K, 4>(V8, ev, U8, eu, M, rows, stride, st);
-            }
-            note_dom<K>("wino88i32_gemm_r3k64_kernel<512,1>");
-            return launch_wino88i32_gemm_r3k64<K, 1>(V8, ev, U8, eu, M, rows, stride, st);
-        }
         if (tpw == 5) {
-            note_dom<K>("wino88i32_gemm_lagt_kernel<512,5,3>");
-            return launch_wino88i32_gemm_lagt<K, 5, 3>(V8, ev, U8, eu, M, rows, stride, st);
+            note_dom<K>("wino88i32_gemm_r3k64_kernel<512,5>");
+            return launch_wino88i32_gemm_r3k64<K, 5>(V8, ev, U8, eu, M, rows, stride, st);
         }
         if (tpw == 4) {
-            note_dom<K>("wino88i32_gemm_lagt_kernel<512,4,3>");
-            return launch_wino88i32_gemm_lagt<K, 4, 3>(V8, ev, U8, eu, M, rows, stride, st);
+            note_dom<K>("wino88i32_gemm_r3k64_kernel<512,4>");
+            return launch_wino88i32_gemm_r3k64<K, 4>(V8, ev, U8, eu, M, rows, stride, st);
         }
-        note_dom<K>("wino88i32_gemm_lagt_kernel<512,1,3>");
-        return launch_wino88i32_gemm_lagt<K, 1, 3>(V8, ev, U8, eu, M, rows, stride, st);
+        note_dom<K>("wino88i32_gemm_r3k64_kernel<512,1>");
+        return launch_wino88i32_gemm_r3k64<K, 1>(V8, ev, U8, eu, M, rows, stride, st);
     }
     if constexpr (K == 512)
         if (seg) {
@@ -2174,13 +2151,12 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
     KV_REQUIRE(V && U && M && rows > 0 && rows % 128 == 0 && rows <= kMaxBoards && (K == 256 || K == 512) &&
                    (digits == 4 || digits == 5) &&
                    (!seg || (seg == 1 && digits == 4 && K == 512) || (seg == 2 && digits == 4) ||
-                    (seg >= 3 && seg <= 5 && digits == 4)),
+                    (seg == 3 && digits == 4)),
                KV_EINVAL, "kv_dev_wino88i: bad arguments (rows %d must be a multiple of 128, K %d 256 or 512, "
-               "digits %d 4 or 5, seg %d: 1 only with 4 digits and K 512, 2 (radix 256) and 3-5 (3 radix-256 "
-               "digits in 4 slots: the product's GEMM / the 32-k / the 64-k kernel) only with 4 digits)",
+               "digits %d 4 or 5, seg %d: 1 only with 4 digits and K 512, 2 (radix 256) and 3 (3 radix-256 "
+               "digits in 96-byte row lines) only with 4 digits)",
                rows, K, digits, seg);
-    const bool r8 = seg == 2, r3 = seg >= 3;
-    const int r3form = seg == 4 ? 0 : seg == 5 ? 1 : -1;
+    const bool r8 = seg == 2, r3 = seg == 3;
     const int nseg = seg == 1 ? 2 : 1;
     KV_HIP(hipSetDevice(device));
     const size_t nv = (size_t)kv::W88_XI * rows * K, nu = (size_t)kv::W88_XI * 512 * K;
@@ -2194,6 +2170,7 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
     KV_HIP(dm.alloc(nm));
     KV_HIP(dmf.alloc(nm));
     KV_HIP(v8.alloc(nv * digits));
+    KV_HIP(hipMemset(v8.p, 0, nv * digits));  // R3 lines fill 3/4 of it
     KV_HIP(u8.alloc(nu * digits));
     KV_HIP(ev.alloc((size_t)kv::W88_XI * rows * nseg));
     KV_HIP(eu.alloc((size_t)kv::W88_XI * 512));
@@ -2227,8 +2204,8 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
                      ? launch_wino88i_slice<256, D, double, 1, false, true>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0)
                      : launch_wino88i_slice<512, D, double, 1, false, true>(dv.p, rows, rows, kv::W88_XI, v8.p, ev.p, 0);
         if (!rc)
-            rc = K == 256 ? i8f32_gemm<256>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, false, 0, true, r3form)
-                          : i8f32_gemm<512>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, false, 0, true, r3form);
+            rc = K == 256 ? i8f32_gemm<256>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, false, 0, true)
+                          : i8f32_gemm<512>(v8.p, ev.p, u8.p, eu.p, dmf.p, rows, rows, false, 0, true);
     } else {  // the fp32 domain: 4 digits, M rounded to fp32 (returned widened)
         constexpr int D = kv::kI8DigitsF32;
         rc = K == 256 ? launch_wino88i_slice<256, D>(du.p, 512, 512, kv::W88_XI, u8.p, eu.p, 0)
@@ -2290,6 +2267,7 @@ int kv_dev_wino88i32_out(int device, const float* M, int rows, const float* scal
     KV_HIP(dy.alloc(ny));
     KV_HIP(dv.alloc(nm));
     KV_HIP(v8.alloc(nm * kv::kI8DigitsF32));
+    KV_HIP(hipMemset(v8.p, 0, nm * kv::kI8DigitsF32));  // R3 lines fill 3/4 of it
     // the per-row fused form: bit 3 the 64-register kernel, bit 5 the persistent one, neither the product's
     // default (KV_I8F32_OUT)
     const bool seg = (fused & 2) != 0, v64 = (fused & 4) != 0, r64 = (fused & 8) != 0, r3 = (fused & 16) != 0;
@@ -2589,14 +2567,11 @@ int kv_dev_gemm_clock(int device, int rows, int digits, double seconds, double* 
     const int tiles = kv::W88_XI * (rows / T::WM) * (512 / T::WN), nwg = tiles / tpw;
     KV_REQUIRE(tiles % (8 * tpw) == 0, KV_EINVAL, "kv_dev_gemm_clock: %d tiles, %d per workgroup", tiles, tpw);
     KV_HIP(stamps.alloc((size_t)nwg * 4));
-    const bool k64 = r3 && i8f32_form().r3k64;  // the stamped build of the form the product launches
-    const int bytes = k64 ? 3 * 4 * 128 * 96 : (r3 ? KV_I8R3_NB : KV_I8F32_NB) * T::STAGE;
-    auto kern = k64 ? (tpw == 5   ? kv::wino88i32_gemm_r3k64_kernel<K, 5, true>
-                       : tpw == 4 ? kv::wino88i32_gemm_r3k64_kernel<K, 4, true>
-                                  : kv::wino88i32_gemm_r3k64_kernel<K, 1, true>)
-               : r3 ? (tpw == 5   ? kv::wino88i32_gemm_lagt_kernel<K, 5, KV_I8R3_LJ, true, 3, KV_I8R3_NB>
-                      : tpw == 4 ? kv::wino88i32_gemm_lagt_kernel<K, 4, KV_I8R3_LJ, true, 3, KV_I8R3_NB>
-                                 : kv::wino88i32_gemm_lagt_kernel<K, 1, KV_I8R3_LJ, true, 3, KV_I8R3_NB>)
+    // the stamped build of the form the product launches (R3: the 64-k-stage kernel)
+    const int bytes = r3 ? 3 * 4 * 128 * 96 : KV_I8F32_NB * T::STAGE;
+    auto kern = r3 ? (tpw == 5   ? kv::wino88i32_gemm_r3k64_kernel<K, 5, true>
+                      : tpw == 4 ? kv::wino88i32_gemm_r3k64_kernel<K, 4, true>
+                                 : kv::wino88i32_gemm_r3k64_kernel<K, 1, true>)
                    : (tpw == 5   ? kv::wino88i32_gemm_lagt_kernel<K, 5, KV_I8F32_LJ, true, 4, KV_I8F32_NB>
                       : tpw == 4 ? kv::wino88i32_gemm_lagt_kernel<K, 4, KV_I8F32_LJ, true, 4, KV_I8F32_NB>
                                  : kv::wino88i32_gemm_lagt_kernel<K, 1, KV_I8F32_LJ, true, 4, KV_I8F32_NB>);

@@ -193,8 +193,8 @@ __device__ inline unsigned i8_quad_transpose(unsigned P, int lane) {
 // 32 channels goes to (((x * K/32 + kc) * slab_rows + r) * 4 + d) * 32 instead
 // -- the 4 digits of one row's chunk are one 128-byte line. NSEG = 2 (K = 512 only): one exponent per
 // 256-channel segment instead of per row (lanes 0-31 hold segment 0), at ex[(x * 2 + seg) * slab_rows + r].
-// R3 (KV_PATH_WINO88_I8F32R3; row lines, D = 4 slots): 3 radix-256 digits (i8_digits_r3) under the radix-256
-// exponent rule of the fp32 or fp64 rows, slot 3 zero
+// R3 (KV_PATH_WINO88_I8F32R3; row lines): 3 radix-256 digits (i8_digits_r3) under the radix-256 exponent rule of
+// the fp32 or fp64 rows, in 96-byte lines (((x * K/32 + kc) * slab_rows + r) * 3 + d) * 32
 template <int K, class T, int D, bool RL = false, int NSEG = 1, bool R8 = false, bool R3 = false>
 __global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict__ src, int n, int slab_rows,
                                                             int nslab, int8_t* __restrict__ dst,
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict_
     static_assert(!RL || D == 4, "row lines hold 4 digits");
     static_assert(NSEG == 1 || (NSEG == 2 && K == 512), "segments of 256 channels");
     static_assert(!R8 || (D == 4 && sizeof(T) == 8 && NSEG == 1), "radix 256: 4 digits of fp64 rows");
-    static_assert(!R3 || (D == 4 && RL && NSEG == 1 && !R8), "3 radix-256 digits in the 4 slots of row lines");
+    static_assert(!R3 || (D == 4 && RL && NSEG == 1 && !R8), "3 radix-256 digits in 96-byte row lines");
     constexpr int CPL = K / 64;  // 4 or 8 channels per lane
     const int lane = threadIdx.x & 63;
     const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -255,10 +255,11 @@ __global__ __launch_bounds__(256) void wino88i_slice_kernel(const T* __restrict_
         for (int d = 0; d < D; ++d) pk[d] |= (unsigned long long)(unsigned char)(signed char)dg[d] << (8 * i);
     }
     const int c = lane * CPL, kc = c / 32;
-    int8_t* o = RL ? dst + (((size_t)x * (K / 32) + kc) * slab_rows + r) * (D * 32) + (c % 32)
+    constexpr int LW = R3 ? 3 * 32 : D * 32;  // row-line bytes (R3: the 3 digits only)
+    int8_t* o = RL ? dst + (((size_t)x * (K / 32) + kc) * slab_rows + r) * LW + (c % 32)
                    : dst + ((((size_t)x * (K / 32) + kc) * D) * slab_rows + r) * 32 + (c % 32);
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
+    for (int d = 0; d < (R3 ? 3 : D); ++d) {
         int8_t* od = o + (size_t)d * (RL ? 32 : slab_rows * 32);
         if constexpr (CPL == 8)
             *(unsigned long long*)od = pk[d];
@@ -782,8 +783,8 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lag_kernel(const int8_t* _
 // STAMP (a diagnostic build, never the product's): wave 0 of each workgroup records the shader clock
 // (s_memtime) and the 100 MHz constant clock (s_memrealtime) at its start and end into stamps[4 * block] -- a
 // buffer of its own that no other code reads; kv_dev_gemm_clock turns them into the clock the chip held.
-// ND = 3 (KV_PATH_WINO88_I8F32R3): the same row lines (4 digit slots per 32-channel chunk), of which digits 0-2
-// hold 3 radix-256 digits (slot 3 zero, never read): the 6 pairs i + j <= 2, 3 exact int32 levels weighted 2^-8l.
+// ND: digit levels (4; round 6's ND = 3 form for KV_PATH_WINO88_I8F32R3 retired with R3's 128-byte lines: R3 runs
+// wino88i32_gemm_r3k64_kernel on 96-byte lines).
 // KV_COPY_SADDR (1): the ring's copies address a wave-uniform 64-bit base plus an unsigned 32-bit lane offset,
 // so they issue in the scalar-base form (one address VGPR per lane); 0: a 64-bit VGPR address pair per lane.
 #ifndef KV_COPY_SADDR
@@ -812,7 +813,7 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_lagt_kernel(const int8_t* 
     constexpr int NT = T::NT, WM = T::WM, WN = T::WN, GL = T::GL;
     constexpr int NK = K / 32, NS = TPW * NK;
     constexpr int NA = ND - LJ;
-    static_assert(GL == 4 && NK >= 3 && LJ >= 1 && LJ < ND && (ND == 4 || ND == 3), "4 pieces per wave and stage");
+    static_assert(GL == 4 && NK >= 3 && LJ >= 1 && LJ < ND && ND == 4, "4 pieces per wave and stage, 4 digits");
     static_assert(NB >= 3 && NB <= 5 && PD < NK, "ring of 3-5 stage buffers (at most 160 KiB)");
     constexpr double kStep = ND == 4 ? 0.0078125 : 0.00390625;  // level weight: radix 128 / 256
 
@@ -1002,15 +1003,16 @@ __device__ __forceinline__ i32x16_t r3mfma(i8x16_t a, i8x16_t b, i32x16_t c) {
 // R3's GEMM (KV_PATH_WINO88_I8F32R3) with 64-k stages: the 32-k lagt kernel gives a wave 12 MFMAs per stage
 // barrier at 3 digits (20 at 4), and its time did not move with 3, 4 or 5 ring buffers (370.6 / 371.3 / 371.6
 // us, profiles/r06_ring_depth_ab.log): the barrier's fixed cost, not the copies' latency, sets it. Here a stage is
-// two 32-channel chunks (24 MFMAs per wave per barrier), and only the 96 live bytes of each 128-byte row line
-// (digit slots 0-2; slot 3 is zero and never read) are copied, so a stage is 48 KiB and the ring keeps 3
-// buffers (144 KiB) with two stages in flight. LDS image per operand and chunk: 128 rows of 96 bytes, 16-byte
+// two 32-channel chunks (24 MFMAs per wave per barrier) of R3's 96-byte row lines [xi][K/32][row][3][32] (3
+// digits, no zero slot), so a stage is 48 KiB and the ring keeps 3 buffers (144 KiB) with two stages in flight.
+// LDS image per operand and chunk: 128 rows of 96 bytes (a contiguous 12 KiB block of the global lines), 16-byte
 // piece c = 2 d + half at position c ^ ((row >> 4) & 1) -- every ds_read_b128 lane group conflict-free
 // (rows 16-31 of a 32-row block land on the odd 16-byte bank groups, rows 0-15 on the even ones). Copies: wave
 // w fills 6 KiB pieces of plane (operand w >> 2, chunk (w >> 1) & 1), pieces 6 (w & 1) .. + 5; lane l of piece
 // pp carries unit u = 64 pp + l = (row u / 6, slot u % 6). Per stage a wave runs chunk 0's 12 MFMAs, chunk 1's
 // B digit 0 (6), and chunk 1's B digits 1-2 (6) after the next barrier under that stage's first reads. Same
-// products, same exact int32 levels, same bits as wino88i32_gemm_lagt_kernel<K, TPW, ., ., 3>.
+// products, same exact int32 levels, same bits as the 32-k lagt form it replaced (measured bit-identical,
+// profiles/r06_r3k64_ab.log; that form read 128-byte lines with a zero 4th slot and was retired with them).
 // ABL (timing ablations, outputs invalid; never the product's): 1 no copies after the prologue, 2 no MFMAs (the
 // fragments still read), 4 no M stores.
 template <int K, int TPW, bool STAMP = false, int ABL = 0>
@@ -1052,12 +1054,12 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
 
     const int wu = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the plane this wave copies
     const int op = wu >> 2, chunk = (wu >> 1) & 1, pp0 = 6 * (wu & 1);
-    const size_t sstep = (op ? (size_t)cout : (size_t)stride) * 128;  // one 32-channel chunk of row lines
+    const size_t sstep = (op ? (size_t)cout : (size_t)stride) * 96;  // one 32-channel chunk of 96-byte row lines
     const int8_t* gb[TPW];
 #pragma unroll
     for (int j = 0; j < TPW; ++j)
-        gb[j] = (op ? U8 + (((size_t)xis[j] * NK) * cout + (size_t)nbs[j]) * 128
-                    : V8 + (((size_t)xis[j] * NK) * stride + (size_t)rbs[j]) * 128) +
+        gb[j] = (op ? U8 + (((size_t)xis[j] * NK) * cout + (size_t)nbs[j]) * 96
+                    : V8 + (((size_t)xis[j] * NK) * stride + (size_t)rbs[j]) * 96) +
                 (size_t)chunk * sstep;
     // this lane's source byte in a chunk's row-line block, per piece: unsigned 32-bit, so the copy takes the
     // scalar-base + 32-bit-offset address form (one address VGPR per lane instead of a 64-bit pair)
@@ -1065,7 +1067,7 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
 #pragma unroll
     for (int g = 0; g < GL; ++g) {
         const int u = (pp0 + g) * 64 + lane, row = u / 6, slot = u - 6 * (u / 6);
-        goff[g] = (unsigned)(row * 128 + 16 * (slot ^ ((row >> 4) & 1)));
+        goff[g] = (unsigned)(row * 96 + 16 * (slot ^ ((row >> 4) & 1)));
     }
     const int ldst = (op * 2 + chunk) * PLANE + pp0 * 1024;
     auto issue1 = [&](int g, int s) {  // piece g of global stage s (tile s / NU, stage s % NU)
@@ -1850,6 +1852,20 @@ __device__ inline void wino88_input_row_of_cols(float (&xc)[4][8], int aa, float
     w88_bt(row, o);
 }
 
+// Row-line width: 4 digit slots (128 bytes) per 32-channel chunk, or R3's 3 (96 bytes: no zero slot in memory)
+template <bool R3>
+constexpr unsigned kI8LineBytes = R3 ? 96u : 128u;
+// The board an output workgroup handles. R3's 96-byte lines of boards 4g .. 4g+3 share 128-byte lines (4 x 96 =
+// 3 x 128), so those 4 boards go to one XCD (workgroups are dealt to the 8 XCDs round-robin: id mod 8), whose L2
+// merges their partial lines; dealt board by board, each shared line took partial writes from two XCDs. A
+// bijection on [0, nb) for nb a multiple of 32.
+template <bool R3>
+__device__ inline int out_board(int id) {
+    if constexpr (!R3) return id;
+    const int x = id & 7, s = id >> 3;
+    return 4 * (x + 8 * (s >> 2)) + (s & 3);
+}
+
 // R3 (KV_PATH_WINO88_I8F32R3): the next V's 3 radix-256 digits (i8_digits_r3 under i8_row_exponent_f32r) in
 // the same lines, slot 3 zero
 template <bool R3>
@@ -1892,7 +1908,7 @@ __global__ __launch_bounds__(1024, 8) void wino88i32_out2_kernel(const float* __
     __shared__ __attribute__((aligned(16))) unsigned red[NW][2][5][16];
     __shared__ int exs[100];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
-    const int c = w * 32 + (lane & 31), b = blockIdx.y;
+    const int c = w * 32 + (lane & 31), b = out_board<R3>((int)blockIdx.y);
     out_stagger(b, stag, first);
     float xc[4][8];  // the half's columns 4h .. 4h+3, all 8 rows (after the half exchange)
     {
@@ -1934,7 +1950,8 @@ __global__ __launch_bounds__(1024, 8) void wino88i32_out2_kernel(const float* __
     }
     __syncthreads();
     const int q = lane & 3;
-    const unsigned off0 = ((unsigned)(c >> 5) * rows + b) * 128 + q * 32 + (c & 28), xstride = NK * rows * 128;
+    const unsigned off0 = ((unsigned)(c >> 5) * rows + b) * kI8LineBytes<R3> + q * 32 + (c & 28),
+                   xstride = NK * rows * kI8LineBytes<R3>;
     unsigned* const dst = (unsigned*)V8;
 #pragma unroll
     for (int aa = 0; aa < 5; ++aa) {
@@ -1945,7 +1962,13 @@ __global__ __launch_bounds__(1024, 8) void wino88i32_out2_kernel(const float* __
         for (int bb = 0; bb < 10; ++bb) {
             const int xi = a * 10 + bb;
             const unsigned P = i8f32_digits<R3>(o[bb], exs[xi]);
-            __builtin_nontemporal_store(i8_quad_transpose(P, lane), &dst[(off0 + (unsigned)xi * xstride) >> 2]);
+            {
+                const unsigned T4 = i8_quad_transpose(P, lane);  // lane q of the quad: digit q's 4 channels
+                if constexpr (!R3)
+                    __builtin_nontemporal_store(T4, &dst[(off0 + (unsigned)xi * xstride) >> 2]);
+                else if (q < 3)  // R3's 96-byte lines share 128-byte lines: ordinary stores, merged in L2
+                    dst[(off0 + (unsigned)xi * xstride) >> 2] = T4;
+            }
         }
     }
 }
@@ -1969,7 +1992,7 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
     __shared__ __attribute__((aligned(16))) unsigned red[NW][2][5][16];
     __shared__ int exs[100];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5;
-    const int seg = blockIdx.x, c = seg * CW + w * 32 + (lane & 31), b = blockIdx.y;
+    const int seg = blockIdx.x, c = seg * CW + w * 32 + (lane & 31), b = out_board<R3>((int)blockIdx.y);
     out_stagger(b, stag, first);
     unsigned long long st[6] = {};
     const bool stamper = STAMP && (w == 0 || w == NW - 1) && lane == 0 && b < kOutStampBoards;
@@ -2021,7 +2044,8 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
     // row line (xi, kc = c / 32, b): 128 bytes, digit d of channel 32 kc + i at byte 32 d + i
     const int q = lane & 3;
     // 32-bit byte offsets (the digits of 100 x rows x 512 values < 2^32 bytes)
-    const unsigned off0 = ((unsigned)(c >> 5) * rows + b) * 128 + q * 32 + (c & 28), xstride = NK * rows * 128;
+    const unsigned off0 = ((unsigned)(c >> 5) * rows + b) * kI8LineBytes<R3> + q * 32 + (c & 28),
+                   xstride = NK * rows * kI8LineBytes<R3>;
     unsigned* const dst = (unsigned*)V8;
 #pragma unroll
     for (int aa = 0; aa < 5; ++aa) {
@@ -2033,7 +2057,13 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
             // non-temporal: the digits are read once, by the next GEMM (forward -1.2 % at 2,048 boards against
             // plain stores, bit-identical; the GEMM's M stored non-temporal instead slowed the output kernel that
             // reads it: profiles/r05_out_nt_ab.log)
-            __builtin_nontemporal_store(i8_quad_transpose(P, lane), &dst[(off0 + (unsigned)xi * xstride) >> 2]);
+            {
+                const unsigned T4 = i8_quad_transpose(P, lane);  // lane q of the quad: digit q's 4 channels
+                if constexpr (!R3)
+                    __builtin_nontemporal_store(T4, &dst[(off0 + (unsigned)xi * xstride) >> 2]);
+                else if (q < 3)  // R3's 96-byte lines share 128-byte lines: ordinary stores, merged in L2
+                    dst[(off0 + (unsigned)xi * xstride) >> 2] = T4;
+            }
         }
     }
     if constexpr (STAMP) {
@@ -2189,7 +2219,8 @@ __global__ __launch_bounds__(1024) void wino88i32_outp_kernel(const float* __res
         __syncthreads();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next board's first two slots (and Y) landed
         const int q = lane & 3;
-        const unsigned off0 = ((unsigned)(c >> 5) * rows + b) * 128 + q * 32 + (c & 28), xstride = NK * rows * 128;
+        const unsigned off0 = ((unsigned)(c >> 5) * rows + b) * kI8LineBytes<R3> + q * 32 + (c & 28),
+                   xstride = NK * rows * kI8LineBytes<R3>;
         unsigned* const dst = (unsigned*)V8;
 #pragma unroll
         for (int aa = 0; aa < 5; ++aa) {
@@ -2198,7 +2229,13 @@ __global__ __launch_bounds__(1024) void wino88i32_outp_kernel(const float* __res
             for (int bb = 0; bb < 10; ++bb) {
                 const int xi = a * 10 + bb;
                 const unsigned P = i8f32_digits<R3>(vk[aa][bb], exs[xi]);
-                __builtin_nontemporal_store(i8_quad_transpose(P, lane), &dst[(off0 + (unsigned)xi * xstride) >> 2]);
+                {
+                const unsigned T4 = i8_quad_transpose(P, lane);  // lane q of the quad: digit q's 4 channels
+                if constexpr (!R3)
+                    __builtin_nontemporal_store(T4, &dst[(off0 + (unsigned)xi * xstride) >> 2]);
+                else if (q < 3)  // R3's 96-byte lines share 128-byte lines: ordinary stores, merged in L2
+                    dst[(off0 + (unsigned)xi * xstride) >> 2] = T4;
+            }
             }
         }
     }

@@ -148,15 +148,9 @@ def split_r3(a, e):
     return np.stack([(((u >> (8 * (2 - i))) & 255) - 128).astype(np.int8) for i in range(3)])
 
 
-def slots_r3(d):
-    """3 digits [3][...] -> the row lines' 4 slots [4][...] (slot 3 zero)."""
-    return np.concatenate([d, np.zeros_like(d[:1])])
-
-
 def gemm_r3(V, U, f32_rows=False):
-    """KV_PATH_WINO88_I8F32R3's GEMM (wino88i32_gemm_lagt_kernel<K, TPW, LJ, false, 3>): V [X][R][K], U [X][C][K]
-    -> (M [X][R][C] rounded to fp32 once, returned widened; V digits [4][X][R][K] with slot 3 zero; V exponents
-    [X][R]). The 6 pairs i + j <= 2 as 3 exact integer levels, combined m = L2, m = m 2^-8 + L_l (exact), scaled
+    """KV_PATH_WINO88_I8F32R3's GEMM (wino88i32_gemm_r3k64_kernel<K, TPW>): V [X][R][K], U [X][C][K]
+    -> (M [X][R][C] rounded to fp32 once, returned widened; V digits [3][X][R][K]; V exponents [X][R]). The 6 pairs i + j <= 2 as 3 exact integer levels, combined m = L2, m = m 2^-8 + L_l (exact), scaled
     by 2^(ev + eu - 14). f32_rows: V's exponents by the fp32-bit rule (the output kernel's and conv2's slice of
     fp32 V), U's always from fp64."""
     ev = row_exponents_r3_f32(V) if f32_rows else row_exponents_r3(V)
@@ -173,4 +167,4 @@ def gemm_r3(V, U, f32_rows=False):
     for l in (1, 0):
         m = m * 0.00390625 + lev[l]  # exact, as the kernel's fma
     M = np.ldexp(m, (ev[:, :, None] + eu[:, None, :] - 14).astype(np.int32)).astype(np.float32).astype(np.float64)
-    return M, slots_r3(dv), ev
+    return M, dv, ev

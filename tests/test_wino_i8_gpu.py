@@ -74,15 +74,13 @@ def test_i8r_gemm_bit_exact(K, rows):
     assert np.array_equal(M.view(np.uint64), Mr.view(np.uint64)), float(np.abs(M - Mr).max())
 
 
-@pytest.mark.parametrize("K,rows,form", [(256, 128, 3), (512, 128, 3), (512, 256, 3), (256, 128, 4), (512, 256, 4),
-                                         (256, 128, 5), (512, 256, 5), (512, 2048, 5)])
-def test_i8r3_gemm_bit_exact(K, rows, form):
+@pytest.mark.parametrize("K,rows", [(256, 128), (512, 128), (512, 256), (512, 2048)])
+def test_i8r3_gemm_bit_exact(K, rows):
     """KV_PATH_WINO88_I8F32R3: the slice kernel's 3 radix-256 digits (balanced bytes of rint(a 2^(23 - e)), the
-    exponent bumped at 127/128 of a power of two; slot 3 of each row line zero) and the 6-pair GEMM (3 digit
-    levels), bit for bit against tests/_i8_digits (split_r3, gemm_r3): digits, exponents, M rounded to fp32.
-    form 3: the product's GEMM; 4: the 32-k-stage lagt kernel; 5: the 64-k-stage kernel copying 96-byte rows
-    (at 2,048 rows: C3's grid, 5 tiles per workgroup). Rows at the exponent rule's edges, an all-zero row,
-    subnormals, +-2^-40."""
+    exponent bumped at 127/128 of a power of two) in 96-byte row lines [100][K/32][rows][3][32], and the 6-pair
+    GEMM (3 digit levels; wino88i32_gemm_r3k64_kernel: 64-k stages, at 2,048 rows C3's grid with 5 tiles per
+    workgroup), bit for bit against tests/_i8_digits (split_r3, gemm_r3): digits, exponents, M rounded to fp32.
+    Rows at the exponent rule's edges, an all-zero row, subnormals, +-2^-40."""
     rng = np.random.default_rng(K + rows + 5)
     V = rng.standard_normal((100, rows, K)) * np.exp2(rng.integers(-20, 20, size=(100, rows, 1)))
     V[0, 0] = 0.0
@@ -93,12 +91,14 @@ def test_i8r3_gemm_bit_exact(K, rows, form):
     V[3, 3] = np.where(rng.random(K) < 0.5, -1.0, 1.0) * np.exp2(-40.0)
     U = rng.standard_normal((100, 512, K)) * 0.05
     U[5, 7] = 0.0
-    M, dg, ex = _run(V, U, 4, seg=form)
+    M, dg, ex = _run(V, U, 4, seg=3)
     Mr, dv, evr = D.gemm_r3(V, U)
     assert np.array_equal(ex, evr.astype(np.int32))
     assert ex[1, 1] == 3 and ex[1, 2] == 4 and ex[1, 3] == 4
-    assert not dg.reshape(100, K // 32, rows, 4, 32)[:, :, :, 3].any()  # slot 3 unused
-    assert np.array_equal(dg.reshape(100, K // 32, rows, 4, 32), D.pack(dv).transpose(0, 1, 3, 2, 4))  # row lines
+    nb = 100 * K * rows * 3  # 96-byte row lines fill the first 3/4 of the (4-digit-sized) buffer
+    lines = dg.reshape(-1)[:nb].reshape(100, K // 32, rows, 3, 32)
+    assert not dg.reshape(-1)[nb:].any()  # nothing written past them
+    assert np.array_equal(lines, D.pack(dv).transpose(0, 1, 3, 2, 4))
     assert np.array_equal(M.view(np.uint64), Mr.view(np.uint64)), float(np.abs(M - Mr).max())
 
 
@@ -178,6 +178,10 @@ def _out(M, scale, shift, resid, flags):
     _lib.check(L.kv_dev_wino88i32_out(0, P(np.ascontiguousarray(M), C.c_float), R, P(scale, C.c_float),
                                       P(shift, C.c_float), rp, int(flags), P(Y, C.c_float), P(dg, C.c_int8),
                                       P(ex, C.c_int32)), "kv_dev_wino88i32_out")
+    if flags & 16:  # R3: 96-byte row lines [100][16][R][3][32] in the first 3/4 of the buffer, nothing after
+        nb = 100 * 16 * R * 96
+        assert not dg.reshape(-1)[nb:].any()
+        dg = dg.reshape(-1)[:nb].reshape(100, 16, R, 3, 32)
     return Y, dg, ex
 
 
@@ -210,8 +214,8 @@ def test_i8f32_out_kernel_writes_the_slice_kernels_digits(rows, resid, seg):
     assert np.array_equal(df, ds)
     assert (ef[..., 5] == 0).all() and not df[:, :, 5].any()
     assert len(np.unique(ef)) > 3  # exponents actually vary across rows
-    if seg & 16:  # 3 radix-256 digits (KV_PATH_WINO88_I8F32R3): slot 3 of every row line zero
-        assert not df[:, :, :, 3].any()
+    if seg & 16:  # 3 radix-256 digits (KV_PATH_WINO88_I8F32R3): 96-byte row lines
+        assert df.shape == (100, 16, rows, 3, 32)
 
 
 @pytest.mark.parametrize("rows,resid", [(128, False), (128, True), (256, True)])
