@@ -1359,6 +1359,9 @@ static int launch_wino88i32_out(kv_net* net, int l, const float* M, int nb, int 
     else if (form == 0 && r3 && out_abl() == 1)  // KV_OUT_ABL=1: timing ablation (outputs invalid)
         hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y, 512, true, false, 1>), dim3(1, nb), dim3(1024), 0,
                            st, M, stride, sc, sh, resid, Y, V8, ev, stag, cus);
+    else if (form == 0 && r3 && WRITE_Y && nb >= 1024)  // Y / residual non-temporal at large batches (YNT)
+        hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y, 512, true, false, 0, true>), dim3(1, nb),
+                           dim3(1024), 0, st, M, stride, sc, sh, resid, Y, V8, ev, stag, cus);
     else if (form == 0 && r3)
         hipLaunchKernelGGL((kv::wino88i32_out_kernel<RESID, WRITE_Y, 512, true>), dim3(1, nb), dim3(1024), 0, st, M,
                            stride, sc, sh, resid, Y, V8, ev, stag, cus);

@@ -1980,7 +1980,7 @@ __global__ __launch_bounds__(1024, 8) void wino88i32_out2_kernel(const float* __
 constexpr int kOutStampBoards = 4096;
 __device__ unsigned long long kOutStamps[kOutStampBoards][2][8];
 
-template <bool RESID, bool WRITE_Y, int CW, bool R3 = false, bool STAMP = false, int ABL = 0>
+template <bool RESID, bool WRITE_Y, int CW, bool R3 = false, bool STAMP = false, int ABL = 0, bool YNT = false>
 __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __restrict__ M, int rows,
                                                                const float* __restrict__ scale,
                                                                const float* __restrict__ shift, const float* resid,
@@ -2002,7 +2002,7 @@ __global__ __launch_bounds__(2 * CW) void wino88i32_out_kernel(const float* __re
         float t2[10][4];  // B10^T of the plane's columns 4h .. 4h+3
         {
             float x2[4][8];
-            wino88_out_plane_half<RESID, WRITE_Y, false, ABL>(M, rows, b, c, h, scale[c], shift[c], resid, Y, x2);
+            wino88_out_plane_half<RESID, WRITE_Y, false, ABL, YNT>(M, rows, b, c, h, scale[c], shift[c], resid, Y, x2);
             wino88_input_cols(x2, h, t2);
         }
 #pragma unroll
