@@ -1014,7 +1014,11 @@ __device__ __forceinline__ i32x16_t r3mfma(i8x16_t a, i8x16_t b, i32x16_t c) {
 // products, same exact int32 levels, same bits as the 32-k lagt form it replaced (measured bit-identical,
 // profiles/r06_r3k64_ab.log; that form read 128-byte lines with a zero 4th slot and was retired with them).
 // ABL (timing ablations, outputs invalid; never the product's): 1 no copies after the prologue, 2 no MFMAs (the
-// fragments still read), 4 no M stores.
+// fragments still read), 4 no M stores. KV_R3_M_NT (1): M stored non-temporally -- the GEMM 339 -> 325 us, the
+// output kernels that read it +2 %, forward -1.5 % at 2,048 boards, neutral at 256 (profiles/r06_mnt_ab.log).
+#ifndef KV_R3_M_NT
+#define KV_R3_M_NT 1
+#endif
 template <int K, int TPW, bool STAMP = false, int ABL = 0>
 __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t* __restrict__ V8,
                                                                    const int* __restrict__ ev,
@@ -1212,6 +1216,8 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
                 const float o = (float)ldexp(mm, evx[row] + ec);
                 if constexpr ((ABL & 4) != 0)
                     asm volatile("" ::"v"(o));
+                else if constexpr (KV_R3_M_NT)
+                    __builtin_nontemporal_store(o, &M[((size_t)xi * stride + r_base + wm * 32 + row) * cout + col]);
                 else
                     M[((size_t)xi * stride + r_base + wm * 32 + row) * cout + col] = o;
             }
