@@ -787,10 +787,7 @@ def main():
                                                                                     FLOP_RES_CONV_PER_BOARD)
             aa_ach = (per * bpl / (aa["conv_ms"] * 1e-3) / 1e12) if aa["conv_ms"] > 0 else None
             out["fp32_" + args.alt_algo] = {
-                "note": ("the same fp32 network with the Winograd F(4x8,3x3) tower (60 points, 2 tiles per board, "
-                         "KV_ALGO_WINOGRAD48): about half the logit error of F(8x8) for 20 % more GEMM FLOPs and "
-                         "transform bytes" if aa["dom_path"] == 1 else
-                         "the same fp32 F(8x8) tower with its GEMMs on v_mfma_f32_32x32x2_f32 (fp32 products, "
+                "note": ("the same fp32 F(8x8) tower with its GEMMs on v_mfma_f32_32x32x2_f32 (fp32 products, "
                          "fp32 accumulation after every product; KV_ALGO_WINOGRAD88)" if aa["dom_path"] == 2
                          else f"the same fp32 network with algo {args.alt_algo}"),
                 "value": (aa["sims"] if mcts else aa["plies"]) / aa["dt"], "unit": unit,

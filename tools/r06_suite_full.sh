@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 6: the whole -m gpu suite and smoke() on the final code, one pass
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+O=$R/gpurun_out/${1:-r06_suite_full}
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/gpu_suite.log 2>&1 \
+    || { tail -40 $O/gpu_suite.log; exit 1; }
+tail -2 $O/gpu_suite.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+tail -1 $O/smoke.log
