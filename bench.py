@@ -104,7 +104,7 @@ def parse():
                          "does) or lazy (only the rows the schedule consumes, identical games); hash: PROFILING "
                          "ONLY -- the MCTS test evaluator (uniform priors, hashed values) instead of the network, "
                          "3 launches per sim-step, so a tree-kernel counter run of a whole 800-sim move stays under "
-                         "rocprofv3's dispatch limit (tools/r03_tree.sh); its line is not a measurement")
+                         "rocprofv3's dispatch limit (tools/runs/r03_tree.sh); its line is not a measurement")
     ap.add_argument("--tree-edge-cap", type=int, default=0,
                     help="MCTS edge pool per slot (0: KV_MAXM x (sims+1), which cannot overflow; an overflow "
                          "fails the run). Profiling runs under rocprofv3 --pmc use a smaller pool")

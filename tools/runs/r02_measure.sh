@@ -19,7 +19,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o c3 -- python3 
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "wino_gemm" -f csv -d $O/pmc_gemm_fetch -o f -- python3 $R/tools/nn_speed.py 2048 > $O/pmc_gemm_fetch.log 2>&1
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "wino_gemm" -f csv -d $O/pmc_gemm_write -o w -- python3 $R/tools/nn_speed.py 2048 > $O/pmc_gemm_write.log 2>&1
 # tree-kernel PMC at C3's 2,048 slots with 300 sims/move: rocprofv3 --pmc segfaults in its host
-# library on the 800-sim run (tools/r02_tree.sh)
+# library on the 800-sim run (tools/runs/r02_tree.sh)
 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_mcts" -f csv -d $O/pmc_tree_fetch -o f -- python3 $R/bench.py $SHORT --warmup 0 --sims 300 > $O/pmc_tree_fetch.log 2>&1
 timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_mcts" -f csv -d $O/pmc_tree_write -o w -- python3 $R/bench.py $SHORT --warmup 0 --sims 300 > $O/pmc_tree_write.log 2>&1
 echo measure-done

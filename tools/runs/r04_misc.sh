@@ -13,5 +13,5 @@ KV_TRAINED_ITERS=20 KV_TRAINED_GAMES=256 KV_TRAINED_MAX_MOVES=80 KV_TRAINED_BOAR
 KV_BENCH_BACKEND=gloo timeout -k 10 400 python -u bench.py --gpus 2 --steps 1 --warmup 1 --slots 256 --sims 50 \
     --alt-precision= --alt-algo= --ref-block 0 --no-cpu-baseline --trained-steps 0 \
     > gpurun_out/r04_bench_gloo2_rehearsal.log 2> gpurun_out/r04_bench_gloo2_rehearsal.err
-bash tools/r04_i8out_pmc.sh r04_i8io_pmc
-AB_ENVS="KV_I8_PRIO=0 KV_I8_PRIO=1 KV_I8_PRIO=0 KV_I8_PRIO=1" bash tools/r04_i8_ab.sh
+bash tools/runs/r04_i8out_pmc.sh r04_i8io_pmc
+AB_ENVS="KV_I8_PRIO=0 KV_I8_PRIO=1 KV_I8_PRIO=0 KV_I8_PRIO=1" bash tools/runs/r04_i8_ab.sh

@@ -30,5 +30,5 @@ cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_row -o run -- python3 $R/tools/ab_forward.py pr 2048 > $O/prof_row.log 2>&1
 KV_I8F32_SEG=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_seg -o run -- python3 $R/tools/ab_forward.py ps 2048 > $O/prof_seg.log 2>&1
-timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES -d $O/maps_prof -o m -- python3 $R/tools/r05_maps.py $O/maps.txt > $O/maps.log 2>&1
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES -d $O/maps_prof -o m -- python3 $R/tools/runs/r05_maps.py $O/maps.txt > $O/maps.log 2>&1
 echo ab3-done

@@ -7,5 +7,5 @@ O=$R/gpurun_out/${1:-r05_gemm_ab}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 300 python -u tools/i8gemm_ab.py 2048 256 > $O/gemm_ab.log 2>&1
-bash tools/r05_fused_out.sh ${1:-r05_gemm_ab}/fused
+bash tools/runs/r05_fused_out.sh ${1:-r05_gemm_ab}/fused
 echo gemm-ab-done

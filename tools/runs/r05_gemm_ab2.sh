@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5: int8-digit GEMM forms A/B (tools/i8gemm_ab.py); the library layout under rocprofv3 --pmc for the
-# round-3 SIGSEGV attribution (tools/r05_maps.py)
+# round-3 SIGSEGV attribution (tools/runs/r05_maps.py)
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
@@ -10,5 +10,5 @@ export PYTHONUNBUFFERED=1
 timeout -k 10 300 python -u tools/i8gemm_ab.py 2048 256 > $O/gemm_ab.log 2>&1
 cd /tmp
 export TMPDIR=/tmp
-timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES -d $O/maps_prof -o m -- python3 $R/tools/r05_maps.py $O/maps.txt > $O/maps.log 2>&1
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES -d $O/maps_prof -o m -- python3 $R/tools/runs/r05_maps.py $O/maps.txt > $O/maps.log 2>&1
 echo gemm-ab-done

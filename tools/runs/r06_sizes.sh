@@ -11,4 +11,4 @@ for rep in 1 2; do
     KV_ALGO=winograd88i8r3 timeout -k 10 200 python -u tools/ab_forward.py sz 256 512 768 1024 1536 2048 >> $O/ab.log 2>&1
 done
 grep -v amdgpu $O/ab.log
-bash tools/r06_gamelen2.sh
+bash tools/runs/r06_gamelen2.sh
