@@ -1111,7 +1111,7 @@ static int launch_wino88i32_gemm_lagt(const int8_t* V8, const int* ev, const int
 template <int K, int TPW>
 static int launch_wino88i32_gemm_r3k64(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
                                        int rows, int stride, hipStream_t st) {
-    constexpr int bytes = 3 * 4 * 128 * 96;
+    constexpr int bytes = 3 * 4 * 128 * 96 + TPW * 1024;  // the ring + every tile's exponents
     auto kern = kv::wino88i32_gemm_r3k64_kernel<K, TPW>;
     if constexpr (K == 512 && TPW == 5) {  // KV_R3K64_ABL: timing ablations (outputs invalid; A/B tooling only)
         static const int abl = [] {
@@ -1123,6 +1123,7 @@ static int launch_wino88i32_gemm_r3k64(const int8_t* V8, const int* ev, const in
         if (abl == 3) kern = kv::wino88i32_gemm_r3k64_kernel<K, TPW, false, 3>;
         if (abl == 4) kern = kv::wino88i32_gemm_r3k64_kernel<K, TPW, false, 4>;
         if (abl == 7) kern = kv::wino88i32_gemm_r3k64_kernel<K, TPW, false, 7>;
+        if (abl == 8) kern = kv::wino88i32_gemm_r3k64_kernel<K, TPW, false, 8>;
     }
     KV_HIP(lds_opt_in((const void*)kern, bytes));
     const int tiles = kv::W88_XI * (rows / 128) * (512 / 128);
@@ -2571,7 +2572,7 @@ int kv_dev_gemm_clock(int device, int rows, int digits, double seconds, double* 
     KV_REQUIRE(tiles % (8 * tpw) == 0, KV_EINVAL, "kv_dev_gemm_clock: %d tiles, %d per workgroup", tiles, tpw);
     KV_HIP(stamps.alloc((size_t)nwg * 4));
     // the stamped build of the form the product launches (R3: the 64-k-stage kernel)
-    const int bytes = r3 ? 3 * 4 * 128 * 96 : KV_I8F32_NB * T::STAGE;
+    const int bytes = r3 ? 3 * 4 * 128 * 96 + tpw * 1024 : KV_I8F32_NB * T::STAGE;
     auto kern = r3 ? (tpw == 5   ? kv::wino88i32_gemm_r3k64_kernel<K, 5, true>
                       : tpw == 4 ? kv::wino88i32_gemm_r3k64_kernel<K, 4, true>
                                  : kv::wino88i32_gemm_r3k64_kernel<K, 1, true>)

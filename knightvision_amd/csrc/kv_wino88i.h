@@ -1014,7 +1014,7 @@ __device__ __forceinline__ i32x16_t r3mfma(i8x16_t a, i8x16_t b, i32x16_t c) {
 // products, same exact int32 levels, same bits as the 32-k lagt form it replaced (measured bit-identical,
 // profiles/r06_r3k64_ab.log; that form read 128-byte lines with a zero 4th slot and was retired with them).
 // ABL (timing ablations, outputs invalid; never the product's): 1 no copies after the prologue, 2 no MFMAs (the
-// fragments still read), 4 no M stores. KV_R3_M_NT (1): M stored non-temporally -- the GEMM 339 -> 325 us, the
+// fragments still read), 4 no M stores, 8 no exponent loads in the epilogue. KV_R3_M_NT (1): M stored non-temporally -- the GEMM 339 -> 325 us, the
 // output kernels that read it +2 %, forward -1.5 % at 2,048 boards, neutral at 256 (profiles/r06_mnt_ab.log).
 #ifndef KV_R3_M_NT
 #define KV_R3_M_NT 1
@@ -1108,6 +1108,18 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
             }
         }
 
+    // every tile's row / column exponents staged in LDS beside the ring (TPW x 1 KiB), loaded before the prologue
+    // copies: the epilogue reads them from LDS instead of waiting on global loads at each tile's end (timing
+    // ablation without the loads: 339 -> 323 us, profiles/r06_r3k64_ablations_final.log)
+    int* const exl = (int*)(L0 + NB * STAGE);  // [TPW][256]: ev rows 0-127, eu columns 128-255
+#pragma unroll
+    for (int q = 0; q < (TPW * 256 + 511) / 512; ++q) {
+        const int t = tid + q * 512;
+        if (t < TPW * 256) {
+            const int jj = t >> 8, k = t & 255;
+            exl[t] = k < 128 ? ev[(size_t)xis[jj] * stride + rbs[jj] + k] : eu[(size_t)xis[jj] * cout + nbs[jj] + k - 128];
+        }
+    }
 #pragma unroll
     for (int p = 0; p < PD; ++p)
 #pragma unroll
@@ -1202,18 +1214,18 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
         }
         h2();
         const int xi = xis[j], n_base = nbs[j], r_base = rbs[j];
-        const int* evx = ev + (size_t)xi * stride + r_base + wm * 32;
+        const int* evx = exl + j * 256 + wm * 32;  // LDS (staged above)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
             const int col = n_base + wn * NT * 32 + nt * 32 + lr;
-            const int ec = eu[(size_t)xi * cout + col] - 14;
+            const int ec = (ABL & 8) ? -14 : exl[j * 256 + 128 + wn * NT * 32 + nt * 32 + lr] - 14;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
                 double mm = (double)acc[ND - 1][nt][r];
 #pragma unroll
                 for (int l = ND - 2; l >= 0; --l) mm = __builtin_fma(mm, kStep, (double)acc[l][nt][r]);  // exact
-                const float o = (float)ldexp(mm, evx[row] + ec);
+                const float o = (float)ldexp(mm, ((ABL & 8) ? 0 : evx[row]) + ec);
                 if constexpr ((ABL & 4) != 0)
                     asm volatile("" ::"v"(o));
                 else if constexpr (KV_R3_M_NT)
