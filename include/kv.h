@@ -334,7 +334,8 @@ int kv_dev_wino88i(int device, const double* V, int rows, const double* U, int K
  * [rows][64][512] (= ReLU(A^T M A * scale + shift (+ resid))) and the next conv's V as row-line digits
  * [100][16][rows][4][32] with row exponents [100][rows]. fused bit 0 set: the product's one-kernel form
  * (KV_I8F32_OUT's choice; with bit 3 also set the 64-register wino88i32_out2_kernel, with bit 5 the
- * persistent LDS-DMA wino88i32_outp_kernel; bit 4: 3 radix-256 digits, KV_ALGO_WINOGRAD88_I8R3's), clear:
+ * persistent LDS-DMA wino88i32_outp_kernel; bit 4: 3 radix-256 digits, KV_ALGO_WINOGRAD88_I8R3's, in 96-byte
+ * lines [100][16][rows][3][32] in the first 3/4 of v_digits, the rest zero), clear:
  * wino88_out_kernel's fp32 V then the slice kernel (bit-identical); bit 1:
  * exponents per 256-channel segment ([100][2][rows]) instead of per row; bit 2 (KV_ALGO_WINOGRAD88_I8V's V,
  * per row): with bit 0 the one-kernel wino88i32v_out_kernel, without it wino88_out_kernel's Y, then

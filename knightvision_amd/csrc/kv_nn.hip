@@ -1002,7 +1002,7 @@ static int wino88d_blocks(kv_net* net, int nb, bool mark, hipStream_t st) {
 // (4 digits: the fp32 domain's row-line layout)
 // (NSEG 2: V's exponents per 256-channel segment, K 512 only)
 // (R8: KV_PATH_WINO88_I8R's 4 radix-256 digits of fp64 rows, row lines)
-// (R3: KV_PATH_WINO88_I8F32R3's 3 radix-256 digits in the 4 slots of row lines)
+// (R3: KV_PATH_WINO88_I8F32R3's 3 radix-256 digits in 96-byte row lines)
 template <int K, int D = kv::kI8Digits, class T, int NSEG = 1, bool R8 = false, bool R3 = false>
 static int launch_wino88i_slice(const T* src, int n, int slab_rows, int nslab, int8_t* dst, int* ex,
                                 hipStream_t st) {
