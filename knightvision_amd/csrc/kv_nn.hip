@@ -696,6 +696,15 @@ static hipError_t lds_opt_in(const void* fn, int bytes) {
 
 // CUs of the current device, cached per device (the F(8x8) point split reads it per launch)
 // KV_OUT_STAG: the output kernels' phase stagger (kv_wino88i.h out_stagger), in units of s_sleep 127
+// KV_R3_ONEROUND=0: the R3 GEMM's TPW-tile groups one per workgroup, in rounds (the A/B form)
+static bool r3_one_round() {
+    static const bool v = [] {
+        const char* e = getenv("KV_R3_ONEROUND");
+        return !e || e[0] != '0';
+    }();
+    return v;
+}
+
 static int out_abl() {  // KV_OUT_ABL: output-kernel timing ablations (A/B tooling only; outputs invalid)
     static const int v = [] {
         const char* e = getenv("KV_OUT_ABL");
@@ -1111,7 +1120,7 @@ static int launch_wino88i32_gemm_lagt(const int8_t* V8, const int* ev, const int
 template <int K, int TPW>
 static int launch_wino88i32_gemm_r3k64(const int8_t* V8, const int* ev, const int8_t* U8, const int* eu, float* M,
                                        int rows, int stride, hipStream_t st) {
-    constexpr int bytes = 3 * 4 * 128 * 96 + TPW * 1024;  // the ring + every tile's exponents
+    constexpr int bytes = 3 * 4 * 128 * 96 + 2 * TPW * 1024;  // the ring + two groups' tile exponents
     auto kern = kv::wino88i32_gemm_r3k64_kernel<K, TPW>;
     if constexpr (K == 512 && TPW == 5) {  // KV_R3K64_ABL: timing ablations (outputs invalid; A/B tooling only)
         static const int abl = [] {
@@ -1129,7 +1138,14 @@ static int launch_wino88i32_gemm_r3k64(const int8_t* V8, const int* ev, const in
     const int tiles = kv::W88_XI * (rows / 128) * (512 / 128);
     KV_REQUIRE(rows % 128 == 0 && stride % 128 == 0 && tiles % (8 * TPW) == 0, KV_EINVAL,
                "wino gemm i8 (r3k64): rows %d / stride %d vs tile 128", rows, stride);
-    hipLaunchKernelGGL(kern, dim3(tiles / TPW), dim3(512), bytes, st, V8, ev, U8, eu, M, rows, 512, stride, nullptr);
+    // one round: when the TPW-tile groups fill whole rounds of the CUs, one workgroup per CU runs all its rounds'
+    // groups back to back, the copy ring running across them (no prologue between them)
+    int nwg = tiles / TPW;
+    const int cus = device_cus();
+    if (r3_one_round() && cus > 0 && cus % 8 == 0 && nwg > cus && nwg % cus == 0) nwg = cus;
+    KV_REQUIRE(nwg % 8 == 0 && tiles % (nwg * TPW) == 0, KV_EINVAL, "wino gemm i8 (r3k64): %d tiles, %d workgroups",
+               tiles, nwg);
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(512), bytes, st, V8, ev, U8, eu, M, rows, 512, stride, nullptr);
     KV_HIP(hipGetLastError());
     return KV_OK;
 }
@@ -2572,7 +2588,7 @@ int kv_dev_gemm_clock(int device, int rows, int digits, double seconds, double* 
     KV_REQUIRE(tiles % (8 * tpw) == 0, KV_EINVAL, "kv_dev_gemm_clock: %d tiles, %d per workgroup", tiles, tpw);
     KV_HIP(stamps.alloc((size_t)nwg * 4));
     // the stamped build of the form the product launches (R3: the 64-k-stage kernel)
-    const int bytes = r3 ? 3 * 4 * 128 * 96 + tpw * 1024 : KV_I8F32_NB * T::STAGE;
+    const int bytes = r3 ? 3 * 4 * 128 * 96 + 2 * tpw * 1024 : KV_I8F32_NB * T::STAGE;
     auto kern = r3 ? (tpw == 5   ? kv::wino88i32_gemm_r3k64_kernel<K, 5, true>
                       : tpw == 4 ? kv::wino88i32_gemm_r3k64_kernel<K, 4, true>
                                  : kv::wino88i32_gemm_r3k64_kernel<K, 1, true>)

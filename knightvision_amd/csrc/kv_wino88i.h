@@ -1033,7 +1033,7 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
     }
     constexpr int ND = 3, NB = 3, PD = NB - 1, GL = 6;
     constexpr int NT = 2, WM = 128, WN = 128, WC = 2;
-    constexpr int NK = K / 32, NU = NK / 2, NS = TPW * NU;
+    constexpr int NK = K / 32, NU = NK / 2, NSG = TPW * NU;  // stages per group of TPW tiles
     constexpr int PLANE = 128 * 96, STAGE = 4 * PLANE;  // [operand][chunk] planes: 48 KiB
     static_assert(NK % 2 == 0 && NU > PD && 8 * GL * 1024 == STAGE, "64-k stages, 6 pieces per wave");
     constexpr double kStep = 0.00390625;  // level weight: radix 256
@@ -1045,26 +1045,27 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
     const int lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WC, wn = wave % WC;
     const int CT = cout / WN, RT = rows / WM;
-    const int nwg = (int)gridDim.x, nv = nwg * TPW;  // nwg a multiple of 8
-    int xis[TPW], nbs[TPW], rbs[TPW];
-#pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-        const int vb = (int)blockIdx.x + j * nwg;
+    // nwg a multiple of 8; a workgroup runs ng groups of TPW tiles (the host makes nv = nwg TPW ng exact): one group
+    // per workgroup in rounds, or, when the groups fill whole rounds of the CUs, ng of them per workgroup in one
+    // round, the copy ring running across the group boundaries too
+    const int nwg = (int)gridDim.x, nv = kv::W88_XI * RT * CT, ng = nv / (nwg * TPW), NST = ng * NSG;
+    auto coords = [&](int T, int& xi, int& nb, int& rb) {  // tile T of this workgroup (XCD-aware order)
+        const int vb = (int)blockIdx.x + T * nwg;
         const int idx = (vb & 7) * (nv >> 3) + (vb >> 3);
-        xis[j] = idx / (CT * RT);
-        nbs[j] = (idx % CT) * WN;
-        rbs[j] = ((idx / CT) % RT) * WM;
-    }
+        xi = idx / (CT * RT);
+        nb = (idx % CT) * WN;
+        rb = ((idx / CT) % RT) * WM;
+    };
+    int xis[TPW], nbs[TPW], rbs[TPW];
 
     const int wu = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the plane this wave copies
     const int op = wu >> 2, chunk = (wu >> 1) & 1, pp0 = 6 * (wu & 1);
     const size_t sstep = (op ? (size_t)cout : (size_t)stride) * 96;  // one 32-channel chunk of 96-byte row lines
-    const int8_t* gb[TPW];
-#pragma unroll
-    for (int j = 0; j < TPW; ++j)
-        gb[j] = (op ? U8 + (((size_t)xis[j] * NK) * cout + (size_t)nbs[j]) * 96
-                    : V8 + (((size_t)xis[j] * NK) * stride + (size_t)rbs[j]) * 96) +
-                (size_t)chunk * sstep;
+    auto tile_base = [&](int xi, int nb, int rb) {
+        return (op ? U8 + (((size_t)xi * NK) * cout + (size_t)nb) * 96 : V8 + (((size_t)xi * NK) * stride + (size_t)rb) * 96) +
+               (size_t)chunk * sstep;
+    };
+    const int8_t* gb[TPW + 1];  // the group's tiles, then the next group's first
     // this lane's source byte in a chunk's row-line block, per piece: unsigned 32-bit, so the copy takes the
     // scalar-base + 32-bit-offset address form (one address VGPR per lane instead of a 64-bit pair)
     unsigned goff[GL];
@@ -1074,13 +1075,13 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
         goff[g] = (unsigned)(row * 96 + 16 * (slot ^ ((row >> 4) & 1)));
     }
     const int ldst = (op * 2 + chunk) * PLANE + pp0 * 1024;
-    auto issue1 = [&](int g, int s) {  // piece g of global stage s (tile s / NU, stage s % NU)
+    auto issue1 = [&](int g, int s, int sg) {  // piece g of the group's stage s (tile s / NU), ring stage sg
         if constexpr ((ABL & 1) != 0)
-            if (s >= PD) return;
+            if (sg >= PD) return;
         const int j = s / NU, ku = s - j * NU;
         const int8_t* base = gb[0];
 #pragma unroll
-        for (int jj = 1; jj < TPW; ++jj) base = j == jj ? gb[jj] : base;
+        for (int jj = 1; jj <= TPW; ++jj) base = j == jj ? gb[jj] : base;
         const int8_t* const sb = base + (size_t)(2 * ku) * sstep;  // wave-uniform
 #if KV_COPY_SADDR
         const void* src = (const void*)(sb + goff[g]);
@@ -1088,7 +1089,7 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
         const void* src = (const void*)(sb + (size_t)(int)goff[g]);
 #endif
         __builtin_amdgcn_global_load_lds(src,
-                                         (__attribute__((address_space(3))) void*)(L0 + (s % NB) * STAGE + ldst +
+                                         (__attribute__((address_space(3))) void*)(L0 + (sg % NB) * STAGE + ldst +
                                                                                    g * 1024),
                                          16, 0, 0);
     };
@@ -1108,22 +1109,40 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
             }
         }
 
-    // every tile's row / column exponents staged in LDS beside the ring (TPW x 1 KiB), loaded before the prologue
-    // copies: the epilogue reads them from LDS instead of waiting on global loads at each tile's end (timing
-    // ablation without the loads: 339 -> 323 us, profiles/r06_r3k64_ablations_final.log)
-    int* const exl = (int*)(L0 + NB * STAGE);  // [TPW][256]: ev rows 0-127, eu columns 128-255
+    // each group's row / column exponents staged in LDS beside the ring (2 x TPW x 1 KiB, by group parity): loaded
+    // into registers at the group's start and stored after its first two stages, so the epilogue reads LDS instead
+    // of waiting on global loads at each tile's end (timing ablation without the loads: 339 -> 323 us,
+    // profiles/r06_r3k64_ablations_final.log)
+    constexpr int NEX = (TPW * 256 + 511) / 512;
+    int* const exl = (int*)(L0 + NB * STAGE);  // [2][TPW][256]: ev rows 0-127, eu columns 128-255
+    for (int gi = 0; gi < ng; ++gi) {
 #pragma unroll
-    for (int q = 0; q < (TPW * 256 + 511) / 512; ++q) {
+    for (int j = 0; j < TPW; ++j) {
+        coords(gi * TPW + j, xis[j], nbs[j], rbs[j]);
+        gb[j] = tile_base(xis[j], nbs[j], rbs[j]);
+    }
+    {
+        int xn, nn, rn;
+        coords(gi + 1 < ng ? (gi + 1) * TPW : gi * TPW, xn, nn, rn);
+        gb[TPW] = tile_base(xn, nn, rn);
+    }
+    int exv[NEX];
+#pragma unroll
+    for (int q = 0; q < NEX; ++q) {
         const int t = tid + q * 512;
+        exv[q] = 0;
         if (t < TPW * 256) {
             const int jj = t >> 8, k = t & 255;
-            exl[t] = k < 128 ? ev[(size_t)xis[jj] * stride + rbs[jj] + k] : eu[(size_t)xis[jj] * cout + nbs[jj] + k - 128];
+            exv[q] = k < 128 ? ev[(size_t)xis[jj] * stride + rbs[jj] + k] : eu[(size_t)xis[jj] * cout + nbs[jj] + k - 128];
         }
     }
+    int* const exg = exl + (gi & 1) * TPW * 256;
+    if (gi == 0) {
 #pragma unroll
-    for (int p = 0; p < PD; ++p)
+        for (int p = 0; p < PD; ++p)
 #pragma unroll
-        for (int g = 0; g < GL; ++g) issue1(g, p);
+            for (int g = 0; g < GL; ++g) issue1(g, p, p);
+    }
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
         i32x16_t acc[ND][NT];
@@ -1142,11 +1161,11 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
                         acc[i + jb][nt] = r3mfma<ABL>(pa[i], pb[jb - 1][nt], acc[i + jb][nt]);
         };
         for (int ku = 0; ku < NU; ++ku) {
-            const int s = j * NU + ku;
-            // stage s's pieces landed (vmcnt counts in issue order): what may stay outstanding is the m later
+            const int s = j * NU + ku, sg = gi * NSG + s;
+            // stage sg's pieces landed (vmcnt counts in issue order): what may stay outstanding is the m later
             // stages already issued and, for a tile's first PD stages, the previous tile's 32 M stores
-            const int m = NS - 1 - s < PD - 1 ? NS - 1 - s : PD - 1;
-            if (j > 0 && ku < PD) {
+            const int m = NST - 1 - sg < PD - 1 ? NST - 1 - sg : PD - 1;
+            if ((gi > 0 || j > 0) && ku < PD) {
                 if (m == 0) vm_lgkm_wait<32>();
                 else vm_lgkm_wait<GL + 32>();
             } else {
@@ -1155,7 +1174,7 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
             }
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-            const char* buf = L0 + (s % NB) * STAGE;
+            const char* buf = L0 + (sg % NB) * STAGE;
             i8x16_t a0[ND], b0[ND][NT], a1[ND], b1[ND][NT];
 #pragma unroll
             for (int d = 0; d < ND; ++d) a0[d] = *(const i8x16_t*)(buf + aoff[0][d]);
@@ -1163,10 +1182,10 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
             for (int nt = 0; nt < NT; ++nt) b0[0][nt] = *(const i8x16_t*)(buf + boff[0][nt][0]);
             __builtin_amdgcn_sched_barrier(0);
             if (ku > 0) h2();
-            if (s + PD < NS) {
-                issue1(0, s + PD);
-                issue1(1, s + PD);
-                issue1(2, s + PD);
+            if (sg + PD < NST) {
+                issue1(0, s + PD, sg + PD);
+                issue1(1, s + PD, sg + PD);
+                issue1(2, s + PD, sg + PD);
             }
             // chunk 0: all 6 pairs
 #pragma unroll
@@ -1186,10 +1205,10 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt)
                         acc[i + jb][nt] = r3mfma<ABL>(a0[i], b0[jb][nt], acc[i + jb][nt]);
-                if (jb == 0 && s + PD < NS) {
-                    issue1(3, s + PD);
-                    issue1(4, s + PD);
-                    issue1(5, s + PD);
+                if (jb == 0 && sg + PD < NST) {
+                    issue1(3, s + PD, sg + PD);
+                    issue1(4, s + PD, sg + PD);
+                    issue1(5, s + PD, sg + PD);
                 }
             }
             // chunk 1: B digit 0 now, digits 1-2 after the next barrier
@@ -1211,14 +1230,19 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
                 pb[0][nt] = b1[1][nt];
                 pb[1][nt] = b1[2][nt];
             }
+            if (j == 0 && ku == 1) {  // the group's exponents (read back after the next barrier)
+#pragma unroll
+                for (int q = 0; q < NEX; ++q)
+                    if (tid + q * 512 < TPW * 256) exg[tid + q * 512] = exv[q];
+            }
         }
         h2();
         const int xi = xis[j], n_base = nbs[j], r_base = rbs[j];
-        const int* evx = exl + j * 256 + wm * 32;  // LDS (staged above)
+        const int* evx = exg + j * 256 + wm * 32;  // LDS (staged above)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
             const int col = n_base + wn * NT * 32 + nt * 32 + lr;
-            const int ec = (ABL & 8) ? -14 : exl[j * 256 + 128 + wn * NT * 32 + nt * 32 + lr] - 14;
+            const int ec = (ABL & 8) ? -14 : exg[j * 256 + 128 + wn * NT * 32 + nt * 32 + lr] - 14;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -1235,6 +1259,7 @@ __global__ __launch_bounds__(512) void wino88i32_gemm_r3k64_kernel(const int8_t*
             }
         }
     }
+    }  // groups
     if constexpr (STAMP) {
         const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         if (threadIdx.x < 4) {  // one vector store per value, lanes 0-3
